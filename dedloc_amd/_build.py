@@ -1,0 +1,106 @@
+"""In-tree native build of dedloc_amd (gfx950 HIP kernels + torch.library bindings + C++ runtime).
+
+The build is deliberately plain: every ``csrc/kernels/*.hip`` file is compiled by ``hipcc
+--offload-arch=gfx950`` into its own object (fast: those translation units include only HIP
+headers), ``csrc/bindings.cpp`` is the single translation unit that includes torch, and everything
+is linked into ``dedloc_amd/_C.so`` next to this file, so the shared object travels with the
+repository snapshot to the GPU box.  The control-plane server (``csrc/runtime``) is linked into a
+separate ``dedloc_amd/_dht.so`` with no torch dependency.
+
+Objects are rebuilt only when their source or any header is newer (mtime), so repeated calls are
+cheap.  Run ``python -m dedloc_amd._build`` to build from the command line.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(os.path.dirname(ROOT), "build", "obj")
+ARCH = os.environ.get("DEDLOC_OFFLOAD_ARCH", "gfx950")
+SO_PATH = os.path.join(ROOT, "_C.so")
+DHT_SO_PATH = os.path.join(ROOT, "_dht.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _torch_paths():
+    import torch
+    import torch.utils.cpp_extension as ce
+
+    abi = int(torch.compiled_with_cxx11_abi())
+    return ce.include_paths(), ce.library_paths(), abi
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build step failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    inc = ["-I", os.path.join(CSRC, "include")]
+    hip_flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-munsafe-fp-atomics"]
+    jobs = jobs or min(8, os.cpu_count() or 4)
+
+    jobs_list = []
+    objs = []
+    for src in hip_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
+        objs.append(obj)
+        if _newer(obj, [src] + headers):
+            jobs_list.append(["hipcc", *hip_flags, *inc, "-c", src, "-o", obj])
+
+    tinc, tlib, abi = _torch_paths()
+    bind_src = os.path.join(CSRC, "bindings.cpp")
+    bind_obj = os.path.join(BUILD, "bindings.o")
+    objs.append(bind_obj)
+    if _newer(bind_obj, [bind_src] + headers):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__",
+               "-DUSE_ROCM", "-I", f"{ROCM}/include", *inc]
+        for p in tinc:
+            cmd += ["-I", p]
+        cmd += ["-I", sysconfig.get_paths()["include"], "-c", bind_src, "-o", bind_obj]
+        jobs_list.append(cmd)
+
+    rt_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    rt_objs = []
+    for src in rt_srcs:
+        obj = os.path.join(BUILD, "rt_" + os.path.basename(src).replace(".cpp", ".o"))
+        rt_objs.append(obj)
+        if _newer(obj, [src] + headers + glob.glob(os.path.join(CSRC, "runtime", "*.h"))):
+            jobs_list.append(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", *inc, "-c", src, "-o", obj])
+
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs_list))
+
+    if _newer(SO_PATH, objs):
+        cmd = ["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", SO_PATH]
+        for p in tlib:
+            cmd += ["-L", p, f"-Wl,-rpath,{p}"]
+        cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+        _run(cmd, verbose)
+    if rt_objs and _newer(DHT_SO_PATH, rt_objs):
+        _run(["g++", "-shared", "-fPIC", *rt_objs, "-o", DHT_SO_PATH, "-lpthread"], verbose)
+    return SO_PATH
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

@@ -1,0 +1,146 @@
+// dedloc_amd — shared device helpers for the gfx950 (CDNA4) kernels.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * bf16 tensors are passed as raw `uint16_t*` (bit patterns); conversion is done with the
+//     round-to-nearest-even helpers below so results are bit-identical to torch's bf16 casts.
+//   * a wave is 64 lanes; all reductions use 64-wide xor shuffles (never warp-32 idioms).
+//   * every launcher takes an explicit hipStream_t and never allocates or synchronises, so the
+//     whole training micro-step can be captured into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DL_WAVE 64
+
+#define DL_HIP_CHECK(expr)                                                              \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+      abort();                                                                          \
+    }                                                                                   \
+  } while (0)
+
+typedef uint16_t bf16_t;
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef short short4_t __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// fp16 (IEEE half) conversions for the FLOAT16 wire format.
+__device__ __forceinline__ uint16_t f2h(float f) {
+  _Float16 h = (_Float16)f;
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+__device__ __forceinline__ float h2f(uint16_t v) {
+  _Float16 h = *reinterpret_cast<_Float16*>(&v);
+  return (float)h;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `scratch` must hold >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  return r;
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  // gelu_new (HF ALBERT): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  float du = k0 * (1.f + 3.f * k1 * x2);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, T1):
+// consecutive logical tiles land on the same XCD so neighbouring tiles share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// Vectorised bf16 <-> fp32 row fragments (cdna_hip_programming.md Guideline 13: never scalar bf16).
+template <int VW>
+__device__ __forceinline__ void load_bf16(const bf16_t* p, float* out) {
+  if constexpr (VW == 8) {
+    uint4 v = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      out[2 * i] = __uint_as_float(w[i] << 16);
+      out[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  } else if constexpr (VW == 4) {
+    uint2 v = *reinterpret_cast<const uint2*>(p);
+    out[0] = __uint_as_float(v.x << 16); out[1] = __uint_as_float(v.x & 0xffff0000u);
+    out[2] = __uint_as_float(v.y << 16); out[3] = __uint_as_float(v.y & 0xffff0000u);
+  } else if constexpr (VW == 2) {
+    uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+    out[0] = __uint_as_float(v << 16); out[1] = __uint_as_float(v & 0xffff0000u);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VW; ++i) out[i] = bf2f(p[i]);
+  }
+}
+
+template <int VW>
+__device__ __forceinline__ void store_bf16(bf16_t* p, const float* in) {
+  if constexpr (VW == 8) {
+    uint4 v;
+    v.x = (uint32_t)f2bf(in[0]) | ((uint32_t)f2bf(in[1]) << 16);
+    v.y = (uint32_t)f2bf(in[2]) | ((uint32_t)f2bf(in[3]) << 16);
+    v.z = (uint32_t)f2bf(in[4]) | ((uint32_t)f2bf(in[5]) << 16);
+    v.w = (uint32_t)f2bf(in[6]) | ((uint32_t)f2bf(in[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = v;
+  } else if constexpr (VW == 4) {
+    uint2 v;
+    v.x = (uint32_t)f2bf(in[0]) | ((uint32_t)f2bf(in[1]) << 16);
+    v.y = (uint32_t)f2bf(in[2]) | ((uint32_t)f2bf(in[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = v;
+  } else if constexpr (VW == 2) {
+    *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(in[0]) | ((uint32_t)f2bf(in[1]) << 16);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VW; ++i) p[i] = f2bf(in[i]);
+  }
+}
+

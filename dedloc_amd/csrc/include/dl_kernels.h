@@ -1,0 +1,60 @@
+// Host-side launcher ABI of the dedloc_amd HIP kernels (all gfx950).  Every launcher enqueues on
+// the given stream, never allocates and never synchronises, and returns 0 on success or -1 when
+// the shape is unsupported (the binding layer turns that into a Python exception).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+
+// layernorm.hip
+int dl_layernorm_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y,
+                     bf16_t* s_out, float* mean, float* rstd, int rows, int D, float eps, hipStream_t st);
+int dl_layernorm_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
+                     bf16_t* ds, float* dg_part, float* db_part, int rows, int D, int nparts, hipStream_t st);
+
+// elementwise.hip
+int dl_gelu_fwd(const bf16_t* h, bf16_t* y, size_t n, hipStream_t st);
+int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStream_t st);
+int dl_tanh_fwd(const bf16_t* x, bf16_t* y, size_t n, hipStream_t st);
+int dl_tanh_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, size_t n, hipStream_t st);
+int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hipStream_t st);
+int dl_colsum_f32(const float* part, float* out, int nparts, int N, int accumulate, hipStream_t st);
+int dl_cast_f32_bf16(const float* x, bf16_t* y, size_t n, hipStream_t st);
+int dl_add_bf16_to_f32(const bf16_t* x, float* y, size_t n, float alpha, hipStream_t st);
+
+// optim.hip
+int dl_lamb_step(float* p, const float* g, float* m, float* v, const int* chunk_tensor, const long* chunk_start,
+                 const int* chunk_len, int nchunks, const float* tensor_wd, float* norms, int ntensors, float beta1,
+                 float beta2, float eps, float step_size, float clamp_value, float grad_scale, float* trust_out,
+                 hipStream_t st);
+int dl_larc_sgd_step(float* p, const float* g, float* buf, const int* chunk_tensor, const long* chunk_start,
+                     const int* chunk_len, int nchunks, const float* tensor_wd, float* norms, int ntensors, float lr,
+                     float momentum, float trust_coef, float eps, int clip, int first_step, float grad_scale,
+                     hipStream_t st);
+int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, hipStream_t st);
+int dl_axpby(float* y, const float* x, size_t n, float a, float b, hipStream_t st);
+
+// comm.hip
+int dl_pack(const float* src, void* dst, int dst_dt, size_t n, float weight, hipStream_t st);
+int dl_reduce_parts(const void* parts, int part_dt, size_t part_stride, int nparts, void* out, int out_dt, size_t n,
+                    float inv_total, hipStream_t st);
+int dl_unpack(const void* src, int src_dt, float* dst, const float* snap, size_t n, hipStream_t st);
+
+// embedding.hip
+int dl_embed_ln_fwd(const long* ids, const long* tt, const float* wemb, const float* pemb, const float* temb,
+                    const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out, float* mean, float* rstd, int T,
+                    int S, int E, float eps, hipStream_t st);
+int dl_embed_bwd(const bf16_t* ds, const long* ids, const long* tt, float* dwemb, float* dpemb, float* dtemb, int B,
+                 int S, int E, int ntypes, hipStream_t st);
+
+// xent.hip
+int dl_xent_fwd_bwd(const bf16_t* logits, const long* labels, bf16_t* dlogits, float* row_loss, float* loss_out,
+                    float* scale_buf, int M, int V, long ld, int ignore_index, hipStream_t st);
+
+// attention.hip
+int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, bf16_t* out, long ldo, float* lse, int B, int H, int S,
+                int D, float scale, hipStream_t st);
+int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const bf16_t* out, const bf16_t* dout, long ldo,
+                const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D, float scale, hipStream_t st);

@@ -1,0 +1,455 @@
+// Flash-style multi-head self-attention for ALBERT: head_dim 64, S % 64 == 0,
+// additive key-padding bias, bf16 in/out, fp32 softmax state, never materialises [B,H,S,S].
+//
+// Inputs come straight from the fused QKV projection: qkv is [B*S, 3*H*64] (Q | K | V, head h at
+// columns h*64 of each third) and the context is written as [B*S, H*64] — exactly the layout the
+// output projection consumes, so no transposes exist anywhere in the attention path.
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 (cdna_hip_programming.md §3).  Every product is arranged so that
+// the "reduction-side" operand comes out of the previous MFMA's accumulator with no lane movement
+// (§3 "An accumulator tile as the next MFMA's operand"), and the other operand is read from LDS
+// either by rows (ds_read_b128) or transposed (ds_read_b64_tr_b16, T10):
+//   fwd   : S^T = K Q^T (query on the lane -> softmax row state is per-lane)
+//           O^T += V^T P^T (P^T accumulator is the B operand; V^T via tr-reads)
+//   bwd dq: S^T, dP^T = V dO^T, dQ^T += K^T dS^T        (query on the lane)
+//   bwd dkdv: S = Q K^T, dP = dO V^T (key on the lane), dV^T += dO^T P, dK^T += Q^T dS
+// One LDS image per 64x64 bf16 tile serves both the row reads and the transposed reads: 16-byte
+// chunk c of row r lives at chunk c ^ f((r>>1)&7), f(x) = x ^ ((x&1)<<2) — conflict-free for the
+// ds_read_b128 lane groups and for the 4-row tr-read blocks (derivation in docs/KERNELS.md).
+#include "dl_common.h"
+#include "dl_kernels.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4_t lds_s4;
+
+constexpr int HD = 64;          // head dim
+constexpr int TILE_BYTES = 64 * 128;
+constexpr float NEG_BIG = -1.0e30f;
+
+__device__ __forceinline__ int swzf(int x) { return x ^ ((x & 1) << 2); }
+__device__ __forceinline__ int chunk_off(int row, int c) { return row * 128 + ((c ^ swzf((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int crow(int i, int hh) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
+
+__device__ __forceinline__ floatx16 mfma32(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// 16-byte row fragment: row `row`, chunk `c` of a swizzled tile
+__device__ __forceinline__ bf16x8 lds_row_frag(const uint8_t* tile, int row, int c) {
+  return *reinterpret_cast<const bf16x8*>(tile + chunk_off(row, c));
+}
+
+// ds_read_b64_tr_b16 on a swizzled tile: the calling lane (index i within its 16-lane group)
+// supplies row row0 + (i>>2), columns col0 + 4*(i&3) .. +3; it receives column col0 + i of the
+// four rows row0..row0+3.
+__device__ __forceinline__ s4_t lds_tr(const uint8_t* tile, int row0, int col0, int i) {
+  const int row = row0 + (i >> 2);
+  const int col = col0 + 4 * (i & 3);
+  const int off = chunk_off(row, col >> 3) + ((col & 7) << 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(tile + off));
+}
+
+// A-operand fragment whose element e is taken from k-row 16*s + 8*(e>>2) + 4*hh + (e&3) of the
+// tile (matching the permuted k order of an accumulator used as B operand), column = 32*t + r.
+__device__ __forceinline__ bf16x8 tr_operand(const uint8_t* tile, int kbase, int hh, int t, int lane) {
+  const int col0 = 32 * t + 16 * ((lane >> 4) & 1);
+  const s4_t lo = lds_tr(tile, kbase + 4 * hh, col0, lane & 15);
+  const s4_t hi = lds_tr(tile, kbase + 8 + 4 * hh, col0, lane & 15);
+  bf16x8 a;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] = __builtin_bit_cast(__bf16, lo[e]);
+    a[4 + e] = __builtin_bit_cast(__bf16, hi[e]);
+  }
+  return a;
+}
+
+// accumulator registers 8s..8s+7 -> bf16 B-operand fragment
+__device__ __forceinline__ bf16x8 pack_acc(const floatx16& x, int s) {
+  bf16x8 b;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) b[e] = (__bf16)x[8 * s + e];
+  return b;
+}
+
+__device__ __forceinline__ bf16x8 gload8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// cooperative 64-row x 64-col tile stage: 256 threads, 2 x 16 B each
+struct TileRegs { uint4 v[2]; };
+
+__device__ __forceinline__ void tile_load(TileRegs& t, const bf16_t* g, long ld, int row0, int rows_valid) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    int row = idx >> 3;
+    const int c = idx & 7;
+    row = min(row0 + row, rows_valid - 1);
+    t.v[k] = *reinterpret_cast<const uint4*>(g + (long)row * ld + c * 8);
+  }
+}
+
+__device__ __forceinline__ void tile_store(const TileRegs& t, uint8_t* tile) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    *reinterpret_cast<uint4*>(tile + chunk_off(idx >> 3, idx & 7)) = t.v[k];
+  }
+}
+
+// store 4 consecutive bf16 (8 bytes)
+__device__ __forceinline__ void store4(bf16_t* p, float a, float b, float c, float d) {
+  uint2 v;
+  v.x = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  v.y = (uint32_t)f2bf(c) | ((uint32_t)f2bf(d) << 16);
+  *reinterpret_cast<uint2*>(p) = v;
+}
+
+// ------------------------------------------------------------------------------------------ fwd
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
+                                                          const float* __restrict__ mbias, bf16_t* __restrict__ out,
+                                                          long ldo, float* __restrict__ lse, int H, int S, float sl2) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
+  const long rb = (long)b * S;
+  const bf16_t* Qg = qkv + rb * ld + h * HD;
+  const bf16_t* Kg = qkv + rb * ld + (long)H * HD + h * HD;
+  const bf16_t* Vg = qkv + rb * ld + 2L * H * HD + h * HD;
+  const float* mb_g = mbias ? mbias + rb : nullptr;
+  float* mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
+
+  const int q = blockIdx.x * 128 + w * 32 + r;
+  const int qc = min(q, S - 1);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = gload8(Qg + (long)qc * ld + ks * 16 + 8 * hh);
+
+  floatx16 o[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
+  float m = NEG_BIG, l = 0.f;
+
+  const int nt = S / 64;
+  TileRegs kr, vr;
+  float mbr = 0.f;
+  tile_load(kr, Kg, ld, 0, S);
+  tile_load(vr, Vg, ld, 0, S);
+  if (threadIdx.x < 64) mbr = mb_g ? mb_g[threadIdx.x] : 0.f;
+  tile_store(kr, smem);
+  tile_store(vr, smem + TILE_BYTES);
+  if (threadIdx.x < 64) mbs[threadIdx.x] = mbr;
+  __syncthreads();
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    const uint8_t* Ks = smem + cur * 2 * TILE_BYTES;
+    const uint8_t* Vs = Ks + TILE_BYTES;
+    const float* mb = mbs + cur * 64;
+    if (kt + 1 < nt) {  // issue next tile's loads early; they land under the MFMAs below (T14)
+      tile_load(kr, Kg, ld, (kt + 1) * 64, S);
+      tile_load(vr, Vg, ld, (kt + 1) * 64, S);
+      if (threadIdx.x < 64) mbr = mb_g ? mb_g[(kt + 1) * 64 + threadIdx.x] : 0.f;
+    }
+    floatx16 s[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[j][i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[j] = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], s[j]);
+    }
+    float mx = NEG_BIG;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float v = s[j][i] * sl2 + mb[32 * j + crow(i, hh)];
+        s[j][i] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = exp2f(s[j][i] - mn);
+        s[j][i] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(s[j], ss);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) o[t] = mfma32(tr_operand(Vs, 32 * j + 16 * ss, hh, t, lane), pb, o[t]);
+      }
+    if (kt + 1 < nt) {
+      uint8_t* Kn = smem + (cur ^ 1) * 2 * TILE_BYTES;
+      tile_store(kr, Kn);
+      tile_store(vr, Kn + TILE_BYTES);
+      if (threadIdx.x < 64) mbs[(cur ^ 1) * 64 + threadIdx.x] = mbr;
+    }
+    __syncthreads();
+  }
+
+  if (q < S) {
+    const float inv = 1.f / l;
+    bf16_t* op = out + (rb + q) * ldo + h * HD;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        store4(op + 32 * t + 8 * u + 4 * hh, o[t][4 * u] * inv, o[t][4 * u + 1] * inv, o[t][4 * u + 2] * inv,
+               o[t][4 * u + 3] * inv);
+    if (hh == 0) lse[((long)b * H + h) * S + q] = m + log2f(l);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ bwd dq
+// Also computes delta = rowsum(dO * O) for its queries and publishes it for the dkdv kernel.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, long ld,
+                                                             const float* __restrict__ mbias,
+                                                             const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
+                                                             long ldo, const float* __restrict__ lse,
+                                                             float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                             int H, int S, float sl2, float scale) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
+  const long rb = (long)b * S;
+  const bf16_t* Qg = qkv + rb * ld + h * HD;
+  const bf16_t* Kg = qkv + rb * ld + (long)H * HD + h * HD;
+  const bf16_t* Vg = qkv + rb * ld + 2L * H * HD + h * HD;
+  const float* mb_g = mbias ? mbias + rb : nullptr;
+  float* mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
+
+  const int q = blockIdx.x * 128 + w * 32 + r;
+  const int qc = min(q, S - 1);
+  bf16x8 qf[4], df[4];
+  float dl = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = gload8(Qg + (long)qc * ld + ks * 16 + 8 * hh);
+    const long oo = (rb + qc) * ldo + h * HD + ks * 16 + 8 * hh;
+    df[ks] = gload8(dout + oo);
+    const bf16x8 of = gload8(out + oo);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dl += (float)df[ks][e] * (float)of[e];
+  }
+  dl += __shfl_xor(dl, 32, 64);
+  const float l2 = lse[((long)b * H + h) * S + qc];
+  if (q < S && hh == 0) delta[((long)b * H + h) * S + q] = dl;
+
+  floatx16 dq[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
+
+  const int nt = S / 64;
+  TileRegs kr, vr;
+  float mbr = 0.f;
+  tile_load(kr, Kg, ld, 0, S);
+  tile_load(vr, Vg, ld, 0, S);
+  if (threadIdx.x < 64) mbr = mb_g ? mb_g[threadIdx.x] : 0.f;
+  tile_store(kr, smem);
+  tile_store(vr, smem + TILE_BYTES);
+  if (threadIdx.x < 64) mbs[threadIdx.x] = mbr;
+  __syncthreads();
+
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    const uint8_t* Ks = smem + cur * 2 * TILE_BYTES;
+    const uint8_t* Vs = Ks + TILE_BYTES;
+    const float* mb = mbs + cur * 64;
+    if (kt + 1 < nt) {
+      tile_load(kr, Kg, ld, (kt + 1) * 64, S);
+      tile_load(vr, Vg, ld, (kt + 1) * 64, S);
+      if (threadIdx.x < 64) mbr = mb_g ? mb_g[(kt + 1) * 64 + threadIdx.x] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      floatx16 st, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { st[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        st = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], st);
+        dp = mfma32(lds_row_frag(Vs, 32 * j + r, 2 * ks + hh), df[ks], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = exp2f(st[i] * sl2 + mb[32 * j + crow(i, hh)] - l2);
+        st[i] = p * (dp[i] - dl);
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(st, ss);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) dq[t] = mfma32(tr_operand(Ks, 32 * j + 16 * ss, hh, t, lane), pb, dq[t]);
+      }
+    }
+    if (kt + 1 < nt) {
+      uint8_t* Kn = smem + (cur ^ 1) * 2 * TILE_BYTES;
+      tile_store(kr, Kn);
+      tile_store(vr, Kn + TILE_BYTES);
+      if (threadIdx.x < 64) mbs[(cur ^ 1) * 64 + threadIdx.x] = mbr;
+    }
+    __syncthreads();
+  }
+  if (q < S) {
+    bf16_t* dp_ = dqkv + (rb + q) * ld + h * HD;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        store4(dp_ + 32 * t + 8 * u + 4 * hh, dq[t][4 * u] * scale, dq[t][4 * u + 1] * scale,
+               dq[t][4 * u + 2] * scale, dq[t][4 * u + 3] * scale);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ bwd dkdv
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, long ld,
+                                                               const float* __restrict__ mbias,
+                                                               const bf16_t* __restrict__ dout, long ldo,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ delta,
+                                                               bf16_t* __restrict__ dqkv, int H, int S, float sl2,
+                                                               float scale) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 2 * 64 * 4];
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
+  const long rb = (long)b * S;
+  const bf16_t* Qg = qkv + rb * ld + h * HD;
+  const bf16_t* Kg = qkv + rb * ld + (long)H * HD + h * HD;
+  const bf16_t* Vg = qkv + rb * ld + 2L * H * HD + h * HD;
+  const bf16_t* dOg = dout + rb * ldo + h * HD;
+  const float* lse_g = lse + ((long)b * H + h) * S;
+  const float* del_g = delta + ((long)b * H + h) * S;
+  float* rowv = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);  // [2 buf][lse 64 | delta 64]
+
+  const int k = blockIdx.x * 128 + w * 32 + r;
+  const int kc = min(k, S - 1);
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = gload8(Kg + (long)kc * ld + ks * 16 + 8 * hh);
+    vf[ks] = gload8(Vg + (long)kc * ld + ks * 16 + 8 * hh);
+  }
+  const float mbk = mbias ? mbias[rb + kc] : 0.f;
+
+  floatx16 dk[2], dv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { dk[t][i] = 0.f; dv[t][i] = 0.f; }
+
+  const int nt = S / 64;
+  TileRegs qr, dr;
+  float rv = 0.f;
+  tile_load(qr, Qg, ld, 0, S);
+  tile_load(dr, dOg, ldo, 0, S);
+  if (threadIdx.x < 128) rv = threadIdx.x < 64 ? lse_g[threadIdx.x] : del_g[threadIdx.x - 64];
+  tile_store(qr, smem);
+  tile_store(dr, smem + TILE_BYTES);
+  if (threadIdx.x < 128) rowv[threadIdx.x] = rv;
+  __syncthreads();
+
+  for (int qt = 0; qt < nt; ++qt) {
+    const int cur = qt & 1;
+    const uint8_t* Qs = smem + cur * 2 * TILE_BYTES;
+    const uint8_t* Ds = Qs + TILE_BYTES;
+    const float* lse_s = rowv + cur * 128;
+    const float* del_s = lse_s + 64;
+    if (qt + 1 < nt) {
+      tile_load(qr, Qg, ld, (qt + 1) * 64, S);
+      tile_load(dr, dOg, ldo, (qt + 1) * 64, S);
+      if (threadIdx.x < 128)
+        rv = threadIdx.x < 64 ? lse_g[(qt + 1) * 64 + threadIdx.x] : del_g[(qt + 1) * 64 + threadIdx.x - 64];
+    }
+#pragma unroll
+    for (int i2 = 0; i2 < 2; ++i2) {
+      floatx16 s, dp;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { s[i] = 0.f; dp[i] = 0.f; }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        s = mfma32(lds_row_frag(Qs, 32 * i2 + r, 2 * ks + hh), kf[ks], s);
+        dp = mfma32(lds_row_frag(Ds, 32 * i2 + r, 2 * ks + hh), vf[ks], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qq = 32 * i2 + crow(i, hh);
+        const float p = exp2f(s[i] * sl2 + mbk - lse_s[qq]);
+        s[i] = p;
+        dp[i] = p * (dp[i] - del_s[qq]);
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(s, ss);
+        const bf16x8 db = pack_acc(dp, ss);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          dv[t] = mfma32(tr_operand(Ds, 32 * i2 + 16 * ss, hh, t, lane), pb, dv[t]);
+          dk[t] = mfma32(tr_operand(Qs, 32 * i2 + 16 * ss, hh, t, lane), db, dk[t]);
+        }
+      }
+    }
+    if (qt + 1 < nt) {
+      uint8_t* Qn = smem + (cur ^ 1) * 2 * TILE_BYTES;
+      tile_store(qr, Qn);
+      tile_store(dr, Qn + TILE_BYTES);
+      if (threadIdx.x < 128) rowv[(cur ^ 1) * 128 + threadIdx.x] = rv;
+    }
+    __syncthreads();
+  }
+  if (k < S) {
+    bf16_t* dkp = dqkv + (rb + k) * ld + (long)H * HD + h * HD;
+    bf16_t* dvp = dqkv + (rb + k) * ld + 2L * H * HD + h * HD;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        store4(dkp + 32 * t + 8 * u + 4 * hh, dk[t][4 * u] * scale, dk[t][4 * u + 1] * scale,
+               dk[t][4 * u + 2] * scale, dk[t][4 * u + 3] * scale);
+        store4(dvp + 32 * t + 8 * u + 4 * hh, dv[t][4 * u], dv[t][4 * u + 1], dv[t][4 * u + 2], dv[t][4 * u + 3]);
+      }
+  }
+}
+
+}  // namespace
+
+int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, bf16_t* out, long ldo, float* lse, int B, int H, int S,
+                int D, float scale, hipStream_t st) {
+  if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
+  const float sl2 = scale * 1.4426950408889634f;
+  dim3 grid((S + 127) / 128, H, B);
+  attn_fwd_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, out, ldo, lse, H, S, sl2);
+  return 0;
+}
+
+int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const bf16_t* out, const bf16_t* dout, long ldo,
+                const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D, float scale, hipStream_t st) {
+  if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
+  const float sl2 = scale * 1.4426950408889634f;
+  dim3 grid((S + 127) / 128, H, B);
+  attn_bwd_dq_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, out, dout, ldo, lse, delta, dqkv, H, S, sl2, scale);
+  attn_bwd_dkdv_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, dout, ldo, lse, delta, dqkv, H, S, sl2, scale);
+  return 0;
+}

@@ -1,0 +1,145 @@
+// Memory-bound elementwise / reduction kernels: gelu_new fwd/bwd, bias-gradient column sums,
+// fp32<->bf16 casts of the flat parameter buffer, tanh for the SOP pooler.
+// All bf16 traffic is 16 B per lane (Guideline 13); grids are capped at 256 CUs x 8 blocks and
+// grid-strided (Guideline 11).
+#include "dl_common.h"
+#include "dl_kernels.h"
+
+namespace {
+
+constexpr int kMaxGrid = 2048;
+
+inline int grid_for(size_t nvec, int block) {
+  size_t g = (nvec + block - 1) / block;
+  return (int)(g < (size_t)kMaxGrid ? (g == 0 ? 1 : g) : kMaxGrid);
+}
+
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ y, size_t nvec) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float v[8];
+    load_bf16<8>(h + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
+    store_bf16<8>(y + i * 8, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
+                                                       bf16_t* __restrict__ dh, size_t nvec) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float g[8], v[8];
+    load_bf16<8>(dy + i * 8, g);
+    load_bf16<8>(h + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] *= gelu_tanh_grad(v[j]);
+    store_bf16<8>(dh + i * 8, g);
+  }
+}
+
+__global__ __launch_bounds__(256) void tanh_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(tanhf(bf2f(x[i])));
+}
+
+__global__ __launch_bounds__(256) void tanh_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                       bf16_t* __restrict__ dx, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float t = bf2f(y[i]);
+    dx[i] = f2bf(bf2f(dy[i]) * (1.f - t * t));
+  }
+}
+
+// Column partial sums of a bf16 [rows, N] matrix: block (px, py) sums rows [py*rpb, ...) of the
+// 8*256 = 2048 columns starting at px*2048 -> part[py][col] (fp32).
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
+                                                          int rows, int N, int rpb) {
+  const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (c0 >= N) return;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) {
+    float v[8];
+    load_bf16<8>(x + (size_t)r * N + c0, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[(size_t)blockIdx.y * N + c0 + j] = acc[j];
+}
+
+// out[c] (+)= sum_p part[p][c]
+__global__ __launch_bounds__(256) void colsum_f32_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                         int nparts, int N, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * N + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
+  const size_t nvec = n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    uint2 o;
+    o.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+    o.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+    reinterpret_cast<uint2*>(y)[i] = o;
+  }
+  for (size_t i = nvec * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+// y (fp32) (+)= bf16 x   -- used to fold bf16 partial gradients into fp32 accumulators
+__global__ __launch_bounds__(256) void add_bf16_to_f32_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
+                                                              size_t n, float alpha) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] += alpha * bf2f(x[i]);
+}
+
+}  // namespace
+
+int dl_gelu_fwd(const bf16_t* h, bf16_t* y, size_t n, hipStream_t st) {
+  if (n % 8) return -1;
+  gelu_fwd_kernel<<<grid_for(n / 8, 256), 256, 0, st>>>(h, y, n / 8);
+  return 0;
+}
+
+int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStream_t st) {
+  if (n % 8) return -1;
+  gelu_bwd_kernel<<<grid_for(n / 8, 256), 256, 0, st>>>(dy, h, dh, n / 8);
+  return 0;
+}
+
+int dl_tanh_fwd(const bf16_t* x, bf16_t* y, size_t n, hipStream_t st) {
+  tanh_fwd_kernel<<<grid_for(n, 256), 256, 0, st>>>(x, y, n);
+  return 0;
+}
+
+int dl_tanh_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, size_t n, hipStream_t st) {
+  tanh_bwd_kernel<<<grid_for(n, 256), 256, 0, st>>>(dy, y, dx, n);
+  return 0;
+}
+
+int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hipStream_t st) {
+  if (N % 8) return -1;
+  const int rpb = (rows + nparts - 1) / nparts;
+  dim3 grid((N / 8 + 255) / 256, nparts);
+  colsum_bf16_kernel<<<grid, 256, 0, st>>>(x, part, rows, N, rpb);
+  return 0;
+}
+
+int dl_colsum_f32(const float* part, float* out, int nparts, int N, int accumulate, hipStream_t st) {
+  colsum_f32_kernel<<<(N + 255) / 256, 256, 0, st>>>(part, out, nparts, N, accumulate);
+  return 0;
+}
+
+int dl_cast_f32_bf16(const float* x, bf16_t* y, size_t n, hipStream_t st) {
+  cast_f32_bf16_kernel<<<grid_for(n / 4 + 1, 256), 256, 0, st>>>(x, y, n);
+  return 0;
+}
+
+int dl_add_bf16_to_f32(const bf16_t* x, float* y, size_t n, float alpha, hipStream_t st) {
+  add_bf16_to_f32_kernel<<<grid_for(n, 256), 256, 0, st>>>(x, y, n, alpha);
+  return 0;
+}

@@ -1,0 +1,194 @@
+// Fused (residual-add +) LayerNorm forward/backward for gfx950.
+//
+// Replaces the reference's torch LayerNorm calls inside HF ALBERT (SURVEY.md §2.7 K1/K5/K6/K7:
+// attention `LayerNorm(ctx_out + x)`, `full_layer_layer_norm(ffn_out + attn_out)`, embedding LN,
+// MLM-head LN).  One 64-lane wave owns one row; each lane keeps D/64 elements in registers, so the
+// row is read once and written once (HBM-bound by design: 2 bf16 reads + 1-2 bf16 writes per elem).
+//
+// fwd:  s = x (+ r);  y = (s - mean) * rstd * gamma + beta;  saves mean/rstd (fp32) and s (bf16)
+// bwd:  ds = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)),  dgamma/dbeta column partials
+#include "dl_common.h"
+#include "dl_kernels.h"
+
+namespace {
+
+template <int D>
+struct RowCfg {
+  static constexpr int EPL = D / 64;                  // elements per lane
+  static constexpr int VW = EPL >= 8 ? 8 : EPL;       // vector width (elements) per load
+  static constexpr int NV = EPL / VW;                 // vector loads per lane
+};
+
+// Column index of vector v of lane `lane`: vectors are interleaved across lanes so that one
+// wave-instruction covers 64*VW contiguous elements (fully coalesced).
+template <int D>
+__device__ __forceinline__ int col_of(int lane, int v) {
+  return (v * 64 + lane) * RowCfg<D>::VW;
+}
+
+template <int D, bool HAS_RES, bool SAVE_SUM>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int rows, float eps) {
+  using C = RowCfg<D>;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const size_t base = (size_t)row * D;
+  float v[C::EPL];
+#pragma unroll
+  for (int i = 0; i < C::NV; ++i) load_bf16<C::VW>(x + base + col_of<D>(lane, i), v + i * C::VW);
+  if constexpr (HAS_RES) {
+    float t[C::EPL];
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) load_bf16<C::VW>(r + base + col_of<D>(lane, i), t + i * C::VW);
+#pragma unroll
+    for (int i = 0; i < C::EPL; ++i) v[i] += t[i];
+  }
+  if constexpr (SAVE_SUM) {
+    // round the residual sum to bf16 first so that bwd sees exactly the normalised values
+#pragma unroll
+    for (int i = 0; i < C::EPL; ++i) v[i] = bf2f(f2bf(v[i]));
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(s_out + base + col_of<D>(lane, i), v + i * C::VW);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < C::EPL; ++i) sum += v[i];
+  const float mean = wave_sum(sum) * (1.f / D);
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < C::EPL; ++i) { float d = v[i] - mean; sq += d * d; }
+  const float rstd = rsqrtf(wave_sum(sq) * (1.f / D) + eps);
+  float o[C::EPL];
+#pragma unroll
+  for (int i = 0; i < C::NV; ++i) {
+#pragma unroll
+    for (int j = 0; j < C::VW; ++j) {
+      const int c = col_of<D>(lane, i) + j;
+      o[i * C::VW + j] = (v[i * C::VW + j] - mean) * rstd * gamma[c] + beta[c];
+    }
+    store_bf16<C::VW>(y + base + col_of<D>(lane, i), o + i * C::VW);
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// Each block handles a contiguous chunk of rows (one wave per row, grid-strided inside the
+// block) and writes one fp32 partial row of dgamma/dbeta; dl_colsum_f32 reduces the partials.
+template <int D>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+                                                     const float* __restrict__ gamma, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, bf16_t* __restrict__ ds,
+                                                     float* __restrict__ dgamma_part, float* __restrict__ dbeta_part,
+                                                     int rows, int rows_per_block) {
+  using C = RowCfg<D>;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float g[C::EPL], dg[C::EPL], db[C::EPL];
+#pragma unroll
+  for (int i = 0; i < C::NV; ++i)
+#pragma unroll
+    for (int j = 0; j < C::VW; ++j) {
+      g[i * C::VW + j] = gamma[col_of<D>(lane, i) + j];
+      dg[i * C::VW + j] = 0.f;
+      db[i * C::VW + j] = 0.f;
+    }
+  for (int row = r0 + wid; row < r1; row += nw) {
+    const size_t base = (size_t)row * D;
+    float gy[C::EPL], xh[C::EPL];
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) {
+      load_bf16<C::VW>(dy + base + col_of<D>(lane, i), gy + i * C::VW);
+      load_bf16<C::VW>(s + base + col_of<D>(lane, i), xh + i * C::VW);
+    }
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::EPL; ++i) {
+      xh[i] = (xh[i] - mean) * rstd;
+      dg[i] += gy[i] * xh[i];
+      db[i] += gy[i];
+      gy[i] *= g[i];
+      a += gy[i];
+      b += gy[i] * xh[i];
+    }
+    a = wave_sum(a) * (1.f / D);
+    b = wave_sum(b) * (1.f / D);
+#pragma unroll
+    for (int i = 0; i < C::EPL; ++i) gy[i] = rstd * (gy[i] - a - xh[i] * b);
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(ds + base + col_of<D>(lane, i), gy + i * C::VW);
+  }
+  // reduce the per-wave column partials through LDS: nw x D floats
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+#pragma unroll
+  for (int i = 0; i < C::NV; ++i)
+#pragma unroll
+    for (int j = 0; j < C::VW; ++j) {
+      const int c = col_of<D>(lane, i) + j;
+      lds[wid * D + c] = dg[i * C::VW + j];
+      lds[(nw + wid) * D + c] = db[i * C::VW + j];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float sg = 0.f, sb = 0.f;
+    for (int w = 0; w < nw; ++w) { sg += lds[w * D + c]; sb += lds[(nw + w) * D + c]; }
+    dgamma_part[(size_t)blockIdx.x * D + c] = sg;
+    dbeta_part[(size_t)blockIdx.x * D + c] = sb;
+  }
+}
+
+template <int D>
+void launch_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,
+                float* mean, float* rstd, int rows, float eps, hipStream_t st) {
+  const int wpb = 4;
+  dim3 grid((rows + wpb - 1) / wpb), block(64 * wpb);
+  if (r) {
+    if (s_out) ln_fwd_kernel<D, true, true><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
+    else ln_fwd_kernel<D, true, false><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
+  } else {
+    ln_fwd_kernel<D, false, false><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
+  }
+}
+
+template <int D>
+void launch_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
+                bf16_t* ds, float* dg_part, float* db_part, int rows, int nparts, hipStream_t st) {
+  const int wpb = 4;
+  const int rpb = (rows + nparts - 1) / nparts;
+  size_t lds = (size_t)2 * wpb * D * sizeof(float);
+  ln_bwd_kernel<D><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, rpb);
+}
+
+}  // namespace
+
+int dl_layernorm_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y,
+                     bf16_t* s_out, float* mean, float* rstd, int rows, int D, float eps, hipStream_t st) {
+  switch (D) {
+    case 128: launch_fwd<128>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
+    case 256: launch_fwd<256>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
+    case 512: launch_fwd<512>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
+    case 768: launch_fwd<768>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
+    case 1024: launch_fwd<1024>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
+    case 2048: launch_fwd<2048>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
+    case 4096: launch_fwd<4096>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+int dl_layernorm_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
+                     bf16_t* ds, float* dg_part, float* db_part, int rows, int D, int nparts, hipStream_t st) {
+  switch (D) {
+    case 128: launch_bwd<128>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
+    case 256: launch_bwd<256>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
+    case 512: launch_bwd<512>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
+    case 768: launch_bwd<768>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
+    case 1024: launch_bwd<1024>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
+    default: return -1;
+  }
+  return 0;
+}

@@ -1,0 +1,373 @@
+"""ALBERT for pre-training (MLM + sentence-order prediction) on dedloc kernels.
+
+Parity target: HF ``AlbertForPreTraining`` as built by ``albert/run_trainer.py:56-70`` from the
+``albert-large-v2`` config.  State-dict keys, shapes, initialisation and
+the ``config.json`` / ``pytorch_model.bin`` checkpoint layout are identical to HF, so checkpoints
+round-trip with ``transformers`` (tested against it in tests/test_albert_model.py).
+
+MI355X-first execution (not a port of HF's module graph):
+  * parameters live in one flat fp32 buffer (``FlatParams``); compute uses its bf16 mirror;
+    Q/K/V weights are adjacent so the three projections run as ONE [3H, H] GEMM;
+  * attention is the fused flash kernel over the packed QKV buffer (no head transposes);
+  * residual add + LayerNorm, embedding gather + LayerNorm and gelu_new are fused HIP kernels;
+  * the MLM head runs only on masked positions, and its decoder + softmax-CE is one fused pass;
+  * every parameter gradient accumulates in fp32 directly in the flat gradient buffer.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import asdict, dataclass, field, fields
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..utils.flat import FlatParams
+
+NEG_BIG = -1.0e30
+
+
+@dataclass
+class AlbertConfig:
+    vocab_size: int = 30000
+    embedding_size: int = 128
+    hidden_size: int = 4096
+    num_hidden_layers: int = 12
+    num_hidden_groups: int = 1
+    num_attention_heads: int = 64
+    intermediate_size: int = 16384
+    inner_group_num: int = 1
+    hidden_act: str = "gelu_new"
+    hidden_dropout_prob: float = 0.0
+    attention_probs_dropout_prob: float = 0.0
+    max_position_embeddings: int = 512
+    type_vocab_size: int = 2
+    initializer_range: float = 0.02
+    layer_norm_eps: float = 1e-12
+    classifier_dropout_prob: float = 0.1
+    pad_token_id: int = 0
+    bos_token_id: int = 2
+    eos_token_id: int = 3
+    model_type: str = "albert"
+    architectures: List[str] = field(default_factory=lambda: ["AlbertForPreTraining"])
+
+    @classmethod
+    def albert_large_v2(cls, **kw) -> "AlbertConfig":
+        """The config the reference downloads at albert/arguments.py:97-99."""
+        base = dict(vocab_size=30000, embedding_size=128, hidden_size=1024, num_hidden_layers=24,
+                    num_hidden_groups=1, num_attention_heads=16, intermediate_size=4096, inner_group_num=1)
+        base.update(kw)
+        return cls(**base)
+
+    @classmethod
+    def tiny(cls, **kw) -> "AlbertConfig":
+        base = dict(vocab_size=512, embedding_size=64, hidden_size=128, num_hidden_layers=3, num_hidden_groups=1,
+                    num_attention_heads=2, intermediate_size=256, max_position_embeddings=128)
+        base.update(kw)
+        return cls(**base)
+
+    def to_dict(self) -> Dict:
+        return asdict(self)
+
+    @classmethod
+    def from_dict(cls, d: Dict) -> "AlbertConfig":
+        names = {f.name for f in fields(cls)}
+        return cls(**{k: v for k, v in d.items() if k in names})
+
+    @classmethod
+    def from_pretrained(cls, path: str) -> "AlbertConfig":
+        """Accepts a directory containing config.json, a json file, or the name 'albert-large-v2'
+        (or the reference's S3 URL of that config — there is no network, so it maps to the
+        built-in copy)."""
+        if path in ("albert-large-v2",) or (isinstance(path, str) and path.endswith("albert-large-v2-config.json")
+                                            and not os.path.exists(path)):
+            return cls.albert_large_v2()
+        if os.path.isdir(path):
+            path = os.path.join(path, "config.json")
+        with open(path) as f:
+            return cls.from_dict(json.load(f))
+
+    def save_pretrained(self, directory: str):
+        os.makedirs(directory, exist_ok=True)
+        with open(os.path.join(directory, "config.json"), "w") as f:
+            json.dump(self.to_dict(), f, indent=2, sort_keys=True)
+
+
+def _layer_prefix(g: int, i: int) -> str:
+    return f"albert.encoder.albert_layer_groups.{g}.albert_layers.{i}."
+
+
+class AlbertForPreTraining(nn.Module):
+    """HF-key-compatible ALBERT pre-training model (fp32 master params, bf16 compute)."""
+
+    def __init__(self, config: AlbertConfig):
+        super().__init__()
+        self.config = c = config
+        self._p: Dict[str, nn.Parameter] = {}
+        E, H, I, V = c.embedding_size, c.hidden_size, c.intermediate_size, c.vocab_size
+
+        def add(name, *shape, init="normal"):
+            t = torch.empty(*shape)
+            if init == "normal":
+                t.normal_(0.0, c.initializer_range)
+            elif init == "ones":
+                t.fill_(1.0)
+            else:
+                t.zero_()
+            p = nn.Parameter(t)
+            self._p[name] = p
+            self.register_parameter(name.replace(".", "__"), p)
+
+        add("albert.embeddings.word_embeddings.weight", V, E)
+        add("albert.embeddings.position_embeddings.weight", c.max_position_embeddings, E)
+        add("albert.embeddings.token_type_embeddings.weight", c.type_vocab_size, E)
+        with torch.no_grad():
+            self._p["albert.embeddings.word_embeddings.weight"][c.pad_token_id].zero_()
+        add("albert.embeddings.LayerNorm.weight", E, init="ones")
+        add("albert.embeddings.LayerNorm.bias", E, init="zeros")
+        add("albert.encoder.embedding_hidden_mapping_in.weight", H, E)
+        add("albert.encoder.embedding_hidden_mapping_in.bias", H, init="zeros")
+        for g in range(c.num_hidden_groups):
+            for i in range(c.inner_group_num):
+                pre = _layer_prefix(g, i)
+                add(pre + "full_layer_layer_norm.weight", H, init="ones")
+                add(pre + "full_layer_layer_norm.bias", H, init="zeros")
+                for n in ("query", "key", "value"):
+                    add(pre + f"attention.{n}.weight", H, H)
+                for n in ("query", "key", "value"):
+                    add(pre + f"attention.{n}.bias", H, init="zeros")
+                add(pre + "attention.dense.weight", H, H)
+                add(pre + "attention.dense.bias", H, init="zeros")
+                add(pre + "attention.LayerNorm.weight", H, init="ones")
+                add(pre + "attention.LayerNorm.bias", H, init="zeros")
+                add(pre + "ffn.weight", I, H)
+                add(pre + "ffn.bias", I, init="zeros")
+                add(pre + "ffn_output.weight", H, I)
+                add(pre + "ffn_output.bias", H, init="zeros")
+        add("albert.pooler.weight", H, H)
+        add("albert.pooler.bias", H, init="zeros")
+        add("predictions.bias", V, init="zeros")
+        add("predictions.dense.weight", E, H)
+        add("predictions.dense.bias", E, init="zeros")
+        add("predictions.LayerNorm.weight", E, init="ones")
+        add("predictions.LayerNorm.bias", E, init="zeros")
+        add("sop_classifier.classifier.weight", 2, H)
+        add("sop_classifier.classifier.bias", 2, init="zeros")
+        self.flat: Optional[FlatParams] = None
+
+    # ------------------------------------------------------------------ parameters / checkpoints
+    def hf_named_parameters(self):
+        return list(self._p.items())
+
+    def materialize(self, device=None) -> FlatParams:
+        """Move parameters into the flat buffers on ``device`` (call once before training)."""
+        device = torch.device(device) if device is not None else next(iter(self._p.values())).device
+        for p in self._p.values():
+            p.data = p.data.to(device)
+        self.flat = FlatParams(self.hf_named_parameters(), device=device)
+        return self.flat
+
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        """state dict with exactly HF AlbertForPreTraining's keys (tied decoder included)."""
+        sd = {k: v.detach() for k, v in self._p.items()}
+        sd["predictions.decoder.weight"] = sd["albert.embeddings.word_embeddings.weight"]
+        sd["predictions.decoder.bias"] = sd["predictions.bias"]
+        return sd
+
+    @torch.no_grad()
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        missing = [k for k in self._p if k not in sd]
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:5]}...")
+        for k, p in self._p.items():
+            if k in sd:
+                p.data.copy_(sd[k].to(p.dtype))
+        if self.flat is not None:
+            self.flat.refresh_bf16()
+
+    def save_pretrained(self, directory: str):
+        os.makedirs(directory, exist_ok=True)
+        self.config.save_pretrained(directory)
+        sd = {k: v.detach().float().cpu().contiguous() for k, v in self.hf_state_dict().items()}
+        sd["predictions.decoder.weight"] = sd["predictions.decoder.weight"].clone()
+        sd["predictions.decoder.bias"] = sd["predictions.decoder.bias"].clone()
+        torch.save(sd, os.path.join(directory, "pytorch_model.bin"))
+
+    @classmethod
+    def from_pretrained(cls, directory: str) -> "AlbertForPreTraining":
+        cfg = AlbertConfig.from_pretrained(directory)
+        model = cls(cfg)
+        sd_path = os.path.join(directory, "pytorch_model.bin")
+        if os.path.exists(sd_path):
+            sd = torch.load(sd_path, map_location="cpu", weights_only=True)
+        else:
+            from safetensors.torch import load_file
+
+            sd = load_file(os.path.join(directory, "model.safetensors"))
+        model.load_hf_state_dict(sd)
+        return model
+
+    def resize_token_embeddings(self, n: int):
+        """HF semantics: grow/shrink the (tied) vocabulary; new rows ~ N(0, init_range)."""
+        c = self.config
+        if n == c.vocab_size:
+            return
+        assert self.flat is None, "resize before materialize()"
+        for key in ("albert.embeddings.word_embeddings.weight", "predictions.bias"):
+            old = self._p[key].data
+            new = torch.empty((n,) + tuple(old.shape[1:]))
+            if key.endswith("weight"):
+                new.normal_(0.0, c.initializer_range)
+            else:
+                new.zero_()
+            k = min(n, old.shape[0])
+            new[:k] = old[:k]
+            self._p[key].data = new
+        c.vocab_size = n
+
+    def no_decay_names(self) -> List[str]:
+        """Reference grouping (albert/run_trainer.py:74-84): names containing 'bias' or
+        'LayerNorm.weight' get no weight decay (full_layer_layer_norm.weight *is* decayed — SURVEY App. C.2)."""
+        return [n for n in self._p if any(nd in n for nd in ("bias", "LayerNorm.weight"))]
+
+    # ------------------------------------------------------------------ forward
+    def _layer_views(self, g: int, i: int):
+        f = self.flat
+        pre = _layer_prefix(g, i)
+        H = self.config.hidden_size
+        return dict(
+            wqkv=f.span(f.bf16, pre + "attention.query.weight", pre + "attention.value.weight", (3 * H, H)),
+            gwqkv=f.span(f.grad, pre + "attention.query.weight", pre + "attention.value.weight", (3 * H, H)),
+            bqkv=f.span(f.bf16, pre + "attention.query.bias", pre + "attention.value.bias", (3 * H,)),
+            gbqkv=f.span(f.grad, pre + "attention.query.bias", pre + "attention.value.bias", (3 * H,)),
+            wo=f.w(pre + "attention.dense.weight"), gwo=f.g(pre + "attention.dense.weight"),
+            bo=f.w(pre + "attention.dense.bias"), gbo=f.g(pre + "attention.dense.bias"),
+            ln1g=f.p(pre + "attention.LayerNorm.weight"), ln1b=f.p(pre + "attention.LayerNorm.bias"),
+            gln1g=f.g(pre + "attention.LayerNorm.weight"), gln1b=f.g(pre + "attention.LayerNorm.bias"),
+            w1=f.w(pre + "ffn.weight"), gw1=f.g(pre + "ffn.weight"), b1=f.w(pre + "ffn.bias"), gb1=f.g(pre + "ffn.bias"),
+            w2=f.w(pre + "ffn_output.weight"), gw2=f.g(pre + "ffn_output.weight"),
+            b2=f.w(pre + "ffn_output.bias"), gb2=f.g(pre + "ffn_output.bias"),
+            ln2g=f.p(pre + "full_layer_layer_norm.weight"), ln2b=f.p(pre + "full_layer_layer_norm.bias"),
+            gln2g=f.g(pre + "full_layer_layer_norm.weight"), gln2b=f.g(pre + "full_layer_layer_norm.bias"),
+        )
+
+    def _albert_layer(self, h, lv, mbias, S):
+        c = self.config
+        eps = c.layer_norm_eps
+        qkv = ops.linear(h, lv["wqkv"], lv["bqkv"], lv["gwqkv"], lv["gbqkv"])
+        ctx = ops.attention(qkv, mbias, c.num_attention_heads, S)
+        a = ops.linear(ctx, lv["wo"], lv["bo"], lv["gwo"], lv["gbo"])
+        h1 = ops.add_layernorm(a, h, lv["ln1g"], lv["ln1b"], lv["gln1g"], lv["gln1b"], eps)
+        f = ops.linear(h1, lv["w1"], lv["b1"], lv["gw1"], lv["gb1"])
+        f = ops.gelu_new(f)
+        f2 = ops.linear(f, lv["w2"], lv["b2"], lv["gw2"], lv["gb2"])
+        return ops.add_layernorm(f2, h1, lv["ln2g"], lv["ln2b"], lv["gln2g"], lv["gln2b"], eps)
+
+    def encode(self, input_ids, attention_mask=None, token_type_ids=None):
+        """Returns (sequence_output [B*S', H] bf16, S') where S' is S padded to a multiple of 64."""
+        assert self.flat is not None, "call model.materialize(device) first"
+        c, f = self.config, self.flat
+        B, S = input_ids.shape
+        Sp = (S + 63) // 64 * 64
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        if Sp != S:
+            pad = Sp - S
+            input_ids = F.pad(input_ids, (0, pad), value=c.pad_token_id)
+            attention_mask = F.pad(attention_mask, (0, pad), value=0)
+            if token_type_ids is not None:
+                token_type_ids = F.pad(token_type_ids, (0, pad), value=0)
+        assert Sp <= c.max_position_embeddings, "sequence longer than max_position_embeddings"
+        mbias = torch.where(attention_mask.bool(), 0.0, NEG_BIG).to(torch.float32).contiguous()
+        emb = "albert.embeddings."
+        x = ops.embed_layernorm(
+            input_ids, token_type_ids, f.p(emb + "word_embeddings.weight"), f.p(emb + "position_embeddings.weight"),
+            f.p(emb + "token_type_embeddings.weight"), f.p(emb + "LayerNorm.weight"), f.p(emb + "LayerNorm.bias"),
+            grads=(f.g(emb + "word_embeddings.weight"), f.g(emb + "position_embeddings.weight"),
+                   f.g(emb + "token_type_embeddings.weight"), f.g(emb + "LayerNorm.weight"),
+                   f.g(emb + "LayerNorm.bias")),
+            eps=c.layer_norm_eps)
+        m = "albert.encoder.embedding_hidden_mapping_in."
+        h = ops.linear(x, f.w(m + "weight"), f.w(m + "bias"), f.g(m + "weight"), f.g(m + "bias"))
+        views = [[self._layer_views(g, i) for i in range(c.inner_group_num)] for g in range(c.num_hidden_groups)]
+        per_group = c.num_hidden_layers // c.num_hidden_groups
+        for layer in range(c.num_hidden_layers):
+            g = int(layer / per_group)
+            for i in range(c.inner_group_num):
+                h = self._albert_layer(h, views[g][i], mbias, Sp)
+        return h, Sp
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, labels=None, sentence_order_label=None,
+                mlm_positions=None, mlm_labels=None, return_logits=False):
+        """HF-compatible pre-training forward.
+
+        MLM targets either as HF ``labels`` [B, S] (-100 = ignore) or as fixed-shape
+        ``mlm_positions``/``mlm_labels`` [B, P] (BERT's max_predictions_per_seq form; -100 pads) —
+        the fixed form needs no host synchronisation and is graph-capturable.
+        """
+        c, f = self.config, self.flat
+        B, S = input_ids.shape
+        h, Sp = self.encode(input_ids, attention_mask, token_type_ids)
+        out = {}
+        # ---- MLM head on masked positions only
+        if mlm_positions is None and labels is not None:
+            flat_lab = labels.reshape(-1)
+            pos = torch.nonzero(flat_lab != -100).squeeze(1)
+            b_idx, s_idx = pos // S, pos % S
+            rows = b_idx * Sp + s_idx
+            tgt = flat_lab[pos]
+        elif mlm_positions is not None:
+            P = mlm_positions.shape[1]
+            rows = (torch.arange(B, device=h.device)[:, None] * Sp + mlm_positions).reshape(-1)
+            tgt = mlm_labels.reshape(-1)
+        else:
+            rows, tgt = None, None
+        loss = None
+        if rows is not None:
+            hm = h.index_select(0, rows)
+            p = "predictions."
+            t = ops.linear(hm, f.w(p + "dense.weight"), f.w(p + "dense.bias"), f.g(p + "dense.weight"),
+                           f.g(p + "dense.bias"))
+            t = ops.gelu_new(t)
+            t = ops.add_layernorm(t, None, f.p(p + "LayerNorm.weight"), f.p(p + "LayerNorm.bias"),
+                                  f.g(p + "LayerNorm.weight"), f.g(p + "LayerNorm.bias"), c.layer_norm_eps)
+            wname = "albert.embeddings.word_embeddings.weight"
+            logits = ops.linear(t, f.w(wname), f.w(p + "bias"), f.g(wname), f.g(p + "bias"))
+            mlm_loss = ops.cross_entropy(logits, tgt)
+            out["mlm_loss"] = mlm_loss
+            loss = mlm_loss
+            if return_logits:
+                out["prediction_logits_masked"] = logits
+        # ---- SOP head on [CLS]
+        cls = h.view(B, Sp, -1)[:, 0].contiguous()
+        pooled = ops.tanh(ops.linear(cls, f.w("albert.pooler.weight"), f.w("albert.pooler.bias"),
+                                     f.g("albert.pooler.weight"), f.g("albert.pooler.bias")))
+        if self.training and c.classifier_dropout_prob > 0:
+            pooled = F.dropout(pooled, c.classifier_dropout_prob, True)
+        s = "sop_classifier.classifier."
+        sop_logits = ops.linear(pooled, f.w(s + "weight"), f.w(s + "bias"), f.g(s + "weight"), f.g(s + "bias"))
+        out["sop_logits"] = sop_logits
+        if sentence_order_label is not None:
+            sop_loss = ops.cross_entropy(sop_logits, sentence_order_label)
+            out["sop_loss"] = sop_loss
+            loss = sop_loss if loss is None else loss + sop_loss
+        out["loss"] = loss
+        return out
+
+    def num_parameters(self) -> int:
+        return sum(p.numel() for p in self._p.values())
+
+
+def flops_per_sample(config: AlbertConfig, seq_len: int, masked_per_seq: int) -> float:
+    """Model FLOPs (fwd+bwd = 3x fwd) per training sample, used for MFU reporting."""
+    c = config
+    H, I, E = c.hidden_size, c.intermediate_size, c.embedding_size
+    per_tok_layer = 2 * (4 * H * H + 2 * H * I)
+    attn = 2 * 2 * seq_len * H
+    fwd = seq_len * (c.num_hidden_layers * (per_tok_layer + attn) + 2 * E * H)
+    fwd += masked_per_seq * (2 * H * E + 2 * E * c.vocab_size)
+    return 3.0 * fwd

@@ -1,0 +1,363 @@
+"""Operator registry: schemas of every ``dedloc::`` op, their CPU implementations and the loader of
+the gfx950 library.
+
+Single code path per device: on a GPU tensor the dispatcher can only reach the HIP kernel that
+``_C.so`` registers under the CUDA key (loading it is mandatory whenever a GPU is visible — a
+missing or stale library raises instead of silently falling back).  The CPU implementations below
+exist for the CPU plumbing configuration (BASELINE.json config 1) and for the non-GPU test tier;
+they mirror the kernels' numerics contract (bf16 storage, fp32 math).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+import torch.nn.functional as F
+
+LIB = torch.library.Library("dedloc", "DEF")
+
+_SCHEMAS = [
+    "layernorm_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+    "layernorm_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, Tensor(a!) dgamma, Tensor(b!) dbeta, bool accumulate) -> Tensor",
+    "gelu_fwd(Tensor h) -> Tensor",
+    "gelu_bwd(Tensor dy, Tensor h) -> Tensor",
+    "tanh_fwd(Tensor x) -> Tensor",
+    "tanh_bwd(Tensor dy, Tensor y) -> Tensor",
+    "bias_grad(Tensor dy, Tensor(a!) dbias, bool accumulate) -> ()",
+    "cast_bf16(Tensor x, Tensor(a!) out) -> ()",
+    "lamb_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(d!) norms, float beta1, float beta2, float eps, float step_size, float clamp_value, float grad_scale) -> ()",
+    "larc_sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(c!) norms, float lr, float momentum, float trust_coef, float eps, bool clip, bool first_step, float grad_scale) -> ()",
+    "grad_norm_clip(Tensor(a!) g, float max_norm, Tensor(b!) part, Tensor(c!) out) -> ()",
+    "axpby(Tensor(a!) y, Tensor x, float a, float b) -> ()",
+    "pack(Tensor src, Tensor(a!) dst, float weight) -> ()",
+    "reduce_parts(Tensor parts, int nparts, Tensor(a!) out, float inv_total) -> ()",
+    "unpack(Tensor src, Tensor(a!) dst, Tensor? snap) -> ()",
+    "embed_ln_fwd(Tensor ids, Tensor? tt, Tensor wemb, Tensor pemb, Tensor temb, Tensor gamma, Tensor beta, int S, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+    "embed_bwd(Tensor ds, Tensor ids, Tensor? tt, Tensor(a!) dwemb, Tensor(b!) dpemb, Tensor(c!) dtemb, int S) -> ()",
+    "xent_fwd_bwd(Tensor logits, Tensor labels, bool inplace, int ignore_index) -> (Tensor, Tensor)",
+    "attn_fwd(Tensor qkv, Tensor? mbias, int H, int S, float scale) -> (Tensor, Tensor)",
+    "attn_bwd(Tensor qkv, Tensor? mbias, Tensor out, Tensor dout, Tensor lse, int H, int S, float scale) -> Tensor",
+    "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
+    "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
+]
+for _s in _SCHEMAS:
+    LIB.define(_s)
+
+_NATIVE = {"loaded": False, "path": None, "error": None}
+
+
+def _impl(name):
+    def deco(fn):
+        LIB.impl(name, fn, "CPU")
+        return fn
+
+    return deco
+
+
+def load_native(required: bool | None = None) -> bool:
+    """Load ``_C.so`` (the gfx950 kernels).  ``required`` defaults to "a GPU is visible"."""
+    if _NATIVE["loaded"]:
+        return True
+    if required is None:
+        required = torch.cuda.is_available()
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+    try:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} not built (run python -m dedloc_amd._build)")
+        torch.ops.load_library(path)
+        _NATIVE.update(loaded=True, path=path)
+        return True
+    except Exception as e:  # noqa: BLE001
+        _NATIVE["error"] = repr(e)
+        if required:
+            raise ImportError(
+                "dedloc_amd: the gfx950 kernel library could not be loaded on a GPU machine; refusing to run "
+                f"without it ({e})"
+            ) from e
+        return False
+
+
+def native_loaded() -> bool:
+    return _NATIVE["loaded"]
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU implementations (plumbing / reference numerics: bf16 storage, fp32 math)
+# ---------------------------------------------------------------------------------------------
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@_impl("layernorm_fwd")
+def _ln_fwd_cpu(x, res, gamma, beta, eps):
+    s = x.float() if res is None else (x.float() + res.float())
+    s_b = _bf(s)
+    sf = s_b.float() if res is not None else x.float()
+    mean = sf.mean(-1)
+    var = ((sf - mean.unsqueeze(-1)) ** 2).mean(-1)
+    rstd = torch.rsqrt(var + eps)
+    y = (sf - mean.unsqueeze(-1)) * rstd.unsqueeze(-1) * gamma + beta
+    D = x.shape[-1]
+    return _bf(y), (s_b if res is not None else x), mean.reshape(-1), rstd.reshape(-1)
+
+
+@_impl("layernorm_bwd")
+def _ln_bwd_cpu(dy, s, gamma, mean, rstd, dgamma, dbeta, accumulate):
+    D = dy.shape[-1]
+    g = dy.float().reshape(-1, D)
+    xh = (s.float().reshape(-1, D) - mean.unsqueeze(-1)) * rstd.unsqueeze(-1)
+    dg = (g * xh).sum(0)
+    db = g.sum(0)
+    if accumulate:
+        dgamma.add_(dg)
+        dbeta.add_(db)
+    else:
+        dgamma.copy_(dg)
+        dbeta.copy_(db)
+    gy = g * gamma
+    a = gy.mean(-1, keepdim=True)
+    b = (gy * xh).mean(-1, keepdim=True)
+    ds = rstd.unsqueeze(-1) * (gy - a - xh * b)
+    return _bf(ds).reshape(dy.shape)
+
+
+def _gelu_tanh(x):
+    return 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * x.pow(3))))
+
+
+@_impl("gelu_fwd")
+def _gelu_fwd_cpu(h):
+    return _bf(_gelu_tanh(h.float()))
+
+
+@_impl("gelu_bwd")
+def _gelu_bwd_cpu(dy, h):
+    x = h.float()
+    k0, k1 = math.sqrt(2.0 / math.pi), 0.044715
+    u = k0 * (x + k1 * x ** 3)
+    t = torch.tanh(u)
+    d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+    return _bf(dy.float() * d)
+
+
+@_impl("tanh_fwd")
+def _tanh_fwd_cpu(x):
+    return _bf(torch.tanh(x.float()))
+
+
+@_impl("tanh_bwd")
+def _tanh_bwd_cpu(dy, y):
+    t = y.float()
+    return _bf(dy.float() * (1 - t * t))
+
+
+@_impl("bias_grad")
+def _bias_grad_cpu(dy, dbias, accumulate):
+    s = dy.float().reshape(-1, dy.shape[-1]).sum(0)
+    if accumulate:
+        dbias.add_(s)
+    else:
+        dbias.copy_(s)
+
+
+@_impl("cast_bf16")
+def _cast_bf16_cpu(x, out):
+    out.copy_(x.to(torch.bfloat16))
+
+
+def _chunks_iter(chunk_tensor, chunk_start, chunk_len):
+    for t, s, n in zip(chunk_tensor.tolist(), chunk_start.tolist(), chunk_len.tolist()):
+        yield t, s, n
+
+
+@_impl("lamb_step")
+def _lamb_cpu(p, g, m, v, chunk_tensor, chunk_start, chunk_len, tensor_wd, norms, beta1, beta2, eps, step_size,
+              clamp_value, grad_scale):
+    norms.zero_()
+    wd = tensor_wd.tolist()
+    chunks = list(_chunks_iter(chunk_tensor, chunk_start, chunk_len))
+    for t, s, n in chunks:
+        gi = g[s:s + n] * grad_scale
+        m[s:s + n].mul_(beta1).add_(gi, alpha=1 - beta1)
+        v[s:s + n].mul_(beta2).addcmul_(gi, gi, value=1 - beta2)
+        u = m[s:s + n] / (v[s:s + n].sqrt() + eps) + wd[t] * p[s:s + n]
+        norms[2 * t] += (p[s:s + n] ** 2).sum()
+        norms[2 * t + 1] += (u ** 2).sum()
+    for t, s, n in chunks:
+        wn = min(max(math.sqrt(norms[2 * t].item()), 0.0), clamp_value)
+        un = math.sqrt(norms[2 * t + 1].item())
+        trust = 1.0 if (wn == 0 or un == 0) else wn / un
+        u = m[s:s + n] / (v[s:s + n].sqrt() + eps) + wd[t] * p[s:s + n]
+        p[s:s + n].add_(u, alpha=-step_size * trust)
+
+
+@_impl("larc_sgd_step")
+def _larc_cpu(p, g, buf, chunk_tensor, chunk_start, chunk_len, tensor_wd, norms, lr, momentum, trust_coef, eps, clip,
+              first_step, grad_scale):
+    norms.zero_()
+    wd = tensor_wd.tolist()
+    chunks = list(_chunks_iter(chunk_tensor, chunk_start, chunk_len))
+    for t, s, n in chunks:
+        norms[2 * t] += (p[s:s + n] ** 2).sum()
+        norms[2 * t + 1] += ((g[s:s + n] * grad_scale) ** 2).sum()
+    for t, s, n in chunks:
+        pn, gn = math.sqrt(norms[2 * t].item()), math.sqrt(norms[2 * t + 1].item())
+        a = 1.0
+        if pn != 0 and gn != 0:
+            a = trust_coef * pn / (gn + pn * wd[t] + eps)
+            if clip:
+                a = min(a / lr, 1.0)
+        d = (g[s:s + n] * grad_scale + wd[t] * p[s:s + n]) * a
+        if first_step:
+            buf[s:s + n].copy_(d)
+        else:
+            buf[s:s + n].mul_(momentum).add_(d)
+        p[s:s + n].add_(buf[s:s + n], alpha=-lr)
+
+
+@_impl("grad_norm_clip")
+def _clip_cpu(g, max_norm, part, out):
+    norm = g.float().norm()
+    finite = bool(torch.isfinite(norm))
+    out[0] = norm
+    out[1] = 1.0 if finite else 0.0
+    if max_norm > 0 and finite:
+        coef = max_norm / (norm.item() + 1e-6)
+        if coef < 1:
+            g.mul_(coef)
+
+
+@_impl("axpby")
+def _axpby_cpu(y, x, a, b):
+    y.mul_(a).add_(x, alpha=b)
+
+
+@_impl("pack")
+def _pack_cpu(src, dst, weight):
+    v = src * weight
+    if dst.dtype == torch.float16:
+        v = v.clamp(-65504.0, 65504.0)
+    dst.copy_(v.to(dst.dtype))
+
+
+@_impl("reduce_parts")
+def _reduce_cpu(parts, nparts, out, inv_total):
+    s = parts.reshape(nparts, -1).float().sum(0) * inv_total
+    if out.dtype == torch.float16:
+        s = s.clamp(-65504.0, 65504.0)
+    out.copy_(s.to(out.dtype))
+
+
+@_impl("unpack")
+def _unpack_cpu(src, dst, snap):
+    if snap is None:
+        dst.copy_(src.float())
+    else:
+        dst.add_(src.float() - snap)
+
+
+@_impl("embed_ln_fwd")
+def _embed_fwd_cpu(ids, tt, wemb, pemb, temb, gamma, beta, S, eps):
+    T = ids.numel()
+    pos = torch.arange(T, device=ids.device) % S
+    s = wemb[ids.reshape(-1)] + pemb[pos] + temb[(tt.reshape(-1) if tt is not None else torch.zeros_like(pos))]
+    s_b = _bf(s)
+    sf = s_b.float()
+    mean = sf.mean(-1)
+    rstd = torch.rsqrt(((sf - mean[:, None]) ** 2).mean(-1) + eps)
+    y = (sf - mean[:, None]) * rstd[:, None] * gamma + beta
+    return _bf(y), s_b, mean, rstd
+
+
+@_impl("embed_bwd")
+def _embed_bwd_cpu(ds, ids, tt, dwemb, dpemb, dtemb, S):
+    g = ds.float().reshape(-1, ds.shape[-1])
+    T = g.shape[0]
+    dwemb.index_add_(0, ids.reshape(-1), g)
+    pos = torch.arange(T) % S
+    dpemb.index_add_(0, pos, g)
+    tti = tt.reshape(-1) if tt is not None else torch.zeros(T, dtype=torch.long)
+    dtemb.index_add_(0, tti, g)
+
+
+@_impl("xent_fwd_bwd")
+def _xent_cpu(logits, labels, inplace, ignore_index):
+    x = logits.float().reshape(-1, logits.shape[-1])
+    lab = labels.reshape(-1)
+    valid = lab != ignore_index
+    cnt = int(valid.sum())
+    lse = torch.logsumexp(x, -1)
+    safe = torch.where(valid, lab, torch.zeros_like(lab))
+    rows = lse - x.gather(1, safe[:, None]).squeeze(1)
+    scale = 1.0 / cnt if cnt > 0 else 0.0
+    loss = (rows * valid).sum() * scale
+    grad = torch.softmax(x, -1)
+    grad[torch.arange(x.shape[0]), safe] -= 1.0
+    grad = grad * valid[:, None] * scale
+    g = _bf(grad).reshape(logits.shape)
+    if inplace:
+        logits.copy_(g)
+        g = logits
+    return loss.float(), g
+
+
+def _attn_probs(qkv, mbias, H, S, scale):
+    T, ld = qkv.shape
+    D = ld // (3 * H)
+    B = T // S
+    x = qkv.float().reshape(B, S, 3, H, D)
+    q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    s = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if mbias is not None:
+        s = s + mbias.reshape(B, 1, 1, S) / math.log2(math.e)
+    return q, k, v, s
+
+
+@_impl("attn_fwd")
+def _attn_fwd_cpu(qkv, mbias, H, S, scale):
+    q, k, v, s = _attn_probs(qkv, mbias, H, S, scale)
+    B, _, _, D = q.shape
+    lse = torch.logsumexp(s, -1)
+    p = torch.softmax(s, -1)
+    o = torch.matmul(p, v).transpose(1, 2).reshape(B * S, H * D)
+    return _bf(o), (lse * math.log2(math.e)).contiguous()
+
+
+@_impl("attn_bwd")
+def _attn_bwd_cpu(qkv, mbias, out, dout, lse, H, S, scale):
+    q, k, v, s = _attn_probs(qkv, mbias, H, S, scale)
+    B, _, _, D = q.shape
+    p = torch.softmax(s, -1)
+    do = dout.float().reshape(B, S, H, D).transpose(1, 2)
+    o = out.float().reshape(B, S, H, D).transpose(1, 2)
+    dv = torch.matmul(p.transpose(-1, -2), do)
+    dp = torch.matmul(do, v.transpose(-1, -2))
+    delta = (do * o).sum(-1, keepdim=True)
+    ds = p * (dp - delta)
+    dq = torch.matmul(ds, k) * scale
+    dk = torch.matmul(ds.transpose(-1, -2), q) * scale
+    g = torch.stack([dq, dk, dv], dim=2)  # B,H,3,S,D
+    g = g.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H * D)
+    return _bf(g)
+
+
+@_impl("gemm")
+def _gemm_cpu(a, b, bias, residual, trans_a, trans_b, epilogue):
+    A = a.float().t() if trans_a else a.float()
+    Bm = b.float().t() if trans_b else b.float()
+    c = A @ Bm
+    if bias is not None:
+        c = c + bias.float()
+    if epilogue == 1:
+        c = _gelu_tanh(c)
+    if residual is not None:
+        c = c + residual.float()
+    return _bf(c)
+
+
+@_impl("gemm_acc_f32")
+def _gemm_acc_cpu(a, b, c, trans_a, trans_b):
+    A = a.float().t() if trans_a else a.float()
+    Bm = b.float().t() if trans_b else b.float()
+    c.add_(A @ Bm)
