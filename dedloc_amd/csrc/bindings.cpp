@@ -71,15 +71,15 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Te
   expect(dgamma, at::kFloat, "dgamma");
   expect(dbeta, at::kFloat, "dbeta");
   const int64_t D = dy.size(-1), rows = dy.numel() / D;
-  const int nparts = (int)std::min<int64_t>(256, std::max<int64_t>(1, rows / 16));
+  const int nparts = (int)std::min<int64_t>(512, std::max<int64_t>(1, rows / 32));
   auto ds = at::empty_like(dy);
-  auto part = at::empty({2, nparts, D}, dy.options().dtype(at::kFloat));
-  auto st = cur_stream(dy);
-  check(dl_layernorm_bwd(cbf(dy), cbf(s), f32(gamma), f32(mean), f32(rstd), bf(ds), f32(part),
-                         f32(part) + (size_t)nparts * D, (int)rows, (int)D, nparts, st),
+  if (!accumulate) {
+    dgamma.zero_();
+    dbeta.zero_();
+  }
+  check(dl_layernorm_bwd(cbf(dy), cbf(s), f32(gamma), f32(mean), f32(rstd), bf(ds), f32(dgamma), f32(dbeta),
+                         (int)rows, (int)D, nparts, cur_stream(dy)),
         "layernorm_bwd");
-  dl_colsum_f32(f32(part), f32(dgamma), nparts, (int)D, accumulate ? 1 : 0, st);
-  dl_colsum_f32(f32(part) + (size_t)nparts * D, f32(dbeta), nparts, (int)D, accumulate ? 1 : 0, st);
   return ds;
 }
 
@@ -119,11 +119,9 @@ void bias_grad(const at::Tensor& dy, at::Tensor dbias, bool accumulate) {
   expect(dbias, at::kFloat, "dbias");
   const int64_t N = dy.size(-1), rows = dy.numel() / N;
   TORCH_CHECK(dbias.numel() == N, "dbias size mismatch");
-  const int nparts = (int)std::min<int64_t>(128, std::max<int64_t>(1, rows / 32));
-  auto part = at::empty({nparts, N}, dy.options().dtype(at::kFloat));
-  auto st = cur_stream(dy);
-  check(dl_colsum_bf16(cbf(dy), f32(part), (int)rows, (int)N, nparts, st), "bias_grad");
-  dl_colsum_f32(f32(part), f32(dbias), nparts, (int)N, accumulate ? 1 : 0, st);
+  const int nparts = (int)std::min<int64_t>(256, std::max<int64_t>(1, rows / 64));
+  if (!accumulate) dbias.zero_();
+  check(dl_colsum_bf16(cbf(dy), f32(dbias), (int)rows, (int)N, nparts, cur_stream(dy)), "bias_grad");
 }
 
 void cast_bf16(const at::Tensor& x, at::Tensor out) {
@@ -298,12 +296,18 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm operands must be GPU tensors");
   const at::Tensor A = trans_a ? a.t() : a;
   const at::Tensor B = trans_b ? b.t() : b;
-  at::Tensor c = bias.has_value() ? at::addmm(bias->to(a.scalar_type()), A, B) : at::mm(A, B);
+  at::Tensor c;
+  if (residual.has_value()) {
+    // C = residual + A.B in one GEMM (beta = 1): fuses the residual-branch gradient sum
+    c = at::addmm(*residual, A, B);
+    if (bias.has_value()) c.add_(*bias);
+  } else {
+    c = bias.has_value() ? at::addmm(bias->to(a.scalar_type()), A, B) : at::mm(A, B);
+  }
   if (epilogue == 1) {
     TORCH_CHECK(c.is_contiguous(), "gemm output must be contiguous");
     check(dl_gelu_fwd(cbf(c), bf(c), c.numel(), cur_stream(c)), "gemm gelu epilogue");
   }
-  if (residual.has_value()) c.add_(*residual);
   return c;
 }
 

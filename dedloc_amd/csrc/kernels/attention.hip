@@ -23,6 +23,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef short s8_t __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s4_t lds_s4;
 
 constexpr int HD = 64;          // head dim
@@ -58,13 +59,10 @@ __device__ __forceinline__ bf16x8 tr_operand(const uint8_t* tile, int kbase, int
   const int col0 = 32 * t + 16 * ((lane >> 4) & 1);
   const s4_t lo = lds_tr(tile, kbase + 4 * hh, col0, lane & 15);
   const s4_t hi = lds_tr(tile, kbase + 8 + 4 * hh, col0, lane & 15);
-  bf16x8 a;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    a[e] = __builtin_bit_cast(__bf16, lo[e]);
-    a[4 + e] = __builtin_bit_cast(__bf16, hi[e]);
-  }
-  return a;
+  // whole-vector shuffle + bit_cast: per-element __bf16 bit_casts of an s4 vector miscompile
+  // (hipcc 7.2 broadcast element 0) — see tests/hip/primitives_test.hip
+  const s8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 // accumulator registers 8s..8s+7 -> bf16 B-operand fragment

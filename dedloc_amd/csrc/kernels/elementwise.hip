@@ -64,7 +64,18 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const bf16_t* __restri
     for (int j = 0; j < 8; ++j) acc[j] += v[j];
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) part[(size_t)blockIdx.y * N + c0 + j] = acc[j];
+  for (int j = 0; j < 8; ++j) atomicAdd(&part[c0 + j], acc[j]);
+}
+
+// scalar variant for N % 8 != 0 (e.g. the 2-way SOP classifier bias)
+__global__ __launch_bounds__(256) void colsum_bf16_scalar_kernel(const bf16_t* __restrict__ x, float* __restrict__ part,
+                                                                 int rows, int N, int rpb) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r) acc += bf2f(x[(size_t)r * N + c]);
+  atomicAdd(&part[c], acc);
 }
 
 // out[c] (+)= sum_p part[p][c]
@@ -122,10 +133,14 @@ int dl_tanh_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, size_t n, hipStre
 }
 
 int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hipStream_t st) {
-  if (N % 8) return -1;
   const int rpb = (rows + nparts - 1) / nparts;
-  dim3 grid((N / 8 + 255) / 256, nparts);
-  colsum_bf16_kernel<<<grid, 256, 0, st>>>(x, part, rows, N, rpb);
+  // `part` is the fp32 [N] destination: every block adds its row-chunk sums atomically
+  if (N % 8) {
+    colsum_bf16_scalar_kernel<<<dim3((N + 255) / 256, nparts), 256, 0, st>>>(x, part, rows, N, rpb);
+    return 0;
+  }
+  dim3 grid((N / 8 + 127) / 128, nparts);
+  colsum_bf16_kernel<<<grid, 128, 0, st>>>(x, part, rows, N, rpb);
   return 0;
 }
 

@@ -133,11 +133,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       lds[(nw + wid) * D + c] = db[i * C::VW + j];
     }
   __syncthreads();
+  // one fp32 atomic per column per block straight into the (accumulating) gradient buffers
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
     float sg = 0.f, sb = 0.f;
     for (int w = 0; w < nw; ++w) { sg += lds[w * D + c]; sb += lds[(nw + w) * D + c]; }
-    dgamma_part[(size_t)blockIdx.x * D + c] = sg;
-    dbeta_part[(size_t)blockIdx.x * D + c] = sb;
+    atomicAdd(&dgamma_part[c], sg);
+    atomicAdd(&dbeta_part[c], sb);
   }
 }
 

@@ -101,6 +101,59 @@ def _layer_prefix(g: int, i: int) -> str:
     return f"albert.encoder.albert_layer_groups.{g}.albert_layers.{i}."
 
 
+class _AlbertLayerFn(torch.autograd.Function):
+    """One application of the shared ALBERT transformer layer with a hand-scheduled backward.
+
+    fwd: qkv = h Wqkv^T + b (one GEMM) -> flash attention -> dense -> LN(. + h) -> ffn -> gelu_new
+         -> ffn_output -> LN(. + h1)
+    bwd: every weight gradient accumulates in fp32 into the flat gradient buffer (beta = 1 GEMMs),
+         and both residual-branch gradient sums are folded into the dgrad GEMMs (C = ds + dY W),
+         so the layer backward launches no standalone elementwise adds.
+    """
+
+    @staticmethod
+    def forward(ctx, h, mbias, lv, H, S, eps):
+        O = ops.OPS
+        qkv = O.gemm(h, lv["wqkv"], lv["bqkv"], None, False, True, 0)
+        att, lse = O.attn_fwd(qkv, mbias, H, S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)))
+        a = O.gemm(att, lv["wo"], lv["bo"], None, False, True, 0)
+        h1, s1, m1, r1 = O.layernorm_fwd(a, h, lv["ln1g"], lv["ln1b"], eps)
+        f = O.gemm(h1, lv["w1"], lv["b1"], None, False, True, 0)
+        g = O.gelu_fwd(f)
+        f2 = O.gemm(g, lv["w2"], lv["b2"], None, False, True, 0)
+        out, s2, m2, r2 = O.layernorm_fwd(f2, h1, lv["ln2g"], lv["ln2b"], eps)
+        ctx.save_for_backward(h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2)
+        ctx.lv, ctx.mbias, ctx.H, ctx.S = lv, mbias, H, S
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        O = ops.OPS
+        h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2 = ctx.saved_tensors
+        lv = ctx.lv
+        dy = dy.contiguous()
+        ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True)
+        O.gemm_acc_f32(ds2, g, lv["gw2"], True, False)
+        O.bias_grad(ds2, lv["gb2"], True)
+        dg = O.gemm(ds2, lv["w2"], None, None, False, False, 0)
+        df = O.gelu_bwd(dg, f)
+        del dg
+        O.gemm_acc_f32(df, h1, lv["gw1"], True, False)
+        O.bias_grad(df, lv["gb1"], True)
+        dh1 = O.gemm(df, lv["w1"], None, ds2, False, False, 0)  # residual branch folded in
+        del df
+        ds1 = O.layernorm_bwd(dh1, s1, lv["ln1g"], m1, r1, lv["gln1g"], lv["gln1b"], True)
+        O.gemm_acc_f32(ds1, att, lv["gwo"], True, False)
+        O.bias_grad(ds1, lv["gbo"], True)
+        datt = O.gemm(ds1, lv["wo"], None, None, False, False, 0)
+        H = ctx.H
+        dqkv = O.attn_bwd(qkv, ctx.mbias, att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)))
+        O.gemm_acc_f32(dqkv, h, lv["gwqkv"], True, False)
+        O.bias_grad(dqkv, lv["gbqkv"], True)
+        dh = O.gemm(dqkv, lv["wqkv"], None, ds1, False, False, 0)
+        return dh, None, None, None, None, None
+
+
 class AlbertForPreTraining(nn.Module):
     """HF-key-compatible ALBERT pre-training model (fp32 master params, bf16 compute)."""
 
@@ -257,15 +310,7 @@ class AlbertForPreTraining(nn.Module):
 
     def _albert_layer(self, h, lv, mbias, S):
         c = self.config
-        eps = c.layer_norm_eps
-        qkv = ops.linear(h, lv["wqkv"], lv["bqkv"], lv["gwqkv"], lv["gbqkv"])
-        ctx = ops.attention(qkv, mbias, c.num_attention_heads, S)
-        a = ops.linear(ctx, lv["wo"], lv["bo"], lv["gwo"], lv["gbo"])
-        h1 = ops.add_layernorm(a, h, lv["ln1g"], lv["ln1b"], lv["gln1g"], lv["gln1b"], eps)
-        f = ops.linear(h1, lv["w1"], lv["b1"], lv["gw1"], lv["gb1"])
-        f = ops.gelu_new(f)
-        f2 = ops.linear(f, lv["w2"], lv["b2"], lv["gw2"], lv["gb2"])
-        return ops.add_layernorm(f2, h1, lv["ln2g"], lv["ln2b"], lv["gln2g"], lv["gln2b"], eps)
+        return _AlbertLayerFn.apply(h, mbias, lv, c.num_attention_heads, S, c.layer_norm_eps)
 
     def encode(self, input_ids, attention_mask=None, token_type_ids=None):
         """Returns (sequence_output [B*S', H] bf16, S') where S' is S padded to a multiple of 64."""

@@ -349,10 +349,10 @@ def _gemm_cpu(a, b, bias, residual, trans_a, trans_b, epilogue):
     c = A @ Bm
     if bias is not None:
         c = c + bias.float()
-    if epilogue == 1:
-        c = _gelu_tanh(c)
     if residual is not None:
         c = c + residual.float()
+    if epilogue == 1:
+        c = _gelu_tanh(c)
     return _bf(c)
 
 

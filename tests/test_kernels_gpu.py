@@ -1,0 +1,282 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (GPU tier)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+OPS = None
+
+
+@pytest.fixture(autouse=True)
+def _ops(cuda):
+    global OPS
+    import dedloc_amd.ops  # noqa: F401
+
+    OPS = torch.ops.dedloc
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("D", [128, 1024])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layernorm(cuda, D, with_res):
+    torch.manual_seed(0)
+    rows = 1000
+    x = torch.randn(rows, D, device=cuda).bfloat16()
+    r = torch.randn(rows, D, device=cuda).bfloat16() if with_res else None
+    g = torch.rand(D, device=cuda) + 0.5
+    b = torch.randn(D, device=cuda)
+    y, s, mean, rstd = OPS.layernorm_fwd(x, r, g, b, 1e-12)
+    s_ref = x.float() + (r.float() if with_res else 0)
+    s_ref.requires_grad_(True)
+    y_ref = F.layer_norm(s_ref, (D,), g, b, 1e-12)
+    assert rel(y, y_ref) < 1e-2
+    dy = torch.randn(rows, D, device=cuda).bfloat16()
+    dg = torch.zeros(D, device=cuda)
+    db = torch.zeros(D, device=cuda)
+    ds = OPS.layernorm_bwd(dy, s, g, mean, rstd, dg, db, False)
+    gref = torch.autograd.grad(y_ref, [s_ref], dy.float())[0]
+    assert rel(ds, gref) < 2e-2
+    xh = (s.float() - mean[:, None]) * rstd[:, None]
+    assert rel(dg, (dy.float() * xh).sum(0)) < 1e-3
+    assert rel(db, dy.float().sum(0)) < 1e-3
+
+
+def test_gelu(cuda):
+    x = torch.randn(4096, 512, device=cuda).bfloat16()
+    y = OPS.gelu_fwd(x)
+    xr = x.float().requires_grad_(True)
+    yr = F.gelu(xr, approximate="tanh")
+    assert rel(y, yr) < 1e-2
+    dy = torch.randn_like(x)
+    dx = OPS.gelu_bwd(dy, x)
+    assert rel(dx, torch.autograd.grad(yr, xr, dy.float())[0]) < 1e-2
+
+
+def _attn_ref(qkv, mask, H, S):
+    T, ld = qkv.shape
+    D = ld // (3 * H)
+    B = T // S
+    x = qkv.float().reshape(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+    q, k, v = x[0], x[1], x[2]
+    bias = torch.where(mask.bool(), 0.0, float("-inf"))[:, None, None, :]
+    o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias)
+    return o.permute(0, 2, 1, 3).reshape(B * S, H * D)
+
+
+@pytest.mark.parametrize("B,H,S", [(2, 2, 64), (2, 4, 128), (4, 16, 512), (1, 3, 192)])
+def test_attention(cuda, B, H, S):
+    torch.manual_seed(1)
+    D = 64
+    qkv = (torch.randn(B * S, 3 * H * D, device=cuda) * 1.5).bfloat16()
+    mask = torch.ones(B, S, device=cuda, dtype=torch.long)
+    mask[-1, S - S // 4:] = 0
+    mbias = torch.where(mask.bool(), 0.0, -1e30).float()
+    out, lse = OPS.attn_fwd(qkv, mbias, H, S, 1 / math.sqrt(D))
+    qkv_r = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qkv_r, mask, H, S)
+    assert rel(out, ref) < 1.5e-2, rel(out, ref)
+    dout = torch.randn_like(out)
+    dqkv = OPS.attn_bwd(qkv, mbias, out, dout, lse, H, S, 1 / math.sqrt(D))
+    g_ref = torch.autograd.grad(ref, qkv_r, dout.float())[0]
+    for part in range(3):
+        sl = slice(part * H * D, (part + 1) * H * D)
+        assert rel(dqkv[:, sl], g_ref[:, sl]) < 3e-2, (part, rel(dqkv[:, sl], g_ref[:, sl]))
+
+
+def test_attention_large_logits(cuda):
+    # forces the online-softmax rescale path: one key spikes late in the sequence
+    B, H, S, D = 1, 2, 256, 64
+    qkv = torch.randn(B * S, 3 * H * D, device=cuda).bfloat16()
+    qkv[200, H * D:2 * H * D] *= 12
+    out, lse = OPS.attn_fwd(qkv, None, H, S, 1 / math.sqrt(D))
+    ref = _attn_ref(qkv.float(), torch.ones(B, S, device=cuda), H, S)
+    assert rel(out, ref) < 1.5e-2
+
+
+def test_embedding(cuda):
+    torch.manual_seed(2)
+    B, S, E, V = 4, 128, 128, 1000
+    ids = torch.randint(0, V, (B * S,), device=cuda)
+    tt = torch.randint(0, 2, (B * S,), device=cuda)
+    w = torch.randn(V, E, device=cuda)
+    p = torch.randn(512, E, device=cuda)
+    t = torch.randn(2, E, device=cuda)
+    g = torch.rand(E, device=cuda) + 0.5
+    b = torch.randn(E, device=cuda)
+    y, s, mean, rstd = OPS.embed_ln_fwd(ids, tt, w, p, t, g, b, S, 1e-12)
+    pos = torch.arange(B * S, device=cuda) % S
+    ref = F.layer_norm(w[ids] + p[pos] + t[tt], (E,), g, b, 1e-12)
+    assert rel(y, ref) < 1e-2
+    ds = torch.randn(B * S, E, device=cuda).bfloat16()
+    dw, dp, dt = torch.zeros_like(w), torch.zeros_like(p), torch.zeros_like(t)
+    OPS.embed_bwd(ds, ids, tt, dw, dp, dt, S)
+    dw_r = torch.zeros_like(w).index_add_(0, ids, ds.float())
+    dp_r = torch.zeros_like(p).index_add_(0, pos, ds.float())
+    dt_r = torch.zeros_like(t).index_add_(0, tt, ds.float())
+    assert rel(dw, dw_r) < 1e-4 and rel(dp, dp_r) < 1e-4 and rel(dt, dt_r) < 1e-4
+
+
+@pytest.mark.parametrize("V", [30000, 2, 31995])
+def test_xent(cuda, V):
+    M = 300
+    x = (torch.randn(M, V, device=cuda) * 3).bfloat16()
+    lab = torch.randint(0, V, (M,), device=cuda)
+    lab[::7] = -100
+    loss, dl = OPS.xent_fwd_bwd(x, lab, False, -100)
+    xr = x.float().requires_grad_(True)
+    lr = F.cross_entropy(xr, lab, ignore_index=-100)
+    assert abs(loss.item() - lr.item()) < 1e-3 * max(1, abs(lr.item()))
+    assert rel(dl, torch.autograd.grad(lr, xr)[0]) < 1e-2
+
+
+def _chunks(sizes, wd, dev, chunk=1000):
+    ct, cs, cl = [], [], []
+    off = 0
+    offs = []
+    for i, n in enumerate(sizes):
+        offs.append(off)
+        for s in range(0, n, chunk):
+            ct.append(i)
+            cs.append(off + s)
+            cl.append(min(chunk, n - s))
+        off += n
+    return (torch.tensor(ct, dtype=torch.int32, device=dev), torch.tensor(cs, dtype=torch.int64, device=dev),
+            torch.tensor(cl, dtype=torch.int32, device=dev), torch.tensor(wd, dtype=torch.float32, device=dev), offs)
+
+
+def test_lamb_matches_reference(cuda):
+    torch.manual_seed(3)
+    sizes = [4096, 1000, 37, 2500]
+    wd = [0.01, 0.0, 0.01, 0.0]
+    n = sum(sizes)
+    p = torch.randn(n, device=cuda)
+    ct, cs, cl, twd, offs = _chunks(sizes, wd, cuda)
+    m = torch.zeros(n, device=cuda)
+    v = torch.zeros(n, device=cuda)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    norms = torch.zeros(2 * len(sizes), device=cuda)
+    lr, b1, b2, eps = 1.76e-3, 0.9, 0.999, 1e-6
+    for step in range(1, 4):
+        g = torch.randn(n, device=cuda)
+        bc = math.sqrt(1 - b2 ** step) / (1 - b1 ** step)
+        OPS.lamb_step(p, g, m, v, ct, cs, cl, twd, norms, b1, b2, eps, lr * bc, 10.0, 1.0)
+        for i, (o, sz) in enumerate(zip(offs, sizes)):  # torch_optimizer.Lamb formula
+            sl = slice(o, o + sz)
+            mr[sl] = b1 * mr[sl] + (1 - b1) * g[sl]
+            vr[sl] = b2 * vr[sl] + (1 - b2) * g[sl] ** 2
+            wn = pr[sl].norm().clamp(0, 10.0)
+            u = mr[sl] / (vr[sl].sqrt() + eps) + wd[i] * pr[sl]
+            un = u.norm()
+            trust = 1.0 if (wn == 0 or un == 0) else (wn / un).item()
+            pr[sl] -= lr * bc * trust * u
+    assert rel(p, pr) < 1e-5 and rel(m, mr) < 1e-5 and rel(v, vr) < 1e-4
+
+
+def test_larc_sgd(cuda):
+    torch.manual_seed(4)
+    sizes = [3000, 64]
+    wd = [1e-6, 1e-6]
+    n = sum(sizes)
+    p = torch.randn(n, device=cuda)
+    buf = torch.zeros(n, device=cuda)
+    ct, cs, cl, twd, offs = _chunks(sizes, wd, cuda)
+    norms = torch.zeros(4, device=cuda)
+    pr, br = p.clone(), buf.clone()
+    lr, mom, trust = 0.3, 0.9, 1e-3
+    for step in range(3):
+        g = torch.randn(n, device=cuda)
+        OPS.larc_sgd_step(p, g, buf, ct, cs, cl, twd, norms, lr, mom, trust, 1e-8, False, step == 0, 1.0)
+        for i, (o, sz) in enumerate(zip(offs, sizes)):
+            sl = slice(o, o + sz)
+            pn, gn = pr[sl].norm(), g[sl].norm()
+            a = trust * pn / (gn + pn * wd[i] + 1e-8)
+            d = (g[sl] + wd[i] * pr[sl]) * a
+            br[sl] = d if step == 0 else mom * br[sl] + d
+            pr[sl] -= lr * br[sl]
+    assert rel(p, pr) < 1e-5
+
+
+def test_clip_and_axpby(cuda):
+    g = torch.randn(100003, device=cuda) * 3
+    ref = g.clone()
+    part = torch.zeros(256, device=cuda)
+    out = torch.zeros(2, device=cuda)
+    OPS.grad_norm_clip(g, 1.0, part, out)
+    n = ref.norm()
+    assert abs(out[0].item() - n.item()) < 1e-3 * n.item() and out[1].item() == 1.0
+    assert rel(g, ref * (1.0 / (n + 1e-6))) < 1e-5
+    y = torch.randn(100003, device=cuda)
+    y0 = y.clone()
+    OPS.axpby(y, g, 0.5, 2.0)
+    assert rel(y, 0.5 * y0 + 2.0 * g) < 1e-6
+    g[5] = float("nan")
+    OPS.grad_norm_clip(g, 1.0, part, out)
+    assert out[1].item() == 0.0
+
+
+@pytest.mark.parametrize("wire", [torch.float16, torch.bfloat16, torch.float32])
+def test_pack_reduce_unpack(cuda, wire):
+    n, k = 10007, 3
+    xs = [torch.randn(n, device=cuda) for _ in range(k)]
+    ws = [1.0, 2.0, 0.5]
+    parts = torch.empty(k, n, dtype=wire, device=cuda)
+    for i in range(k):
+        OPS.pack(xs[i], parts[i], ws[i])
+    avg = torch.empty(n, dtype=wire, device=cuda)
+    OPS.reduce_parts(parts, k, avg, 1.0 / sum(ws))
+    ref = sum(w * x for w, x in zip(ws, xs)) / sum(ws)
+    tol = 1e-6 if wire == torch.float32 else (2e-3 if wire == torch.float16 else 1e-2)
+    assert rel(avg, ref) < tol
+    dst = torch.zeros(n, device=cuda)
+    OPS.unpack(avg, dst, None)
+    assert rel(dst, ref) < tol
+    snap = torch.randn(n, device=cuda)
+    loc = snap + 1.0
+    OPS.unpack(avg, loc, snap)  # delta rule
+    assert rel(loc, ref + 1.0) < tol * 3
+
+
+def test_gemm_paths(cuda):
+    a = torch.randn(300, 128, device=cuda).bfloat16()
+    w = torch.randn(200, 128, device=cuda).bfloat16()
+    b = torch.randn(200, device=cuda).bfloat16()
+    y = OPS.gemm(a, w, b, None, False, True, 0)
+    assert rel(y, a.float() @ w.float().t() + b.float()) < 1e-2
+    c = torch.ones(200, 128, device=cuda)
+    dy = torch.randn(300, 200, device=cuda).bfloat16()
+    OPS.gemm_acc_f32(dy, a, c, True, False)
+    assert rel(c, 1 + dy.float().t() @ a.float()) < 1e-2
+
+
+def test_albert_gpu_matches_cpu(cuda):
+    from dedloc_amd.models.albert import AlbertConfig, AlbertForPreTraining
+
+    torch.manual_seed(0)
+    cfg = AlbertConfig.tiny(hidden_size=256, num_attention_heads=4, intermediate_size=1024, embedding_size=128)
+    m_cpu = AlbertForPreTraining(cfg)
+    m_gpu = AlbertForPreTraining(cfg)
+    m_gpu.load_hf_state_dict(m_cpu.hf_state_dict())
+    m_cpu.materialize("cpu")
+    m_gpu.materialize(cuda)
+    m_cpu.eval()
+    m_gpu.eval()
+    B, S = 2, 128
+    ids = torch.randint(5, cfg.vocab_size, (B, S))
+    am = torch.ones(B, S, dtype=torch.long)
+    am[1, 100:] = 0
+    labels = torch.full((B, S), -100)
+    labels[:, 3:20] = ids[:, 3:20]
+    sop = torch.tensor([0, 1])
+    oc = m_cpu(ids, am, None, labels=labels, sentence_order_label=sop)
+    og = m_gpu(ids.to(cuda), am.to(cuda), None, labels=labels.to(cuda), sentence_order_label=sop.to(cuda))
+    assert abs(oc["loss"].item() - og["loss"].item()) < 2e-2
+    oc["loss"].backward()
+    og["loss"].backward()
+    assert rel(m_gpu.flat.grad.cpu(), m_cpu.flat.grad) < 5e-2
