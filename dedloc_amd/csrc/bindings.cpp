@@ -169,13 +169,14 @@ void grad_norm_clip(at::Tensor g, double max_norm, at::Tensor part, at::Tensor o
         "grad_norm_clip");
 }
 
-void axpby(at::Tensor y, const at::Tensor& x, double a, double b) {
+void axpby(at::Tensor y, const at::Tensor& x, double a, double b, const c10::optional<at::Tensor>& flag) {
   expect(y, at::kFloat, "y");
   expect(x, at::kFloat, "x");
   TORCH_CHECK(x.numel() == y.numel(), "axpby size mismatch");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
               "axpby needs 16-byte aligned buffers");
-  dl_axpby(f32(y), f32(x), y.numel(), (float)a, (float)b, cur_stream(y));
+  const float* fp = flag.has_value() ? f32(*flag) : nullptr;
+  dl_axpby(f32(y), f32(x), y.numel(), (float)a, (float)b, fp, cur_stream(y));
 }
 
 // ------------------------------------------------------------------ averaging data plane

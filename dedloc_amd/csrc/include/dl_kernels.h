@@ -34,7 +34,7 @@ int dl_larc_sgd_step(float* p, const float* g, float* buf, const int* chunk_tens
                      float momentum, float trust_coef, float eps, int clip, int first_step, float grad_scale,
                      hipStream_t st);
 int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, hipStream_t st);
-int dl_axpby(float* y, const float* x, size_t n, float a, float b, hipStream_t st);
+int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, hipStream_t st);
 
 // comm.hip
 int dl_pack(const float* src, void* dst, int dst_dt, size_t n, float weight, hipStream_t st);

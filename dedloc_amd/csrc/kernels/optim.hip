@@ -158,19 +158,24 @@ __global__ __launch_bounds__(kBlock) void clip_kernel(float* __restrict__ x, siz
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) x[i] *= coef;
 }
 
-// y = a*y + b*x  (fp32)
+// y = a*y + b*x  (fp32).  With `flag` (device scalar, e.g. the finite flag of dl_grad_norm_clip)
+// the update is skipped entirely when *flag == 0, so a non-finite step never reaches y.
 __global__ __launch_bounds__(kBlock) void axpby_kernel(float* __restrict__ y, const float* __restrict__ x, size_t n,
-                                                       float a, float b) {
+                                                       float a, float b, const float* __restrict__ flag) {
+  if (flag != nullptr && flag[0] == 0.f) return;
   const size_t nvec = n / 4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     float4 yv = reinterpret_cast<float4*>(y)[i];
     const float4 xv = reinterpret_cast<const float4*>(x)[i];
-    yv.x = a * yv.x + b * xv.x; yv.y = a * yv.y + b * xv.y;
-    yv.z = a * yv.z + b * xv.z; yv.w = a * yv.w + b * xv.w;
+    // a == 0 / b == 0 drop the term entirely (so NaN * 0 never leaks: used to clear bad grads)
+    yv.x = (a != 0.f ? a * yv.x : 0.f) + (b != 0.f ? b * xv.x : 0.f);
+    yv.y = (a != 0.f ? a * yv.y : 0.f) + (b != 0.f ? b * xv.y : 0.f);
+    yv.z = (a != 0.f ? a * yv.z : 0.f) + (b != 0.f ? b * xv.z : 0.f);
+    yv.w = (a != 0.f ? a * yv.w : 0.f) + (b != 0.f ? b * xv.w : 0.f);
     reinterpret_cast<float4*>(y)[i] = yv;
   }
   for (size_t i = nvec * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    y[i] = a * y[i] + b * x[i];
+    y[i] = (a != 0.f ? a * y[i] : 0.f) + (b != 0.f ? b * x[i] : 0.f);
 }
 
 inline int grid_for(size_t n) {
@@ -209,7 +214,7 @@ int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int npart
   return 0;
 }
 
-int dl_axpby(float* y, const float* x, size_t n, float a, float b, hipStream_t st) {
-  axpby_kernel<<<grid_for(n), kBlock, 0, st>>>(y, x, n, a, b);
+int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, hipStream_t st) {
+  axpby_kernel<<<grid_for(n), kBlock, 0, st>>>(y, x, n, a, b, flag);
   return 0;
 }

@@ -259,6 +259,8 @@ class DHT:
         self._refresher: Optional[threading.Thread] = None
         self.port: Optional[int] = None
         self.endpoint: Optional[str] = None
+        self._started = time.time()
+        self._birth: Dict[str, float] = {}
         if start:
             self.run_in_background()
 
@@ -272,6 +274,7 @@ class DHT:
             self.port = self._server.port
             adv = self.endpoint_host or ("127.0.0.1" if bind_host == "0.0.0.0" else bind_host)
             self.endpoint = f"{adv}:{self.port}"
+            self._birth[self.endpoint] = self._started
             self._add_replica(self.endpoint)
         for p in self.initial_peers:
             self._add_replica(p)
@@ -310,15 +313,18 @@ class DHT:
 
     def _announce(self):
         if self.endpoint:
-            self._raw_store_all(DHT_NODES_KEY, self.endpoint.encode(), msgpack.packb(self.endpoint),
+            self._raw_store_all(DHT_NODES_KEY, self.endpoint.encode(),
+                                msgpack.packb([self.endpoint, self._started]),
                                 get_dht_time() + 3 * self.replica_refresh)
 
     def _sync_replicas(self):
         r = self._merged_get(DHT_NODES_KEY)
         if r is not None and r[0] == "dict":
             for sub, (val, _exp) in r[1].items():
-                ep = msgpack.unpackb(val)
-                if ep:
+                rec = msgpack.unpackb(val)
+                if rec:
+                    ep, started = rec
+                    self._birth[ep] = started
                     self._add_replica(ep)
 
     def _refresh_loop(self):
@@ -405,8 +411,14 @@ class DHT:
         return ValueWithExpiration(out, max(v.expiration_time for v in out.values()))
 
     def primary(self) -> DHTClient:
-        """Replica used for matchmaking: lowest endpoint that answers a ping."""
-        for ep in self.replicas():
+        """Replica used for matchmaking: the OLDEST live replica.
+
+        Every node learns all older replicas when it starts (it syncs ``_dht_nodes`` from its initial
+        peers), so all peers agree on the oldest live one without waiting for replica discovery —
+        a newcomer can never split matchmaking by being "lowest".
+        """
+        order = sorted(self.replicas(), key=lambda ep: (self._birth.get(ep, float("inf")), ep))
+        for ep in order:
             c = self._clients[ep]
             try:
                 if c.ping():

@@ -29,7 +29,7 @@ _SCHEMAS = [
     "lamb_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(d!) norms, float beta1, float beta2, float eps, float step_size, float clamp_value, float grad_scale) -> ()",
     "larc_sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(c!) norms, float lr, float momentum, float trust_coef, float eps, bool clip, bool first_step, float grad_scale) -> ()",
     "grad_norm_clip(Tensor(a!) g, float max_norm, Tensor(b!) part, Tensor(c!) out) -> ()",
-    "axpby(Tensor(a!) y, Tensor x, float a, float b) -> ()",
+    "axpby(Tensor(a!) y, Tensor x, float a, float b, Tensor? flag=None) -> ()",
     "pack(Tensor src, Tensor(a!) dst, float weight) -> ()",
     "reduce_parts(Tensor parts, int nparts, Tensor(a!) out, float inv_total) -> ()",
     "unpack(Tensor src, Tensor(a!) dst, Tensor? snap) -> ()",
@@ -229,8 +229,11 @@ def _clip_cpu(g, max_norm, part, out):
 
 
 @_impl("axpby")
-def _axpby_cpu(y, x, a, b):
-    y.mul_(a).add_(x, alpha=b)
+def _axpby_cpu(y, x, a, b, flag=None):
+    if flag is not None and float(flag.reshape(-1)[0]) == 0.0:
+        return
+    r = (y * a if a != 0 else torch.zeros_like(y)) + (x * b if b != 0 else 0.0)
+    y.copy_(r)
 
 
 @_impl("pack")

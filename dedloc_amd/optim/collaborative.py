@@ -1,0 +1,353 @@
+"""CollaborativeOptimizer — global-batch collaborative training (hivemind 0.9.x semantics, SURVEY.md
+§2.2 H4-H6, App. A.2; reference call sites albert/run_trainer.py:251-264, run_aux.py:243-262,
+run_first_peer.py:97-121, sgd_collaborative.py:145-171).
+
+Peers of different speed accumulate gradients locally until the *collaboration* has processed
+``target_batch_size`` samples (tracked through ``{prefix}_progress`` records on the DHT, with an
+ETA-driven refresh period), then they average parameters and gradients (sample-weighted,
+butterfly all-reduce) and apply one synchronised optimizer step; the LR schedule follows the
+global step.  Out-of-sync peers download the state from a donor instead of contributing.
+
+Flat-buffer implementation: gradients arrive in ``opt.flat.grad`` (fp32), the accumulator is one
+flat fp32 buffer, and every accumulate/average/apply is a single multi-tensor HIP launch; the
+fast path of ``step()`` (most calls) costs one kernel and a few Python statements.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import threading
+import time
+from dataclasses import dataclass
+from typing import Any, Dict, Optional
+
+import torch
+from pydantic import BaseModel, StrictBool, StrictFloat, confloat, conint
+
+from ..averaging.averager import DecentralizedAverager
+from ..dht import DHT, get_dht_time
+from .performance_ema import PerformanceEMA
+
+logger = logging.getLogger(__name__)
+
+
+class TrainingState(BaseModel):
+    peer_id: bytes
+    step: conint(ge=0, strict=True)
+    samples_accumulated: conint(ge=0, strict=True)
+    samples_per_second: confloat(ge=0.0, strict=True)
+    time: StrictFloat
+    client_mode: StrictBool
+    auxiliary: bool = False
+
+
+@dataclass
+class CollaborationState:
+    optimizer_step: int
+    samples_accumulated: int
+    target_batch_size: int
+    num_peers: int
+    num_clients: int
+    eta_next_step: float
+    next_fetch_time: float
+
+    @property
+    def ready_for_step(self) -> bool:
+        return self.samples_accumulated >= self.target_batch_size or get_dht_time() >= self.eta_next_step
+
+    def register_step(self, local_step: int):
+        self.optimizer_step = max(local_step, self.optimizer_step)
+        self.samples_accumulated = 0
+        self.eta_next_step = float("inf")
+
+
+class CollaborativeOptimizer:
+    def __init__(self, opt, *, dht: DHT, prefix: str, target_batch_size: int, batch_size_per_step: Optional[int] = None,
+                 scheduler=None, min_refresh_period: float = 0.5, max_refresh_period: float = 30,
+                 default_refresh_period: float = 3, expected_drift_peers: float = 3, expected_drift_rate: float = 0.2,
+                 performance_ema_alpha: float = 0.1, metadata_expiration: float = 30.0,
+                 averaging_timeout: Optional[float] = None, step_tolerance: int = 1, client_mode: bool = False,
+                 auxiliary: bool = False, allow_state_sharing: bool = True, verbose: bool = False, start: bool = True,
+                 compression_type: str = "FLOAT16", compression: Optional[str] = None, throughput: Optional[float] = None,
+                 peer_id: Optional[bytes] = None, max_grad_norm: Optional[float] = None, **averager_kwargs):
+        self.opt, self.dht, self.prefix = opt, dht, prefix
+        self.flat = opt.flat
+        self.scheduler = scheduler
+        self.target_batch_size = target_batch_size
+        self.batch_size_per_step = batch_size_per_step
+        self.min_refresh_period, self.max_refresh_period = min_refresh_period, max_refresh_period
+        self.default_refresh_period = default_refresh_period
+        self.expected_drift_peers, self.expected_drift_rate = expected_drift_peers, expected_drift_rate
+        self.metadata_expiration = metadata_expiration
+        self.averaging_timeout = averaging_timeout or 30.0
+        self.step_tolerance = step_tolerance
+        self.client_mode, self.auxiliary = client_mode, auxiliary
+        self.verbose = verbose
+        self.status_loglevel = logging.INFO if verbose else logging.DEBUG
+        if peer_id is None:
+            import os
+
+            peer_id = f"peer-{os.getpid()}-{id(self):x}".encode()
+        self.peer_id = peer_id
+
+        self.accumulator = torch.zeros_like(self.flat.fp32) if not auxiliary else None
+        self.local_samples_accumulated = 0
+        self.local_steps_accumulated = 0
+        self.local_step = 0
+        self.performance_ema = PerformanceEMA(alpha=performance_ema_alpha)
+        self.last_step_time = None
+        self.last_group: Optional[Dict] = None
+        self.stats = {"global_steps": 0, "averaging_rounds": 0, "averaging_failed": 0, "state_loads": 0}
+
+        self.averager = DecentralizedAverager(
+            [self.flat.fp32, self.flat.grad], dht, prefix, peer_id=peer_id,
+            compression=compression or compression_type, throughput=throughput, client_mode=client_mode,
+            auxiliary=auxiliary, allow_state_sharing=allow_state_sharing, metadata_expiration=metadata_expiration,
+            averaging_timeout=self.averaging_timeout, **averager_kwargs)
+        self.averager.get_current_state = self._get_current_state
+
+        self.lock_collaboration_state = threading.Lock()
+        self.lock_local_progress = threading.Lock()
+        self.lock_step = threading.RLock()
+        self.should_report_progress = threading.Event()
+        self.collaboration_state_updated = threading.Event()
+        self._stop = threading.Event()
+        self.collaboration_state = self.fetch_collaboration_state()
+        self._threads = []
+        if start:
+            for target, name in ((self._report_loop, "progress-reporter"), (self._update_loop, "collab-updater")):
+                t = threading.Thread(target=target, daemon=True, name=name)
+                t.start()
+                self._threads.append(t)
+            self.averager.publish_state_sharing(self.local_step)
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def is_synchronized(self) -> bool:
+        return self.local_step >= self.collaboration_state.optimizer_step - self.step_tolerance
+
+    @property
+    def is_alive(self) -> bool:
+        return not self._stop.is_set()
+
+    # ------------------------------------------------------------------ state
+    def _get_current_state(self):
+        with self.lock_step:
+            meta = {"step": int(self.local_step), "opt_step": int(self.opt.step_count),
+                    "lr_sched": self.scheduler.state_dict() if self.scheduler is not None else None}
+            tensors = [self.flat.fp32.detach().clone()] + [t.detach().clone() for t in self.opt.state_tensors()]
+        return meta, tensors
+
+    @torch.no_grad()
+    def load_state_from_peers(self, **kwargs) -> bool:
+        """Download params + optimizer state from the freshest donor (App. A.7)."""
+        with self.lock_step:
+            res = self.averager.load_state_from_peers(**kwargs)
+            if res is None:
+                logger.log(self.status_loglevel, "no peers to load state from; keeping local state")
+                return False
+            meta, tensors = res
+            self.flat.fp32.copy_(tensors[0].to(self.flat.fp32.device))
+            for dst, src in zip(self.opt.state_tensors(), tensors[1:]):
+                dst.copy_(src.to(dst.device))
+            self.opt.step_count = int(meta.get("opt_step", self.opt.step_count))
+            self.local_step = max(self.local_step, int(meta.get("step", 0)))
+            self.flat.refresh_bf16()
+            self._reset_accumulators()
+            self.update_scheduler()
+            self.stats["state_loads"] += 1
+            self.averager.publish_state_sharing(self.local_step)
+        return True
+
+    def _reset_accumulators(self):
+        if self.accumulator is not None:
+            self.accumulator.zero_()
+        with self.lock_local_progress:
+            self.local_samples_accumulated = 0
+            self.local_steps_accumulated = 0
+
+    def update_scheduler(self):
+        if self.scheduler is not None:
+            while self.scheduler._step_count < self.local_step:
+                self.scheduler.step()
+
+    # ------------------------------------------------------------------ training step
+    def zero_grad(self, *args, **kwargs):
+        self.opt.zero_grad()
+
+    def step(self, batch_size: Optional[int] = None, **kwargs):
+        """Accumulate this step's gradients; run a global step when the collaboration is ready."""
+        if self.batch_size_per_step is None:
+            if batch_size is None:
+                raise ValueError("specify batch_size_per_step or pass batch_size")
+            self.batch_size_per_step = batch_size
+        batch_size = batch_size if batch_size is not None else self.batch_size_per_step
+
+        if not self.is_synchronized:
+            logger.log(self.status_loglevel, "peer is out of sync; loading state from peers")
+            self.load_state_from_peers()
+            return None
+        if self.last_step_time is not None and get_dht_time() - self.last_step_time > self.metadata_expiration:
+            logger.warning(f"training step took {get_dht_time() - self.last_step_time:.1f}s, longer than "
+                           f"metadata_expiration; other peers may have considered this one dead")
+
+        with self.lock_local_progress:
+            torch.ops.dedloc.axpby(self.accumulator, self.flat.grad, 1.0, batch_size / self.batch_size_per_step)
+            self.local_samples_accumulated += batch_size
+            self.local_steps_accumulated += 1
+            self.performance_ema.update(num_processed=batch_size)
+            self.should_report_progress.set()
+
+        if not self.collaboration_state.ready_for_step:
+            return None
+
+        logger.log(self.status_loglevel, f"beginning global optimizer step #{self.collaboration_state.optimizer_step}")
+        self.collaboration_state = self.fetch_collaboration_state()
+        self.collaboration_state_updated.set()
+        if not self.is_synchronized:
+            self.load_state_from_peers()
+            return None
+
+        with self.performance_ema.pause(), self.lock_collaboration_state, self.lock_step:
+            cs = self.collaboration_state
+            # grads = accumulator / local_steps   (hivemind apply_accumulated_grads_)
+            torch.ops.dedloc.axpby(self.flat.grad, self.accumulator, 0.0, 1.0 / max(1, self.local_steps_accumulated))
+            group = None
+            if cs.num_peers > 1:
+                mean_samples = self.target_batch_size / cs.num_peers
+                weight = self.local_samples_accumulated / mean_samples
+                group = self.averager.step(weight=weight, timeout=self.averaging_timeout,
+                                           expected_group_size=cs.num_peers)
+                self.stats["averaging_rounds"] += 1
+                if group is None:
+                    self.stats["averaging_failed"] += 1
+                    logger.log(self.status_loglevel, "Skipped averaging: collaboration consists of this peer only "
+                                                     "or the round failed; applying local gradients")
+            else:
+                logger.log(self.status_loglevel, "Skipped averaging: collaboration consists of this peer alone")
+            self.opt.step()
+            self._reset_accumulators()
+            self.collaboration_state.register_step(self.local_step + 1)
+            self.local_step += 1
+            self.update_scheduler()
+            self.last_group = group
+            self.stats["global_steps"] += 1
+            self.should_report_progress.set()
+        self.averager.publish_state_sharing(self.local_step)
+        self.last_step_time = get_dht_time()
+        logger.log(self.status_loglevel, f"optimizer step #{self.local_step} done")
+        return group
+
+    def step_aux(self, **kwargs):
+        """Auxiliary peer: join the averaging rounds as a reducer only (run_aux.py:260-262)."""
+        if not self.collaboration_state.ready_for_step:
+            self.should_report_progress.set()
+            return None
+        self.collaboration_state = self.fetch_collaboration_state()
+        self.collaboration_state_updated.set()
+        with self.lock_collaboration_state, self.lock_step:
+            group = None
+            if self.collaboration_state.num_peers > 1:
+                group = self.averager.step(weight=0.0, timeout=self.averaging_timeout,
+                                           expected_group_size=self.collaboration_state.num_peers)
+            self.collaboration_state.register_step(self.local_step + 1)
+            self.local_step += 1
+            self.last_group = group
+            self.should_report_progress.set()
+        return group
+
+    # ------------------------------------------------------------------ background threads
+    def _report_loop(self):
+        while not self._stop.is_set():
+            self.should_report_progress.wait()
+            self.should_report_progress.clear()
+            if self._stop.is_set():
+                break
+            self.report_training_progress()
+
+    def report_training_progress(self):
+        with self.lock_local_progress:
+            st = TrainingState(peer_id=self.peer_id, step=int(self.local_step),
+                               samples_accumulated=int(self.local_samples_accumulated),
+                               samples_per_second=float(self.performance_ema.samples_per_second),
+                               time=float(get_dht_time()), client_mode=bool(self.client_mode),
+                               auxiliary=bool(self.auxiliary))
+        try:
+            self.dht.store(f"{self.prefix}_progress", st.model_dump(), get_dht_time() + self.metadata_expiration,
+                           subkey=self.peer_id)
+        except Exception as e:  # noqa: BLE001
+            logger.debug(f"progress report failed: {e}")
+
+    def _update_loop(self):
+        while not self._stop.is_set():
+            delay = max(0.0, self.collaboration_state.next_fetch_time - get_dht_time())
+            if self.collaboration_state_updated.wait(delay):
+                self.collaboration_state_updated.clear()
+                continue
+            if self._stop.is_set():
+                break
+            try:
+                with self.lock_collaboration_state:
+                    self.collaboration_state = self.fetch_collaboration_state()
+            except Exception as e:  # noqa: BLE001
+                logger.debug(f"collaboration state update failed: {e}")
+
+    def fetch_collaboration_state(self) -> CollaborationState:
+        now = get_dht_time()
+        rec = self.dht.get(f"{self.prefix}_progress", latest=True)
+        peers = []
+        if rec is not None and isinstance(rec.value, dict):
+            for sub, v in rec.value.items():
+                try:
+                    peers.append(TrainingState.model_validate(v.value))
+                except Exception:  # noqa: BLE001
+                    continue
+        if not peers:
+            local_eta = max(0, self.target_batch_size - self.local_samples_accumulated) / max(
+                self.performance_ema.samples_per_second, 1e-9)
+            return CollaborationState(self.local_step, self.local_samples_accumulated, self.target_batch_size,
+                                      num_peers=0, num_clients=0, eta_next_step=now + local_eta,
+                                      next_fetch_time=now + self.default_refresh_period)
+        num_peers = len(peers)
+        num_clients = sum(p.client_mode for p in peers)
+        global_step = max(0, self.local_step, *[p.step for p in peers if not p.client_mode] or [0])
+        total_sps = sum(p.samples_per_second for p in peers)
+        samples_acc, est = 0, 0.0
+        for p in peers:
+            if p.step == global_step:
+                samples_acc += p.samples_accumulated
+                est += p.samples_accumulated + max(0.0, now - p.time) * p.samples_per_second
+        eta = max(0.0, self.target_batch_size - est) / max(total_sps, 1e-9)
+        expected_max_peers = max(num_peers + self.expected_drift_peers, num_peers * (1 + self.expected_drift_rate))
+        refresh = eta * num_peers / expected_max_peers
+        next_fetch = now + min(max(refresh, self.min_refresh_period), self.max_refresh_period)
+        return CollaborationState(global_step, samples_acc, self.target_batch_size, num_peers, num_clients,
+                                  eta_next_step=now + eta, next_fetch_time=next_fetch)
+
+    # ------------------------------------------------------------------ misc
+    def state_dict(self) -> Dict[str, Any]:
+        return {"opt": self.opt.state_dict(), "local_step": self.local_step,
+                "scheduler": self.scheduler.state_dict() if self.scheduler is not None else None}
+
+    def load_state_dict(self, sd: Dict[str, Any]):
+        self.opt.load_state_dict(sd["opt"])
+        self.local_step = int(sd.get("local_step", self.local_step))
+        if self.scheduler is not None and sd.get("scheduler"):
+            self.scheduler.load_state_dict(sd["scheduler"])
+
+    def shutdown(self):
+        self._stop.set()
+        self.should_report_progress.set()
+        self.collaboration_state_updated.set()
+        try:  # tombstone own progress entry
+            self.dht.store(f"{self.prefix}_progress", None, get_dht_time() + self.metadata_expiration,
+                           subkey=self.peer_id)
+        except Exception:  # noqa: BLE001
+            pass
+        self.averager.shutdown()
+
+    def __del__(self):
+        try:
+            self._stop.set()
+        except Exception:  # noqa: BLE001
+            pass

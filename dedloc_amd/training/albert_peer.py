@@ -1,0 +1,196 @@
+"""ALBERT collaborative trainer peer — the engine behind ``run_trainer`` (albert/run_trainer.py:210-293,
+sahajbert/run_trainer.py:215-300).
+
+Replaces the reference's HF ``Trainer`` + ``CollaborativeCallback`` + ``NoOpScheduler`` stack with
+an explicit loop over device-resident batches:
+
+  HF step = gradient_accumulation_steps micro-batches (fwd + bwd into the flat fp32 grad buffer)
+          -> clip_grad_norm(max_grad_norm) + finite flag (one fused kernel pair, no host sync)
+          -> CollaborativeOptimizer.step(batch_size)  (accumulate; global step when ready)
+          -> zero_grad
+          -> callback: publish LocalMetrics to {prefix}_metrics when the collaborative step changes
+
+Deliberate differences from the reference: non-finite gradients are dropped on
+the device (the reference's state_dict-alias rollback is a no-op, C.1); the loss is accumulated
+on the device and read once per collaborative step instead of once per step.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import shutil
+import time
+from pathlib import Path
+from typing import Dict, Optional
+
+import torch
+
+from ..data.synthetic_mlm import SyntheticSOPStream, peer_seed
+from ..dht import DHT, get_dht_time
+from ..metrics import LocalMetrics, make_validators
+from ..models.albert import AlbertConfig, AlbertForPreTraining
+from ..optim.collaborative import CollaborativeOptimizer
+from ..optim.lamb import FusedLamb, get_linear_schedule_with_warmup
+
+logger = logging.getLogger(__name__)
+
+
+def latest_checkpoint(output_dir: str) -> Optional[Path]:
+    return max(Path(output_dir).glob("checkpoint*"), default=None, key=os.path.getctime)
+
+
+def get_model(training_args, config: AlbertConfig) -> AlbertForPreTraining:
+    """Resume from the newest output_dir/checkpoint* (by ctime) else random init (run_trainer.py:56-70)."""
+    ckpt = latest_checkpoint(training_args.output_dir)
+    if ckpt is not None and (ckpt / "config.json").exists():
+        logger.info(f"Loading model from {ckpt}")
+        return AlbertForPreTraining.from_pretrained(str(ckpt))
+    logger.info("Training from scratch")
+    return AlbertForPreTraining(config)
+
+
+def build_optimizer(model: AlbertForPreTraining, training_args):
+    opt = FusedLamb(model.flat, lr=training_args.learning_rate,
+                    betas=(training_args.adam_beta1, training_args.adam_beta2), eps=training_args.adam_epsilon,
+                    weight_decay=training_args.weight_decay, clamp_value=training_args.clamp_value, debias=True,
+                    no_decay=model.no_decay_names())
+    sched = get_linear_schedule_with_warmup(opt, training_args.warmup_steps, training_args.max_steps)
+    return opt, sched
+
+
+class AlbertPeer:
+    """Everything one GPU peer owns: model, optimizer, DHT node, collaborative optimizer, data."""
+
+    def __init__(self, training_args, dataset_args, collab_args, device, pg=None, rank: int = 0,
+                 dht: Optional[DHT] = None, auxiliary: bool = False, publish_only_synchronized: bool = False):
+        self.args, self.dargs, self.cargs = training_args, dataset_args, collab_args
+        self.device = torch.device(device)
+        self.auxiliary = auxiliary
+        self.publish_only_synchronized = publish_only_synchronized
+        torch.manual_seed(training_args.seed)
+        config = AlbertConfig.from_pretrained(dataset_args.config_path)
+        if getattr(dataset_args, "vocab_size", None):
+            config.vocab_size = dataset_args.vocab_size
+        self.model = get_model(training_args, config)
+        self.model.materialize(self.device)
+        self.model.train()
+        self.opt, self.scheduler = build_optimizer(self.model, training_args)
+        ca = collab_args
+        validators, self.local_public_key = make_validators(ca.experiment_prefix)
+        self.dht = dht or DHT(initial_peers=ca.initial_peers, listen=not ca.client_mode, listen_on=ca.dht_listen_on,
+                              endpoint=ca.endpoint, start=True, record_validators=validators)
+        self.batch_size_per_step = training_args.per_device_train_batch_size * training_args.gradient_accumulation_steps
+        self.collab_opt = CollaborativeOptimizer(
+            self.opt, dht=self.dht, scheduler=self.scheduler, prefix=ca.experiment_prefix,
+            compression_type=ca.compression, batch_size_per_step=self.batch_size_per_step,
+            throughput=ca.bandwidth, target_batch_size=ca.target_batch_size - ca.batch_size_lead,
+            client_mode=ca.client_mode, verbose=True, start=True, auxiliary=auxiliary,
+            allow_state_sharing=not auxiliary, peer_id=self.local_public_key,
+            averaging_expiration=ca.averaging_expiration, averaging_timeout=ca.averaging_timeout,
+            listen_on=ca.listen_on, min_refresh_period=ca.min_refresh_period, max_refresh_period=ca.max_refresh_period,
+            default_refresh_period=ca.default_refresh_period, expected_drift_peers=ca.expected_drift_peers,
+            expected_drift_rate=ca.expected_drift_rate, performance_ema_alpha=ca.performance_ema_alpha,
+            target_group_size=ca.target_group_size, metadata_expiration=ca.metadata_expiration, pg=pg, rank=rank)
+        self.statistics_expiration = ca.statistics_expiration
+        seed = peer_seed(self.local_public_key, training_args.seed)
+        self.data = SyntheticSOPStream(training_args.per_device_train_batch_size, training_args.seq_length,
+                                       self.model.config.vocab_size, seed=seed, device=self.device,
+                                       mask_mode=getattr(dataset_args, "mask_mode", "fixed"),
+                                       length_mode=getattr(dataset_args, "length_mode", "full"))
+        flat = self.model.flat
+        self._clip_part = torch.zeros(256, device=self.device)
+        self._clip_out = torch.zeros(2, device=self.device)
+        self._loss_sum = torch.zeros((), device=self.device)
+        self.mini_steps = 0
+        self.samples = 0
+        self.total_samples_processed = 0
+        self.last_reported_collaboration_step = -1
+        self.hf_step = 0
+        self.metrics_log = []
+        self._flat = flat
+
+    # ------------------------------------------------------------------ one HF step
+    def train_step(self):
+        a = self.args
+        ga = a.gradient_accumulation_steps
+        for _ in range(ga):
+            batch = self.data.next_batch()
+            out = self.model(batch["input_ids"], batch["attention_mask"], batch["token_type_ids"],
+                             labels=batch.get("labels"), sentence_order_label=batch["sentence_order_label"],
+                             mlm_positions=batch.get("mlm_positions"), mlm_labels=batch.get("mlm_labels"))
+            loss = out["loss"] / ga if ga > 1 else out["loss"]
+            loss.backward()
+            self._loss_sum += loss.detach()
+        torch.ops.dedloc.grad_norm_clip(self._flat.grad, float(a.max_grad_norm or 0.0), self._clip_part,
+                                        self._clip_out)
+        self._drop_if_nonfinite()
+        self.collab_opt.step(batch_size=self.batch_size_per_step)
+        self.opt.zero_grad()
+        self.mini_steps += 1
+        self.hf_step += 1
+        if a.throttle > 0:
+            time.sleep(a.throttle)
+        self.on_step_end()
+
+    def _drop_if_nonfinite(self):
+        # device-side: zero the whole step's gradient when the finite flag is 0 (no host sync)
+        torch.ops.dedloc.axpby(self._flat.grad, self._flat.grad, 0.0, 0.0, 1.0 - self._clip_out[1:2])
+
+    def on_step_end(self):
+        co = self.collab_opt
+        if co.local_step != self.last_reported_collaboration_step:
+            self.last_reported_collaboration_step = co.local_step
+            self.total_samples_processed += self.samples
+            loss = float(self._loss_sum.item())
+            stats = LocalMetrics(step=int(co.local_step), samples_per_second=float(co.performance_ema.samples_per_second),
+                                 samples_accumulated=int(self.samples), loss=loss, mini_steps=int(self.mini_steps))
+            logger.info(f"Step {co.local_step}")
+            logger.info(f"Your current contribution: {self.total_samples_processed} samples")
+            if self.mini_steps:
+                logger.info(f"Local loss: {loss / self.mini_steps:.5f}")
+            if (not self.publish_only_synchronized) or co.is_synchronized:
+                self.dht.store(co.prefix + "_metrics", stats.model_dump(),
+                               expiration_time=get_dht_time() + self.statistics_expiration,
+                               subkey=self.local_public_key, return_future=True)
+            rec = dict(stats.model_dump(), time=time.time(), hf_step=self.hf_step,
+                       lr=self.opt.param_groups[0]["lr"], group=(co.last_group or {}).get("size"))
+            self.metrics_log.append(rec)
+            if self.args.metrics_file:
+                with open(self.args.metrics_file, "a") as f:
+                    f.write(json.dumps(rec) + "\n")
+            self._loss_sum.zero_()
+            self.mini_steps = 0
+        self.samples = co.local_samples_accumulated
+        if self.args.save_steps and self.hf_step % self.args.save_steps == 0:
+            self.save_checkpoint()
+
+    # ------------------------------------------------------------------ checkpoints (HF layout)
+    def save_checkpoint(self):
+        out = Path(self.args.output_dir) / f"checkpoint-{self.hf_step}"
+        self.model.save_pretrained(str(out))
+        torch.save(self.collab_opt.opt.state_dict(), out / "optimizer.pt")
+        torch.save({}, out / "scheduler.pt")  # NoOpScheduler state (albert/run_trainer.py:203-204)
+        with open(out / "trainer_state.json", "w") as f:
+            json.dump({"global_step": self.hf_step, "collaborative_step": self.collab_opt.local_step}, f)
+        ckpts = sorted(Path(self.args.output_dir).glob("checkpoint-*"), key=os.path.getctime)
+        for old in ckpts[:-self.args.save_total_limit] if self.args.save_total_limit else []:
+            shutil.rmtree(old, ignore_errors=True)
+
+    def train(self, max_steps: Optional[int] = None, stop_after_global_steps: Optional[int] = None,
+              max_seconds: Optional[float] = None):
+        logger.warning("Loading state from peers")
+        self.collab_opt.load_state_from_peers()
+        t0 = time.time()
+        max_steps = max_steps or self.args.max_steps
+        start_global = self.collab_opt.local_step
+        while self.hf_step < max_steps:
+            self.train_step()
+            if stop_after_global_steps is not None and self.collab_opt.local_step - start_global >= stop_after_global_steps:
+                break
+            if max_seconds is not None and time.time() - t0 > max_seconds:
+                break
+
+    def shutdown(self):
+        self.collab_opt.shutdown()
+        self.dht.shutdown()
