@@ -1,0 +1,145 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-node samples/sec of collaborative ALBERT-large MLM+SOP pre-training.
+
+Metric/config from BASELINE.json: "samples/sec (whole node) ALBERT-large MLM pretrain at 1/2/4/8
+peers".  One process per GPU = one collaboration peer (run_trainer semantics): bf16 compute,
+synthetic WikiText-103-shaped SOP instances (seq 512, 15 % MLM), random-init albert-large-v2
+weights, LAMB + linear-warmup schedule, target_batch_size 4096 samples per collaborative step,
+FLOAT16 butterfly averaging of parameters + gradients over RCCL between all peers, exactly as the
+reference's CollaborativeOptimizer does it (nothing is skipped inside the timed region).
+
+A bench "step" = ONE collaborative (global) optimizer step = 4096 samples summed over all peers.
+The total work per step is fixed as N grows, so scaling is "strong".
+
+    python bench.py                         # 1 GPU
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "samples/sec (whole node) ALBERT-large MLM pretrain at 1/2/4/8 peers"
+# Measured PyTorch-eager reference on MI355X (HF AlbertForPreTraining, bf16 autocast, SDPA, eager
+# torch LAMB; bench/model_step.py --impl hf --with_optimizer), samples/s per GPU.  BASELINE.md.
+EAGER_BASELINE_SPS_PER_GPU = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed collaborative steps")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed collaborative steps")
+    ap.add_argument("--micro_batch", type=int, default=32)
+    ap.add_argument("--grad_accum", type=int, default=1)
+    ap.add_argument("--seq_len", type=int, default=512)
+    ap.add_argument("--target_batch_size", type=int, default=4096)
+    ap.add_argument("--compression", default="FLOAT16")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    logging.basicConfig(level=logging.INFO if args.verbose else logging.WARNING,
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    from dedloc_amd.parallel import init_world
+
+    rank, world, dev = init_world()
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    from dedloc_amd.cli.arguments import AlbertTrainingArguments, CollaborationArguments, DatasetArguments
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.training.albert_peer import AlbertPeer
+
+    # control plane: rank 0 hosts the DHT root, everyone else bootstraps from it
+    root = DHT(listen_on="127.0.0.1:*") if rank == 0 else None
+    ep = [root.endpoint if root is not None else None]
+    if world > 1:
+        dist.broadcast_object_list(ep, src=0)
+    targs = AlbertTrainingArguments(per_device_train_batch_size=args.micro_batch,
+                                    gradient_accumulation_steps=args.grad_accum, seq_length=args.seq_len,
+                                    save_steps=0, output_dir=f"/tmp/dedloc_bench_{os.getpid()}", seed=1234)
+    dargs = DatasetArguments(config_path="albert-large-v2")
+    cargs = CollaborationArguments(experiment_prefix="bench", initial_peers=[ep[0]], dht_listen_on="127.0.0.1:*",
+                                   target_batch_size=args.target_batch_size, compression=args.compression,
+                                   listen_on="127.0.0.1:*", averaging_expiration=5.0, averaging_timeout=60.0,
+                                   min_refresh_period=0.2, default_refresh_period=0.5)
+    peer = AlbertPeer(targs, dargs, cargs, dev, rank=rank, dht=None)
+    co = peer.collab_opt
+    bs = args.micro_batch * args.grad_accum
+
+    def run_until(step):
+        n = 0
+        while co.local_step < step:
+            peer.train_step()
+            n += bs
+        return n
+
+    if world > 1:
+        dist.barrier()
+    co.load_state_from_peers()  # joins the collaboration like run_trainer does (on_train_begin)
+    if world > 1:
+        dist.barrier()
+    base = co.local_step
+    run_until(base + args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ema_start = co.performance_ema.samples_per_second
+    t0 = time.perf_counter()
+    samples = run_until(base + args.warmup + args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ema = co.performance_ema.samples_per_second
+    stats = torch.tensor([samples, dt, ema], dtype=torch.float64, device=dev)
+    if world > 1:
+        gathered = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(gathered, stats)
+    else:
+        gathered = [stats]
+    total_samples = sum(float(g[0]) for g in gathered)
+    max_dt = max(float(g[1]) for g in gathered)
+    ema_sum = sum(float(g[2]) for g in gathered)
+    if rank == 0:
+        value = total_samples / max_dt
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(max_dt / args.steps * 1e3, 2),
+               "higher_is_better": True, "scaling": "strong",
+               "vs_baseline": (round(value / (EAGER_BASELINE_SPS_PER_GPU * world), 3)
+                               if EAGER_BASELINE_SPS_PER_GPU else None),
+               "dtype": "bf16", "data": "synthetic (WikiText-103 SOP shapes, seq 512, 15% MLM; random-init weights)",
+               "config": {"model": "albert-large-v2", "global_batch": args.target_batch_size,
+                          "seq_len": args.seq_len, "parallelism": f"collaborative-dp{world}",
+                          "micro_batch": args.micro_batch, "grad_accum": args.grad_accum,
+                          "compression": args.compression, "optimizer": "LAMB"},
+               "ema_samples_per_s_sum": round(ema_sum, 2), "averaging_rounds": co.stats["averaging_rounds"],
+               "averaging_failed": co.stats["averaging_failed"],
+               "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"}}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+    peer.shutdown()
+    if root is not None:
+        root.shutdown()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -5,6 +5,7 @@
                 the "PyTorch-eager on MI355X" baseline BASELINE.md asks to record.
 """
 import argparse
+import math
 import json
 import time
 
@@ -32,6 +33,8 @@ def main():
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--with_optimizer", action="store_true",
+                    help="include clip + LAMB every micro-step (upper bound on optimizer cost)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     from dedloc_amd.models.albert import AlbertConfig, AlbertForPreTraining, flops_per_sample
@@ -54,12 +57,37 @@ def main():
         hcfg = transformers.AlbertConfig(**{k: v for k, v in cfg.to_dict().items()
                                             if k not in ("architectures", "model_type")})
         model = transformers.AlbertForPreTraining(hcfg).to(dev).train()
+        params = [p for p in model.parameters() if p.requires_grad]
+        state = {id(p): (torch.zeros_like(p), torch.zeros_like(p)) for p in params}
+        t_opt = [0]
+
+        @torch.no_grad()
+        def eager_lamb(lr=1.76e-3, b1=0.9, b2=0.999, eps=1e-6, wd=0.01, clamp=1e4):
+            # torch_optimizer.Lamb(debias=True) written with per-tensor torch ops (reference behaviour)
+            t_opt[0] += 1
+            t = t_opt[0]
+            bc = math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+            for p in params:
+                if p.grad is None:
+                    continue
+                m, v = state[id(p)]
+                m.mul_(b1).add_(p.grad, alpha=1 - b1)
+                v.mul_(b2).addcmul_(p.grad, p.grad, value=1 - b2)
+                wn = p.norm().clamp(0, clamp)
+                u = m / (v.sqrt() + eps) + wd * p
+                un = u.norm()
+                trust = torch.where((wn > 0) & (un > 0), wn / un, torch.ones_like(wn))
+                p.add_(u * (-lr * bc * trust))
 
         def step():
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 out = model(input_ids=ids, attention_mask=am, token_type_ids=tt, labels=labels,
                             sentence_order_label=sop)
             out.loss.backward()
+            if args.with_optimizer:
+                torch.nn.utils.clip_grad_norm_(params, 1.0)
+                eager_lamb()
+                model.zero_grad(set_to_none=False)
             return out.loss
 
     for _ in range(args.warmup):

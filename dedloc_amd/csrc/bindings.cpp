@@ -65,7 +65,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_fwd(const a
 }
 
 at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Tensor& gamma, const at::Tensor& mean,
-                         const at::Tensor& rstd, at::Tensor dgamma, at::Tensor dbeta, bool accumulate) {
+                         const at::Tensor& rstd, at::Tensor dgamma, at::Tensor dbeta, bool accumulate,
+                         const c10::optional<at::Tensor>& dsum) {
   expect(dy, at::kBFloat16, "dy");
   expect(s, at::kBFloat16, "s");
   expect(dgamma, at::kFloat, "dgamma");
@@ -77,7 +78,13 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Te
     dgamma.zero_();
     dbeta.zero_();
   }
-  check(dl_layernorm_bwd(cbf(dy), cbf(s), f32(gamma), f32(mean), f32(rstd), bf(ds), f32(dgamma), f32(dbeta),
+  float* dsp = nullptr;
+  if (dsum.has_value()) {
+    expect(*dsum, at::kFloat, "dsum");
+    TORCH_CHECK(dsum->numel() == D, "dsum size mismatch");
+    dsp = f32(*dsum);
+  }
+  check(dl_layernorm_bwd(cbf(dy), cbf(s), f32(gamma), f32(mean), f32(rstd), bf(ds), f32(dgamma), f32(dbeta), dsp,
                          (int)rows, (int)D, nparts, cur_stream(dy)),
         "layernorm_bwd");
   return ds;
@@ -91,10 +98,18 @@ at::Tensor gelu_fwd(const at::Tensor& h) {
   return y;
 }
 
-at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& h) {
+at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& h, const c10::optional<at::Tensor>& dbias) {
   expect(dy, at::kBFloat16, "dy");
   expect(h, at::kBFloat16, "h");
   auto dh = at::empty_like(h);
+  if (dbias.has_value()) {  // fused bias gradient of the producing Linear (accumulating)
+    expect(*dbias, at::kFloat, "dbias");
+    const int64_t N = h.size(-1);
+    TORCH_CHECK(dbias->numel() == N, "dbias size mismatch");
+    check(dl_gelu_bwd_colsum(cbf(dy), cbf(h), bf(dh), f32(*dbias), (int)(h.numel() / N), (int)N, cur_stream(h)),
+          "gelu_bwd(colsum)");
+    return dh;
+  }
   check(dl_gelu_bwd(cbf(dy), cbf(h), bf(dh), h.numel(), cur_stream(h)), "gelu_bwd");
   return dh;
 }

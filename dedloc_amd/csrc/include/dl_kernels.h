@@ -12,11 +12,13 @@ typedef uint16_t bf16_t;
 int dl_layernorm_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y,
                      bf16_t* s_out, float* mean, float* rstd, int rows, int D, float eps, hipStream_t st);
 int dl_layernorm_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-                     bf16_t* ds, float* dg_part, float* db_part, int rows, int D, int nparts, hipStream_t st);
+                     bf16_t* ds, float* dg_part, float* db_part, float* dsum, int rows, int D, int nparts,
+                     hipStream_t st);
 
 // elementwise.hip
 int dl_gelu_fwd(const bf16_t* h, bf16_t* y, size_t n, hipStream_t st);
 int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStream_t st);
+int dl_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* h, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st);
 int dl_tanh_fwd(const bf16_t* x, bf16_t* y, size_t n, hipStream_t st);
 int dl_tanh_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, size_t n, hipStream_t st);
 int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hipStream_t st);

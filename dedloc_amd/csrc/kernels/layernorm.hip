@@ -82,12 +82,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ ds,
                                                      float* __restrict__ dgamma_part, float* __restrict__ dbeta_part,
-                                                     int rows, int rows_per_block) {
+                                                     float* __restrict__ dsum, int rows, int rows_per_block) {
   using C = RowCfg<D>;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  float g[C::EPL], dg[C::EPL], db[C::EPL];
+  float g[C::EPL], dg[C::EPL], db[C::EPL], dx[C::EPL];
 #pragma unroll
   for (int i = 0; i < C::NV; ++i)
 #pragma unroll
@@ -95,6 +95,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       g[i * C::VW + j] = gamma[col_of<D>(lane, i) + j];
       dg[i * C::VW + j] = 0.f;
       db[i * C::VW + j] = 0.f;
+      dx[i * C::VW + j] = 0.f;
     }
   for (int row = r0 + wid; row < r1; row += nw) {
     const size_t base = (size_t)row * D;
@@ -118,11 +119,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
     a = wave_sum(a) * (1.f / D);
     b = wave_sum(b) * (1.f / D);
 #pragma unroll
-    for (int i = 0; i < C::EPL; ++i) gy[i] = rstd * (gy[i] - a - xh[i] * b);
+    for (int i = 0; i < C::EPL; ++i) {
+      gy[i] = bf2f(f2bf(rstd * (gy[i] - a - xh[i] * b)));
+      dx[i] += gy[i];
+    }
 #pragma unroll
     for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(ds + base + col_of<D>(lane, i), gy + i * C::VW);
   }
-  // reduce the per-wave column partials through LDS: nw x D floats
+  // reduce the per-wave column partials through LDS: 3 x nw x D floats
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #pragma unroll
   for (int i = 0; i < C::NV; ++i)
@@ -131,14 +135,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       const int c = col_of<D>(lane, i) + j;
       lds[wid * D + c] = dg[i * C::VW + j];
       lds[(nw + wid) * D + c] = db[i * C::VW + j];
+      lds[(2 * nw + wid) * D + c] = dx[i * C::VW + j];
     }
   __syncthreads();
-  // one fp32 atomic per column per block straight into the (accumulating) gradient buffers
+  // one fp32 atomic per column per block straight into the (accumulating) gradient buffers;
+  // dsum = column sum of ds = the bias gradient of the Linear that produced the LN input
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float sg = 0.f, sb = 0.f;
-    for (int w = 0; w < nw; ++w) { sg += lds[w * D + c]; sb += lds[(nw + w) * D + c]; }
+    float sg = 0.f, sb = 0.f, sx = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      sg += lds[w * D + c];
+      sb += lds[(nw + w) * D + c];
+      sx += lds[(2 * nw + w) * D + c];
+    }
     atomicAdd(&dgamma_part[c], sg);
     atomicAdd(&dbeta_part[c], sb);
+    if (dsum) atomicAdd(&dsum[c], sx);
   }
 }
 
@@ -157,11 +168,11 @@ void launch_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const floa
 
 template <int D>
 void launch_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-                bf16_t* ds, float* dg_part, float* db_part, int rows, int nparts, hipStream_t st) {
+                bf16_t* ds, float* dg_part, float* db_part, float* dsum, int rows, int nparts, hipStream_t st) {
   const int wpb = 4;
   const int rpb = (rows + nparts - 1) / nparts;
-  size_t lds = (size_t)2 * wpb * D * sizeof(float);
-  ln_bwd_kernel<D><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, rpb);
+  size_t lds = (size_t)3 * wpb * D * sizeof(float);
+  ln_bwd_kernel<D><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
 }
 
 }  // namespace
@@ -182,13 +193,14 @@ int dl_layernorm_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const
 }
 
 int dl_layernorm_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-                     bf16_t* ds, float* dg_part, float* db_part, int rows, int D, int nparts, hipStream_t st) {
+                     bf16_t* ds, float* dg_part, float* db_part, float* dsum, int rows, int D, int nparts,
+                     hipStream_t st) {
   switch (D) {
-    case 128: launch_bwd<128>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
-    case 256: launch_bwd<256>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
-    case 512: launch_bwd<512>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
-    case 768: launch_bwd<768>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
-    case 1024: launch_bwd<1024>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, rows, nparts, st); break;
+    case 128: launch_bwd<128>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
+    case 256: launch_bwd<256>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
+    case 512: launch_bwd<512>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
+    case 768: launch_bwd<768>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
+    case 1024: launch_bwd<1024>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
     default: return -1;
   }
   return 0;

@@ -132,19 +132,17 @@ class _AlbertLayerFn(torch.autograd.Function):
         h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2 = ctx.saved_tensors
         lv = ctx.lv
         dy = dy.contiguous()
-        ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True)
+        # LN backward also accumulates colsum(ds) = the bias grad of the Linear that fed it
+        ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True, lv["gb2"])
         O.gemm_acc_f32(ds2, g, lv["gw2"], True, False)
-        O.bias_grad(ds2, lv["gb2"], True)
         dg = O.gemm(ds2, lv["w2"], None, None, False, False, 0)
-        df = O.gelu_bwd(dg, f)
+        df = O.gelu_bwd(dg, f, lv["gb1"])  # gelu' fused with the ffn bias gradient
         del dg
         O.gemm_acc_f32(df, h1, lv["gw1"], True, False)
-        O.bias_grad(df, lv["gb1"], True)
         dh1 = O.gemm(df, lv["w1"], None, ds2, False, False, 0)  # residual branch folded in
         del df
-        ds1 = O.layernorm_bwd(dh1, s1, lv["ln1g"], m1, r1, lv["gln1g"], lv["gln1b"], True)
+        ds1 = O.layernorm_bwd(dh1, s1, lv["ln1g"], m1, r1, lv["gln1g"], lv["gln1b"], True, lv["gbo"])
         O.gemm_acc_f32(ds1, att, lv["gwo"], True, False)
-        O.bias_grad(ds1, lv["gbo"], True)
         datt = O.gemm(ds1, lv["wo"], None, None, False, False, 0)
         H = ctx.H
         dqkv = O.attn_bwd(qkv, ctx.mbias, att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)))

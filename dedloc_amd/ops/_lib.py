@@ -19,9 +19,9 @@ LIB = torch.library.Library("dedloc", "DEF")
 
 _SCHEMAS = [
     "layernorm_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
-    "layernorm_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, Tensor(a!) dgamma, Tensor(b!) dbeta, bool accumulate) -> Tensor",
+    "layernorm_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd, Tensor(a!) dgamma, Tensor(b!) dbeta, bool accumulate, Tensor(c!)? dsum=None) -> Tensor",
     "gelu_fwd(Tensor h) -> Tensor",
-    "gelu_bwd(Tensor dy, Tensor h) -> Tensor",
+    "gelu_bwd(Tensor dy, Tensor h, Tensor(a!)? dbias=None) -> Tensor",
     "tanh_fwd(Tensor x) -> Tensor",
     "tanh_bwd(Tensor dy, Tensor y) -> Tensor",
     "bias_grad(Tensor dy, Tensor(a!) dbias, bool accumulate) -> ()",
@@ -103,7 +103,7 @@ def _ln_fwd_cpu(x, res, gamma, beta, eps):
 
 
 @_impl("layernorm_bwd")
-def _ln_bwd_cpu(dy, s, gamma, mean, rstd, dgamma, dbeta, accumulate):
+def _ln_bwd_cpu(dy, s, gamma, mean, rstd, dgamma, dbeta, accumulate, dsum=None):
     D = dy.shape[-1]
     g = dy.float().reshape(-1, D)
     xh = (s.float().reshape(-1, D) - mean.unsqueeze(-1)) * rstd.unsqueeze(-1)
@@ -118,8 +118,10 @@ def _ln_bwd_cpu(dy, s, gamma, mean, rstd, dgamma, dbeta, accumulate):
     gy = g * gamma
     a = gy.mean(-1, keepdim=True)
     b = (gy * xh).mean(-1, keepdim=True)
-    ds = rstd.unsqueeze(-1) * (gy - a - xh * b)
-    return _bf(ds).reshape(dy.shape)
+    ds = _bf(rstd.unsqueeze(-1) * (gy - a - xh * b))
+    if dsum is not None:
+        dsum.add_(ds.float().sum(0))
+    return ds.reshape(dy.shape)
 
 
 def _gelu_tanh(x):
@@ -132,13 +134,16 @@ def _gelu_fwd_cpu(h):
 
 
 @_impl("gelu_bwd")
-def _gelu_bwd_cpu(dy, h):
+def _gelu_bwd_cpu(dy, h, dbias=None):
     x = h.float()
     k0, k1 = math.sqrt(2.0 / math.pi), 0.044715
     u = k0 * (x + k1 * x ** 3)
     t = torch.tanh(u)
     d = 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
-    return _bf(dy.float() * d)
+    dh = _bf(dy.float() * d)
+    if dbias is not None:
+        dbias.add_(dh.float().reshape(-1, dh.shape[-1]).sum(0))
+    return dh
 
 
 @_impl("tanh_fwd")

@@ -144,6 +144,11 @@ class CollaborativeOptimizer:
         with self.lock_step:
             res = self.averager.load_state_from_peers(**kwargs)
             if res is None:
+                # nobody shares state: keep our parameters but adopt the collaboration's step, otherwise
+                # an out-of-sync peer would retry forever without contributing
+                if self.local_step < self.collaboration_state.optimizer_step:
+                    self.local_step = self.collaboration_state.optimizer_step
+                    self.update_scheduler()
                 logger.log(self.status_loglevel, "no peers to load state from; keeping local state")
                 return False
             meta, tensors = res
@@ -217,7 +222,8 @@ class CollaborativeOptimizer:
                 mean_samples = self.target_batch_size / cs.num_peers
                 weight = self.local_samples_accumulated / mean_samples
                 group = self.averager.step(weight=weight, timeout=self.averaging_timeout,
-                                           expected_group_size=cs.num_peers)
+                                           expected_group_size=cs.num_peers + self._num_aux(),
+                                           gather={"step": int(self.local_step)})
                 self.stats["averaging_rounds"] += 1
                 if group is None:
                     self.stats["averaging_failed"] += 1
@@ -239,22 +245,42 @@ class CollaborativeOptimizer:
         return group
 
     def step_aux(self, **kwargs):
-        """Auxiliary peer: join the averaging rounds as a reducer only (run_aux.py:260-262)."""
+        """Auxiliary peer: join the averaging rounds as a reducer only (run_aux.py:260-262).
+
+        Like hivemind, an auxiliary peer never publishes training progress (it must not move the
+        collaboration's global step or ETA); it announces itself under ``{prefix}_aux`` so that
+        trainers wait for it during matchmaking, and it adopts the step gathered from its group.
+        """
+        self._announce_aux()
         if not self.collaboration_state.ready_for_step:
-            self.should_report_progress.set()
             return None
         self.collaboration_state = self.fetch_collaboration_state()
         self.collaboration_state_updated.set()
         with self.lock_collaboration_state, self.lock_step:
-            group = None
-            if self.collaboration_state.num_peers > 1:
+            group, current = None, max(self.local_step, self.collaboration_state.optimizer_step)
+            if self.collaboration_state.num_peers >= 1:
                 group = self.averager.step(weight=0.0, timeout=self.averaging_timeout,
-                                           expected_group_size=self.collaboration_state.num_peers)
-            self.collaboration_state.register_step(self.local_step + 1)
-            self.local_step += 1
+                                           expected_group_size=self.collaboration_state.num_peers + self._num_aux())
+                if group is not None:
+                    steps = [g.get("step") for g in group["gathered"] if isinstance(g.get("step"), int)]
+                    current = max([current] + steps)
+            self.collaboration_state.register_step(current + 1)
+            self.local_step = current + 1
             self.last_group = group
-            self.should_report_progress.set()
         return group
+
+    def _announce_aux(self):
+        now = get_dht_time()
+        if now - getattr(self, "_last_aux_announce", 0.0) > self.metadata_expiration / 3:
+            self._last_aux_announce = now
+            self.dht.store(f"{self.prefix}_aux", True, now + self.metadata_expiration, subkey=self.peer_id,
+                           return_future=True)
+
+    def _num_aux(self) -> int:
+        rec = self.dht.get(f"{self.prefix}_aux", latest=True)
+        if rec is None or not isinstance(rec.value, dict):
+            return 0
+        return sum(1 for k, v in rec.value.items() if v.value is True and k != self.peer_id)
 
     # ------------------------------------------------------------------ background threads
     def _report_loop(self):
@@ -263,7 +289,8 @@ class CollaborativeOptimizer:
             self.should_report_progress.clear()
             if self._stop.is_set():
                 break
-            self.report_training_progress()
+            if not self.auxiliary:
+                self.report_training_progress()
 
     def report_training_progress(self):
         with self.lock_local_progress:
