@@ -307,9 +307,57 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
 // (bf16 in, fp32 accumulate; the fp32-accumulating form writes straight into the fp32 gradient
 // buffer with beta=1 so the shared ALBERT layer's 24 weight-gradient contributions never round
 // through bf16.)
+// The dedloc MFMA kernel (gemm.hip) handles every layer GEMM of the model; shapes it does not
+// cover (odd vocabulary sizes, tiny pooler/classifier GEMMs) use hipBLASLt.  DEDLOC_GEMM=lib
+// forces the library for A/B measurements.
+bool use_mfma_gemm() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DEDLOC_GEMM");
+    v = (e && std::string(e) == "lib") ? 0 : 1;
+  }
+  return v == 1;
+}
+
+struct Mat {  // (rows, k) operand view: K-inner means element (r, k) at p[r*ld + k]
+  const at::Tensor& t;
+  bool kouter;
+  int64_t rows, k, ld;
+};
+
+// op(a) is [M, K]; trans_a=False -> a is [M,K] K-inner; trans_a=True -> a is [K,M] (K-outer)
+inline Mat a_view(const at::Tensor& a, bool trans_a) {
+  return trans_a ? Mat{a, true, a.size(1), a.size(0), a.stride(0)} : Mat{a, false, a.size(0), a.size(1), a.stride(0)};
+}
+// op(b) is [K, N]; trans_b=True -> b is [N,K] (K-inner); trans_b=False -> b is [K,N] (K-outer)
+inline Mat b_view(const at::Tensor& b, bool trans_b) {
+  return trans_b ? Mat{b, false, b.size(0), b.size(1), b.stride(0)} : Mat{b, true, b.size(1), b.size(0), b.stride(0)};
+}
+
+inline bool mfma_ok(const at::Tensor& a, const at::Tensor& b) {
+  return use_mfma_gemm() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
+         a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1;
+}
+
+inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias) {
+  if (!bias.has_value()) return at::Tensor();
+  return bias->scalar_type() == at::kFloat ? bias->contiguous() : bias->to(at::kFloat).contiguous();
+}
+
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& residual, bool trans_a, bool trans_b, int64_t epilogue) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm operands must be GPU tensors");
+  if (mfma_ok(a, b) && epilogue == 0 && (!residual.has_value() || residual->is_contiguous())) {
+    const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
+    TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
+    auto c = at::empty({A.rows, B.rows}, a.options());
+    const at::Tensor bf = f32_bias(bias);
+    const int rc = dl_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
+                           bf(c), B.rows, nullptr, 0, bf.defined() ? f32(bf) : nullptr,
+                           residual.has_value() ? cbf(*residual) : nullptr, B.rows, nullptr, 0, nullptr, 1,
+                           cur_stream(a));
+    if (rc == 0) return c;
+  }
   const at::Tensor A = trans_a ? a.t() : a;
   const at::Tensor B = trans_b ? b.t() : b;
   at::Tensor c;
@@ -320,6 +368,7 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
   } else {
     c = bias.has_value() ? at::addmm(bias->to(a.scalar_type()), A, B) : at::mm(A, B);
   }
+  if (!c.is_contiguous()) c = c.contiguous();
   if (epilogue == 1) {
     TORCH_CHECK(c.is_contiguous(), "gemm output must be contiguous");
     check(dl_gelu_fwd(cbf(c), bf(c), c.numel(), cur_stream(c)), "gemm gelu epilogue");
@@ -329,9 +378,55 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
 
 void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b) {
   expect(c, at::kFloat, "c");
+  if (mfma_ok(a, b)) {
+    const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
+    TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
+    // split the reduction so that at least ~2 workgroups per CU exist (wgrad: few output tiles,
+    // very long token reduction); splits accumulate with fp32 atomics
+    const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(A.k / 1024, (512 + tiles - 1) / tiles));
+    const int rc = dl_gemm(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
+                           nullptr, 0, f32(c), c.stride(0), nullptr, nullptr, 0, nullptr, 0, nullptr, splits,
+                           cur_stream(a));
+    if (rc == 0) return;
+  }
   const at::Tensor A = trans_a ? a.t() : a;
   const at::Tensor B = trans_b ? b.t() : b;
   at::_ops::addmm_dtype_out::call(c, A, B, at::kFloat, 1, 1, c);
+}
+
+// fused FFN-up: H = x W^T + b (pre-activation, kept for backward), G = gelu_new(H)
+std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias) {
+  auto H = at::empty({x.size(0), w.size(0)}, x.options());
+  auto G = at::empty_like(H);
+  if (mfma_ok(x, w)) {
+    const at::Tensor bf = f32_bias(bias);
+    const int rc = dl_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0),
+                           (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bf), nullptr, 0, bf(H), H.size(1), nullptr,
+                           1, cur_stream(x));
+    if (rc == 0) return {H, G};
+  }
+  H = at::addmm(bias.to(x.scalar_type()), x, w.t()).contiguous();
+  check(dl_gelu_fwd(cbf(H), bf(G), H.numel(), cur_stream(H)), "gelu_fwd");
+  return {H, G};
+}
+
+// fused FFN dgrad: C = (dy W) * gelu_new'(F), dbias += colsum(C)
+at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& F, at::Tensor dbias) {
+  expect(F, at::kBFloat16, "F");
+  expect(dbias, at::kFloat, "dbias");
+  if (mfma_ok(dy, w)) {
+    auto C = at::empty({dy.size(0), w.size(1)}, dy.options());
+    const int rc = dl_gemm(0, 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0), (int)w.size(1),
+                           (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0,
+                           f32(dbias), 1, cur_stream(dy));
+    if (rc == 0) return C;
+  }
+  auto dg = at::mm(dy, w).contiguous();
+  auto dh = at::empty_like(dg);
+  check(dl_gelu_bwd_colsum(cbf(dg), cbf(F), bf(dh), f32(dbias), (int)dg.size(0), (int)dg.size(1), cur_stream(dg)),
+        "gelu_bwd");
+  return dh;
 }
 
 }  // namespace
@@ -359,6 +454,8 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("gemm", &gemm);
   m.impl("gemm_acc_f32", &gemm_acc_f32);
+  m.impl("gemm_gelu", &gemm_gelu);
+  m.impl("gemm_dgelu", &gemm_dgelu);
 }
 
 // a tiny C entry point so that the loader can verify the library really is the gfx950 build

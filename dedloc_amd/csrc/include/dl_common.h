@@ -75,18 +75,24 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return r;
 }
 
+// tanh through one v_exp_f32 (libm tanhf is a long VALU sequence): 1 - 2 / (1 + e^{2u});
+// saturates correctly at +-inf and is accurate to ~1e-7 relative, far below bf16 resolution.
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f / (1.f + __builtin_amdgcn_exp2f(2.8853900817779268f * u));
+}
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   // gelu_new (HF ALBERT): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return 0.5f * x * (1.f + fast_tanh(u));
 }
 
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float x2 = x * x;
   float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
+  float t = fast_tanh(u);
   float du = k0 * (1.f + 3.f * k1 * x2);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
 }

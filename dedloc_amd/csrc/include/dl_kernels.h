@@ -55,6 +55,11 @@ int dl_embed_bwd(const bf16_t* ds, const long* ids, const long* tt, float* dwemb
 int dl_xent_fwd_bwd(const bf16_t* logits, const long* labels, bf16_t* dlogits, float* row_loss, float* loss_out,
                     float* scale_buf, int M, int V, long ld, int ignore_index, hipStream_t st);
 
+// gemm.hip  (epi: 0 store(+bias,+residual), 1 bias+gelu (H and gelu(H)), 2 dgelu(+colsum), 3 fp32 +=)
+int dl_gemm(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N,
+            int K, bf16_t* C, long ldc, float* Cf, long ldcf, const float* bias, const bf16_t* R, long ldr, bf16_t* H,
+            long ldh, float* dbias, int splits, hipStream_t st);
+
 // attention.hip
 int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, bf16_t* out, long ldo, float* lse, int B, int H, int S,
                 int D, float scale, hipStream_t st);

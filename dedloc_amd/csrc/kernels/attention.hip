@@ -75,26 +75,24 @@ __device__ __forceinline__ bf16x8 pack_acc(const floatx16& x, int s) {
 
 __device__ __forceinline__ bf16x8 gload8(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// cooperative 64-row x 64-col tile stage: 256 threads, 2 x 16 B each
-struct TileRegs { uint4 v[2]; };
+// cooperative 64-row x 64-col tile stage: 256 threads, 2 x 16 B each (two named registers —
+// an indexed array of uint4 was demoted to scratch by hipcc)
+struct TileRegs { uint4 a, b; };
+
+__device__ __forceinline__ uint4 tile_ld1(const bf16_t* g, long ld, int row0, int rows_valid, int idx) {
+  const int row = min(row0 + (idx >> 3), rows_valid - 1);
+  return *reinterpret_cast<const uint4*>(g + (long)row * ld + (idx & 7) * 8);
+}
 
 __device__ __forceinline__ void tile_load(TileRegs& t, const bf16_t* g, long ld, int row0, int rows_valid) {
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int idx = threadIdx.x + 256 * k;
-    int row = idx >> 3;
-    const int c = idx & 7;
-    row = min(row0 + row, rows_valid - 1);
-    t.v[k] = *reinterpret_cast<const uint4*>(g + (long)row * ld + c * 8);
-  }
+  t.a = tile_ld1(g, ld, row0, rows_valid, threadIdx.x);
+  t.b = tile_ld1(g, ld, row0, rows_valid, threadIdx.x + 256);
 }
 
 __device__ __forceinline__ void tile_store(const TileRegs& t, uint8_t* tile) {
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int idx = threadIdx.x + 256 * k;
-    *reinterpret_cast<uint4*>(tile + chunk_off(idx >> 3, idx & 7)) = t.v[k];
-  }
+  const int i0 = threadIdx.x, i1 = threadIdx.x + 256;
+  *reinterpret_cast<uint4*>(tile + chunk_off(i0 >> 3, i0 & 7)) = t.a;
+  *reinterpret_cast<uint4*>(tile + chunk_off(i1 >> 3, i1 & 7)) = t.b;
 }
 
 // store 4 consecutive bf16 (8 bytes)
@@ -172,13 +170,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
     float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(s[j][i] - mn);
+        const float p = __builtin_amdgcn_exp2f(s[j][i] - mn);
         s[j][i] = p;
         rs += p;
       }
@@ -293,7 +291,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(st[i] * sl2 + mb[32 * j + crow(i, hh)] - l2);
+        const float p = __builtin_amdgcn_exp2f(st[i] * sl2 + mb[32 * j + crow(i, hh)] - l2);
         st[i] = p * (dp[i] - dl);
       }
 #pragma unroll
@@ -394,7 +392,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qq = 32 * i2 + crow(i, hh);
-        const float p = exp2f(s[i] * sl2 + mbk - lse_s[qq]);
+        const float p = __builtin_amdgcn_exp2f(s[i] * sl2 + mbk - lse_s[qq]);
         s[i] = p;
         dp[i] = p * (dp[i] - del_s[qq]);
       }

@@ -36,49 +36,66 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// gelu_new backward fused with the bias gradient of the producing Linear: dh = dy * gelu'(h) and
-// dbias[c] += sum_rows dh[:, c].  Block (px, py) owns 8*blockDim columns x rpb rows.
-__global__ __launch_bounds__(128) void gelu_bwd_colsum_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
-                                                              bf16_t* __restrict__ dh, float* __restrict__ dbias,
-                                                              int rows, int N, int rpb) {
-  const int c0 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (c0 >= N) return;
+// Column sums over a [rows, N] bf16 matrix, optionally fused with gelu_new backward
+// (GELU: dh = dy * gelu'(h) is written out and summed).  Block = 4 waves x (64 lanes x 8 columns):
+// 512 columns x rpb rows; wave w takes rows w, w+4, ... with 4 rows of 16-byte loads in flight per
+// lane.  The 4 wave partials meet in LDS and leave as lane-contiguous fp32 atomics (256 B per wave
+// instruction, Guideline 12) — one atomic per column per block.
+template <bool GELU>
+__global__ __launch_bounds__(256) void colsum_tile_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ h,
+                                                          bf16_t* __restrict__ dh, float* __restrict__ out, int rows,
+                                                          int N, int rpb) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cb = blockIdx.x * 512;
+  const int c0 = cb + lane * 8;
+  const bool active = c0 < N;
   const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int r = r0;
-  for (; r + 4 <= r1; r += 4) {
-    uint4 gr[4], hr[4];
+  if (active) {
+    int r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      uint4 xr[4], hr[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      gr[u] = *reinterpret_cast<const uint4*>(dy + (size_t)(r + u) * N + c0);
-      hr[u] = *reinterpret_cast<const uint4*>(h + (size_t)(r + u) * N + c0);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float g[8], v[8];
-      load_bf16<8>(reinterpret_cast<const bf16_t*>(&gr[u]), g);
-      load_bf16<8>(reinterpret_cast<const bf16_t*>(&hr[u]), v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
-        acc[j] += g[j];
+      for (int u = 0; u < 4; ++u) {
+        xr[u] = *reinterpret_cast<const uint4*>(x + (size_t)(r + 4 * u) * N + c0);
+        if (GELU) hr[u] = *reinterpret_cast<const uint4*>(h + (size_t)(r + 4 * u) * N + c0);
       }
-      store_bf16<8>(dh + (size_t)(r + u) * N + c0, g);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float g[8];
+        load_bf16<8>(reinterpret_cast<const bf16_t*>(&xr[u]), g);
+        if (GELU) {
+          float v[8];
+          load_bf16<8>(reinterpret_cast<const bf16_t*>(&hr[u]), v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
+          store_bf16<8>(dh + (size_t)(r + 4 * u) * N + c0, g);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += g[j];
+      }
+    }
+    for (; r < r1; r += 4) {
+      float g[8];
+      load_bf16<8>(x + (size_t)r * N + c0, g);
+      if (GELU) {
+        float v[8];
+        load_bf16<8>(h + (size_t)r * N + c0, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
+        store_bf16<8>(dh + (size_t)r * N + c0, g);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += g[j];
     }
   }
-  for (; r < r1; ++r) {
-    float g[8], v[8];
-    load_bf16<8>(dy + (size_t)r * N + c0, g);
-    load_bf16<8>(h + (size_t)r * N + c0, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
-      acc[j] += g[j];
-    }
-    store_bf16<8>(dh + (size_t)r * N + c0, g);
+  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    if (cb + c < N) atomicAdd(&out[cb + c], red[0][c] + red[1][c] + red[2][c] + red[3][c]);
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) atomicAdd(&dbias[c0 + j], acc[j]);
 }
 
 __global__ __launch_bounds__(256) void tanh_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
@@ -183,9 +200,9 @@ int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStre
 
 int dl_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* h, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st) {
   if (N % 8) return -1;
-  const int rpb = 32;
-  dim3 grid((N / 8 + 127) / 128, (rows + rpb - 1) / rpb);
-  gelu_bwd_colsum_kernel<<<grid, 128, 0, st>>>(dy, h, dh, dbias, rows, N, rpb);
+  const int rpb = 256;
+  dim3 grid((N + 511) / 512, (rows + rpb - 1) / rpb);
+  colsum_tile_kernel<true><<<grid, 256, 0, st>>>(dy, h, dh, dbias, rows, N, rpb);
   return 0;
 }
 
@@ -206,8 +223,10 @@ int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hi
     colsum_bf16_scalar_kernel<<<dim3((N + 255) / 256, nparts), 256, 0, st>>>(x, part, rows, N, rpb);
     return 0;
   }
-  dim3 grid((N / 8 + 127) / 128, nparts);
-  colsum_bf16_kernel<<<grid, 128, 0, st>>>(x, part, rows, N, rpb);
+  const int rpb2 = 256;
+  dim3 grid((N + 511) / 512, (rows + rpb2 - 1) / rpb2);
+  colsum_tile_kernel<false><<<grid, 256, 0, st>>>(x, nullptr, nullptr, part, rows, N, rpb2);
+  (void)rpb;
   return 0;
 }
 

@@ -114,13 +114,12 @@ class _AlbertLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, mbias, lv, H, S, eps):
         O = ops.OPS
-        qkv = O.gemm(h, lv["wqkv"], lv["bqkv"], None, False, True, 0)
+        qkv = O.gemm(h, lv["wqkv"], lv["bqkv32"], None, False, True, 0)
         att, lse = O.attn_fwd(qkv, mbias, H, S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)))
-        a = O.gemm(att, lv["wo"], lv["bo"], None, False, True, 0)
+        a = O.gemm(att, lv["wo"], lv["bo32"], None, False, True, 0)
         h1, s1, m1, r1 = O.layernorm_fwd(a, h, lv["ln1g"], lv["ln1b"], eps)
-        f = O.gemm(h1, lv["w1"], lv["b1"], None, False, True, 0)
-        g = O.gelu_fwd(f)
-        f2 = O.gemm(g, lv["w2"], lv["b2"], None, False, True, 0)
+        f, g = O.gemm_gelu(h1, lv["w1"], lv["b132"])  # bias + gelu_new fused in the GEMM epilogue
+        f2 = O.gemm(g, lv["w2"], lv["b232"], None, False, True, 0)
         out, s2, m2, r2 = O.layernorm_fwd(f2, h1, lv["ln2g"], lv["ln2b"], eps)
         ctx.save_for_backward(h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2)
         ctx.lv, ctx.mbias, ctx.H, ctx.S = lv, mbias, H, S
@@ -135,9 +134,7 @@ class _AlbertLayerFn(torch.autograd.Function):
         # LN backward also accumulates colsum(ds) = the bias grad of the Linear that fed it
         ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True, lv["gb2"])
         O.gemm_acc_f32(ds2, g, lv["gw2"], True, False)
-        dg = O.gemm(ds2, lv["w2"], None, None, False, False, 0)
-        df = O.gelu_bwd(dg, f, lv["gb1"])  # gelu' fused with the ffn bias gradient
-        del dg
+        df = O.gemm_dgelu(ds2, lv["w2"], f, lv["gb1"])  # dgrad * gelu'(f) + ffn bias grad, one kernel
         O.gemm_acc_f32(df, h1, lv["gw1"], True, False)
         dh1 = O.gemm(df, lv["w1"], None, ds2, False, False, 0)  # residual branch folded in
         del df
@@ -294,6 +291,8 @@ class AlbertForPreTraining(nn.Module):
             wqkv=f.span(f.bf16, pre + "attention.query.weight", pre + "attention.value.weight", (3 * H, H)),
             gwqkv=f.span(f.grad, pre + "attention.query.weight", pre + "attention.value.weight", (3 * H, H)),
             bqkv=f.span(f.bf16, pre + "attention.query.bias", pre + "attention.value.bias", (3 * H,)),
+            bqkv32=f.span(f.fp32, pre + "attention.query.bias", pre + "attention.value.bias", (3 * H,)),
+            bo32=f.p(pre + "attention.dense.bias"), b132=f.p(pre + "ffn.bias"), b232=f.p(pre + "ffn_output.bias"),
             gbqkv=f.span(f.grad, pre + "attention.query.bias", pre + "attention.value.bias", (3 * H,)),
             wo=f.w(pre + "attention.dense.weight"), gwo=f.g(pre + "attention.dense.weight"),
             bo=f.w(pre + "attention.dense.bias"), gbo=f.g(pre + "attention.dense.bias"),

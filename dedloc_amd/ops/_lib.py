@@ -40,6 +40,8 @@ _SCHEMAS = [
     "attn_bwd(Tensor qkv, Tensor? mbias, Tensor out, Tensor dout, Tensor lse, int H, int S, float scale) -> Tensor",
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
+    "gemm_gelu(Tensor x, Tensor w, Tensor bias) -> (Tensor, Tensor)",
+    "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias) -> Tensor",
 ]
 for _s in _SCHEMAS:
     LIB.define(_s)
@@ -362,6 +364,18 @@ def _gemm_cpu(a, b, bias, residual, trans_a, trans_b, epilogue):
     if epilogue == 1:
         c = _gelu_tanh(c)
     return _bf(c)
+
+
+@_impl("gemm_gelu")
+def _gemm_gelu_cpu(x, w, bias):
+    h = _bf(x.float() @ w.float().t() + bias.float())
+    return h, _bf(_gelu_tanh(h.float()))
+
+
+@_impl("gemm_dgelu")
+def _gemm_dgelu_cpu(dy, w, F, dbias):
+    dg = _bf(dy.float() @ w.float())
+    return _gelu_bwd_cpu(dg, F, dbias)
 
 
 @_impl("gemm_acc_f32")

@@ -280,3 +280,52 @@ def test_albert_gpu_matches_cpu(cuda):
     oc["loss"].backward()
     og["loss"].backward()
     assert rel(m_gpu.flat.grad.cpu(), m_cpu.flat.grad) < 5e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (1000, 512, 256), (4096, 3072, 1024)])
+def test_mfma_gemm_nt_nn(cuda, M, N, K):
+    torch.manual_seed(5)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = torch.randn(N, K, device=cuda).bfloat16()
+    bias = torch.randn(N, device=cuda)
+    res = torch.randn(M, N, device=cuda).bfloat16()
+    ref = a.float() @ w.float().t() + bias
+    y = OPS.gemm(a, w, bias, None, False, True, 0)
+    assert rel(y, ref) < 1e-2
+    y = OPS.gemm(a, w, bias, res, False, True, 0)
+    assert rel(y, ref + res.float()) < 1e-2
+    # dgrad form: dy [M, N] @ w [N, K]  (B operand K-outer)
+    dy = torch.randn(M, N, device=cuda).bfloat16()
+    dx = OPS.gemm(dy, w, None, None, False, False, 0)
+    assert rel(dx, dy.float() @ w.float()) < 1e-2
+
+
+@pytest.mark.parametrize("T,N,K", [(2048, 256, 256), (8192, 1024, 512)])
+def test_mfma_gemm_wgrad_splitk(cuda, T, N, K):
+    torch.manual_seed(6)
+    dy = torch.randn(T, N, device=cuda).bfloat16()
+    x = torch.randn(T, K, device=cuda).bfloat16()
+    g = torch.ones(N, K, device=cuda)
+    OPS.gemm_acc_f32(dy, x, g, True, False)
+    assert rel(g, 1 + dy.float().t() @ x.float()) < 1e-3
+
+
+def test_mfma_gemm_gelu_epilogues(cuda):
+    torch.manual_seed(7)
+    M, H, I = 1024, 256, 1024
+    x = torch.randn(M, H, device=cuda).bfloat16()
+    w1 = (torch.randn(I, H, device=cuda) * 0.1).bfloat16()
+    b1 = torch.randn(I, device=cuda)
+    f, g = OPS.gemm_gelu(x, w1, b1)
+    fr = x.float() @ w1.float().t() + b1
+    assert rel(f, fr) < 1e-2
+    assert rel(g, F.gelu(fr, approximate="tanh")) < 2e-2
+    w2 = (torch.randn(H, I, device=cuda) * 0.1).bfloat16()
+    ds = torch.randn(M, H, device=cuda).bfloat16()
+    db = torch.zeros(I, device=cuda)
+    df = OPS.gemm_dgelu(ds, w2, f, db)
+    fr2 = f.float().requires_grad_(True)
+    gr = F.gelu(fr2, approximate="tanh")
+    dref = torch.autograd.grad(gr, fr2, ds.float() @ w2.float())[0]
+    assert rel(df, dref) < 2e-2
+    assert rel(db, df.float().sum(0)) < 1e-3
