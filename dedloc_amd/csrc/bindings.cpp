@@ -351,9 +351,9 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
     const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
     TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
     auto c = at::empty({A.rows, B.rows}, a.options());
-    const at::Tensor bf = f32_bias(bias);
+    const at::Tensor bias32 = f32_bias(bias);
     const int rc = dl_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
-                           bf(c), B.rows, nullptr, 0, bf.defined() ? f32(bf) : nullptr,
+                           bf(c), B.rows, nullptr, 0, bias32.defined() ? f32(bias32) : nullptr,
                            residual.has_value() ? cbf(*residual) : nullptr, B.rows, nullptr, 0, nullptr, 1,
                            cur_stream(a));
     if (rc == 0) return c;
@@ -400,9 +400,9 @@ std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tens
   auto H = at::empty({x.size(0), w.size(0)}, x.options());
   auto G = at::empty_like(H);
   if (mfma_ok(x, w)) {
-    const at::Tensor bf = f32_bias(bias);
+    const at::Tensor bias32 = f32_bias(bias);
     const int rc = dl_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0),
-                           (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bf), nullptr, 0, bf(H), H.size(1), nullptr,
+                           (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1), nullptr,
                            1, cur_stream(x));
     if (rc == 0) return {H, G};
   }
