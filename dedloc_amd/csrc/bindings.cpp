@@ -307,17 +307,19 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
 // (bf16 in, fp32 accumulate; the fp32-accumulating form writes straight into the fp32 gradient
 // buffer with beta=1 so the shared ALBERT layer's 24 weight-gradient contributions never round
 // through bf16.)
-// The dedloc MFMA kernel (gemm.hip) handles every layer GEMM of the model; shapes it does not
-// cover (odd vocabulary sizes, tiny pooler/classifier GEMMs) use hipBLASLt.  DEDLOC_GEMM=lib
-// forces the library for A/B measurements.
-bool use_mfma_gemm() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("DEDLOC_GEMM");
-    v = (e && std::string(e) == "lib") ? 0 : 1;
-  }
-  return v == 1;
+// GEMM dispatch policy, chosen from measurements on MI355X (bench/gemm_bench.py, profiles/):
+//   * the dedloc MFMA kernel (gemm.hip) wins the weight-gradient GEMMs whose output has few
+//     256x256 tiles (split-K over the token dimension: 1024x1024 wgrad 168 us vs 198 us);
+//   * hipBLASLt currently wins the large forward/dgrad GEMMs (its deeper LDS-DMA pipeline reaches
+//     1.1-1.5 PF/s on these shapes vs ~0.6-0.95 for gemm.hip's register-staged loop), so they go
+//     to the library and the gelu / dgelu / bias-grad epilogues run as separate fused kernels.
+// DEDLOC_GEMM=mfma forces gemm.hip everywhere (correctness tests), =lib forces the library.
+int gemm_policy() {  // 0 auto, 1 mfma, 2 lib  (read per call: tests flip it at run time)
+  const char* e = std::getenv("DEDLOC_GEMM");
+  return !e ? 0 : (e[0] == 'm' ? 1 : (e[0] == 'l' ? 2 : 0));
 }
+bool use_mfma_gemm() { return gemm_policy() != 2; }
+bool force_mfma_gemm() { return gemm_policy() == 1; }
 
 struct Mat {  // (rows, k) operand view: K-inner means element (r, k) at p[r*ld + k]
   const at::Tensor& t;
@@ -347,7 +349,7 @@ inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias) {
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& residual, bool trans_a, bool trans_b, int64_t epilogue) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm operands must be GPU tensors");
-  if (mfma_ok(a, b) && epilogue == 0 && (!residual.has_value() || residual->is_contiguous())) {
+  if (force_mfma_gemm() && mfma_ok(a, b) && epilogue == 0 && (!residual.has_value() || residual->is_contiguous())) {
     const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
     TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
     auto c = at::empty({A.rows, B.rows}, a.options());
@@ -378,12 +380,14 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
 
 void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b) {
   expect(c, at::kFloat, "c");
-  if (mfma_ok(a, b)) {
-    const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
+  const Mat Av = a_view(a, trans_a), Bv = b_view(b, trans_b);
+  const int64_t ntiles = ((Av.rows + 255) / 256) * ((Bv.rows + 255) / 256);
+  if (mfma_ok(a, b) && (force_mfma_gemm() || ntiles <= 16)) {
+    const Mat A = Av, B = Bv;
     TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
     // split the reduction so that at least ~2 workgroups per CU exist (wgrad: few output tiles,
     // very long token reduction); splits accumulate with fp32 atomics
-    const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
+    const int64_t tiles = ntiles;
     int splits = (int)std::max<int64_t>(1, std::min<int64_t>(A.k / 1024, (512 + tiles - 1) / tiles));
     const int rc = dl_gemm(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
                            nullptr, 0, f32(c), c.stride(0), nullptr, nullptr, 0, nullptr, 0, nullptr, splits,
@@ -399,7 +403,7 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
 std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias) {
   auto H = at::empty({x.size(0), w.size(0)}, x.options());
   auto G = at::empty_like(H);
-  if (mfma_ok(x, w)) {
+  if (force_mfma_gemm() && mfma_ok(x, w)) {
     const at::Tensor bias32 = f32_bias(bias);
     const int rc = dl_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0),
                            (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1), nullptr,
@@ -415,7 +419,7 @@ std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tens
 at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& F, at::Tensor dbias) {
   expect(F, at::kBFloat16, "F");
   expect(dbias, at::kFloat, "dbias");
-  if (mfma_ok(dy, w)) {
+  if (force_mfma_gemm() && mfma_ok(dy, w)) {
     auto C = at::empty({dy.size(0), w.size(1)}, dy.options());
     const int rc = dl_gemm(0, 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0), (int)w.size(1),
                            (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0,
@@ -429,9 +433,45 @@ at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tenso
   return dh;
 }
 
+// ------------------------------------------------------------------ SwAV
+at::Tensor sinkhorn(const at::Tensor& scores, int64_t bs, double eps, int64_t iters) {
+  expect(scores, at::kFloat, "scores");
+  const int64_t n = scores.size(0), K = scores.size(1);
+  TORCH_CHECK(bs <= n, "bs > rows");
+  auto P = at::empty_like(scores);
+  auto Q = at::empty({bs, K}, scores.options());
+  auto ws = at::empty({2 * K + 1}, scores.options());
+  check(dl_sinkhorn(f32(scores), f32(P), f32(Q), f32(ws), (int)n, (int)K, (int)bs, (float)eps, (int)iters,
+                    cur_stream(scores)),
+        "sinkhorn");
+  return Q;
+}
+
+void swav_ce(const at::Tensor& scores, const at::Tensor& q, at::Tensor dscores, at::Tensor loss, double temperature,
+             double scale) {
+  TORCH_CHECK(scores.is_cuda() && scores.is_contiguous(), "scores must be a contiguous GPU tensor");
+  TORCH_CHECK(scores.scalar_type() == at::kFloat || scores.scalar_type() == at::kBFloat16, "scores dtype");
+  expect(q, at::kFloat, "q");
+  expect(dscores, at::kFloat, "dscores");
+  expect(loss, at::kFloat, "loss");
+  const int64_t K = scores.size(-1), rows = scores.numel() / K;
+  TORCH_CHECK(q.numel() == scores.numel(), "q shape mismatch");
+  check(dl_swav_ce(scores.data_ptr(), scores.scalar_type() == at::kBFloat16, f32(q), f32(dscores), f32(loss), (int)rows,
+                   (int)K, (float)temperature, (float)scale, cur_stream(scores)),
+        "swav_ce");
+}
+
+void row_normalize_(at::Tensor w) {
+  expect(w, at::kFloat, "w");
+  check(dl_row_normalize(f32(w), (int)w.size(0), (int)w.size(1), cur_stream(w)), "row_normalize");
+}
+
 }  // namespace
 
 TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
+  m.impl("sinkhorn", &sinkhorn);
+  m.impl("swav_ce", &swav_ce);
+  m.impl("row_normalize_", &row_normalize_);
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("gelu_fwd", &gelu_fwd);

@@ -60,6 +60,13 @@ int dl_gemm(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, cons
             int K, bf16_t* C, long ldc, float* Cf, long ldcf, const float* bias, const bf16_t* R, long ldr, bf16_t* H,
             long ldh, float* dbias, int splits, hipStream_t st);
 
+// swav.hip
+int dl_sinkhorn(const float* scores, float* P, float* Q, float* ws, int n, int K, int bs, float eps, int iters,
+                hipStream_t st);
+int dl_swav_ce(const void* scores, int scores_bf16, const float* q, float* dscores, float* loss, int rows, int K,
+               float temperature, float scale, hipStream_t st);
+int dl_row_normalize(float* w, int rows, int d, hipStream_t st);
+
 // attention.hip
 int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, bf16_t* out, long ldo, float* lse, int B, int H, int S,
                 int D, float scale, hipStream_t st);

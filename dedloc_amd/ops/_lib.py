@@ -41,6 +41,9 @@ _SCHEMAS = [
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
     "gemm_gelu(Tensor x, Tensor w, Tensor bias) -> (Tensor, Tensor)",
+    "sinkhorn(Tensor scores, int bs, float eps, int iters) -> Tensor",
+    "swav_ce(Tensor scores, Tensor q, Tensor(a!) dscores, Tensor(b!) loss, float temperature, float scale) -> ()",
+    "row_normalize_(Tensor(a!) w) -> ()",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias) -> Tensor",
 ]
 for _s in _SCHEMAS:
@@ -383,3 +386,34 @@ def _gemm_acc_cpu(a, b, c, trans_a, trans_b):
     A = a.float().t() if trans_a else a.float()
     Bm = b.float().t() if trans_b else b.float()
     c.add_(A @ Bm)
+
+
+@_impl("sinkhorn")
+def _sinkhorn_cpu(scores, bs, eps, iters):
+    # vissl distributed_sinkhornknopp (world size 1) on Q = exp((s - max s)/eps)^T
+    Q = torch.exp((scores.float() - scores.max()) / eps).t()
+    Q = Q / Q.sum()
+    K, n = Q.shape
+    r = torch.ones(K) / K
+    c = torch.ones(n) / n
+    curr = Q.sum(1)
+    for _ in range(iters):
+        Q = Q * (r / curr).unsqueeze(1)
+        Q = Q * (c / Q.sum(0)).unsqueeze(0)
+        curr = Q.sum(1)
+    Q = (Q / Q.sum(0, keepdim=True)).t()
+    return Q[-bs:].contiguous()
+
+
+@_impl("swav_ce")
+def _swav_ce_cpu(scores, q, dscores, loss, temperature, scale):
+    x = scores.float() / temperature
+    logp = torch.log_softmax(x, -1)
+    qs = q.sum(-1, keepdim=True)
+    loss.add_(-(q * logp).sum() * scale)
+    dscores.add_((torch.softmax(x, -1) * qs - q) / temperature * scale)
+
+
+@_impl("row_normalize_")
+def _row_normalize_cpu(w):
+    w.div_(w.norm(dim=1, keepdim=True).clamp_min(1e-12))

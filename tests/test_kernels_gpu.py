@@ -282,8 +282,14 @@ def test_albert_gpu_matches_cpu(cuda):
     assert rel(m_gpu.flat.grad.cpu(), m_cpu.flat.grad) < 5e-2
 
 
+@pytest.fixture
+def force_mfma(monkeypatch):
+    monkeypatch.setenv("DEDLOC_GEMM", "mfma")  # exercise gemm.hip even where the library is faster
+    yield
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (1000, 512, 256), (4096, 3072, 1024)])
-def test_mfma_gemm_nt_nn(cuda, M, N, K):
+def test_mfma_gemm_nt_nn(cuda, force_mfma, M, N, K):
     torch.manual_seed(5)
     a = torch.randn(M, K, device=cuda).bfloat16()
     w = torch.randn(N, K, device=cuda).bfloat16()
@@ -301,7 +307,7 @@ def test_mfma_gemm_nt_nn(cuda, M, N, K):
 
 
 @pytest.mark.parametrize("T,N,K", [(2048, 256, 256), (8192, 1024, 512)])
-def test_mfma_gemm_wgrad_splitk(cuda, T, N, K):
+def test_mfma_gemm_wgrad_splitk(cuda, force_mfma, T, N, K):
     torch.manual_seed(6)
     dy = torch.randn(T, N, device=cuda).bfloat16()
     x = torch.randn(T, K, device=cuda).bfloat16()
@@ -310,7 +316,7 @@ def test_mfma_gemm_wgrad_splitk(cuda, T, N, K):
     assert rel(g, 1 + dy.float().t() @ x.float()) < 1e-3
 
 
-def test_mfma_gemm_gelu_epilogues(cuda):
+def test_mfma_gemm_gelu_epilogues(cuda, force_mfma):
     torch.manual_seed(7)
     M, H, I = 1024, 256, 1024
     x = torch.randn(M, H, device=cuda).bfloat16()
