@@ -1,0 +1,145 @@
+"""SwAV ResNet-50 (vissl trunk + swav_head) for the collaborative SwAV experiment.
+
+Reference: ``swav/vissl/vissl/models/trunks/resnext.py:48-172``
+(torchvision Bottleneck ResNet-50, depth 50, width 1), ``swav_prototypes_head.py:10-112``
+(MLP 2048-2048(BN,ReLU)-128, L2 normalisation, 3000 prototypes without bias),
+``base_ssl_model.py:76-105`` (one trunk pass per crop with SINGLE_PASS_EVERY_CROP, features
+concatenated before the head).
+
+MI355X-first choices: channels-last bf16 activations under autocast (fp32 master weights live in the
+flat parameter buffer and receive their gradients in place), optional per-resolution batching of
+the crops (``single_pass_every_crop=False``: 2 trunk passes instead of 8), optional activation
+checkpointing per stage (off by default: 288 GB HBM makes the recompute pointless).
+Parameter names match torchvision/vissl (``trunk.*``, ``heads.0.*``) for checkpoint interchange.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import torch
+import torch.nn as nn
+
+from .. import ops as _ops  # noqa: F401  (registers torch.ops.dedloc.*)
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)  # ResNet v1.5
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return self.relu(out + idt)
+
+
+class ResNet50Trunk(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), zero_init_residual=False, checkpoint_stages: bool = False):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], stride=2)
+        self.layer3 = self._make_layer(256, layers[2], stride=2)
+        self.layer4 = self._make_layer(512, layers[3], stride=2)
+        self.checkpoint_stages = checkpoint_stages
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def _make_layer(self, planes, blocks, stride=1):
+        down = None
+        if stride != 1 or self.inplanes != planes * 4:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                                 nn.BatchNorm2d(planes * 4))
+        layers = [Bottleneck(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * 4
+        layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
+            if self.checkpoint_stages and self.training and x.requires_grad:
+                x = checkpoint(stage, x, use_reentrant=False)
+            else:
+                x = stage(x)
+        return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
+class SwAVPrototypesHead(nn.Module):
+    """MLP [2048, 2048, 128] with BN+ReLU, L2 normalisation, prototypes 128 -> 3000 (no bias)."""
+
+    def __init__(self, dims: Sequence[int] = (2048, 2048, 128), num_prototypes: int = 3000, use_bn: bool = True):
+        super().__init__()
+        layers: List[nn.Module] = []
+        for i in range(len(dims) - 2):
+            layers += [nn.Linear(dims[i], dims[i + 1])]
+            if use_bn:
+                layers += [nn.BatchNorm1d(dims[i + 1])]
+            layers += [nn.ReLU(inplace=True)]
+        layers += [nn.Linear(dims[-2], dims[-1])]
+        self.projection_head = nn.Sequential(*layers)
+        self.prototypes0 = nn.Linear(dims[-1], num_prototypes, bias=False)
+
+    def forward(self, x):
+        emb = F.normalize(self.projection_head(x), dim=1, p=2)
+        return emb, self.prototypes0(emb)
+
+
+class SwAVModel(nn.Module):
+    def __init__(self, num_prototypes: int = 3000, single_pass_every_crop: bool = True,
+                 checkpoint_stages: bool = False):
+        super().__init__()
+        self.trunk = ResNet50Trunk(checkpoint_stages=checkpoint_stages)
+        self.heads = nn.ModuleList([SwAVPrototypesHead(num_prototypes=num_prototypes)])
+        self.single_pass_every_crop = single_pass_every_crop
+
+    def forward(self, crops: List[torch.Tensor]):
+        """crops: list of [B, 3, H, W] (channels-last) tensors -> (embeddings, scores) over all crops."""
+        if self.single_pass_every_crop:
+            feats = [self.trunk(c) for c in crops]
+        else:  # one pass per run of equal-resolution crops (original SwAV's idx_crops grouping)
+            feats, i = [], 0
+            while i < len(crops):
+                j = i
+                while j < len(crops) and crops[j].shape[-1] == crops[i].shape[-1]:
+                    j += 1
+                feats.append(self.trunk(torch.cat(crops[i:j])))
+                i = j
+        return self.heads[0](torch.cat(feats))
+
+    @torch.no_grad()
+    def normalize_prototypes(self):
+        """NormalizePrototypesHook (swav_hooks.py:63-92): L2-normalise every prototype row."""
+        w = self.heads[0].prototypes0.weight.data
+        if w.is_cuda:
+            torch.ops.dedloc.row_normalize_(w)
+        else:
+            w.div_(w.norm(dim=1, keepdim=True).clamp_min(1e-12))
+
+    def prototype_param_names(self):
+        return [n for n, _ in self.named_parameters() if "prototypes" in n]

@@ -1,0 +1,224 @@
+"""Collaborative SwAV peer: vissl's SelfSupervisionTrainer + standard_train_step + swav hooks, with the
+``sgd_collaborative`` optimizer, flattened into one explicit loop.
+
+Per local iteration (reference ``vissl/trainer/train_steps/standard_train_step.py:87-229``):
+
+    crops (8 x [b, 3, S, S], generated on the GPU)         V11  data/multicrop.py
+    -> embeddings, scores = model(crops)  (bf16 autocast)    V7/V8  models/resnet_swav.py
+    -> SwAV loss with the GLOBAL collaborative step          V9/D18 models/swav_loss.py
+    -> backward (grads land in the flat fp32 buffer)
+    -> freeze prototypes for the first N local iterations    V10 FreezeParametersHook
+    -> CollaborativeOptimizer.step(batch)                    D17 (LARC-SGD, target 32768, FLOAT16 wire)
+    -> L2-normalise prototypes                              V10 NormalizePrototypesHook
+
+Deliberate differences: bf16 autocast instead of apex O1 fp16 + loss scaling (V15); activation
+checkpointing off by default (P11); optimizer state is shared through the DHT state server and saved
+in local checkpoints (the reference's ``get_classy_state`` returns None, D17).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import time
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+from ..data.multicrop import MultiCropAugment, SyntheticMultiCropStream
+from ..dht import DHT, get_dht_time
+from ..metrics import LocalMetrics, make_validators
+from ..models.resnet_swav import SwAVModel
+from ..models.swav_loss import SwAVLoss
+from ..optim.collaborative import CollaborativeOptimizer
+from ..optim.lamb import FusedLarcSGD, LinearWarmupCosineAnnealingLR
+from ..utils.flat import FlatParams
+
+logger = logging.getLogger(__name__)
+
+
+def _no_decay_names(model, regularize_bn: bool, regularize_bias: bool):
+    """vissl optimizer_helper.py:25-43: split BN / bias params out of weight decay when not regularized."""
+    out = set()
+    bn_types = (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)
+    for mname, m in model.named_modules():
+        for pname, _ in m.named_parameters(recurse=False):
+            full = f"{mname}.{pname}" if mname else pname
+            if isinstance(m, bn_types) and not regularize_bn:
+                out.add(full)
+            elif pname == "bias" and not regularize_bias:
+                out.add(full)
+    return out
+
+
+def _port_endpoint(port) -> str:
+    return "0.0.0.0:*" if str(port) in ("any", "*", "0", "None") else f"0.0.0.0:{port}"
+
+
+class SwavPeer:
+    def __init__(self, cfg, device, dht: Optional[DHT] = None, pg=None, rank: int = 0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        torch.manual_seed(int(cfg.get("SEED_VALUE", 0)))
+        mcfg, lcfg, ocfg = cfg.MODEL, cfg.LOSS.swav_loss, cfg.OPTIMIZER
+        dcfg = cfg.DATA.TRAIN
+        self.batch_size = int(dcfg.BATCHSIZE_PER_REPLICA)
+        self.model = SwAVModel(num_prototypes=int(mcfg.HEAD.num_clusters),
+                               single_pass_every_crop=bool(mcfg.SINGLE_PASS_EVERY_CROP),
+                               checkpoint_stages=bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING))
+        self.model.to(self.device).train()
+        self.flat = FlatParams(self.model.named_parameters(), device=self.device, with_bf16=False, autograd=True,
+                               channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
+        self.model.normalize_prototypes()
+        larc = ocfg.larc_config
+        assert ocfg.use_larc, "we can't use collab sgd without larc (sgd_collaborative.py:138)"
+        self.opt = FusedLarcSGD(self.flat, lr=float(ocfg.lr), momentum=float(ocfg.momentum),
+                                weight_decay=float(ocfg.weight_decay), nesterov=bool(ocfg.nesterov),
+                                trust_coefficient=float(larc.trust_coefficient), clip=bool(larc.clip),
+                                eps=float(larc.eps),
+                                no_decay=_no_decay_names(self.model, bool(ocfg.regularize_bn),
+                                                         bool(ocfg.regularize_bias)))
+        self.scheduler = LinearWarmupCosineAnnealingLR(self.opt, warmup_epochs=int(ocfg.warmup_epochs),
+                                                       max_epochs=int(ocfg.max_epochs),
+                                                       warmup_start_lr=float(ocfg.warmup_start_lr),
+                                                       eta_min=float(ocfg.eta_min))
+        validators, self.local_public_key = make_validators(ocfg.exp_prefix)
+        self.dht = dht or DHT(initial_peers=list(ocfg.dht_initial_peers or []),
+                              listen_on=_port_endpoint(ocfg.dht_listen_on_port), start=True,
+                              record_validators=validators)
+        self.collab_opt = CollaborativeOptimizer(
+            self.opt, dht=self.dht, scheduler=self.scheduler, prefix=ocfg.exp_prefix,
+            compression_type=str(ocfg.get("compression", "FLOAT16")),
+            target_batch_size=int(ocfg.get("target_batch_size", 32768)),
+            batch_size_per_step=int(ocfg.batch_size_for_tracking), verbose=True, start=True,
+            peer_id=self.local_public_key, target_group_size=int(ocfg.target_group_size),
+            listen_on=_port_endpoint(ocfg.averager_listen_on_port),
+            averaging_expiration=float(ocfg.get("averaging_expiration", 5.0)),
+            metadata_expiration=float(ocfg.get("metadata_expiration", 30)),
+            averaging_timeout=float(ocfg.get("averaging_timeout", 30)), pg=pg, rank=rank)
+        q = lcfg.queue
+        self.loss_fn = SwAVLoss(num_crops=sum(dcfg.MULTICROP.num_crops), crops_for_assign=lcfg.crops_for_assign,
+                                temperature=float(lcfg.temperature), epsilon=float(lcfg.epsilon),
+                                num_iters=int(lcfg.num_iters), num_prototypes=int(mcfg.HEAD.num_clusters),
+                                embedding_dim=int(mcfg.HEAD.dims[-1]), queue_length=int(q.queue_length),
+                                queue_start_iter=int(q.start_iter), batch_size=self.batch_size,
+                                temp_hard_assignment_iters=int(lcfg.get("temp_hard_assignment_iters", 0)))
+        self.loss_fn.to(self.device)
+        mc = dcfg.MULTICROP
+        aug = MultiCropAugment(size_crops=mc.size_crops, num_crops=mc.num_crops,
+                               crop_scales=[tuple(s) for s in mc.crop_scales], flip_p=float(mc.flip_p),
+                               color_strength=float(mc.color_strength), blur_p=float(mc.blur_p),
+                               blur_radius=tuple(mc.blur_radius))
+        seed = int.from_bytes(self.local_public_key[-8:], "little") ^ int(cfg.get("SEED_VALUE", 0))
+        self.data = SyntheticMultiCropStream(self.batch_size, self.device, seed=seed,
+                                             pool_size=int(dcfg.get("SYNTHETIC_POOL_SIZE", 1024)),
+                                             image_size=int(dcfg.get("SYNTHETIC_IMAGE_SIZE", 256)), augment=aug,
+                                             out_dtype=torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        self.frozen = [(name, int(iters)) for name, iters in (mcfg.get("TEMP_FROZEN_PARAMS_ITER_MAP") or [])]
+        self.iteration = 0
+        self._loss_sum = torch.zeros((), device=self.device)
+        self.mini_steps = 0
+        self.last_reported_step = -1
+        self.metrics_log = []
+
+    # ------------------------------------------------------------------ one local iteration
+    def train_step(self, crops=None):
+        crops = crops if crops is not None else self.data.next_batch()
+        with torch.autocast(device_type=self.device.type, dtype=torch.bfloat16,
+                            enabled=self.device.type == "cuda"):
+            emb, scores = self.model(crops)
+        proto = self.model.heads[0].prototypes0.weight
+        loss = self.loss_fn(emb.float(), scores, proto, training_iterations=int(self.collab_opt.local_step))
+        loss.backward()
+        for name, iters in self.frozen:  # FreezeParametersHook (state_update_hooks.py:235-280)
+            if self.iteration < iters:
+                name = name[len("module."):] if name.startswith("module.") else name
+                self.flat.view(self.flat.grad, name).zero_()
+        self._loss_sum += loss.detach()
+        self.collab_opt.step(batch_size=self.batch_size)
+        self.opt.zero_grad()
+        self.model.normalize_prototypes()  # NormalizePrototypesHook.on_update (swav_hooks.py:63-92)
+        self.iteration += 1
+        self.mini_steps += 1
+        self._on_step_end()
+        return loss.detach()
+
+    def _on_step_end(self):
+        co = self.collab_opt
+        if co.local_step == self.last_reported_step:
+            return
+        self.last_reported_step = co.local_step
+        loss = float(self._loss_sum.item())
+        stats = LocalMetrics(step=int(co.local_step), samples_per_second=float(co.performance_ema.samples_per_second),
+                             samples_accumulated=int(co.local_samples_accumulated), loss=loss,
+                             mini_steps=int(self.mini_steps))
+        self.dht.store(co.prefix + "_metrics", stats.model_dump(), expiration_time=get_dht_time() + 600,
+                       subkey=self.local_public_key, return_future=True)
+        rec = dict(stats.model_dump(), time=time.time(), iteration=self.iteration, lr=self.opt.param_groups[0]["lr"],
+                   queue=bool(self.loss_fn.use_queue))
+        self.metrics_log.append(rec)
+        if self.cfg.get("METRICS_FILE"):
+            with open(self.cfg.METRICS_FILE, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+        logger.info(f"collaborative step {co.local_step}: loss {loss / max(1, self.mini_steps):.4f} "
+                    f"lr {self.opt.param_groups[0]['lr']:.4g}")
+        self._loss_sum.zero_()
+        self.mini_steps = 0
+
+    # ------------------------------------------------------------------ checkpoints (V19)
+    def state_dict(self):
+        return {"model": {k: v.detach().cpu().contiguous() for k, v in self.model.state_dict().items()},
+                "optimizer": self.opt.state_dict(), "iteration": self.iteration,
+                "collab_step": int(self.collab_opt.local_step),
+                "loss": {k: v.cpu() for k, v in self.loss_fn.state_dict().items()}}
+
+    def save_checkpoint(self, directory: Optional[str] = None):
+        d = Path(directory or self.cfg.CHECKPOINT.DIR)
+        d.mkdir(parents=True, exist_ok=True)
+        path = d / f"model_iteration{self.iteration}.torch"
+        torch.save(self.state_dict(), path)
+        link = d / "checkpoint.torch"
+        if link.is_symlink() or link.exists():
+            link.unlink()
+        link.symlink_to(path.name)
+        return path
+
+    @torch.no_grad()
+    def load_checkpoint(self, path: str):
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        own = self.model.state_dict()
+        for k, v in sd["model"].items():
+            own[k].copy_(v)
+        self.opt.load_state_dict(sd["optimizer"])
+        self.iteration = int(sd["iteration"])
+        self.collab_opt.local_step = max(self.collab_opt.local_step, int(sd["collab_step"]))
+        self.collab_opt.update_scheduler()
+        self.loss_fn.load_state_dict({k: v.to(self.device) for k, v in sd["loss"].items()})
+
+    def maybe_resume(self):
+        if not self.cfg.CHECKPOINT.get("AUTO_RESUME", False):
+            return False
+        link = Path(self.cfg.CHECKPOINT.DIR) / "checkpoint.torch"
+        if link.exists():
+            logger.info(f"resuming from {link.resolve()}")
+            self.load_checkpoint(str(link))
+            return True
+        return False
+
+    def train(self, max_iterations: Optional[int] = None, stop_after_global_steps: Optional[int] = None,
+              max_seconds: Optional[float] = None):
+        self.collab_opt.load_state_from_peers()
+        t0, start = time.time(), self.collab_opt.local_step
+        freq = int(self.cfg.CHECKPOINT.get("CHECKPOINT_ITER_FREQUENCY", 0) or 0)
+        while max_iterations is None or self.iteration < max_iterations:
+            self.train_step()
+            if freq and self.iteration % freq == 0:
+                self.save_checkpoint()
+            if stop_after_global_steps is not None and self.collab_opt.local_step - start >= stop_after_global_steps:
+                break
+            if max_seconds is not None and time.time() - t0 > max_seconds:
+                break
+
+    def shutdown(self):
+        self.collab_opt.shutdown()
+        self.dht.shutdown()

@@ -23,12 +23,18 @@ def _round_up(n: int, a: int = ALIGN) -> int:
 class FlatParams:
     """Re-homes ``named_params`` into a flat fp32 buffer; parameters become views into it.
 
-    ``groups``: optional list of name lists that must be laid out contiguously and in order (e.g.
-    query/key/value weights so a fused [3H, H] view exists).
+    Two modes:
+      * manual-backward models (ALBERT): parameters stop requiring grad; the layer Functions write
+        their weight gradients straight into ``grad`` views;
+      * ``autograd=True`` (torch-module models such as the SwAV ResNet): parameters keep
+        ``requires_grad`` and their ``.grad`` is pre-bound to the ``grad`` view, so autograd's
+        AccumulateGrad adds in place into the flat buffer.  With ``channels_last=True`` every 4-D
+        parameter (conv weight) is laid out NHWC inside the flat buffer, matching channels-last
+        activations so MIOpen never transposes weights.
     """
 
     def __init__(self, named_params: Iterable[Tuple[str, torch.nn.Parameter]], device=None,
-                 with_bf16: bool = True):
+                 with_bf16: bool = True, autograd: bool = False, channels_last: bool = False):
         named = list(named_params)
         seen = {}
         self.names: List[str] = []
@@ -50,19 +56,33 @@ class FlatParams:
         self.fp32 = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.bf16 = torch.zeros(self.numel, dtype=torch.bfloat16, device=self.device) if with_bf16 else None
+        self.autograd = autograd
+        self.nhwc = {n for n in self.names if channels_last and self.params[n].dim() == 4}
         for n in self.names:
             p = self.params[n]
             v = self.view(self.fp32, n)
             v.copy_(p.data)
             p.data = v
-            p.requires_grad_(False)
+            if autograd:
+                p.grad = self.view(self.grad, n)
+            else:
+                p.requires_grad_(False)
         self.refresh_bf16()
 
     # ------------------------------------------------------------------ views
     def view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
         p = self.params[name]
         o = self.offsets[name]
+        if name in self.nhwc:
+            k, c, h, w = p.shape
+            return buf[o:o + p.numel()].view(k, h, w, c).permute(0, 3, 1, 2)
         return buf[o:o + p.numel()].view(p.shape)
+
+    def rebind_grads(self):
+        """Re-attach ``.grad`` views (after something replaced or cleared a parameter's grad)."""
+        if self.autograd:
+            for n in self.names:
+                self.params[n].grad = self.view(self.grad, n)
 
     def span(self, buf: torch.Tensor, first: str, last: str, shape) -> torch.Tensor:
         """A view over the contiguous range [first, last] (requires the names to be adjacent)."""

@@ -1,0 +1,282 @@
+"""SwAV path: loss/Sinkhorn semantics vs the vissl formulas, config overrides, multi-crop, LR schedule,
+flat autograd params, and one collaborative SwAV peer step (CPU); HIP kernels vs fp32 references (GPU).
+
+The reference formulas below are transcriptions of the math in
+``swav/vissl/vissl/losses/swav_loss.py:177-326`` written directly in torch (vissl is not importable here).
+"""
+import math
+
+import pytest
+import torch
+
+import dedloc_amd.ops  # noqa: F401
+from dedloc_amd.models.swav_loss import SwAVLoss
+from dedloc_amd.optim.lamb import FusedLarcSGD, LinearWarmupCosineAnnealingLR
+from dedloc_amd.utils.config import load_config, parse_cli
+from dedloc_amd.utils.flat import FlatParams
+
+
+def vissl_sinkhorn(scores, eps, iters):
+    """Q = exp((s - max)/eps)^T, r = 1/K, c = 1/n, iters x (row scale, col scale), final col normalise."""
+    Q = torch.exp((scores - scores.max()) / eps).t().double()
+    Q /= Q.sum()
+    K, n = Q.shape
+    r, c = torch.ones(K, dtype=Q.dtype) / K, torch.ones(n, dtype=Q.dtype) / n
+    for _ in range(iters):
+        u = Q.sum(1)
+        Q *= (r / u).unsqueeze(1)
+        Q *= (c / Q.sum(0)).unsqueeze(0)
+    return (Q / Q.sum(0, keepdim=True)).t().float()
+
+
+def vissl_loss(scores, bs, num_crops, crops_for_assign, eps, iters, T, queue_scores=None):
+    total = 0
+    for i, cid in enumerate(crops_for_assign):
+        with torch.no_grad():
+            s = scores[bs * cid: bs * (cid + 1)].detach()
+            if queue_scores is not None:
+                s = torch.cat([s, queue_scores[i]])  # vissl: batch first, queue after, take [:bs]
+            q = vissl_sinkhorn(s, eps, iters)[:bs]
+        loss = 0
+        for v in [v for v in range(num_crops) if v != cid]:
+            loss -= torch.mean(torch.sum(q * torch.log_softmax(scores[bs * v: bs * (v + 1)] / T, dim=1), dim=1))
+        total += loss / (num_crops - 1)
+    return total / len(crops_for_assign)
+
+
+def test_sinkhorn_cpu_matches_vissl():
+    torch.manual_seed(0)
+    s = torch.randn(40, 30) * 0.3
+    q = torch.ops.dedloc.sinkhorn(s, 8, 0.05, 3)
+    ref = vissl_sinkhorn(s, 0.05, 3)[-8:]
+    assert torch.allclose(q, ref, atol=1e-5, rtol=1e-4)
+    assert torch.allclose(q.sum(1), torch.ones(8), atol=1e-5)
+
+
+@pytest.mark.parametrize("use_queue", [False, True])
+def test_swav_loss_and_grad_vs_vissl(use_queue):
+    torch.manual_seed(1)
+    bs, nc, K, D, L = 6, 4, 20, 16, 12
+    protos = torch.nn.functional.normalize(torch.randn(K, D), dim=1)
+    emb = torch.nn.functional.normalize(torch.randn(nc * bs, D), dim=1)
+    scores = (emb @ protos.t()).requires_grad_(True)
+    crit = SwAVLoss(num_crops=nc, crops_for_assign=(0, 1), temperature=0.1, epsilon=0.05, num_iters=3,
+                    num_prototypes=K, embedding_dim=D, queue_length=L if use_queue else 0, queue_start_iter=5,
+                    batch_size=bs)
+    queue_before = crit.queue.clone() if use_queue else None
+    loss = crit(emb, scores, protos, training_iterations=7)
+    (g,) = torch.autograd.grad(loss, scores)
+    s2 = scores.detach().clone().requires_grad_(True)
+    qs = [queue_before[i] @ protos.t() for i in range(2)] if use_queue else None
+    ref = vissl_loss(s2, bs, nc, (0, 1), 0.05, 3, 0.1, qs)
+    (gref,) = torch.autograd.grad(ref, s2)
+    assert abs(loss.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
+    assert torch.allclose(g, gref, atol=1e-5, rtol=1e-3)
+    if use_queue:  # the newest batch embeddings entered the queue
+        assert torch.allclose(crit.queue[0, :bs], emb[:bs]) and torch.allclose(crit.queue[1, :bs], emb[bs:2 * bs])
+
+
+def test_swav_queue_gated_by_global_step():
+    crit = SwAVLoss(num_crops=2, crops_for_assign=(0,), num_prototypes=8, embedding_dim=4, queue_length=4,
+                    queue_start_iter=10, batch_size=2)
+    emb = torch.nn.functional.normalize(torch.randn(4, 4), dim=1)
+    protos = torch.nn.functional.normalize(torch.randn(8, 4), dim=1)
+    crit(emb, emb @ protos.t(), protos, training_iterations=9)
+    assert not crit.use_queue
+    crit(emb, emb @ protos.t(), protos, training_iterations=10)
+    assert crit.use_queue
+
+
+def test_hard_assignment_warmup():
+    crit = SwAVLoss(num_crops=2, crops_for_assign=(0,), num_prototypes=8, embedding_dim=4, batch_size=3,
+                    temp_hard_assignment_iters=1)
+    captured = []
+    orig = crit._sinkhorn
+    crit._sinkhorn = lambda s, bs: captured.append(orig(s, bs)) or captured[-1]
+    emb = torch.nn.functional.normalize(torch.randn(6, 4), dim=1)
+    protos = torch.nn.functional.normalize(torch.randn(8, 4), dim=1)
+    l1 = crit(emb, emb @ protos.t(), protos)
+    l2 = crit(emb, emb @ protos.t(), protos)
+    assert l1.item() != pytest.approx(l2.item())  # first call used one-hot targets, second soft ones
+
+
+def test_config_overrides():
+    name, ov, rest = parse_cli(["config=pretrain/swav/swav_1node_resnet_submit",
+                                "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=32", "+config.OPTIMIZER.lr=1.2",
+                                "+config.OPTIMIZER.dht_initial_peers=['1.2.3.4:5']", "--max_iterations", "3"])
+    assert rest == ["--max_iterations", "3"]
+    cfg = load_config(name, ov)
+    assert cfg.DATA.TRAIN.BATCHSIZE_PER_REPLICA == 32
+    assert cfg.OPTIMIZER.lr == 1.2
+    assert cfg.OPTIMIZER.dht_initial_peers == ["1.2.3.4:5"]
+    assert cfg.LOSS.swav_loss.queue.queue_length == 3840 and cfg.LOSS.swav_loss.epsilon == 0.03
+    assert cfg.get_path("OPTIMIZER.larc_config.trust_coefficient") == 0.001
+
+
+def test_linear_warmup_cosine_matches_reference_closed_form():
+    """sgd_collaborative.py:73-84 closed form (warmup_epochs > 1)."""
+    w = torch.nn.Parameter(torch.zeros(4))
+    flat = FlatParams([("w", w)], with_bf16=False)
+    opt = FusedLarcSGD(flat, lr=2.4)
+    sch = LinearWarmupCosineAnnealingLR(opt, warmup_epochs=5, max_epochs=20, warmup_start_lr=0.3, eta_min=0.0048)
+    for e in range(25):
+        if e < 5:
+            ref = 0.3 + e * (2.4 - 0.3) / 4
+        else:
+            ref = 0.0048 + 0.5 * (2.4 - 0.0048) * (1 + math.cos(math.pi * (e - 5) / 15))
+        assert opt.param_groups[0]["lr"] == pytest.approx(ref, rel=1e-9)
+        sch.step()
+
+
+def test_flat_autograd_channels_last_grads_accumulate_in_place():
+    conv = torch.nn.Conv2d(3, 8, 3, bias=True)
+    ref = torch.nn.Conv2d(3, 8, 3, bias=True)
+    ref.load_state_dict(conv.state_dict())
+    flat = FlatParams(conv.named_parameters(), with_bf16=False, autograd=True, channels_last=True)
+    assert conv.weight.is_contiguous(memory_format=torch.channels_last)
+    x = torch.randn(2, 3, 9, 9)
+    for _ in range(2):
+        conv(x).square().sum().backward()
+        ref(x).square().sum().backward()
+    assert conv.weight.grad.data_ptr() == flat.view(flat.grad, "weight").data_ptr()
+    assert torch.allclose(flat.view(flat.grad, "weight"), ref.weight.grad, atol=1e-5)
+    assert torch.allclose(flat.view(flat.grad, "bias"), ref.bias.grad, atol=1e-5)
+    flat.zero_grad()
+    assert conv.weight.grad.abs().sum() == 0
+
+
+def test_multicrop_shapes_cpu():
+    from dedloc_amd.data.multicrop import MultiCropAugment, SyntheticMultiCropStream
+
+    aug = MultiCropAugment(size_crops=(32, 16), num_crops=(2, 3))
+    s = SyntheticMultiCropStream(3, "cpu", seed=1, pool_size=4, image_size=48, augment=aug, out_dtype=torch.float32)
+    crops = s.next_batch()
+    assert [tuple(c.shape) for c in crops] == [(3, 3, 32, 32)] * 2 + [(3, 3, 16, 16)] * 3
+    assert all(torch.isfinite(c).all() for c in crops)
+    assert crops[0].is_contiguous(memory_format=torch.channels_last)
+
+
+def _tiny_cfg(extra=()):
+    return load_config("swav_1node_resnet_submit", [
+        "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=2", "config.DATA.TRAIN.MULTICROP.size_crops=[32,16]",
+        "config.DATA.TRAIN.MULTICROP.num_crops=[2,2]",
+        "config.DATA.TRAIN.SYNTHETIC_POOL_SIZE=4", "config.DATA.TRAIN.SYNTHETIC_IMAGE_SIZE=48",
+        "config.MODEL.HEAD.num_clusters=16", "config.LOSS.swav_loss.queue.queue_length=4",
+        "config.LOSS.swav_loss.queue.start_iter=0", "config.OPTIMIZER.target_batch_size=4",
+        "config.OPTIMIZER.batch_size_for_tracking=2",
+        "config.MODEL.TEMP_FROZEN_PARAMS_ITER_MAP=[['heads.0.prototypes0.weight', 1]]",
+        "config.OPTIMIZER.warmup_epochs=2", "config.OPTIMIZER.max_epochs=10", *extra])
+
+
+def test_swav_peer_cpu_steps_and_checkpoint(tmp_path):
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.training.swav_peer import SwavPeer
+
+    cfg = _tiny_cfg([f"config.CHECKPOINT.DIR={tmp_path}"])
+    dht = DHT(start=True)
+    peer = SwavPeer(cfg, "cpu", dht=dht)
+    try:
+        w = peer.model.heads[0].prototypes0.weight
+        w0 = w.detach().clone()
+        peer.train_step()  # iteration 0: prototypes frozen (their grad is zeroed)
+        assert torch.allclose(w.norm(dim=1), torch.ones(w.shape[0]), atol=1e-5)
+        losses = [float(peer.train_step()) for _ in range(3)]
+        assert all(math.isfinite(x) for x in losses)
+        trunk_w = peer.model.trunk.conv1.weight
+        assert trunk_w.grad.abs().sum() == 0  # zeroed after each collaborative step() call
+        path = peer.save_checkpoint()
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        assert sd["iteration"] == 4 and "heads.0.prototypes0.weight" in sd["model"]
+        snapshot = w.detach().clone()
+        with torch.no_grad():
+            w.add_(1.0)
+        peer.load_checkpoint(str(tmp_path / "checkpoint.torch"))
+        assert torch.allclose(w, snapshot)
+        assert not torch.allclose(w0, snapshot) or peer.collab_opt.local_step == 0
+    finally:
+        peer.shutdown()
+        dht.shutdown()
+
+
+# ----------------------------------------------------------------------------- GPU tier
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bs,K", [(64, 64, 3000), (64 + 3840, 64, 3000), (100, 37, 777)])
+def test_sinkhorn_gpu_vs_fp32_reference(cuda, n, bs, K):
+    torch.manual_seed(0)
+    e = torch.nn.functional.normalize(torch.randn(n, 128, device=cuda), dim=1)
+    p = torch.nn.functional.normalize(torch.randn(K, 128, device=cuda), dim=1)
+    s = (e @ p.t()).contiguous()
+    q = torch.ops.dedloc.sinkhorn(s, bs, 0.03, 3)
+    ref = torch.ops.dedloc.sinkhorn(s.cpu(), bs, 0.03, 3)
+    assert q.shape == (bs, K)
+    assert torch.allclose(q.cpu(), ref, atol=1e-6, rtol=2e-3), (q.cpu() - ref).abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_swav_ce_gpu_vs_fp32_reference(cuda, dtype):
+    torch.manual_seed(0)
+    rows, K = 64, 3000
+    s = (torch.randn(rows, K, device=cuda) * 0.5).to(dtype)
+    q = torch.softmax(torch.randn(rows, K, device=cuda) * 3, -1)
+    ds = torch.zeros(rows, K, device=cuda)
+    loss = torch.zeros(1, device=cuda)
+    torch.ops.dedloc.swav_ce(s, q, ds, loss, 0.1, 1.0 / rows)
+    sr = s.float().cpu().requires_grad_(True)
+    lref = -(q.cpu() * torch.log_softmax(sr / 0.1, -1)).sum(1).mean()
+    (g,) = torch.autograd.grad(lref, sr)
+    assert abs(loss.item() - lref.item()) < 1e-4 * abs(lref.item())
+    assert torch.allclose(ds.cpu(), g, atol=1e-6, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_row_normalize_gpu(cuda):
+    w = torch.randn(3000, 128, device=cuda)
+    ref = torch.nn.functional.normalize(w, dim=1)
+    torch.ops.dedloc.row_normalize_(w)
+    assert torch.allclose(w, ref, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_swav_loss_gpu_matches_cpu(cuda):
+    torch.manual_seed(2)
+    bs, nc, K, D = 16, 8, 3000, 128
+    protos = torch.nn.functional.normalize(torch.randn(K, D), dim=1)
+    emb = torch.nn.functional.normalize(torch.randn(nc * bs, D), dim=1)
+    scores = emb @ protos.t()
+    kw = dict(num_crops=nc, crops_for_assign=(0, 1), num_prototypes=K, embedding_dim=D, queue_length=64,
+              queue_start_iter=0, batch_size=bs)
+    torch.manual_seed(3)
+    c_cpu = SwAVLoss(**kw)
+    torch.manual_seed(3)
+    c_gpu = SwAVLoss(**kw).to(cuda)
+    s1 = scores.clone().requires_grad_(True)
+    s2 = scores.to(cuda).requires_grad_(True)
+    l1 = c_cpu(emb, s1, protos, 5)
+    l2 = c_gpu(emb.to(cuda), s2, protos.to(cuda), 5)
+    l1.backward()
+    l2.backward()
+    assert abs(l1.item() - l2.item()) < 1e-3 * abs(l1.item())
+    assert torch.allclose(s2.grad.cpu(), s1.grad, atol=1e-6, rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_swav_peer_gpu_step(cuda, tmp_path):
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.training.swav_peer import SwavPeer
+
+    cfg = load_config("swav_1node_resnet_submit", [
+        "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=8", "config.DATA.TRAIN.SYNTHETIC_POOL_SIZE=16",
+        "config.LOSS.swav_loss.queue.start_iter=0", "config.LOSS.swav_loss.queue.queue_length=64",
+        "config.OPTIMIZER.target_batch_size=16", "config.OPTIMIZER.batch_size_for_tracking=8",
+        f"config.CHECKPOINT.DIR={tmp_path}"])
+    dht = DHT(start=True)
+    peer = SwavPeer(cfg, cuda, dht=dht)
+    try:
+        losses = [float(peer.train_step()) for _ in range(3)]
+        assert all(math.isfinite(x) for x in losses), losses
+        w = peer.model.heads[0].prototypes0.weight
+        assert torch.allclose(w.norm(dim=1), torch.ones(w.shape[0], device=cuda), atol=1e-4)
+    finally:
+        peer.shutdown()
+        dht.shutdown()
