@@ -45,8 +45,13 @@ class GroupSpec:
 
 
 def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compression: str = "FLOAT16",
-                        pg=None, timeout: Optional[float] = 30.0, snapshots: Optional[Sequence[torch.Tensor]] = None):
-    """Average ``tensors`` in place across the group described by ``spec``."""
+                        pg=None, timeout: Optional[float] = 30.0, snapshots: Optional[Sequence[torch.Tensor]] = None,
+                        sources: Optional[Sequence[torch.Tensor]] = None):
+    """Average ``tensors`` in place across the group described by ``spec``.
+
+    ``sources``: pack these instead of ``tensors`` (same shapes) — used by delayed parameter
+    averaging, which averages a snapshot while the live parameters keep training.
+    ``snapshots``: delta rule on unpack (``t += avg - snapshot``)."""
     ops = torch.ops.dedloc
     wire = WIRE_DTYPES[compression]
     dev = tensors[0].device
@@ -67,7 +72,7 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
     send = torch.empty(V, dtype=wire, device=dev)
     if spec.contributes[me]:
         o = 0
-        for t, n in zip(tensors, sizes):
+        for t, n in zip(sources if sources is not None else tensors, sizes):
             ops.pack(t.reshape(-1), send[o:o + n], float(spec.weights[me]))
             o += n
     contrib_idx = [j for j in range(spec.size) if spec.contributes[j]]

@@ -117,7 +117,7 @@ class DecentralizedAverager:
                  averaging_timeout: float = 30.0, compression: str = "FLOAT16", throughput: Optional[float] = None,
                  client_mode: bool = False, auxiliary: bool = False, allow_state_sharing: bool = True,
                  listen_on: str = "0.0.0.0:*", metadata_expiration: float = 30.0, pg=None, rank: Optional[int] = None,
-                 **_unused):
+                 emulate_transfer_delay: bool = False, **_unused):
         self.averaged_tensors = list(averaged_tensors)
         self.dht, self.prefix, self.peer_id = dht, prefix, peer_id
         self.target_group_size, self.min_group_size = target_group_size, min_group_size
@@ -136,11 +136,18 @@ class DecentralizedAverager:
         self.state_server = StateServer(self._serve_state, listen_on.replace("[::]", "0.0.0.0")) \
             if self.allow_state_sharing else None
         self.local_step_for_state = 0
+        self.emulate_transfer_delay = emulate_transfer_delay
 
     # ------------------------------------------------------------------ averaging
     def step(self, weight: float = 1.0, timeout: Optional[float] = None, expected_group_size: int = 0,
-             gather: Optional[Dict[str, Any]] = None) -> Optional[Dict]:
-        """Matchmake and average.  Returns {"group_id", "size", "gathered"} or None on failure."""
+             gather: Optional[Dict[str, Any]] = None, tensors: Optional[Sequence[torch.Tensor]] = None,
+             sources: Optional[Sequence[torch.Tensor]] = None, key_suffix: str = "") -> Optional[Dict]:
+        """Matchmake and average.  Returns {"group_id", "size", "gathered"} or None on failure.
+
+        ``tensors`` overrides the averaged set for this round (e.g. gradients only), ``sources`` packs
+        snapshots instead of the live tensors, ``key_suffix`` selects an independent matchmaking key
+        (so a delayed parameter round never mixes with a gradient round)."""
+        tensors = list(tensors) if tensors is not None else self.averaged_tensors
         if not (dist.is_available() and dist.is_initialized()):
             logger.warning("averaging requires the collaboration's world communicator; skipping")
             return None
@@ -150,7 +157,7 @@ class DecentralizedAverager:
         window = self.averaging_expiration
         t_join = time.perf_counter()
         try:
-            ok, gid, members = self.dht.join_group(f"{self.prefix}_averaging".encode(), self.peer_id, info,
+            ok, gid, members = self.dht.join_group(f"{self.prefix}_averaging{key_suffix}".encode(), self.peer_id, info,
                                                    self.target_group_size, self.min_group_size,
                                                    expected_group_size, window, timeout=window + 10.0)
         except Exception as e:  # noqa: BLE001
@@ -162,7 +169,7 @@ class DecentralizedAverager:
             return None
         infos = [m[1] for m in members]
         my_index = [m[0] for m in members].index(self.peer_id)
-        V = sum(t.numel() for t in self.averaged_tensors)
+        V = sum(t.numel() for t in tensors)
         parts = load_balance_peers(V, [i["bandwidth"] for i in infos], min_size=0)
         spec = GroupSpec(ranks=[i["rank"] for i in infos], part_sizes=list(parts),
                          weights=[i["weight"] for i in infos], contributes=[not i["aux"] for i in infos],
@@ -172,11 +179,19 @@ class DecentralizedAverager:
         t0 = time.perf_counter()
         try:
             with self.lock_averaged_tensors:
-                butterfly_allreduce(self.averaged_tensors, spec, self.compression, pg=self.pg,
-                                    timeout=timeout or self.averaging_timeout)
+                butterfly_allreduce(tensors, spec, self.compression, pg=self.pg,
+                                    timeout=timeout or self.averaging_timeout, sources=sources)
         except (AllreduceException, RuntimeError) as e:
             logger.warning(f"all-reduce failed ({e}); skipping this round")
             return None
+        if self.emulate_transfer_delay and bw > 0:  # emulate the volunteer's link (AWS_runner wondershaper caps)
+            from ..emulation.heterogeneity import emulated_transfer_seconds
+
+            wire_bytes = torch.empty(0, dtype=WIRE_DTYPES[self.compression]).element_size()
+            want = 2 * emulated_transfer_seconds(V, wire_bytes, len(members), parts[my_index] / max(1, V), bw)
+            spent = time.perf_counter() - t0
+            if want > spent:
+                time.sleep(want - spent)
         self.last_group = {"group_id": gid, "size": len(members), "gathered": [i["gather"] for i in infos],
                            "matchmaking_s": t_match, "allreduce_s": time.perf_counter() - t0, "parts": list(parts)}
         return self.last_group

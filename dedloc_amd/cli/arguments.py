@@ -44,6 +44,11 @@ class CollaborativeOptimizerArguments:
 class CollaborationArguments(AveragerArguments, CollaborativeOptimizerArguments, BaseTrainingArguments):
     statistics_expiration: float = field(default=600, metadata={"help": "Statistics will be removed if not updated in this many seconds"})
     endpoint: Optional[str] = field(default=None, metadata={"help": "This node's IP for inbound connections"})
+    # ---- MI355X additions: fault-tolerance path and bandwidth emulation
+    delay_param_averaging: bool = field(default=False, metadata={"help": "average gradients synchronously but parameters in the background (delta rule)"})
+    peer_bandwidths: Optional[str] = field(default=None, metadata={"help": "per-rank emulated bandwidth list (Mbps), e.g. 200,100,100,50"})
+    peer_client_mode: Optional[str] = field(default=None, metadata={"help": "per-rank client-mode flags, e.g. 0,0,0,1"})
+    emulate_transfer_delay: bool = field(default=False, metadata={"help": "also delay each all-reduce to the emulated bandwidth's transfer time"})
 
 
 @dataclass
@@ -91,7 +96,11 @@ class AlbertTrainingArguments:
     device: Optional[str] = None
     # ---- MI355X emulation of the reference's heterogeneous AWS fleet
     throttle: float = field(default=0.0, metadata={"help": "extra idle seconds per training step (emulates a slower peer)"})
-    churn_schedule: Optional[str] = field(default=None, metadata={"help": "leave/rejoin schedule 'leave_at:duration,...' in global steps/seconds"})
+    slowdown: float = field(default=1.0, metadata={"help": "emulate slower hardware: each step takes this many times longer"})
+    churn_schedule: Optional[str] = field(default=None, metadata={"help": "drop-out/drop-in schedule '[leave|restart@]AT[s]:DURATION,...' (emulation/churn.py)"})
+    peer_batch_sizes: Optional[str] = field(default=None, metadata={"help": "per-rank micro-batch list, e.g. 32,16,8,4 (cycled over ranks)"})
+    peer_slowdowns: Optional[str] = field(default=None, metadata={"help": "per-rank slowdown list, e.g. 1,1.3,2"})
+    peer_churn: Optional[str] = field(default=None, metadata={"help": "per-rank churn schedules separated by ';' (empty = none)"})
     stop_after_global_steps: Optional[int] = field(default=None, metadata={"help": "exit after this many collaborative steps"})
     metrics_file: Optional[str] = field(default=None, metadata={"help": "append per-global-step JSONL metrics here"})
 

@@ -326,6 +326,10 @@ class DHT:
                     ep, started = rec
                     self._birth[ep] = started
                     self._add_replica(ep)
+            # gossip the membership table back to every replica, so a node that bootstraps from ANY
+            # replica (not only the oldest) learns the whole replica set immediately
+            for sub, (val, exp) in r[1].items():
+                self._raw_store_all(DHT_NODES_KEY, sub, val, exp)
 
     def _refresh_loop(self):
         while not self._stop.wait(self.replica_refresh):

@@ -11,6 +11,13 @@ global step.  Out-of-sync peers download the state from a donor instead of contr
 Flat-buffer implementation: gradients arrive in ``opt.flat.grad`` (fp32), the accumulator is one
 flat fp32 buffer, and every accumulate/average/apply is a single multi-tensor HIP launch; the
 fast path of ``step()`` (most calls) costs one kernel and a few Python statements.
+
+``delay_param_averaging=True`` (BASELINE config 5; not in hivemind 0.9.x): the
+global step averages only the gradients synchronously, applies the optimizer, then averages a
+snapshot of the parameters on a side HIP stream in a background thread while the next
+accumulation proceeds; the result is applied with the delta rule ``p += avg(snap) - snap`` (App. A.7)
+at the next ``step()`` that finds the round finished (and always before the next averaging round,
+so only one thread drives the communicator at a time).
 """
 from __future__ import annotations
 
@@ -69,7 +76,8 @@ class CollaborativeOptimizer:
                  averaging_timeout: Optional[float] = None, step_tolerance: int = 1, client_mode: bool = False,
                  auxiliary: bool = False, allow_state_sharing: bool = True, verbose: bool = False, start: bool = True,
                  compression_type: str = "FLOAT16", compression: Optional[str] = None, throughput: Optional[float] = None,
-                 peer_id: Optional[bytes] = None, max_grad_norm: Optional[float] = None, **averager_kwargs):
+                 peer_id: Optional[bytes] = None, max_grad_norm: Optional[float] = None,
+                 delay_param_averaging: bool = False, **averager_kwargs):
         self.opt, self.dht, self.prefix = opt, dht, prefix
         self.flat = opt.flat
         self.scheduler = scheduler
@@ -106,6 +114,15 @@ class CollaborativeOptimizer:
             averaging_timeout=self.averaging_timeout, **averager_kwargs)
         self.averager.get_current_state = self._get_current_state
 
+        self.delay_param_averaging = delay_param_averaging
+        self._param_round: Optional[threading.Thread] = None
+        self._param_round_result = None
+        self._param_done_event = None
+        if delay_param_averaging:
+            self._param_snapshot = torch.empty_like(self.flat.fp32)
+            self._param_avg = torch.empty_like(self.flat.fp32)
+            self._side_stream = torch.cuda.Stream(self.flat.fp32.device) if self.flat.fp32.is_cuda else None
+
         self.lock_collaboration_state = threading.Lock()
         self.lock_local_progress = threading.Lock()
         self.lock_step = threading.RLock()
@@ -141,6 +158,7 @@ class CollaborativeOptimizer:
     @torch.no_grad()
     def load_state_from_peers(self, **kwargs) -> bool:
         """Download params + optimizer state from the freshest donor (App. A.7)."""
+        self._finish_param_round(apply=False)
         with self.lock_step:
             res = self.averager.load_state_from_peers(**kwargs)
             if res is None:
@@ -203,10 +221,13 @@ class CollaborativeOptimizer:
             self.performance_ema.update(num_processed=batch_size)
             self.should_report_progress.set()
 
+        if self._param_round is not None and not self._param_round.is_alive():
+            self._finish_param_round()
         if not self.collaboration_state.ready_for_step:
             return None
 
         logger.log(self.status_loglevel, f"beginning global optimizer step #{self.collaboration_state.optimizer_step}")
+        self._finish_param_round()
         self.collaboration_state = self.fetch_collaboration_state()
         self.collaboration_state_updated.set()
         if not self.is_synchronized:
@@ -223,7 +244,8 @@ class CollaborativeOptimizer:
                 weight = self.local_samples_accumulated / mean_samples
                 group = self.averager.step(weight=weight, timeout=self.averaging_timeout,
                                            expected_group_size=cs.num_peers + self._num_aux(),
-                                           gather={"step": int(self.local_step)})
+                                           gather={"step": int(self.local_step)},
+                                           tensors=[self.flat.grad] if self.delay_param_averaging else None)
                 self.stats["averaging_rounds"] += 1
                 if group is None:
                     self.stats["averaging_failed"] += 1
@@ -232,6 +254,8 @@ class CollaborativeOptimizer:
             else:
                 logger.log(self.status_loglevel, "Skipped averaging: collaboration consists of this peer alone")
             self.opt.step()
+            if self.delay_param_averaging and group is not None:
+                self._start_param_round(weight, cs.num_peers + self._num_aux())
             self._reset_accumulators()
             self.collaboration_state.register_step(self.local_step + 1)
             self.local_step += 1
@@ -259,8 +283,12 @@ class CollaborativeOptimizer:
         with self.lock_collaboration_state, self.lock_step:
             group, current = None, max(self.local_step, self.collaboration_state.optimizer_step)
             if self.collaboration_state.num_peers >= 1:
-                group = self.averager.step(weight=0.0, timeout=self.averaging_timeout,
-                                           expected_group_size=self.collaboration_state.num_peers + self._num_aux())
+                expected = self.collaboration_state.num_peers + self._num_aux()
+                group = self.averager.step(weight=0.0, timeout=self.averaging_timeout, expected_group_size=expected,
+                                           tensors=[self.flat.grad] if self.delay_param_averaging else None)
+                if group is not None and self.delay_param_averaging:  # help with the delayed parameter round
+                    self.averager.step(weight=0.0, timeout=self.averaging_timeout, expected_group_size=expected,
+                                       tensors=[self.flat.fp32], key_suffix="_params")
                 if group is not None:
                     steps = [g.get("step") for g in group["gathered"] if isinstance(g.get("step"), int)]
                     current = max([current] + steps)
@@ -282,6 +310,75 @@ class CollaborativeOptimizer:
             return 0
         return sum(1 for k, v in rec.value.items() if v.value is True and k != self.peer_id)
 
+    # ------------------------------------------------------------------ churn
+    def leave(self):
+        """Stop participating: finish any background round, drop local progress and tombstone our
+        progress record so the collaboration's ETA and peer count exclude us immediately."""
+        self._finish_param_round(apply=False)
+        self._reset_accumulators()
+        self._left = True
+        try:
+            self.dht.store(f"{self.prefix}_progress", None, get_dht_time() + self.metadata_expiration,
+                           subkey=self.peer_id)
+        except Exception:  # noqa: BLE001
+            pass
+
+    def rejoin(self):
+        self._left = False
+        self.collaboration_state = self.fetch_collaboration_state()
+        self.load_state_from_peers()
+        self.performance_ema.reset_timer()
+        self.should_report_progress.set()
+
+    # ------------------------------------------------------------------ delayed parameter averaging
+    def _start_param_round(self, weight: float, expected_group_size: int):
+        self._param_snapshot.copy_(self.flat.fp32)
+        ready = None
+        if self._side_stream is not None:
+            ready = torch.cuda.Event()
+            ready.record()
+            self._param_done_event = torch.cuda.Event()
+
+        def run():
+            try:
+                if self._side_stream is not None:
+                    with torch.cuda.stream(self._side_stream):
+                        self._side_stream.wait_event(ready)
+                        res = self.averager.step(weight=weight, timeout=self.averaging_timeout,
+                                                 expected_group_size=expected_group_size, tensors=[self._param_avg],
+                                                 sources=[self._param_snapshot], key_suffix="_params")
+                        self._param_done_event.record(self._side_stream)
+                else:
+                    res = self.averager.step(weight=weight, timeout=self.averaging_timeout,
+                                             expected_group_size=expected_group_size, tensors=[self._param_avg],
+                                             sources=[self._param_snapshot], key_suffix="_params")
+            except Exception as e:  # noqa: BLE001
+                logger.warning(f"delayed parameter averaging failed: {e}")
+                res = None
+            self._param_round_result = res
+
+        self._param_round_result = None
+        self._param_round = threading.Thread(target=run, daemon=True, name="param-averaging")
+        self._param_round.start()
+
+    def _finish_param_round(self, apply: bool = True):
+        if self._param_round is None:
+            return
+        self._param_round.join()
+        self._param_round = None
+        res, self._param_round_result = self._param_round_result, None
+        if self._param_done_event is not None:
+            torch.cuda.current_stream().wait_event(self._param_done_event)
+        if res is None or not apply:
+            self.stats["param_rounds_failed"] = self.stats.get("param_rounds_failed", 0) + int(res is None)
+            return
+        ops = torch.ops.dedloc
+        with self.lock_step:
+            ops.axpby(self.flat.fp32, self._param_avg, 1.0, 1.0)       # p += avg(snapshot)
+            ops.axpby(self.flat.fp32, self._param_snapshot, 1.0, -1.0)  # p -= snapshot
+            self.flat.refresh_bf16()
+        self.stats["param_rounds"] = self.stats.get("param_rounds", 0) + 1
+
     # ------------------------------------------------------------------ background threads
     def _report_loop(self):
         while not self._stop.is_set():
@@ -289,7 +386,7 @@ class CollaborativeOptimizer:
             self.should_report_progress.clear()
             if self._stop.is_set():
                 break
-            if not self.auxiliary:
+            if not self.auxiliary and not getattr(self, "_left", False):
                 self.report_training_progress()
 
     def report_training_progress(self):
@@ -363,6 +460,10 @@ class CollaborativeOptimizer:
             self.scheduler.load_state_dict(sd["scheduler"])
 
     def shutdown(self):
+        try:
+            self._finish_param_round(apply=False)
+        except Exception:  # noqa: BLE001
+            pass
         self._stop.set()
         self.should_report_progress.set()
         self.collaboration_state_updated.set()

@@ -28,6 +28,7 @@ import torch
 
 from ..data.synthetic_mlm import SyntheticSOPStream, peer_seed
 from ..dht import DHT, get_dht_time
+from ..emulation import ChurnController, StepThrottle, parse_churn_schedule, profile_for_rank
 from ..metrics import LocalMetrics, make_validators
 from ..models.albert import AlbertConfig, AlbertForPreTraining
 from ..optim.collaborative import CollaborativeOptimizer
@@ -66,6 +67,22 @@ class AlbertPeer:
                  dht: Optional[DHT] = None, auxiliary: bool = False, publish_only_synchronized: bool = False):
         self.args, self.dargs, self.cargs = training_args, dataset_args, collab_args
         self.device = torch.device(device)
+        # per-rank heterogeneity (emulation/heterogeneity.py): micro-batch, speed, bandwidth, client mode
+        prof = profile_for_rank(rank, getattr(training_args, "peer_batch_sizes", None),
+                                getattr(training_args, "peer_slowdowns", None),
+                                getattr(collab_args, "peer_bandwidths", None),
+                                getattr(collab_args, "peer_client_mode", None),
+                                getattr(training_args, "peer_churn", None))
+        if prof.micro_batch:
+            training_args.per_device_train_batch_size = prof.micro_batch
+        if prof.bandwidth is not None:
+            collab_args.bandwidth = prof.bandwidth
+        if prof.client_mode:
+            collab_args.client_mode = True
+        self.throttle = StepThrottle(slowdown=prof.slowdown * getattr(training_args, "slowdown", 1.0),
+                                     throttle=training_args.throttle,
+                                     sync=torch.cuda.synchronize if self.device.type == "cuda" else None)
+        self.churn = ChurnController(parse_churn_schedule(prof.churn or training_args.churn_schedule), time.time())
         self.auxiliary = auxiliary
         self.publish_only_synchronized = publish_only_synchronized
         torch.manual_seed(training_args.seed)
@@ -91,7 +108,9 @@ class AlbertPeer:
             listen_on=ca.listen_on, min_refresh_period=ca.min_refresh_period, max_refresh_period=ca.max_refresh_period,
             default_refresh_period=ca.default_refresh_period, expected_drift_peers=ca.expected_drift_peers,
             expected_drift_rate=ca.expected_drift_rate, performance_ema_alpha=ca.performance_ema_alpha,
-            target_group_size=ca.target_group_size, metadata_expiration=ca.metadata_expiration, pg=pg, rank=rank)
+            target_group_size=ca.target_group_size, metadata_expiration=ca.metadata_expiration, pg=pg, rank=rank,
+            delay_param_averaging=getattr(ca, "delay_param_averaging", False),
+            emulate_transfer_delay=getattr(ca, "emulate_transfer_delay", False))
         self.statistics_expiration = ca.statistics_expiration
         seed = peer_seed(self.local_public_key, training_args.seed)
         self.data = SyntheticSOPStream(training_args.per_device_train_batch_size, training_args.seq_length,
@@ -114,6 +133,7 @@ class AlbertPeer:
     def train_step(self):
         a = self.args
         ga = a.gradient_accumulation_steps
+        self.throttle.begin()
         for _ in range(ga):
             batch = self.data.next_batch()
             out = self.model(batch["input_ids"], batch["attention_mask"], batch["token_type_ids"],
@@ -129,9 +149,31 @@ class AlbertPeer:
         self.opt.zero_grad()
         self.mini_steps += 1
         self.hf_step += 1
-        if a.throttle > 0:
-            time.sleep(a.throttle)
+        self.throttle.end()
         self.on_step_end()
+        ev = self.churn.due(self.collab_opt.local_step, time.time())
+        if ev is not None:
+            self.drop_out(ev.duration, restart=ev.mode == "restart")
+
+    # ------------------------------------------------------------------ churn (emulation/churn.py)
+    def drop_out(self, duration: float, restart: bool = False):
+        """Leave the collaboration for ``duration`` s (tombstone progress so the others re-plan at
+        once); with ``restart`` also lose all local state like a respawned spot instance."""
+        co = self.collab_opt
+        logger.warning(f"churn: leaving for {duration:.1f}s (restart={restart}) at step {co.local_step}")
+        co.leave()
+        if restart:
+            with torch.no_grad():
+                self._flat.fp32.normal_(0.0, 0.02)
+                self._flat.refresh_bf16()
+                for t in co.opt.state_tensors():
+                    t.zero_()
+            co.opt.step_count = 0
+            co.local_step = 0
+            self.hf_step = 0
+        time.sleep(duration)
+        co.rejoin()
+        self.stats_churn = getattr(self, "stats_churn", 0) + 1
 
     def _drop_if_nonfinite(self):
         # device-side: zero the whole step's gradient when the finite flag is 0 (no host sync)

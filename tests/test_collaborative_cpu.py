@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _peer(rank, world, port, dht_ep, out_q, cfg):
+def _peer(rank, world, port, dht_ep, out_q, cfg, mode=""):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -39,12 +39,19 @@ def _peer(rank, world, port, dht_ep, out_q, cfg):
                                     warmup_steps=2, max_steps=1000, learning_rate=3e-3, save_steps=0,
                                     output_dir=f"/tmp/dedloc_test_out_{port}_{rank}", seed=rank)
     dargs = DatasetArguments(config_path=cfg)
-    aux = rank in cfg_aux(world)
+    aux = rank in cfg_aux(world) and mode == ""
     cargs = CollaborationArguments(experiment_prefix="test", initial_peers=[dht_ep], dht_listen_on="127.0.0.1:*",
                                    target_batch_size=8, averaging_expiration=3.0, compression="NONE",
                                    min_refresh_period=0.05, default_refresh_period=0.2, metadata_expiration=20,
                                    listen_on="127.0.0.1:*", bandwidth=100.0 + 50 * rank)
-    late = rank == world - 1 and world == 3 and not aux
+    late = rank == world - 1 and world == 3 and not aux and mode == ""
+    if mode == "delay":
+        cargs.delay_param_averaging = True
+    elif mode == "hetero":
+        targs.peer_batch_sizes, targs.peer_slowdowns = "2,1,3", "1,2,1"
+        cargs.peer_bandwidths = "200,50,100"
+    elif mode == "churn":
+        targs.peer_churn = ";;restart@2:4"  # rank 2 is preempted after global step 2 and respawned 4 s later
     if late:
         targs.throttle = 0.0
     else:
@@ -62,12 +69,18 @@ def _peer(rank, world, port, dht_ep, out_q, cfg):
                 time.sleep(0.05)
         else:
             steps = 3 if world == 2 else (6 if late else 12)
-            peer.train(max_steps=600, stop_after_global_steps=steps, max_seconds=60)
+            if mode == "churn":
+                steps = 8
+            peer.train(max_steps=600, stop_after_global_steps=steps, max_seconds=60 if mode != "churn" else 90)
+            peer.collab_opt._finish_param_round()
         res["local_step"] = peer.collab_opt.local_step
         res["stats"] = dict(peer.collab_opt.stats)
         res["params"] = peer.model.flat.fp32.clone()
         res["metrics"] = peer.metrics_log
         res["state_loads"] = peer.collab_opt.stats["state_loads"]
+        res["batch"] = peer.args.per_device_train_batch_size
+        res["bandwidth"] = peer.cargs.bandwidth
+        res["churned"] = getattr(peer, "stats_churn", 0)
     finally:
         out_q.put(res)
         time.sleep(2.0)  # keep serving state/averaging for the others a little longer
@@ -87,7 +100,7 @@ def _tiny_cfg(tmp_path):
     return str(d)
 
 
-def _run(world, tmp_path):
+def _run(world, tmp_path, mode=""):
     from dedloc_amd.dht import DHT
 
     root = DHT(listen_on="127.0.0.1:*")
@@ -95,7 +108,7 @@ def _run(world, tmp_path):
     cfg = _tiny_cfg(tmp_path)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_peer, args=(r, world, port, root.endpoint, q, cfg)) for r in range(world)]
+    procs = [ctx.Process(target=_peer, args=(r, world, port, root.endpoint, q, cfg, mode)) for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=180) for _ in range(world)]
@@ -130,3 +143,34 @@ def test_aux_peer_and_late_joiner(tmp_path):
     # once two trainers overlap they average (with the auxiliary peer as an extra reducer)
     assert late["stats"]["averaging_rounds"] >= 1
     assert aux["local_step"] >= 1
+
+
+@pytest.mark.timeout(300)
+def test_delayed_parameter_averaging(tmp_path):
+    res = _run(2, tmp_path, mode="delay")
+    for r in res:
+        assert r["local_step"] >= 3, r
+        assert r["stats"].get("param_rounds", 0) >= 1, r["stats"]
+    failed = sum(r["stats"]["averaging_failed"] + r["stats"].get("param_rounds_failed", 0) for r in res)
+    d = (res[0]["params"] - res[1]["params"]).abs().max().item()
+    assert d < (1e-5 if failed == 0 else 5e-2), (d, [r["stats"] for r in res])
+
+
+@pytest.mark.timeout(300)
+def test_heterogeneous_peers(tmp_path):
+    res = _run(3, tmp_path, mode="hetero")
+    assert [r["batch"] for r in res] == [2, 1, 3]
+    assert [r["bandwidth"] for r in res] == [200.0, 50.0, 100.0]
+    for r in res:
+        assert r["local_step"] >= 6, r
+    assert sum(r["stats"]["averaging_rounds"] for r in res) >= 3
+
+
+@pytest.mark.timeout(300)
+def test_churn_restart_rejoins_through_state_download(tmp_path):
+    res = _run(3, tmp_path, mode="churn")
+    survivor, _, churned = res
+    assert churned["churned"] == 1
+    assert churned["state_loads"] >= 1  # lost its state -> downloaded it from a live peer
+    assert churned["local_step"] >= 8 and survivor["local_step"] >= 8
+    assert survivor["stats"]["global_steps"] >= 8  # the others kept training while it was away
