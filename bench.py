@@ -41,11 +41,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3, help="timed collaborative steps")
     ap.add_argument("--warmup", type=int, default=1, help="untimed collaborative steps")
-    ap.add_argument("--micro_batch", type=int, default=32)
+    ap.add_argument("--micro_batch", type=int, default=64)
     ap.add_argument("--grad_accum", type=int, default=1)
     ap.add_argument("--seq_len", type=int, default=512)
     ap.add_argument("--target_batch_size", type=int, default=4096)
     ap.add_argument("--compression", default="FLOAT16")
+    ap.add_argument("--impl", default="dedloc", choices=["dedloc", "eager"],
+                    help="eager = HF AlbertForPreTraining + per-tensor torch LAMB (the measured baseline)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -76,7 +78,9 @@ def main():
                                    target_batch_size=args.target_batch_size, compression=args.compression,
                                    listen_on="127.0.0.1:*", averaging_expiration=5.0, averaging_timeout=60.0,
                                    min_refresh_period=0.2, default_refresh_period=0.5)
-    peer = AlbertPeer(targs, dargs, cargs, dev, rank=rank, dht=None)
+    if args.impl == "eager":
+        dargs.mask_mode = "hf"
+    peer = AlbertPeer(targs, dargs, cargs, dev, rank=rank, dht=None, impl=args.impl)
     co = peer.collab_opt
     bs = args.micro_batch * args.grad_accum
 
@@ -127,7 +131,7 @@ def main():
                "config": {"model": "albert-large-v2", "global_batch": args.target_batch_size,
                           "seq_len": args.seq_len, "parallelism": f"collaborative-dp{world}",
                           "micro_batch": args.micro_batch, "grad_accum": args.grad_accum,
-                          "compression": args.compression, "optimizer": "LAMB"},
+                          "compression": args.compression, "optimizer": "LAMB", "impl": args.impl},
                "ema_samples_per_s_sum": round(ema_sum, 2), "averaging_rounds": co.stats["averaging_rounds"],
                "averaging_failed": co.stats["averaging_failed"],
                "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"}}

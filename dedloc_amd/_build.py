@@ -80,6 +80,14 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         cmd += ["-I", sysconfig.get_paths()["include"], "-c", bind_src, "-o", bind_obj]
         jobs_list.append(cmd)
 
+    # host-side C++ that talks to ROCm libraries (hipBLASLt) but not to torch
+    for src in sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))):
+        obj = os.path.join(BUILD, "host_" + os.path.basename(src).replace(".cpp", ".o"))
+        objs.append(obj)
+        if _newer(obj, [src] + headers):
+            jobs_list.append(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I",
+                              f"{ROCM}/include", *inc, "-c", src, "-o", obj])
+
     rt_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     rt_objs = []
     for src in rt_srcs:
@@ -95,7 +103,8 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         cmd = ["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", SO_PATH]
         for p in tlib:
             cmd += ["-L", p, f"-Wl,-rpath,{p}"]
-        cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64"]
+        cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-L", f"{ROCM}/lib",
+                f"-Wl,-rpath,{ROCM}/lib", "-lhipblaslt"]
         _run(cmd, verbose)
     if rt_objs and _newer(DHT_SO_PATH, rt_objs):
         _run(["g++", "-shared", "-fPIC", *rt_objs, "-o", DHT_SO_PATH, "-lpthread"], verbose)

@@ -9,6 +9,7 @@
 #include <c10/hip/HIPStream.h>
 
 #include "dl_kernels.h"
+#include "dl_lt.h"
 
 namespace {
 
@@ -303,7 +304,9 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
 }
 
 // ------------------------------------------------------------------ GEMM (library path)
-// Plain GEMMs go to hipBLASLt through ATen; fused-epilogue variants add the dedloc kernels.
+// Plain and fused-epilogue GEMMs go straight to hipBLASLt (csrc/host/lt_gemm.cpp: fp32 bias read
+// in the epilogue, GELU_AUX_BIAS for the FFN-up forward, DGELU_BGRAD for the FFN dgrad, per-shape
+// autotuned algorithm); ATen is only the fallback when hipBLASLt offers no solution.
 // (bf16 in, fp32 accumulate; the fp32-accumulating form writes straight into the fp32 gradient
 // buffer with beta=1 so the shared ALBERT layer's 24 weight-gradient contributions never round
 // through bf16.)
@@ -311,15 +314,19 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
 //   * the dedloc MFMA kernel (gemm.hip) wins the weight-gradient GEMMs whose output has few
 //     256x256 tiles (split-K over the token dimension: 1024x1024 wgrad 168 us vs 198 us);
 //   * hipBLASLt currently wins the large forward/dgrad GEMMs (its deeper LDS-DMA pipeline reaches
-//     1.1-1.5 PF/s on these shapes vs ~0.6-0.95 for gemm.hip's register-staged loop), so they go
-//     to the library and the gelu / dgelu / bias-grad epilogues run as separate fused kernels.
-// DEDLOC_GEMM=mfma forces gemm.hip everywhere (correctness tests), =lib forces the library.
+//     1.1-1.5 PF/s on these shapes vs ~0.6-0.95 for gemm.hip's register-staged loop).
+// DEDLOC_GEMM=mfma forces gemm.hip everywhere (correctness tests), =lib forces the library;
+// DEDLOC_LT=0 routes the library path through ATen instead of the direct hipBLASLt calls.
 int gemm_policy() {  // 0 auto, 1 mfma, 2 lib  (read per call: tests flip it at run time)
   const char* e = std::getenv("DEDLOC_GEMM");
   return !e ? 0 : (e[0] == 'm' ? 1 : (e[0] == 'l' ? 2 : 0));
 }
 bool use_mfma_gemm() { return gemm_policy() != 2; }
 bool force_mfma_gemm() { return gemm_policy() == 1; }
+bool use_lt() {
+  const char* e = std::getenv("DEDLOC_LT");
+  return !(e && e[0] == '0');
+}
 
 struct Mat {  // (rows, k) operand view: K-inner means element (r, k) at p[r*ld + k]
   const at::Tensor& t;
@@ -341,6 +348,27 @@ inline bool mfma_ok(const at::Tensor& a, const at::Tensor& b) {
          a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1;
 }
 
+inline bool lt_ok(const at::Tensor& a, const at::Tensor& b) {
+  return use_lt() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
+         b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1;
+}
+
+inline DlLtArgs lt_args(const at::Tensor& a, const at::Tensor& b, bool trans_a, bool trans_b) {
+  const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
+  TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
+  DlLtArgs l;
+  l.transA = trans_a;
+  l.transB = trans_b;
+  l.M = (int)A.rows;
+  l.N = (int)B.rows;
+  l.K = (int)A.k;
+  l.A = a.data_ptr();
+  l.lda = a.stride(0);
+  l.B = b.data_ptr();
+  l.ldb = b.stride(0);
+  return l;
+}
+
 inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias) {
   if (!bias.has_value()) return at::Tensor();
   return bias->scalar_type() == at::kFloat ? bias->contiguous() : bias->to(at::kFloat).contiguous();
@@ -359,6 +387,25 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
                            residual.has_value() ? cbf(*residual) : nullptr, B.rows, nullptr, 0, nullptr, 1,
                            cur_stream(a));
     if (rc == 0) return c;
+  }
+  if (lt_ok(a, b) && (!residual.has_value() || (residual->is_contiguous() && residual->scalar_type() == at::kBFloat16))) {
+    DlLtArgs l = lt_args(a, b, trans_a, trans_b);
+    auto c = at::empty({l.M, l.N}, a.options());
+    const at::Tensor bias32 = f32_bias(bias);
+    l.D = c.data_ptr();
+    l.ldd = l.N;
+    if (residual.has_value()) {  // C = residual: the residual-branch gradient sum rides in the GEMM
+      l.C = residual->data_ptr();
+      l.beta = 1.f;
+    }
+    if (bias32.defined()) {
+      l.epilogue = epilogue == 1 ? DL_LT_GELU_BIAS : DL_LT_BIAS;
+      l.bias = bias32.data_ptr();
+    }
+    if (dl_lt_matmul(l, cur_stream(a)) == 0) {
+      if (epilogue == 1 && !bias32.defined()) check(dl_gelu_fwd(cbf(c), bf(c), c.numel(), cur_stream(c)), "gemm gelu");
+      return c;
+    }
   }
   const at::Tensor A = trans_a ? a.t() : a;
   const at::Tensor B = trans_b ? b.t() : b;
@@ -394,6 +441,14 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
                            cur_stream(a));
     if (rc == 0) return;
   }
+  if (lt_ok(a, b) && c.stride(1) == 1) {
+    DlLtArgs l = lt_args(a, b, trans_a, trans_b);
+    l.D = c.data_ptr();
+    l.ldd = c.stride(0);
+    l.d_f32 = 1;
+    l.beta = 1.f;
+    if (dl_lt_matmul(l, cur_stream(a)) == 0) return;
+  }
   const at::Tensor A = trans_a ? a.t() : a;
   const at::Tensor B = trans_b ? b.t() : b;
   at::_ops::addmm_dtype_out::call(c, A, B, at::kFloat, 1, 1, c);
@@ -410,6 +465,17 @@ std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tens
                            1, cur_stream(x));
     if (rc == 0) return {H, G};
   }
+  const at::Tensor bias32 = f32_bias(bias);
+  if (lt_ok(x, w)) {  // one hipBLASLt kernel: G = gelu(x W^T + b), aux H = pre-activation
+    DlLtArgs l = lt_args(x, w, false, true);
+    l.D = G.data_ptr();
+    l.ldd = G.size(1);
+    l.epilogue = DL_LT_GELU_AUX_BIAS;
+    l.bias = bias32.data_ptr();
+    l.aux = H.data_ptr();
+    l.ldaux = H.size(1);
+    if (dl_lt_matmul(l, cur_stream(x)) == 0) return {H, G};
+  }
   H = at::addmm(bias.to(x.scalar_type()), x, w.t()).contiguous();
   check(dl_gelu_fwd(cbf(H), bf(G), H.numel(), cur_stream(H)), "gelu_fwd");
   return {H, G};
@@ -425,6 +491,21 @@ at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tenso
                            (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0,
                            f32(dbias), 1, cur_stream(dy));
     if (rc == 0) return C;
+  }
+  if (lt_ok(dy, w) && F.is_contiguous()) {  // one hipBLASLt kernel: dgrad * gelu'(F) + bias grad
+    auto dh = at::empty({dy.size(0), w.size(1)}, dy.options());
+    auto bgrad = at::empty({w.size(1)}, dbias.options());
+    DlLtArgs l = lt_args(dy, w, false, false);
+    l.D = dh.data_ptr();
+    l.ldd = dh.size(1);
+    l.epilogue = DL_LT_DGELU_BGRAD;
+    l.bias = bgrad.data_ptr();
+    l.aux = const_cast<void*>(F.data_ptr());
+    l.ldaux = F.size(1);
+    if (dl_lt_matmul(l, cur_stream(dy)) == 0) {
+      check(dl_axpby(f32(dbias), f32(bgrad), dbias.numel(), 1.f, 1.f, nullptr, cur_stream(dy)), "dbias accumulate");
+      return dh;
+    }
   }
   auto dg = at::mm(dy, w).contiguous();
   auto dh = at::empty_like(dg);

@@ -1,0 +1,225 @@
+// Library GEMMs with fused epilogues through hipBLASLt, called directly (no ATen detour), with a
+// per-shape algorithm cache and first-call autotuning.
+//
+// Row-major contract used by the rest of dedloc (all matrices row-major):
+//   D[M,N] = op(A)[M,K] · op(B)[K,N]  (+ beta·D) (+ bias[N]) -> epilogue
+//   A is [M,K] (lda) or, with transA, [K,M];  B is [K,N] (ldb) or, with transB, [N,K].
+// hipBLASLt is column-major, so we hand it the transposed problem D^T[N,M] = op(B)^T · op(A)^T:
+// its matrix "A" is our B and its "B" is our A, with m = N, n = M.  Bias vectors then run along
+// the column-major rows = our output features, exactly what Linear layers need, and the
+// DGELU_BGRAD bias gradient is the sum over tokens.
+//
+// Epilogues used by ALBERT's FFN: GELU_AUX_BIAS (forward: D = gelu(x W^T + b), aux = pre-activation)
+// and DGELU_BGRAD (backward: D = (dy W) * gelu'(aux), bias-grad = colsum(D)); gelu is the tanh form,
+// i.e. HF "gelu_new".  Removes the separate gelu / gelu-backward / bias-grad passes over [T, 4096].
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "dl_lt.h"
+
+namespace {
+
+struct Key {
+  int ta, tb, M, N, K;
+  long lda, ldb, ldd, ldaux;
+  int d_f32, in_f32, beta_nz, epi, bias_f32, dev;
+  bool operator<(const Key& o) const {
+    return std::tie(ta, tb, M, N, K, lda, ldb, ldd, ldaux, d_f32, in_f32, beta_nz, epi, bias_f32, dev) <
+           std::tie(o.ta, o.tb, o.M, o.N, o.K, o.lda, o.ldb, o.ldd, o.ldaux, o.d_f32, o.in_f32, o.beta_nz, o.epi,
+                    o.bias_f32, o.dev);
+  }
+};
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, ld = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  size_t ws = 0;
+  bool ok = false;
+};
+
+struct DevState {
+  hipblasLtHandle_t handle = nullptr;
+  void* workspace = nullptr;
+  size_t ws_size = 0;
+  void* scratch = nullptr;  // autotuning output sink
+  size_t scratch_size = 0;
+};
+
+std::mutex g_mu;
+std::map<Key, Plan> g_plans;
+std::map<int, DevState> g_dev;
+
+constexpr size_t kWorkspace = 128ull << 20;
+
+hipblasLtEpilogue_t to_lt(int epi) {
+  switch (epi) {
+    case DL_LT_BIAS: return HIPBLASLT_EPILOGUE_BIAS;
+    case DL_LT_GELU_AUX_BIAS: return HIPBLASLT_EPILOGUE_GELU_AUX_BIAS;
+    case DL_LT_DGELU_BGRAD: return HIPBLASLT_EPILOGUE_DGELU_BGRAD;
+    case DL_LT_GELU_BIAS: return HIPBLASLT_EPILOGUE_GELU_BIAS;
+    default: return HIPBLASLT_EPILOGUE_DEFAULT;
+  }
+}
+
+DevState* dev_state(int dev) {
+  DevState& s = g_dev[dev];
+  if (!s.handle) {
+    if (hipblasLtCreate(&s.handle) != HIPBLAS_STATUS_SUCCESS) return nullptr;
+    if (hipMalloc(&s.workspace, kWorkspace) != hipSuccess) return nullptr;
+    s.ws_size = kWorkspace;
+  }
+  return &s;
+}
+
+bool set_ptrs(hipblasLtMatmulDesc_t desc, const DlLtArgs& a) {
+  if (a.epilogue != DL_LT_NONE) {
+    const void* bias = a.bias;
+    if (hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)) !=
+        HIPBLAS_STATUS_SUCCESS)
+      return false;
+  }
+  if (a.epilogue == DL_LT_GELU_AUX_BIAS || a.epilogue == DL_LT_DGELU_BGRAD) {
+    void* aux = a.aux;
+    if (hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_POINTER, &aux, sizeof(aux)) !=
+        HIPBLAS_STATUS_SUCCESS)
+      return false;
+  }
+  return true;
+}
+
+bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
+  const hipDataType in_t = a.in_f32 ? HIP_R_32F : HIP_R_16BF;
+  const hipDataType d_t = a.d_f32 ? HIP_R_32F : HIP_R_16BF;
+  if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return false;
+  // hip "A" = our B, hip "B" = our A
+  const hipblasOperation_t opA = a.transB ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  const hipblasOperation_t opB = a.transA ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA));
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB));
+  const hipblasLtEpilogue_t epi = to_lt(a.epilogue);
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi));
+  if (a.epilogue != DL_LT_NONE) {
+    const int32_t bt = a.bias_f32 ? HIP_R_32F : HIP_R_16BF;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+  }
+  if (a.epilogue == DL_LT_GELU_AUX_BIAS || a.epilogue == DL_LT_DGELU_BGRAD) {
+    const int64_t ldaux = a.ldaux;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_LD, &ldaux, sizeof(ldaux));
+    const int32_t at = HIP_R_16BF;
+    hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE_AUX_DATA_TYPE, &at, sizeof(at));
+  }
+  // stored (pre-op) shapes, column-major
+  const uint64_t a_rows = a.transB ? a.K : a.N, a_cols = a.transB ? a.N : a.K;
+  const uint64_t b_rows = a.transA ? a.M : a.K, b_cols = a.transA ? a.K : a.M;
+  if (hipblasLtMatrixLayoutCreate(&p.la, in_t, a_rows, a_cols, a.ldb) != HIPBLAS_STATUS_SUCCESS) return false;
+  if (hipblasLtMatrixLayoutCreate(&p.lb, in_t, b_rows, b_cols, a.lda) != HIPBLAS_STATUS_SUCCESS) return false;
+  if (hipblasLtMatrixLayoutCreate(&p.ld, d_t, a.N, a.M, a.ldd) != HIPBLAS_STATUS_SUCCESS) return false;
+  if (!set_ptrs(p.desc, a)) return false;
+
+  hipblasLtMatmulPreference_t pref;
+  hipblasLtMatmulPreferenceCreate(&pref);
+  uint64_t wsz = s->ws_size;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz));
+  const char* tune_env = std::getenv("DEDLOC_LT_TUNE");
+  const int want = (tune_env && tune_env[0] == '0') ? 1 : 16;
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(want);
+  int n = 0;
+  const hipblasStatus_t hs =
+      hipblasLtMatmulAlgoGetHeuristic(s->handle, p.desc, p.la, p.lb, p.ld, p.ld, pref, want, res.data(), &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (hs != HIPBLAS_STATUS_SUCCESS || n <= 0) return false;
+
+  int best = 0;
+  if (n > 1) {
+    // autotune: time every candidate into a scratch output (inputs are read-only; beta=0)
+    const size_t d_bytes = (size_t)a.ldd * a.M * (a.d_f32 ? 4 : 2);
+    const size_t aux_bytes = (a.aux ? (size_t)a.ldaux * a.M * 2 : 0);
+    const size_t bias_bytes = (size_t)a.N * 4;
+    const size_t need = d_bytes + aux_bytes + bias_bytes + 256;
+    if (s->scratch_size < need) {
+      if (s->scratch) hipFree(s->scratch);
+      s->scratch = nullptr;
+      s->scratch_size = 0;
+      if (hipMalloc(&s->scratch, need) == hipSuccess) s->scratch_size = need;
+    }
+    if (s->scratch) {
+      char* base = static_cast<char*>(s->scratch);
+      DlLtArgs t = a;
+      t.D = base;
+      if (a.epilogue == DL_LT_GELU_AUX_BIAS) t.aux = base + d_bytes;  // aux is an output there
+      if (a.epilogue == DL_LT_DGELU_BGRAD) t.bias = base + d_bytes + aux_bytes;  // bias-grad output
+      set_ptrs(p.desc, t);
+      hipEvent_t e0, e1;
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+      const float one = 1.f, zero = 0.f;
+      float best_ms = 1e30f;
+      for (int i = 0; i < n; ++i) {
+        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > s->ws_size) continue;
+        auto run = [&]() {
+          return hipblasLtMatmul(s->handle, p.desc, &one, a.B, p.la, a.A, p.lb, &zero, t.D, p.ld, t.D, p.ld,
+                                 &res[i].algo, s->workspace, s->ws_size, st);
+        };
+        if (run() != HIPBLAS_STATUS_SUCCESS) continue;
+        hipEventRecord(e0, st);
+        for (int r = 0; r < 3; ++r) run();
+        hipEventRecord(e1, st);
+        hipEventSynchronize(e1);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best_ms) {
+          best_ms = ms;
+          best = i;
+        }
+      }
+      hipEventDestroy(e0);
+      hipEventDestroy(e1);
+      set_ptrs(p.desc, a);
+    }
+  }
+  p.algo = res[best].algo;
+  p.ws = res[best].workspaceSize;
+  p.ok = true;
+  return true;
+}
+
+}  // namespace
+
+int dl_lt_matmul(const DlLtArgs& a, hipStream_t st) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  Key k{a.transA, a.transB, a.M, a.N, a.K, a.lda, a.ldb, a.ldd, a.ldaux, a.d_f32, a.in_f32, a.beta != 0.f,
+        a.epilogue, a.bias_f32, dev};
+  std::lock_guard<std::mutex> lock(g_mu);
+  DevState* s = dev_state(dev);
+  if (!s) return -2;
+  auto it = g_plans.find(k);
+  if (it == g_plans.end()) {
+    Plan p;
+    if (!build_plan(p, a, s, st)) p.ok = false;
+    it = g_plans.emplace(k, p).first;
+  }
+  Plan& p = it->second;
+  if (!p.ok) return -1;
+  if (!set_ptrs(p.desc, a)) return -3;
+  const float one = 1.f;
+  const float beta = a.beta;
+  const void* C = a.C ? a.C : a.D;
+  const hipblasStatus_t r = hipblasLtMatmul(s->handle, p.desc, &one, a.B, p.la, a.A, p.lb, &beta, C, p.ld, a.D,
+                                            p.ld, &p.algo, s->workspace, s->ws_size, st);
+  return r == HIPBLAS_STATUS_SUCCESS ? 0 : -4;
+}
+
+int dl_lt_plan_count() {
+  std::lock_guard<std::mutex> lock(g_mu);
+  return (int)g_plans.size();
+}

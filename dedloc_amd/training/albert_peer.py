@@ -64,7 +64,8 @@ class AlbertPeer:
     """Everything one GPU peer owns: model, optimizer, DHT node, collaborative optimizer, data."""
 
     def __init__(self, training_args, dataset_args, collab_args, device, pg=None, rank: int = 0,
-                 dht: Optional[DHT] = None, auxiliary: bool = False, publish_only_synchronized: bool = False):
+                 dht: Optional[DHT] = None, auxiliary: bool = False, publish_only_synchronized: bool = False,
+                 impl: str = "dedloc"):
         self.args, self.dargs, self.cargs = training_args, dataset_args, collab_args
         self.device = torch.device(device)
         # per-rank heterogeneity (emulation/heterogeneity.py): micro-batch, speed, bandwidth, client mode
@@ -89,10 +90,21 @@ class AlbertPeer:
         config = AlbertConfig.from_pretrained(dataset_args.config_path)
         if getattr(dataset_args, "vocab_size", None):
             config.vocab_size = dataset_args.vocab_size
-        self.model = get_model(training_args, config)
-        self.model.materialize(self.device)
-        self.model.train()
-        self.opt, self.scheduler = build_optimizer(self.model, training_args)
+        self.impl = impl
+        if impl == "eager":  # PyTorch-eager reference stack (training/eager_baseline.py)
+            from .eager_baseline import EagerAlbertModel, EagerLamb
+
+            self.model = EagerAlbertModel(config, self.device)
+            a = training_args
+            self.opt = EagerLamb(self.model.flat, lr=a.learning_rate, betas=(a.adam_beta1, a.adam_beta2),
+                                 eps=a.adam_epsilon, weight_decay=a.weight_decay, clamp_value=a.clamp_value,
+                                 debias=True, no_decay=self.model.no_decay_names())
+            self.scheduler = get_linear_schedule_with_warmup(self.opt, a.warmup_steps, a.max_steps)
+        else:
+            self.model = get_model(training_args, config)
+            self.model.materialize(self.device)
+            self.model.train()
+            self.opt, self.scheduler = build_optimizer(self.model, training_args)
         ca = collab_args
         validators, self.local_public_key = make_validators(ca.experiment_prefix)
         self.dht = dht or DHT(initial_peers=ca.initial_peers, listen=not ca.client_mode, listen_on=ca.dht_listen_on,
@@ -142,9 +154,13 @@ class AlbertPeer:
             loss = out["loss"] / ga if ga > 1 else out["loss"]
             loss.backward()
             self._loss_sum += loss.detach()
-        torch.ops.dedloc.grad_norm_clip(self._flat.grad, float(a.max_grad_norm or 0.0), self._clip_part,
-                                        self._clip_out)
-        self._drop_if_nonfinite()
+        if self.impl == "eager":
+            if a.max_grad_norm:
+                torch.nn.utils.clip_grad_norm_(self.model.module.parameters(), a.max_grad_norm)
+        else:
+            torch.ops.dedloc.grad_norm_clip(self._flat.grad, float(a.max_grad_norm or 0.0), self._clip_part,
+                                            self._clip_out)
+            self._drop_if_nonfinite()
         self.collab_opt.step(batch_size=self.batch_size_per_step)
         self.opt.zero_grad()
         self.mini_steps += 1

@@ -51,7 +51,8 @@ def _peer(rank, world, port, dht_ep, out_q, cfg, mode=""):
         targs.peer_batch_sizes, targs.peer_slowdowns = "2,1,3", "1,2,1"
         cargs.peer_bandwidths = "200,50,100"
     elif mode == "churn":
-        targs.peer_churn = ";;restart@2:4"  # rank 2 is preempted after global step 2 and respawned 4 s later
+        targs.peer_churn = ";;restart@2:2"  # rank 2 is preempted after global step 2 and respawned 2 s later
+        targs.throttle = 0.1  # keep the survivors training (and serving state) while rank 2 is away
     if late:
         targs.throttle = 0.0
     else:
@@ -70,7 +71,7 @@ def _peer(rank, world, port, dht_ep, out_q, cfg, mode=""):
         else:
             steps = 3 if world == 2 else (6 if late else 12)
             if mode == "churn":
-                steps = 8
+                steps = 8 if rank == 2 else 20
             peer.train(max_steps=600, stop_after_global_steps=steps, max_seconds=60 if mode != "churn" else 90)
             peer.collab_opt._finish_param_round()
         res["local_step"] = peer.collab_opt.local_step
