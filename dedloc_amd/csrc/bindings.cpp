@@ -271,8 +271,15 @@ std::tuple<at::Tensor, at::Tensor> xent_fwd_bwd(const at::Tensor& logits, const 
 }
 
 // ------------------------------------------------------------------ attention
+inline const int* kvinfo_ptr(const c10::optional<at::Tensor>& kvinfo, int64_t B) {
+  if (!kvinfo.has_value()) return nullptr;
+  expect(*kvinfo, at::kInt, "kvinfo");
+  TORCH_CHECK(kvinfo->numel() == B + 1, "kvinfo must be int32[B + 1] (lengths, prefix flag)");
+  return kvinfo->data_ptr<int>();
+}
+
 std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbias, int64_t H,
-                                            int64_t S, double scale) {
+                                            int64_t S, double scale, const c10::optional<at::Tensor>& kvinfo) {
   expect(qkv, at::kBFloat16, "qkv");
   const int64_t ld = qkv.size(-1), T = qkv.numel() / ld, D = ld / (3 * H), B = T / S;
   auto out = at::empty({T, H * D}, qkv.options());
@@ -282,14 +289,15 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& qkv, const c10::op
     expect(*mbias, at::kFloat, "mbias");
     mb = f32(*mbias);
   }
-  check(dl_attn_fwd(cbf(qkv), ld, mb, bf(out), H * D, f32(lse), (int)B, (int)H, (int)S, (int)D, (float)scale,
-                    cur_stream(qkv)),
+  check(dl_attn_fwd(cbf(qkv), ld, mb, kvinfo_ptr(kvinfo, B), bf(out), H * D, f32(lse), (int)B, (int)H, (int)S,
+                    (int)D, (float)scale, cur_stream(qkv)),
         "attn_fwd");
   return {out, lse};
 }
 
 at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbias, const at::Tensor& out,
-                    const at::Tensor& dout, const at::Tensor& lse, int64_t H, int64_t S, double scale) {
+                    const at::Tensor& dout, const at::Tensor& lse, int64_t H, int64_t S, double scale,
+                    const c10::optional<at::Tensor>& kvinfo) {
   expect(qkv, at::kBFloat16, "qkv");
   expect(out, at::kBFloat16, "out");
   expect(dout, at::kBFloat16, "dout");
@@ -297,8 +305,8 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
   auto dqkv = at::empty_like(qkv);
   auto delta = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
   const float* mb = mbias.has_value() ? f32(*mbias) : nullptr;
-  check(dl_attn_bwd(cbf(qkv), ld, mb, cbf(out), cbf(dout), H * D, f32(lse), f32(delta), bf(dqkv), (int)B, (int)H,
-                    (int)S, (int)D, (float)scale, cur_stream(qkv)),
+  check(dl_attn_bwd(cbf(qkv), ld, mb, kvinfo_ptr(kvinfo, B), cbf(out), cbf(dout), H * D, f32(lse), f32(delta),
+                    bf(dqkv), (int)B, (int)H, (int)S, (int)D, (float)scale, cur_stream(qkv)),
         "attn_bwd");
   return dqkv;
 }
@@ -465,16 +473,19 @@ std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tens
                            1, cur_stream(x));
     if (rc == 0) return {H, G};
   }
+  // hipBLASLt on ROCm 7.2 has no gfx950 solution for GELU_AUX_BIAS (scripts/lt_debug.py), so the
+  // library path is a bias-epilogue GEMM (fp32 bias, no cast kernel) + the gelu kernel
   const at::Tensor bias32 = f32_bias(bias);
-  if (lt_ok(x, w)) {  // one hipBLASLt kernel: G = gelu(x W^T + b), aux H = pre-activation
+  if (lt_ok(x, w)) {
     DlLtArgs l = lt_args(x, w, false, true);
-    l.D = G.data_ptr();
-    l.ldd = G.size(1);
-    l.epilogue = DL_LT_GELU_AUX_BIAS;
+    l.D = H.data_ptr();
+    l.ldd = H.size(1);
+    l.epilogue = DL_LT_BIAS;
     l.bias = bias32.data_ptr();
-    l.aux = H.data_ptr();
-    l.ldaux = H.size(1);
-    if (dl_lt_matmul(l, cur_stream(x)) == 0) return {H, G};
+    if (dl_lt_matmul(l, cur_stream(x)) == 0) {
+      check(dl_gelu_fwd(cbf(H), bf(G), H.numel(), cur_stream(H)), "gelu_fwd");
+      return {H, G};
+    }
   }
   H = at::addmm(bias.to(x.scalar_type()), x, w.t()).contiguous();
   check(dl_gelu_fwd(cbf(H), bf(G), H.numel(), cur_stream(H)), "gelu_fwd");
@@ -492,18 +503,18 @@ at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tenso
                            f32(dbias), 1, cur_stream(dy));
     if (rc == 0) return C;
   }
-  if (lt_ok(dy, w) && F.is_contiguous()) {  // one hipBLASLt kernel: dgrad * gelu'(F) + bias grad
-    auto dh = at::empty({dy.size(0), w.size(1)}, dy.options());
-    auto bgrad = at::empty({w.size(1)}, dbias.options());
+  // (hipBLASLt's DGELU_BGRAD epilogue returns wrong results for this layout on ROCm 7.2 —
+  // scripts/lt_debug.py — so the dgrad is a plain GEMM followed by the fused gelu'/bias-grad kernel)
+  if (lt_ok(dy, w)) {
+    auto dg = at::empty({dy.size(0), w.size(1)}, dy.options());
     DlLtArgs l = lt_args(dy, w, false, false);
-    l.D = dh.data_ptr();
-    l.ldd = dh.size(1);
-    l.epilogue = DL_LT_DGELU_BGRAD;
-    l.bias = bgrad.data_ptr();
-    l.aux = const_cast<void*>(F.data_ptr());
-    l.ldaux = F.size(1);
+    l.D = dg.data_ptr();
+    l.ldd = dg.size(1);
     if (dl_lt_matmul(l, cur_stream(dy)) == 0) {
-      check(dl_axpby(f32(dbias), f32(bgrad), dbias.numel(), 1.f, 1.f, nullptr, cur_stream(dy)), "dbias accumulate");
+      auto dh = at::empty_like(dg);
+      check(dl_gelu_bwd_colsum(cbf(dg), cbf(F), bf(dh), f32(dbias), (int)dg.size(0), (int)dg.size(1),
+                               cur_stream(dg)),
+            "gelu_bwd");
       return dh;
     }
   }

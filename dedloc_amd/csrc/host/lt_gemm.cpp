@@ -9,13 +9,15 @@
 // the column-major rows = our output features, exactly what Linear layers need, and the
 // DGELU_BGRAD bias gradient is the sum over tokens.
 //
-// Epilogues used by ALBERT's FFN: GELU_AUX_BIAS (forward: D = gelu(x W^T + b), aux = pre-activation)
-// and DGELU_BGRAD (backward: D = (dy W) * gelu'(aux), bias-grad = colsum(D)); gelu is the tanh form,
-// i.e. HF "gelu_new".  Removes the separate gelu / gelu-backward / bias-grad passes over [T, 4096].
+// Epilogues: BIAS (fp32 bias read in the epilogue — no per-call bias cast kernel) and beta=1
+// accumulation with a separate C (residual-branch sums, fp32 weight-gradient accumulation).
+// GELU_AUX_BIAS / DGELU_BGRAD are wired but NOT used: on ROCm 7.2 / gfx950 the former has no
+// solution and the latter returned wrong results for our layout (scripts/lt_debug.py, measured).
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -136,6 +138,9 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
   const hipblasStatus_t hs =
       hipblasLtMatmulAlgoGetHeuristic(s->handle, p.desc, p.la, p.lb, p.ld, p.ld, pref, want, res.data(), &n);
   hipblasLtMatmulPreferenceDestroy(pref);
+  if (std::getenv("DEDLOC_LT_DEBUG"))
+    std::fprintf(stderr, "[lt] plan ta=%d tb=%d M=%d N=%d K=%d epi=%d d_f32=%d beta=%g: heuristic status %d, %d algos\n",
+                 a.transA, a.transB, a.M, a.N, a.K, a.epilogue, a.d_f32, a.beta, (int)hs, n);
   if (hs != HIPBLAS_STATUS_SUCCESS || n <= 0) return false;
 
   int best = 0;

@@ -68,7 +68,8 @@ int dl_swav_ce(const void* scores, int scores_bf16, const float* q, float* dscor
 int dl_row_normalize(float* w, int rows, int d, hipStream_t st);
 
 // attention.hip
-int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, bf16_t* out, long ldo, float* lse, int B, int H, int S,
-                int D, float scale, hipStream_t st);
-int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const bf16_t* out, const bf16_t* dout, long ldo,
-                const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D, float scale, hipStream_t st);
+int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, bf16_t* out, long ldo, float* lse,
+                int B, int H, int S, int D, float scale, hipStream_t st);
+int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, const bf16_t* out,
+                const bf16_t* dout, long ldo, const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D,
+                float scale, hipStream_t st);

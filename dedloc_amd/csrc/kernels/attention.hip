@@ -104,9 +104,30 @@ __device__ __forceinline__ void store4(bf16_t* p, float a, float b, float c, flo
 }
 
 // ------------------------------------------------------------------------------------------ fwd
+// Key masking comes in two forms.  kvinfo = int32[B + 1] (lengths of right-padded key masks plus a
+// device-side "every mask is a prefix" flag in kvinfo[B], computed by the model without a host
+// sync): then tiles past the batch's length are skipped and only the boundary tile is masked.
+// Otherwise (or when kvinfo[B] == 0) the generic additive bias mbias[B, S] (log2 units) is used.
+// Interior tiles run the lean softmax: one FMA (scale, -max) + exp2 + add per score, row max via
+// max3, and the online-softmax rescale of O is deferred until a row's max grows by more than
+// 2^RESCALE_THR (cdna_hip_programming.md T13: P <= 2^8 is exact enough in bf16 for P.V; the
+// rescale decision precedes the tile's exponentiation, so nothing is ever scaled twice).
+constexpr float RESCALE_THR = 8.f;
+
+__device__ __forceinline__ int kv_end_of(const int* kvinfo, int B, int b, int S, bool& use_len) {
+  use_len = false;
+  if (kvinfo == nullptr || kvinfo[B] == 0) return S;
+  const int len = kvinfo[b];
+  if (len <= 0 || len > S) return S;  // empty / malformed rows take the generic path
+  use_len = true;
+  return len;
+}
+
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
-                                                          const float* __restrict__ mbias, bf16_t* __restrict__ out,
-                                                          long ldo, float* __restrict__ lse, int H, int S, float sl2) {
+                                                          const float* __restrict__ mbias,
+                                                          const int* __restrict__ kvinfo, bf16_t* __restrict__ out,
+                                                          long ldo, float* __restrict__ lse, int B, int H, int S,
+                                                          float sl2) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
@@ -114,7 +135,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   const bf16_t* Qg = qkv + rb * ld + h * HD;
   const bf16_t* Kg = qkv + rb * ld + (long)H * HD + h * HD;
   const bf16_t* Vg = qkv + rb * ld + 2L * H * HD + h * HD;
-  const float* mb_g = mbias ? mbias + rb : nullptr;
+  bool use_len;
+  const int kv_end = kv_end_of(kvinfo, B, b, S, use_len);
+  const float* mb_g = (!use_len && mbias) ? mbias + rb : nullptr;
   float* mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
 
   const int q = blockIdx.x * 128 + w * 32 + r;
@@ -130,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
   float m = NEG_BIG, l = 0.f;
 
-  const int nt = S / 64;
+  const int nt = (kv_end + 63) / 64;
   TileRegs kr, vr;
   float mbr = 0.f;
   tile_load(kr, Kg, ld, 0, S);
@@ -159,34 +182,47 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) s[j] = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], s[j]);
     }
+    // fold the additive mask into the raw scores only where one exists (bias path / boundary tile)
+    const bool lean = mb_g == nullptr && (kt + 1) * 64 <= kv_end;
+    if (!lean) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kt * 64 + 32 * j + crow(i, hh);
+          const float bias = mb_g ? mb[32 * j + crow(i, hh)] : (key < kv_end ? 0.f : NEG_BIG);
+          s[j][i] = s[j][i] * sl2 + bias;
+        }
+    }
+    const float sc = lean ? sl2 : 1.f;  // lean tiles keep raw scores; scaled inside the exp FMA
     float mx = NEG_BIG;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float v = s[j][i] * sl2 + mb[32 * j + crow(i, hh)];
-        s[j][i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      for (int i = 0; i < 16; i += 2) mx = fmaxf(mx, fmaxf(s[j][i], s[j][i + 1]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sc;
+    const bool grow = mx > m + RESCALE_THR;
+    if (__ballot(grow) != 0) {
+      const float mn = grow ? mx : m;
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
+    }
     float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[j][i] - mn);
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[j][i], sc, -m));
         s[j][i] = p;
         rs += p;
       }
     rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
+    l += rs;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -221,10 +257,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
 // Also computes delta = rowsum(dO * O) for its queries and publishes it for the dkdv kernel.
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                              const float* __restrict__ mbias,
+                                                             const int* __restrict__ kvinfo,
                                                              const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
                                                              long ldo, const float* __restrict__ lse,
                                                              float* __restrict__ delta, bf16_t* __restrict__ dqkv,
-                                                             int H, int S, float sl2, float scale) {
+                                                             int B, int H, int S, float sl2, float scale) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
@@ -232,7 +269,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
   const bf16_t* Qg = qkv + rb * ld + h * HD;
   const bf16_t* Kg = qkv + rb * ld + (long)H * HD + h * HD;
   const bf16_t* Vg = qkv + rb * ld + 2L * H * HD + h * HD;
-  const float* mb_g = mbias ? mbias + rb : nullptr;
+  bool use_len;
+  const int kv_end = kv_end_of(kvinfo, B, b, S, use_len);
+  const float* mb_g = (!use_len && mbias) ? mbias + rb : nullptr;
   float* mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
 
   const int q = blockIdx.x * 128 + w * 32 + r;
@@ -258,7 +297,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
 
-  const int nt = S / 64;
+  const int nt = (kv_end + 63) / 64;
   TileRegs kr, vr;
   float mbr = 0.f;
   tile_load(kr, Kg, ld, 0, S);
@@ -289,10 +328,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
         st = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], st);
         dp = mfma32(lds_row_frag(Vs, 32 * j + r, 2 * ks + hh), df[ks], dp);
       }
+      if (mb_g == nullptr && (kt + 1) * 64 <= kv_end) {  // interior tile: no mask
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(st[i] * sl2 + mb[32 * j + crow(i, hh)] - l2);
-        st[i] = p * (dp[i] - dl);
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[i], sl2, -l2));
+          st[i] = p * (dp[i] - dl);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kt * 64 + 32 * j + crow(i, hh);
+          const float bias = mb_g ? mb[32 * j + crow(i, hh)] : (key < kv_end ? 0.f : NEG_BIG);
+          const float p = __builtin_amdgcn_exp2f(st[i] * sl2 + bias - l2);
+          st[i] = p * (dp[i] - dl);
+        }
       }
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
@@ -323,11 +372,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
 // ------------------------------------------------------------------------------------------ bwd dkdv
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                                const float* __restrict__ mbias,
+                                                               const int* __restrict__ kvinfo,
                                                                const bf16_t* __restrict__ dout, long ldo,
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
-                                                               bf16_t* __restrict__ dqkv, int H, int S, float sl2,
-                                                               float scale) {
+                                                               bf16_t* __restrict__ dqkv, int B, int H, int S,
+                                                               float sl2, float scale) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 2 * 64 * 4];
   const int b = blockIdx.z, h = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
@@ -342,13 +392,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 
   const int k = blockIdx.x * 128 + w * 32 + r;
   const int kc = min(k, S - 1);
+  bool use_len;
+  const int kv_end = kv_end_of(kvinfo, B, b, S, use_len);
+  if (use_len && blockIdx.x * 128 >= kv_end) {  // every key of this block is padding: dK = dV = 0
+    if (k < S) {
+      bf16_t* dkp = dqkv + (rb + k) * ld + (long)H * HD + h * HD;
+      bf16_t* dvp = dqkv + (rb + k) * ld + 2L * H * HD + h * HD;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        store4(dkp + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
+        store4(dvp + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
+        store4(dkp + 32 + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
+        store4(dvp + 32 + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    return;
+  }
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     kf[ks] = gload8(Kg + (long)kc * ld + ks * 16 + 8 * hh);
     vf[ks] = gload8(Vg + (long)kc * ld + ks * 16 + 8 * hh);
   }
-  const float mbk = mbias ? mbias[rb + kc] : 0.f;
+  const float mbk = use_len ? (k < kv_end ? 0.f : NEG_BIG) : (mbias ? mbias[rb + kc] : 0.f);
 
   floatx16 dk[2], dv[2];
 #pragma unroll
@@ -431,21 +497,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 
 }  // namespace
 
-int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, bf16_t* out, long ldo, float* lse, int B, int H, int S,
-                int D, float scale, hipStream_t st) {
+int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, bf16_t* out, long ldo, float* lse,
+                int B, int H, int S, int D, float scale, hipStream_t st) {
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid((S + 127) / 128, H, B);
-  attn_fwd_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, out, ldo, lse, H, S, sl2);
+  attn_fwd_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2);
   return 0;
 }
 
-int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const bf16_t* out, const bf16_t* dout, long ldo,
-                const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D, float scale, hipStream_t st) {
+int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, const bf16_t* out,
+                const bf16_t* dout, long ldo, const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D,
+                float scale, hipStream_t st) {
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid((S + 127) / 128, H, B);
-  attn_bwd_dq_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, out, dout, ldo, lse, delta, dqkv, H, S, sl2, scale);
-  attn_bwd_dkdv_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, dout, ldo, lse, delta, dqkv, H, S, sl2, scale);
+  attn_bwd_dq_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, B, H, S, sl2,
+                                           scale);
+  attn_bwd_dkdv_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2, scale);
   return 0;
 }

@@ -112,17 +112,18 @@ class _AlbertLayerFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, h, mbias, lv, H, S, eps):
+    def forward(ctx, h, mask, lv, H, S, eps):
         O = ops.OPS
+        mbias, kvinfo = mask
         qkv = O.gemm(h, lv["wqkv"], lv["bqkv32"], None, False, True, 0)
-        att, lse = O.attn_fwd(qkv, mbias, H, S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)))
+        att, lse = O.attn_fwd(qkv, mbias, H, S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)), kvinfo)
         a = O.gemm(att, lv["wo"], lv["bo32"], None, False, True, 0)
         h1, s1, m1, r1 = O.layernorm_fwd(a, h, lv["ln1g"], lv["ln1b"], eps)
         f, g = O.gemm_gelu(h1, lv["w1"], lv["b132"])  # bias + gelu_new fused in the GEMM epilogue
         f2 = O.gemm(g, lv["w2"], lv["b232"], None, False, True, 0)
         out, s2, m2, r2 = O.layernorm_fwd(f2, h1, lv["ln2g"], lv["ln2b"], eps)
         ctx.save_for_backward(h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2)
-        ctx.lv, ctx.mbias, ctx.H, ctx.S = lv, mbias, H, S
+        ctx.lv, ctx.mask, ctx.H, ctx.S = lv, mask, H, S
         return out
 
     @staticmethod
@@ -142,7 +143,8 @@ class _AlbertLayerFn(torch.autograd.Function):
         O.gemm_acc_f32(ds1, att, lv["gwo"], True, False)
         datt = O.gemm(ds1, lv["wo"], None, None, False, False, 0)
         H = ctx.H
-        dqkv = O.attn_bwd(qkv, ctx.mbias, att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)))
+        dqkv = O.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
+                          ctx.mask[1])
         O.gemm_acc_f32(dqkv, h, lv["gwqkv"], True, False)
         O.bias_grad(dqkv, lv["gbqkv"], True)
         dh = O.gemm(dqkv, lv["wqkv"], None, ds1, False, False, 0)
@@ -305,9 +307,9 @@ class AlbertForPreTraining(nn.Module):
             gln2g=f.g(pre + "full_layer_layer_norm.weight"), gln2b=f.g(pre + "full_layer_layer_norm.bias"),
         )
 
-    def _albert_layer(self, h, lv, mbias, S):
+    def _albert_layer(self, h, lv, mask, S):
         c = self.config
-        return _AlbertLayerFn.apply(h, mbias, lv, c.num_attention_heads, S, c.layer_norm_eps)
+        return _AlbertLayerFn.apply(h, mask, lv, c.num_attention_heads, S, c.layer_norm_eps)
 
     def encode(self, input_ids, attention_mask=None, token_type_ids=None):
         """Returns (sequence_output [B*S', H] bf16, S') where S' is S padded to a multiple of 64."""
@@ -324,7 +326,14 @@ class AlbertForPreTraining(nn.Module):
             if token_type_ids is not None:
                 token_type_ids = F.pad(token_type_ids, (0, pad), value=0)
         assert Sp <= c.max_position_embeddings, "sequence longer than max_position_embeddings"
-        mbias = torch.where(attention_mask.bool(), 0.0, NEG_BIG).to(torch.float32).contiguous()
+        am = attention_mask.bool()
+        mbias = torch.where(am, 0.0, NEG_BIG).to(torch.float32).contiguous()
+        # right-padded masks (the usual case) let the attention kernels skip padded key tiles: pass
+        # the lengths plus an on-device "every row is a prefix mask" flag (no host sync)
+        lens = am.sum(1, dtype=torch.int32)
+        prefix = (am == (torch.arange(Sp, device=am.device) < lens[:, None])).all()
+        kvinfo = torch.cat([lens, prefix.to(torch.int32).view(1)]).contiguous()
+        mask = (mbias, kvinfo)
         emb = "albert.embeddings."
         x = ops.embed_layernorm(
             input_ids, token_type_ids, f.p(emb + "word_embeddings.weight"), f.p(emb + "position_embeddings.weight"),
@@ -340,7 +349,7 @@ class AlbertForPreTraining(nn.Module):
         for layer in range(c.num_hidden_layers):
             g = int(layer / per_group)
             for i in range(c.inner_group_num):
-                h = self._albert_layer(h, views[g][i], mbias, Sp)
+                h = self._albert_layer(h, views[g][i], mask, Sp)
         return h, Sp
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, labels=None, sentence_order_label=None,

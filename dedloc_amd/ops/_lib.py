@@ -36,8 +36,9 @@ _SCHEMAS = [
     "embed_ln_fwd(Tensor ids, Tensor? tt, Tensor wemb, Tensor pemb, Tensor temb, Tensor gamma, Tensor beta, int S, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
     "embed_bwd(Tensor ds, Tensor ids, Tensor? tt, Tensor(a!) dwemb, Tensor(b!) dpemb, Tensor(c!) dtemb, int S) -> ()",
     "xent_fwd_bwd(Tensor logits, Tensor labels, bool inplace, int ignore_index) -> (Tensor, Tensor)",
-    "attn_fwd(Tensor qkv, Tensor? mbias, int H, int S, float scale) -> (Tensor, Tensor)",
-    "attn_bwd(Tensor qkv, Tensor? mbias, Tensor out, Tensor dout, Tensor lse, int H, int S, float scale) -> Tensor",
+    "attn_fwd(Tensor qkv, Tensor? mbias, int H, int S, float scale, Tensor? kvinfo=None) -> (Tensor, Tensor)",
+    "attn_bwd(Tensor qkv, Tensor? mbias, Tensor out, Tensor dout, Tensor lse, int H, int S, float scale, "
+    "Tensor? kvinfo=None) -> Tensor",
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
     "gemm_gelu(Tensor x, Tensor w, Tensor bias) -> (Tensor, Tensor)",
@@ -328,7 +329,7 @@ def _attn_probs(qkv, mbias, H, S, scale):
 
 
 @_impl("attn_fwd")
-def _attn_fwd_cpu(qkv, mbias, H, S, scale):
+def _attn_fwd_cpu(qkv, mbias, H, S, scale, kvinfo=None):
     q, k, v, s = _attn_probs(qkv, mbias, H, S, scale)
     B, _, _, D = q.shape
     lse = torch.logsumexp(s, -1)
@@ -338,7 +339,7 @@ def _attn_fwd_cpu(qkv, mbias, H, S, scale):
 
 
 @_impl("attn_bwd")
-def _attn_bwd_cpu(qkv, mbias, out, dout, lse, H, S, scale):
+def _attn_bwd_cpu(qkv, mbias, out, dout, lse, H, S, scale, kvinfo=None):
     q, k, v, s = _attn_probs(qkv, mbias, H, S, scale)
     B, _, _, D = q.shape
     p = torch.softmax(s, -1)

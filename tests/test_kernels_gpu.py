@@ -100,6 +100,75 @@ def test_attention_large_logits(cuda):
     assert rel(out, ref) < 1.5e-2
 
 
+def _kvinfo(mask):
+    lens = mask.sum(1).int()
+    prefix = (mask.bool() == (torch.arange(mask.shape[1], device=mask.device) < lens[:, None])).all()
+    return torch.cat([lens, prefix.int().view(1)]).contiguous()
+
+
+@pytest.mark.parametrize("lens", [(256, 200, 64, 37), (256, 256, 256, 256), (1, 65, 128, 255)])
+def test_attention_kv_lengths(cuda, lens):
+    """Right-padded masks via kvinfo: padded key tiles are skipped, the boundary tile is masked."""
+    torch.manual_seed(3)
+    B, H, S, D = len(lens), 2, 256, 64
+    qkv = (torch.randn(B * S, 3 * H * D, device=cuda) * 1.5).bfloat16()
+    mask = (torch.arange(S, device=cuda)[None, :] < torch.tensor(lens, device=cuda)[:, None]).long()
+    mbias = torch.where(mask.bool(), 0.0, -1e30).float()
+    kvinfo = _kvinfo(mask)
+    assert kvinfo[-1].item() == 1
+    out, lse = OPS.attn_fwd(qkv, mbias, H, S, 1 / math.sqrt(D), kvinfo)
+    out_b, _ = OPS.attn_fwd(qkv, mbias, H, S, 1 / math.sqrt(D))  # generic bias path
+    qkv_r = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qkv_r, mask, H, S)
+    assert rel(out, ref) < 1.5e-2, rel(out, ref)
+    assert rel(out, out_b) < 1e-2
+    dout = torch.randn_like(out)
+    dqkv = OPS.attn_bwd(qkv, mbias, out, dout, lse, H, S, 1 / math.sqrt(D), kvinfo)
+    g_ref = torch.autograd.grad(ref, qkv_r, dout.float())[0]
+    for part in range(3):
+        sl = slice(part * H * D, (part + 1) * H * D)
+        assert rel(dqkv[:, sl], g_ref[:, sl]) < 3e-2, (part, rel(dqkv[:, sl], g_ref[:, sl]))
+    # keys past a row's length get exactly zero dK / dV
+    for b, n in enumerate(lens):
+        if n < S:
+            assert dqkv[b * S + n:(b + 1) * S, H * D:].abs().max().item() == 0.0
+
+
+def test_attention_non_prefix_mask_falls_back_to_bias(cuda):
+    torch.manual_seed(4)
+    B, H, S, D = 2, 2, 128, 64
+    qkv = torch.randn(B * S, 3 * H * D, device=cuda).bfloat16()
+    mask = torch.ones(B, S, device=cuda, dtype=torch.long)
+    mask[0, 10:20] = 0  # a hole: not a prefix mask
+    mbias = torch.where(mask.bool(), 0.0, -1e30).float()
+    kvinfo = _kvinfo(mask)
+    assert kvinfo[-1].item() == 0
+    out, lse = OPS.attn_fwd(qkv, mbias, H, S, 1 / math.sqrt(D), kvinfo)
+    ref = _attn_ref(qkv.float(), mask, H, S)
+    assert rel(out, ref) < 1.5e-2
+
+
+def test_attention_deferred_rescale_ramp(cuda):
+    """Data-dependent deferred-max rescale: key magnitudes ramp up tile by tile, at different rates per
+    head, so some rows cross the rescale threshold at different tiles and others never do."""
+    torch.manual_seed(5)
+    B, H, S, D = 2, 4, 512, 64
+    qkv = torch.randn(B * S, 3 * H * D, device=cuda)
+    ramp = 1.0 + torch.arange(S, device=cuda).float() / 64.0  # grows per 64-key tile
+    for h in range(H):
+        cols = slice(H * D + h * D, H * D + (h + 1) * D)
+        qkv[:, cols] *= (ramp.repeat(B) ** (0.5 * h))[:, None]
+    qkv = qkv.bfloat16()
+    out, lse = OPS.attn_fwd(qkv, None, H, S, 1 / math.sqrt(D))
+    qkv_r = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qkv_r, torch.ones(B, S, device=cuda), H, S)
+    assert rel(out, ref) < 1.5e-2, rel(out, ref)
+    dout = torch.randn_like(out)
+    dqkv = OPS.attn_bwd(qkv, None, out, dout, lse, H, S, 1 / math.sqrt(D))
+    g_ref = torch.autograd.grad(ref, qkv_r, dout.float())[0]
+    assert rel(dqkv, g_ref) < 3e-2
+
+
 def test_embedding(cuda):
     torch.manual_seed(2)
     B, S, E, V = 4, 128, 128, 1000
