@@ -31,9 +31,11 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 METRIC = "samples/sec (whole node) ALBERT-large MLM pretrain at 1/2/4/8 peers"
-# Measured PyTorch-eager reference on MI355X (HF AlbertForPreTraining, bf16 autocast, SDPA, eager
-# torch LAMB; bench/model_step.py --impl hf --with_optimizer), samples/s per GPU.  BASELINE.md.
-EAGER_BASELINE_SPS_PER_GPU = None
+# Measured PyTorch-eager reference on MI355X: the reference's compute stack (HF AlbertForPreTraining,
+# bf16 autocast, SDPA attention, per-tensor torch LAMB, clip_grad_norm_) driven by this repo's
+# collaborative engine — `python bench.py --impl eager` (training/eager_baseline.py), samples/s per
+# GPU at N=1, micro-batch 64 (BASELINE.md "Measured MI355X results").  vs_baseline = value / (this x N).
+EAGER_BASELINE_SPS_PER_GPU = 263.48
 
 
 def parse():

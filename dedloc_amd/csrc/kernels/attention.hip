@@ -123,6 +123,116 @@ __device__ __forceinline__ int kv_end_of(const int* kvinfo, int B, int b, int S,
   return len;
 }
 
+// v_max3_f32 without the canonicalising v_max the compiler inserts in front of fmaxf on MFMA results
+// (MI355X_MICROARCH.md pitfalls): one instruction per two new scores
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Forward tile loop over key tiles [kt0, kt1) of nt, with the next tile's K/V (and per-key bias)
+// prefetched through registers while this tile computes (T14).  Tile kt0 must already be staged.
+// LEAN: unmasked tiles — raw scores, the softmax scale rides in the exp FMA, no bias reads.
+// !LEAN: s = s*sl2 + bias[key] with the bias staged in LDS (additive mask or 0/-1e30 from the
+// key length).  The two instantiations run as consecutive loops (lean body, then the boundary
+// tile), never in one loop body, so they do not add register pressure to each other.
+struct FwdCtx {
+  const bf16_t* Kg;
+  const bf16_t* Vg;
+  long ld;
+  int S, kv_end;
+  const float* mb_g;
+  float sl2;
+  uint8_t* smem;
+  float* mbs;
+};
+
+__device__ __forceinline__ float key_bias(const FwdCtx& c, int key) {
+  return c.mb_g ? c.mb_g[key] : (key < c.kv_end ? 0.f : NEG_BIG);
+}
+
+template <bool LEAN>
+__device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int nt, const bf16x8 (&qf)[4],
+                                          floatx16 (&o)[2], float& m, float& l, int r, int hh, int lane) {
+  TileRegs kr, vr;
+  float mbr = 0.f;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int cur = kt & 1;
+    const uint8_t* Ks = c.smem + cur * 2 * TILE_BYTES;
+    const uint8_t* Vs = Ks + TILE_BYTES;
+    const float* mb = c.mbs + cur * 64;
+    const bool more = kt + 1 < nt;
+    if (more) {  // issue next tile's loads early; they land under the MFMAs below
+      tile_load(kr, c.Kg, c.ld, (kt + 1) * 64, c.S);
+      tile_load(vr, c.Vg, c.ld, (kt + 1) * 64, c.S);
+      if (threadIdx.x < 64) mbr = key_bias(c, (kt + 1) * 64 + threadIdx.x);
+    }
+    floatx16 s[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[j][i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[j] = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], s[j]);
+    }
+    if (!LEAN) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[j][i] = fmaf(s[j][i], c.sl2, mb[32 * j + crow(i, hh)]);
+    }
+    float mx = vmax3(s[0][0], s[0][1], s[0][2]);
+#pragma unroll
+    for (int i = 3; i < 15; i += 2) mx = vmax3(mx, s[0][i], s[0][i + 1]);
+    mx = vmax3(mx, s[0][15], s[1][0]);
+#pragma unroll
+    for (int i = 1; i < 15; i += 2) mx = vmax3(mx, s[1][i], s[1][i + 1]);
+    mx = fmaxf(mx, s[1][15]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (LEAN) mx *= c.sl2;
+    const bool grow = mx > m + RESCALE_THR;
+    if (__ballot(grow) != 0) {  // rare after the first tile: rescale O and l to the new max
+      const float mn = grow ? mx : m;
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
+    }
+    const float nm = -m;
+    float rsa[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent add chains (latency, not issue, bound)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(LEAN ? fmaf(s[j][i], c.sl2, nm) : s[j][i] + nm);
+        s[j][i] = p;
+        rsa[i & 3] += p;
+      }
+    float rs = (rsa[0] + rsa[1]) + (rsa[2] + rsa[3]);
+    rs += __shfl_xor(rs, 32, 64);
+    l += rs;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(s[j], ss);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) o[t] = mfma32(tr_operand(Vs, 32 * j + 16 * ss, hh, t, lane), pb, o[t]);
+      }
+    if (more) {
+      uint8_t* Kn = c.smem + (cur ^ 1) * 2 * TILE_BYTES;
+      tile_store(kr, Kn);
+      tile_store(vr, Kn + TILE_BYTES);
+      if (threadIdx.x < 64) c.mbs[(cur ^ 1) * 64 + threadIdx.x] = mbr;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                           const float* __restrict__ mbias,
                                                           const int* __restrict__ kvinfo, bf16_t* __restrict__ out,
@@ -133,12 +243,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
   const long rb = (long)b * S;
   const bf16_t* Qg = qkv + rb * ld + h * HD;
-  const bf16_t* Kg = qkv + rb * ld + (long)H * HD + h * HD;
-  const bf16_t* Vg = qkv + rb * ld + 2L * H * HD + h * HD;
   bool use_len;
-  const int kv_end = kv_end_of(kvinfo, B, b, S, use_len);
-  const float* mb_g = (!use_len && mbias) ? mbias + rb : nullptr;
-  float* mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
+  FwdCtx c;
+  c.Kg = qkv + rb * ld + (long)H * HD + h * HD;
+  c.Vg = qkv + rb * ld + 2L * H * HD + h * HD;
+  c.ld = ld;
+  c.S = S;
+  c.kv_end = kv_end_of(kvinfo, B, b, S, use_len);
+  c.mb_g = (!use_len && mbias) ? mbias + rb : nullptr;
+  c.sl2 = sl2;
+  c.smem = smem;
+  c.mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
 
   const int q = blockIdx.x * 128 + w * 32 + r;
   const int qc = min(q, S - 1);
@@ -153,92 +268,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
   float m = NEG_BIG, l = 0.f;
 
-  const int nt = (kv_end + 63) / 64;
-  TileRegs kr, vr;
-  float mbr = 0.f;
-  tile_load(kr, Kg, ld, 0, S);
-  tile_load(vr, Vg, ld, 0, S);
-  if (threadIdx.x < 64) mbr = mb_g ? mb_g[threadIdx.x] : 0.f;
-  tile_store(kr, smem);
-  tile_store(vr, smem + TILE_BYTES);
-  if (threadIdx.x < 64) mbs[threadIdx.x] = mbr;
-  __syncthreads();
-
-  for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
-    const uint8_t* Ks = smem + cur * 2 * TILE_BYTES;
-    const uint8_t* Vs = Ks + TILE_BYTES;
-    const float* mb = mbs + cur * 64;
-    if (kt + 1 < nt) {  // issue next tile's loads early; they land under the MFMAs below (T14)
-      tile_load(kr, Kg, ld, (kt + 1) * 64, S);
-      tile_load(vr, Vg, ld, (kt + 1) * 64, S);
-      if (threadIdx.x < 64) mbr = mb_g ? mb_g[(kt + 1) * 64 + threadIdx.x] : 0.f;
-    }
-    floatx16 s[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[j][i] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) s[j] = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], s[j]);
-    }
-    // fold the additive mask into the raw scores only where one exists (bias path / boundary tile)
-    const bool lean = mb_g == nullptr && (kt + 1) * 64 <= kv_end;
-    if (!lean) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = kt * 64 + 32 * j + crow(i, hh);
-          const float bias = mb_g ? mb[32 * j + crow(i, hh)] : (key < kv_end ? 0.f : NEG_BIG);
-          s[j][i] = s[j][i] * sl2 + bias;
-        }
-    }
-    const float sc = lean ? sl2 : 1.f;  // lean tiles keep raw scores; scaled inside the exp FMA
-    float mx = NEG_BIG;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) mx = fmaxf(mx, fmaxf(s[j][i], s[j][i + 1]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * sc;
-    const bool grow = mx > m + RESCALE_THR;
-    if (__ballot(grow) != 0) {
-      const float mn = grow ? mx : m;
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      l *= alpha;
-      m = mn;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
-    }
-    float rs = 0.f;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[j][i], sc, -m));
-        s[j][i] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 32, 64);
-    l += rs;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack_acc(s[j], ss);
-#pragma unroll
-        for (int t = 0; t < 2; ++t) o[t] = mfma32(tr_operand(Vs, 32 * j + 16 * ss, hh, t, lane), pb, o[t]);
-      }
-    if (kt + 1 < nt) {
-      uint8_t* Kn = smem + (cur ^ 1) * 2 * TILE_BYTES;
-      tile_store(kr, Kn);
-      tile_store(vr, Kn + TILE_BYTES);
-      if (threadIdx.x < 64) mbs[(cur ^ 1) * 64 + threadIdx.x] = mbr;
-    }
-    __syncthreads();
+  const int nt = (c.kv_end + 63) / 64;
+  {
+    TileRegs kr, vr;
+    tile_load(kr, c.Kg, ld, 0, S);
+    tile_load(vr, c.Vg, ld, 0, S);
+    const float mbr = threadIdx.x < 64 ? key_bias(c, threadIdx.x) : 0.f;
+    tile_store(kr, smem);
+    tile_store(vr, smem + TILE_BYTES);
+    if (threadIdx.x < 64) c.mbs[threadIdx.x] = mbr;
   }
+  __syncthreads();
+  // lean tiles first (every tile when there is no mask), then the masked remainder: the boundary
+  // tile of a length mask, or all tiles of a generic additive mask
+  const int nlean = c.mb_g ? 0 : c.kv_end / 64;
+  fwd_tiles<true>(c, 0, nlean, nt, qf, o, m, l, r, hh, lane);
+  fwd_tiles<false>(c, nlean, nt, nt, qf, o, m, l, r, hh, lane);
 
   if (q < S) {
     const float inv = 1.f / l;
@@ -399,11 +444,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
       bf16_t* dkp = dqkv + (rb + k) * ld + (long)H * HD + h * HD;
       bf16_t* dvp = dqkv + (rb + k) * ld + 2L * H * HD + h * HD;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 8; ++u) {  // the same 64 columns the regular epilogue covers (32t + 8u' + 4hh)
         store4(dkp + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
         store4(dvp + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
-        store4(dkp + 32 + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
-        store4(dvp + 32 + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
       }
     }
     return;
