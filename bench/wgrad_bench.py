@@ -51,6 +51,11 @@ def main():
         os.environ["DEDLOC_GEMM"] = "mfma"
         rec("mfma_auto", lambda: O.gemm_acc_f32(dy, x, g, True, False))
         os.environ.pop("DEDLOC_GEMM", None)
+        for sp in (2, 4, 8):  # batched split-K through the library: [sp, N, K] partials + a sum
+            dyv = dy.view(sp, T // sp, N).transpose(1, 2)
+            xv = x.view(sp, T // sp, K)
+            rec(f"bmm_split{sp}", lambda: g.add_(torch.bmm(dyv, xv).sum(0)))
+            rec(f"bmm_split{sp}_only", lambda: torch.bmm(dyv, xv))
         for L in (2, 4):  # K-concatenated reduction over L layers (per-layer cost reported)
             xx = torch.randn(L * T, K, device=dev).bfloat16()
             dd = torch.randn(L * T, N, device=dev).bfloat16()

@@ -433,11 +433,23 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
   return c;
 }
 
+// Weight gradients (dW[N_out, K_in] += dY^T X over T tokens) have few output tiles and a very long
+// reduction, which under-fills 256 CUs.  Split the token dimension into S slices run as ONE strided
+// batched hipBLASLt GEMM into fp32 partial slabs, then add the slabs into the fp32 gradient:
+// measured at T=32768 (bench/wgrad_bench.py) 1024x1024: 174 -> ~80 us, 4096x1024: 307 -> ~280 us,
+// 3072x1024: 244 -> ~200 us.  S = largest power of two <= min(8, 256 / #256x256-tiles).
+int wgrad_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  int s = 1;
+  while (s < 8 && tiles * s * 2 <= 256 && K % (s * 2 * 64) == 0 && K / (s * 2) >= 1024) s *= 2;
+  return s;
+}
+
 void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b) {
   expect(c, at::kFloat, "c");
   const Mat Av = a_view(a, trans_a), Bv = b_view(b, trans_b);
   const int64_t ntiles = ((Av.rows + 255) / 256) * ((Bv.rows + 255) / 256);
-  if (mfma_ok(a, b) && (force_mfma_gemm() || ntiles <= 16)) {
+  if (force_mfma_gemm() && mfma_ok(a, b)) {
     const Mat A = Av, B = Bv;
     TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
     // split the reduction so that at least ~2 workgroups per CU exist (wgrad: few output tiles,
@@ -451,11 +463,36 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
   }
   if (lt_ok(a, b) && c.stride(1) == 1) {
     DlLtArgs l = lt_args(a, b, trans_a, trans_b);
+    const int S = (trans_a && !trans_b && c.is_contiguous()) ? wgrad_splits(l.M, l.N, l.K) : 1;
+    if (S > 1) {  // token-split batched GEMM into fp32 slabs + slab sum
+      auto slabs = at::empty({S, l.M, l.N}, c.options());
+      const long kslice = l.K / S;
+      l.K = (int)kslice;
+      l.batch = S;
+      l.strideA = kslice * l.lda;  // A = dY stored [T, M]: slice s starts at row s*kslice
+      l.strideB = kslice * l.ldb;  // B = X stored [T, N]
+      l.strideD = (long)l.M * l.N;
+      l.D = slabs.data_ptr();
+      l.ldd = l.N;
+      l.d_f32 = 1;
+      if (dl_lt_matmul(l, cur_stream(a)) == 0) {
+        check(dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), cur_stream(a)), "sum_slabs");
+        return;
+      }
+      l = lt_args(a, b, trans_a, trans_b);
+    }
     l.D = c.data_ptr();
     l.ldd = c.stride(0);
     l.d_f32 = 1;
     l.beta = 1.f;
     if (dl_lt_matmul(l, cur_stream(a)) == 0) return;
+  }
+  if (mfma_ok(a, b) && ntiles <= 16) {
+    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(Av.k / 1024, (512 + ntiles - 1) / ntiles));
+    const int rc = dl_gemm(Av.kouter, Bv.kouter, 3, cbf(a), Av.ld, cbf(b), Bv.ld, (int)Av.rows, (int)Bv.rows,
+                           (int)Av.k, nullptr, 0, f32(c), c.stride(0), nullptr, nullptr, 0, nullptr, 0, nullptr,
+                           splits, cur_stream(a));
+    if (rc == 0) return;
   }
   const at::Tensor A = trans_a ? a.t() : a;
   const at::Tensor B = trans_b ? b.t() : b;

@@ -32,11 +32,12 @@ namespace {
 struct Key {
   int ta, tb, M, N, K;
   long lda, ldb, ldd, ldaux;
-  int d_f32, in_f32, beta_nz, epi, bias_f32, dev;
+  int d_f32, in_f32, beta_nz, epi, bias_f32, dev, batch;
+  long sA, sB, sD;
   bool operator<(const Key& o) const {
-    return std::tie(ta, tb, M, N, K, lda, ldb, ldd, ldaux, d_f32, in_f32, beta_nz, epi, bias_f32, dev) <
-           std::tie(o.ta, o.tb, o.M, o.N, o.K, o.lda, o.ldb, o.ldd, o.ldaux, o.d_f32, o.in_f32, o.beta_nz, o.epi,
-                    o.bias_f32, o.dev);
+    return std::tie(ta, tb, M, N, K, lda, ldb, ldd, ldaux, d_f32, in_f32, beta_nz, epi, bias_f32, dev, batch, sA, sB,
+                    sD) < std::tie(o.ta, o.tb, o.M, o.N, o.K, o.lda, o.ldb, o.ldd, o.ldaux, o.d_f32, o.in_f32,
+                                   o.beta_nz, o.epi, o.bias_f32, o.dev, o.batch, o.sA, o.sB, o.sD);
   }
 };
 
@@ -125,6 +126,16 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
   if (hipblasLtMatrixLayoutCreate(&p.la, in_t, a_rows, a_cols, a.ldb) != HIPBLAS_STATUS_SUCCESS) return false;
   if (hipblasLtMatrixLayoutCreate(&p.lb, in_t, b_rows, b_cols, a.lda) != HIPBLAS_STATUS_SUCCESS) return false;
   if (hipblasLtMatrixLayoutCreate(&p.ld, d_t, a.N, a.M, a.ldd) != HIPBLAS_STATUS_SUCCESS) return false;
+  if (a.batch > 1) {
+    const int32_t bc = a.batch;
+    const int64_t sa = a.strideB, sb = a.strideA, sd = a.strideD;  // hip "A" = our B, hip "B" = our A
+    hipblasLtMatrixLayoutSetAttribute(p.la, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc));
+    hipblasLtMatrixLayoutSetAttribute(p.la, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sa, sizeof(sa));
+    hipblasLtMatrixLayoutSetAttribute(p.lb, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc));
+    hipblasLtMatrixLayoutSetAttribute(p.lb, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sb, sizeof(sb));
+    hipblasLtMatrixLayoutSetAttribute(p.ld, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc));
+    hipblasLtMatrixLayoutSetAttribute(p.ld, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sd, sizeof(sd));
+  }
   if (!set_ptrs(p.desc, a)) return false;
 
   hipblasLtMatmulPreference_t pref;
@@ -146,7 +157,7 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
   int best = 0;
   if (n > 1) {
     // autotune: time every candidate into a scratch output (inputs are read-only; beta=0)
-    const size_t d_bytes = (size_t)a.ldd * a.M * (a.d_f32 ? 4 : 2);
+    const size_t d_bytes = (size_t)(a.batch > 1 ? a.strideD * a.batch : a.ldd * a.M) * (a.d_f32 ? 4 : 2);
     const size_t aux_bytes = (a.aux ? (size_t)a.ldaux * a.M * 2 : 0);
     const size_t bias_bytes = (size_t)a.N * 4;
     const size_t need = d_bytes + aux_bytes + bias_bytes + 256;
@@ -203,7 +214,7 @@ int dl_lt_matmul(const DlLtArgs& a, hipStream_t st) {
   int dev = 0;
   hipGetDevice(&dev);
   Key k{a.transA, a.transB, a.M, a.N, a.K, a.lda, a.ldb, a.ldd, a.ldaux, a.d_f32, a.in_f32, a.beta != 0.f,
-        a.epilogue, a.bias_f32, dev};
+        a.epilogue, a.bias_f32, dev, a.batch, a.strideA, a.strideB, a.strideD};
   std::lock_guard<std::mutex> lock(g_mu);
   DevState* s = dev_state(dev);
   if (!s) return -2;

@@ -37,6 +37,7 @@ int dl_larc_sgd_step(float* p, const float* g, float* buf, const int* chunk_tens
                      hipStream_t st);
 int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, hipStream_t st);
 int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, hipStream_t st);
+int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st);
 
 // comm.hip
 int dl_pack(const float* src, void* dst, int dst_dt, size_t n, float weight, hipStream_t st);

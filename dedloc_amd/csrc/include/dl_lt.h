@@ -22,6 +22,10 @@ struct DlLtArgs {
   int bias_f32 = 1;
   void* aux = nullptr;         // [M, N] bf16 (ldaux): GELU pre-activation (written fwd, read bwd)
   long ldaux = 0;
+  // strided batch (e.g. split-K over the token dimension: batch b reads A/B at +b*strideA/B and
+  // writes its own partial D at +b*strideD); strides in elements
+  int batch = 1;
+  long strideA = 0, strideB = 0, strideD = 0;
 };
 
 // 0 on success; < 0 when hipBLASLt has no solution (callers fall back)

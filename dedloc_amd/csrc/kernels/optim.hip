@@ -178,6 +178,25 @@ __global__ __launch_bounds__(kBlock) void axpby_kernel(float* __restrict__ y, co
     y[i] = (a != 0.f ? a * y[i] : 0.f) + (b != 0.f ? b * x[i] : 0.f);
 }
 
+// out += sum_j slabs[j * n : (j + 1) * n]   (split-K partial reduction, fp32, float4 lanes)
+__global__ __launch_bounds__(kBlock) void sum_slabs_kernel(float* __restrict__ out, const float* __restrict__ slabs,
+                                                           int s, size_t n) {
+  const size_t nvec = n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float4 acc = reinterpret_cast<float4*>(out)[i];
+    for (int j = 0; j < s; ++j) {
+      const float4 v = reinterpret_cast<const float4*>(slabs + (size_t)j * n)[i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = acc;
+  }
+  for (size_t i = nvec * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    for (int j = 0; j < s; ++j) out[i] += slabs[(size_t)j * n + i];
+}
+
 inline int grid_for(size_t n) {
   size_t g = (n / 4 + kBlock - 1) / kBlock;
   return (int)(g < 2048 ? (g == 0 ? 1 : g) : 2048);
@@ -211,6 +230,11 @@ int dl_larc_sgd_step(float* p, const float* g, float* buf, const int* chunk_tens
 int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, hipStream_t st) {
   sumsq_kernel<<<nparts, kBlock, 0, st>>>(x, n, part);
   clip_kernel<<<grid_for(n), kBlock, 0, st>>>(x, n, part, nparts, max_norm, out);
+  return 0;
+}
+
+int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st) {
+  sum_slabs_kernel<<<grid_for(n), kBlock, 0, st>>>(out, slabs, s, n);
   return 0;
 }
 

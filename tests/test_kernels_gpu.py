@@ -324,6 +324,29 @@ def test_gemm_paths(cuda):
     assert rel(c, 1 + dy.float().t() @ a.float()) < 1e-2
 
 
+@pytest.mark.parametrize("T,N,K", [(8192, 1024, 1024), (4096, 768, 256), (8192, 4096, 1024)])
+def test_gemm_acc_f32_token_split(cuda, T, N, K):
+    """Weight-gradient path: the token dimension is split into a strided batched GEMM + slab sum."""
+    torch.manual_seed(7)
+    x = torch.randn(T, K, device=cuda).bfloat16()
+    dy = torch.randn(T, N, device=cuda).bfloat16()
+    c = torch.randn(N, K, device=cuda)
+    ref = c + dy.float().t() @ x.float()
+    OPS.gemm_acc_f32(dy, x, c, True, False)
+    assert rel(c, ref) < 1e-5, rel(c, ref)
+
+
+def test_gemm_residual_and_bias_epilogue(cuda):
+    torch.manual_seed(8)
+    x = torch.randn(1024, 512, device=cuda).bfloat16()
+    w = torch.randn(768, 512, device=cuda).bfloat16()
+    b = torch.randn(768, device=cuda)
+    r = torch.randn(1024, 768, device=cuda).bfloat16()
+    assert rel(OPS.gemm(x, w, b, None, False, True, 0), x.float() @ w.float().t() + b) < 1e-2
+    w2 = torch.randn(512, 768, device=cuda).bfloat16()
+    assert rel(OPS.gemm(x, w2, None, r, False, False, 0), r.float() + x.float() @ w2.float()) < 1e-2
+
+
 def test_albert_gpu_matches_cpu(cuda):
     from dedloc_amd.models.albert import AlbertConfig, AlbertForPreTraining
 
