@@ -124,13 +124,15 @@ class MultiCropAugment:
         std = torch.tensor(self.std, device=images.device).view(1, 3, 1, 1)
         crops = []
         for size, n, scale in zip(self.size_crops, self.num_crops, self.crop_scales):
-            for _ in range(n):
-                theta = self._rrc_theta(b, scale, (3 / 4, 4 / 3), self.flip_p, gen, images.device)
-                grid = F.affine_grid(theta, [b, 3, size, size], align_corners=False)
-                x = F.grid_sample(images, grid, mode="bilinear", padding_mode="border", align_corners=False)
-                x = self._blur(self._color(x, gen), gen)
-                x = ((x - mean) / std).to(out_dtype).contiguous(memory_format=torch.channels_last)
-                crops.append(x)
+            # all n crops of one resolution in one batched pass (n*b images): ~70 launches per
+            # resolution instead of per crop — the iteration is launch-bound at b=64
+            src = images.repeat(n, 1, 1, 1) if n > 1 else images
+            theta = self._rrc_theta(n * b, scale, (3 / 4, 4 / 3), self.flip_p, gen, images.device)
+            grid = F.affine_grid(theta, [n * b, 3, size, size], align_corners=False)
+            x = F.grid_sample(src, grid, mode="bilinear", padding_mode="border", align_corners=False)
+            x = self._blur(self._color(x, gen), gen)
+            x = ((x - mean) / std).to(out_dtype).contiguous(memory_format=torch.channels_last)
+            crops.extend(x.split(b))
         return crops
 
 
