@@ -595,9 +595,64 @@ void row_normalize_(at::Tensor w) {
   check(dl_row_normalize(f32(w), (int)w.size(0), (int)w.size(1), cur_stream(w)), "row_normalize");
 }
 
+// ------------------------------------------------------------------ BatchNorm (channels-last, fused act)
+inline void expect_nhwc(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " has dtype ", t.scalar_type(), ", expected BFloat16");
+  TORCH_CHECK(t.dim() == 4 && t.is_contiguous(at::MemoryFormat::ChannelsLast), name,
+              " must be a channels-last [N, C, H, W] tensor");
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                                      const at::Tensor& gamma, const at::Tensor& beta,
+                                                      const c10::optional<at::Tensor>& running_mean,
+                                                      const c10::optional<at::Tensor>& running_var, double eps,
+                                                      double momentum, bool relu, int64_t groups) {
+  expect_nhwc(x, "x");
+  if (res.has_value()) expect_nhwc(*res, "res");
+  expect(gamma, at::kFloat, "gamma");
+  expect(beta, at::kFloat, "beta");
+  const int64_t C = x.size(1), G = groups;
+  TORCH_CHECK(G >= 1 && x.size(0) % G == 0, "batch must split into `groups` equal statistics groups");
+  const int64_t R = x.numel() / C / G;
+  auto y = at::empty_like(x);
+  auto stats = at::empty({4 * G * C}, gamma.options());  // sums[G,2C] | mean[G,C] | rstd[G,C]
+  float* rm = running_mean.has_value() ? f32(*running_mean) : nullptr;
+  float* rv = running_var.has_value() ? f32(*running_var) : nullptr;
+  check(dl_bn_fwd(cbf(x), res.has_value() ? cbf(*res) : nullptr, bf(y), f32(gamma), f32(beta), f32(stats),
+                  f32(stats) + 2 * G * C, f32(stats) + 3 * G * C, rm, rv, R, (int)C, (int)G, (float)eps,
+                  (float)momentum, relu, cur_stream(x)),
+        "bn_fwd (channels must be 64..2048, a power-of-two multiple of 8)");
+  return {y, stats.narrow(0, 2 * G * C, G * C).view({G, C}), stats.narrow(0, 3 * G * C, G * C).view({G, C})};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& y,
+                                                                  const at::Tensor& x, const at::Tensor& mean,
+                                                                  const at::Tensor& rstd, const at::Tensor& gamma,
+                                                                  bool relu, bool want_dres) {
+  const int64_t G = mean.dim() == 2 ? mean.size(0) : 1;
+  expect_nhwc(x, "x");
+  expect_nhwc(y, "y");
+  const at::Tensor g = dy.is_contiguous(at::MemoryFormat::ChannelsLast) ? dy
+                                                                        : dy.contiguous(at::MemoryFormat::ChannelsLast);
+  expect_nhwc(g, "dy");
+  const int64_t C = x.size(1), R = x.numel() / C / G;
+  auto dx = at::empty_like(x);
+  auto dres = want_dres ? at::empty_like(x) : at::Tensor();
+  auto ws = at::empty({2 * G * C + 2 * C}, gamma.options());  // sums[G,2C] | dgamma[C] | dbeta[C]
+  check(dl_bn_bwd(cbf(g), cbf(y), cbf(x), f32(mean), f32(rstd), f32(gamma), f32(ws), bf(dx),
+                  want_dres ? bf(dres) : nullptr, f32(ws) + 2 * G * C, f32(ws) + 2 * G * C + C, R, (int)C, (int)G,
+                  relu, cur_stream(x)),
+        "bn_bwd");
+  return {dx, want_dres ? dres : at::empty({0}, x.options()), ws.narrow(0, 2 * G * C, C),
+          ws.narrow(0, 2 * G * C + C, C)};
+}
+
 }  // namespace
 
 TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
+  m.impl("bn_fwd", &bn_fwd);
+  m.impl("bn_bwd", &bn_bwd);
   m.impl("sinkhorn", &sinkhorn);
   m.impl("swav_ce", &swav_ce);
   m.impl("row_normalize_", &row_normalize_);

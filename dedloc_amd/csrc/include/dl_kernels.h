@@ -67,6 +67,12 @@ int dl_sinkhorn(const float* scores, float* P, float* Q, float* ws, int n, int K
 int dl_swav_ce(const void* scores, int scores_bf16, const float* q, float* dscores, float* loss, int rows, int K,
                float temperature, float scale, hipStream_t st);
 int dl_row_normalize(float* w, int rows, int d, hipStream_t st);
+int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta, float* sums,
+              float* mean, float* rstd, float* run_mean, float* run_var, long R, int C, int G, float eps,
+              float momentum, int relu, hipStream_t st);
+int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
+              const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
+              int G, int relu, hipStream_t st);
 
 // attention.hip
 int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, bf16_t* out, long ldo, float* lse,

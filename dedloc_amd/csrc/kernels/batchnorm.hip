@@ -1,0 +1,292 @@
+// Training-mode BatchNorm for channels-last bf16 activations, with the ResNet epilogues fused:
+//   y = act(BN(x) [+ residual]),  act in {identity, ReLU}
+// (SwAV ResNet-50 Bottleneck bn1+relu, bn2+relu, bn3+residual+relu, downsample bn).
+//
+// Layout: x is [R, C] with C contiguous (NHWC, R = N*H*W).  A thread owns 8 consecutive channels
+// (one 16-byte vector); CV = C/8 vectors per row must divide 256 (C in {64,...,2048}, all ResNet-50
+// widths), so a 256-thread block covers 256/CV rows per iteration with fully coalesced loads.
+//
+// forward : (memset) stats  -> per-channel sum / sum of squares (block partials in LDS, one
+//           lane-contiguous atomic per channel per block), normalize -> every block rebuilds
+//           scale/shift for all C channels in LDS from the sums, block 0 also writes mean/rstd and
+//           updates the running statistics (momentum, unbiased variance like torch).
+// backward: (memset) stats  -> sum g and sum g*xhat (g = dy masked by y > 0 when ReLU was fused),
+//           dx       -> dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)); d(residual) = g;
+//                       block 0 writes dgamma = sum g*xhat and dbeta = sum g.
+// MIOpen's path for the same work is 4 kernels forward + 3 backward + separate ReLU / add kernels.
+//
+// Statistics groups: the rows may be G equal consecutive groups with SEPARATE batch statistics
+// (gridDim.y = group).  SwAV runs all crops of one resolution through the trunk as one batch but
+// normalises every crop with its own statistics — exactly the reference's SINGLE_PASS_EVERY_CROP
+// semantics (one trunk pass per crop) with 8x fewer, 6x larger kernels; the running statistics
+// take the G momentum updates in crop order.
+#include "dl_common.h"
+#include "dl_kernels.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ void ld8(const bf16_t* p, float (&v)[8]) { load_bf16<8>(p, v); }
+
+// ---------------------------------------------------------------------------------- forward stats
+__global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ sums,
+                                                            long R, int C, long rpb) {
+  __shared__ float red[kThreads * 16];
+  const int CV = C >> 3, rpi = kThreads / CV;
+  const int cv = threadIdx.x % CV, rsub = threadIdx.x / CV;
+  x += (long)blockIdx.y * R * C;  // R = rows per statistics group
+  sums += (long)blockIdx.y * 2 * C;
+  const long r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (long r = r0 + rsub; r < r1; r += rpi) {
+    float v[8];
+    ld8(x + r * C + cv * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += v[j];
+      q[j] = fmaf(v[j], v[j], q[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[threadIdx.x * 16 + j] = s[j];
+    red[threadIdx.x * 16 + 8 + j] = q[j];
+  }
+  __syncthreads();
+  // threads [0, 2C) each sum one (channel, moment) over the rpi row-lanes, then one atomic
+  for (int i = threadIdx.x; i < 2 * C; i += kThreads) {
+    const int moment = i / C, c = i % C, v = c >> 3, j = c & 7;
+    float a = 0.f;
+    for (int k = 0; k < rpi; ++k) a += red[(k * CV + v) * 16 + moment * 8 + j];
+    atomicAdd(&sums[i], a);
+  }
+}
+
+// ---------------------------------------------------------------------------------- forward apply
+__global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+                                                            const float* __restrict__ sums,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out, float* __restrict__ run_mean,
+                                                            float* __restrict__ run_var, long R, int C, float eps,
+                                                            float momentum, int relu) {
+  __shared__ float sc[2048], sh[2048];
+  const int grp = blockIdx.y, G = gridDim.y;
+  const float invR = 1.f / (float)R;
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float* sg = sums + (long)grp * 2 * C;
+    const float mean = sg[c] * invR;
+    const float var = fmaxf(sg[C + c] * invR - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + eps);
+    const float g = gamma[c] * rstd;
+    sc[c] = g;
+    sh[c] = beta[c] - mean * g;
+    if (blockIdx.x == 0) {
+      mean_out[(long)grp * C + c] = mean;
+      rstd_out[(long)grp * C + c] = rstd;
+    }
+    if (blockIdx.x == 0 && grp == 0 && run_mean != nullptr) {  // G momentum updates, in group order
+      float rm = run_mean[c], rv = run_var[c];
+      for (int k = 0; k < G; ++k) {
+        const float* sk = sums + (long)k * 2 * C;
+        const float mk = sk[c] * invR;
+        const float vk = fmaxf(sk[C + c] * invR - mk * mk, 0.f);
+        rm = (1.f - momentum) * rm + momentum * mk;
+        rv = (1.f - momentum) * rv + momentum * vk * ((float)R / (float)max(R - 1, 1L));
+      }
+      run_mean[c] = rm;
+      run_var[c] = rv;
+    }
+  }
+  __syncthreads();
+  const int CV = C >> 3;
+  const long nvec = R * CV, base = (long)grp * R * C;
+  x += base;
+  y += base;
+  if (res != nullptr) res += base;
+  for (long i = blockIdx.x * (long)kThreads + threadIdx.x; i < nvec; i += (long)gridDim.x * kThreads) {
+    const int c0 = (int)(i % CV) * 8;
+    float v[8];
+    ld8(x + i * 8, v);
+    float rr[8];
+    if (res != nullptr) ld8(res + i * 8, rr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = fmaf(v[j], sc[c0 + j], sh[c0 + j]);
+      if (res != nullptr) o += rr[j];
+      v[j] = relu ? fmaxf(o, 0.f) : o;
+    }
+    store_bf16<8>(y + i * 8, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------- backward stats
+__global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __restrict__ dy,
+                                                                const bf16_t* __restrict__ y,
+                                                                const bf16_t* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd, float* __restrict__ sums,
+                                                                long R, int C, long rpb, int relu) {
+  __shared__ float red[kThreads * 16];
+  const int CV = C >> 3, rpi = kThreads / CV;
+  const int cv = threadIdx.x % CV, rsub = threadIdx.x / CV;
+  const long base = (long)blockIdx.y * R * C;
+  dy += base;
+  x += base;
+  if (y != nullptr) y += base;
+  mean += (long)blockIdx.y * C;
+  rstd += (long)blockIdx.y * C;
+  sums += (long)blockIdx.y * 2 * C;
+  const long r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+  float mu[8], rs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = mean[cv * 8 + j];
+    rs[j] = rstd[cv * 8 + j];
+  }
+  float sg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sgx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (long r = r0 + rsub; r < r1; r += rpi) {
+    const long off = r * C + cv * 8;
+    float g[8], xv[8];
+    ld8(dy + off, g);
+    ld8(x + off, xv);
+    if (relu) {
+      float yv[8];
+      ld8(y + off, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sg[j] += g[j];
+      sgx[j] = fmaf(g[j], (xv[j] - mu[j]) * rs[j], sgx[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[threadIdx.x * 16 + j] = sg[j];
+    red[threadIdx.x * 16 + 8 + j] = sgx[j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += kThreads) {
+    const int moment = i / C, c = i % C, v = c >> 3, j = c & 7;
+    float a = 0.f;
+    for (int k = 0; k < rpi; ++k) a += red[(k * CV + v) * 16 + moment * 8 + j];
+    atomicAdd(&sums[i], a);
+  }
+}
+
+// ---------------------------------------------------------------------------------- backward dx
+__global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ y,
+                                                             const bf16_t* __restrict__ x,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ sums, bf16_t* __restrict__ dx,
+                                                             bf16_t* __restrict__ dres, float* __restrict__ dgamma,
+                                                             float* __restrict__ dbeta, long R, int C, int relu) {
+  __shared__ float k1[2048], mg[2048], mgx[2048], mu_s[2048], rs_s[2048];
+  const int grp = blockIdx.y, G = gridDim.y;
+  const float invR = 1.f / (float)R;
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float* sg = sums + (long)grp * 2 * C;
+    rs_s[c] = rstd[(long)grp * C + c];
+    mu_s[c] = mean[(long)grp * C + c];
+    k1[c] = gamma[c] * rs_s[c];
+    mg[c] = sg[c] * invR;
+    mgx[c] = sg[C + c] * invR;
+    if (blockIdx.x == 0 && grp == 0) {  // parameter grads: sum over the statistics groups
+      float db = 0.f, dg = 0.f;
+      for (int k = 0; k < G; ++k) {
+        db += sums[(long)k * 2 * C + c];
+        dg += sums[(long)k * 2 * C + C + c];
+      }
+      dbeta[c] = db;
+      dgamma[c] = dg;
+    }
+  }
+  __syncthreads();
+  const long base = (long)grp * R * C;
+  dy += base;
+  x += base;
+  dx += base;
+  if (y != nullptr) y += base;
+  if (dres != nullptr) dres += base;
+  const int CV = C >> 3;
+  const long nvec = R * CV;
+  for (long i = blockIdx.x * (long)kThreads + threadIdx.x; i < nvec; i += (long)gridDim.x * kThreads) {
+    const int c0 = (int)(i % CV) * 8;
+    float g[8], xv[8];
+    ld8(dy + i * 8, g);
+    ld8(x + i * 8, xv);
+    if (relu) {
+      float yv[8];
+      ld8(y + i * 8, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+    if (dres != nullptr) store_bf16<8>(dres + i * 8, g);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float xh = (xv[j] - mu_s[c]) * rs_s[c];
+      o[j] = k1[c] * (g[j] - mg[c] - xh * mgx[c]);
+    }
+    store_bf16<8>(dx + i * 8, o);
+  }
+}
+
+inline bool bn_shape_ok(int C) {
+  if (C % 8 || C > 2048) return false;
+  const int CV = C / 8;
+  return (kThreads % CV) == 0;
+}
+
+inline int stats_blocks(long R, long& rpb) {
+  long nb = (R + 63) / 64;
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  rpb = (R + nb - 1) / nb;
+  return (int)((R + rpb - 1) / rpb);
+}
+
+inline int apply_blocks(long nvec) {
+  long g = (nvec + kThreads - 1) / kThreads;
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
+}  // namespace
+
+// sums: fp32 [2C] workspace; mean/rstd: fp32 [C] outputs; run_mean/run_var may be null
+// R = rows per statistics group, G groups (the tensor holds G*R rows); sums [G, 2C], mean/rstd [G, C]
+int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta, float* sums,
+              float* mean, float* rstd, float* run_mean, float* run_var, long R, int C, int G, float eps,
+              float momentum, int relu, hipStream_t st) {
+  if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
+  DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
+  long rpb;
+  const int nb = stats_blocks(R, rpb);
+  bn_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(x, sums, R, C, rpb);
+  const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
+  bn_apply_kernel<<<dim3(na, G), kThreads, 0, st>>>(x, res, y, sums, gamma, beta, mean, rstd, run_mean, run_var, R, C,
+                                                    eps, momentum, relu);
+  return 0;
+}
+
+int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
+              const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
+              int G, int relu, hipStream_t st) {
+  if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
+  DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
+  long rpb;
+  const int nb = stats_blocks(R, rpb);
+  bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu);
+  const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
+  bn_bwd_dx_kernel<<<dim3(na, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
+                                                     relu);
+  return 0;
+}

@@ -24,26 +24,74 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 
+class _BNAct(torch.autograd.Function):
+    """Training-mode BN (+ residual) (+ ReLU) on channels-last bf16 via the fused HIP kernels."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, relu, eps, momentum, groups):
+        y, mean, rstd = torch.ops.dedloc.bn_fwd(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu,
+                                                groups)
+        ctx.save_for_backward(x, y, mean, rstd, gamma)
+        ctx.relu, ctx.has_res = relu, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd, gamma = ctx.saved_tensors
+        dx, dres, dgamma, dbeta = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, gamma, ctx.relu, ctx.has_res)
+        return dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None
+
+
+class BNAct(nn.BatchNorm2d):
+    """BatchNorm2d with the Bottleneck epilogue fused: ``act(BN(x) [+ res])``.
+
+    Same parameters / buffers / state-dict keys as ``nn.BatchNorm2d``.  In training on channels-last
+    bf16 GPU activations it runs csrc/kernels/batchnorm.hip (2 kernels forward, 2 backward, ReLU and
+    the residual add folded in — MIOpen needs 4 + 3 plus separate add/ReLU kernels); otherwise it is
+    the stock module followed by the add / ReLU.
+    """
+
+    def __init__(self, num_features, relu: bool = False, fused: bool = True):
+        super().__init__(num_features)
+        self.relu, self.fused = relu, fused
+        self.stat_groups = 1  # >1: the batch holds that many crops, each normalised with its own stats
+
+    def forward(self, x, res=None):
+        G = self.stat_groups if self.training else 1
+        if (self.fused and self.training and x.is_cuda and x.dtype == torch.bfloat16
+                and x.is_contiguous(memory_format=torch.channels_last)
+                and (res is None or (res.dtype == torch.bfloat16
+                                     and res.is_contiguous(memory_format=torch.channels_last)))):
+            self.num_batches_tracked.add_(G)
+            return _BNAct.apply(x, self.weight, self.bias, res, self.running_mean, self.running_var, self.relu,
+                                self.eps, self.momentum, G)
+        if G > 1:  # reference semantics without the fused kernel: one BN call per crop chunk
+            y = torch.cat([super(BNAct, self).forward(c) for c in x.chunk(G)])
+        else:
+            y = super().forward(x)
+        if res is not None:
+            y = y + res
+        return F.relu(y) if self.relu else y
+
+
 class Bottleneck(nn.Module):
     expansion = 4
 
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = BNAct(planes, relu=True)
         self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)  # ResNet v1.5
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = BNAct(planes, relu=True)
         self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = BNAct(planes * 4, relu=True)  # relu(bn3(conv3) + identity), add fused
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), idt)
 
 
 class ResNet50Trunk(nn.Module):
@@ -51,8 +99,7 @@ class ResNet50Trunk(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BNAct(64, relu=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(64, layers[0])
         self.layer2 = self._make_layer(128, layers[1], stride=2)
@@ -62,7 +109,7 @@ class ResNet50Trunk(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # includes BNAct
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
         if zero_init_residual:
@@ -74,14 +121,14 @@ class ResNet50Trunk(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * 4:
             down = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
-                                 nn.BatchNorm2d(planes * 4))
+                                 BNAct(planes * 4))
         layers = [Bottleneck(self.inplanes, planes, stride, down)]
         self.inplanes = planes * 4
         layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
             if self.checkpoint_stages and self.training and x.requires_grad:
                 x = checkpoint(stage, x, use_reentrant=False)
@@ -118,18 +165,29 @@ class SwAVModel(nn.Module):
         self.heads = nn.ModuleList([SwAVPrototypesHead(num_prototypes=num_prototypes)])
         self.single_pass_every_crop = single_pass_every_crop
 
+    def set_bn_stat_groups(self, g: int):
+        for m in self.trunk.modules():
+            if isinstance(m, BNAct):
+                m.stat_groups = g
+
     def forward(self, crops: List[torch.Tensor]):
-        """crops: list of [B, 3, H, W] (channels-last) tensors -> (embeddings, scores) over all crops."""
-        if self.single_pass_every_crop:
-            feats = [self.trunk(c) for c in crops]
-        else:  # one pass per run of equal-resolution crops (original SwAV's idx_crops grouping)
-            feats, i = [], 0
-            while i < len(crops):
-                j = i
-                while j < len(crops) and crops[j].shape[-1] == crops[i].shape[-1]:
-                    j += 1
-                feats.append(self.trunk(torch.cat(crops[i:j])))
-                i = j
+        """crops: list of [B, 3, H, W] (channels-last) tensors -> (embeddings, scores) over all crops.
+
+        Equal-resolution crops always run through the trunk as ONE batch.  With
+        ``single_pass_every_crop`` (the reference setting) every BatchNorm still normalises each
+        crop with that crop's own batch statistics (BNAct statistics groups), which is exactly what
+        one trunk pass per crop computes — every other trunk op is per-sample.  Without it, BN
+        statistics span the whole resolution group (original SwAV's idx_crops grouping).
+        """
+        feats, i = [], 0
+        while i < len(crops):
+            j = i
+            while j < len(crops) and crops[j].shape[-1] == crops[i].shape[-1]:
+                j += 1
+            self.set_bn_stat_groups(j - i if self.single_pass_every_crop else 1)
+            feats.append(self.trunk(torch.cat(crops[i:j]) if j - i > 1 else crops[i]))
+            i = j
+        self.set_bn_stat_groups(1)
         return self.heads[0](torch.cat(feats))
 
     @torch.no_grad()

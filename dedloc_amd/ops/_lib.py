@@ -45,6 +45,10 @@ _SCHEMAS = [
     "sinkhorn(Tensor scores, int bs, float eps, int iters) -> Tensor",
     "swav_ce(Tensor scores, Tensor q, Tensor(a!) dscores, Tensor(b!) loss, float temperature, float scale) -> ()",
     "row_normalize_(Tensor(a!) w) -> ()",
+    "bn_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+    "float eps, float momentum, bool relu, int groups=1) -> (Tensor, Tensor, Tensor)",
+    "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres) "
+    "-> (Tensor, Tensor, Tensor, Tensor)",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias) -> Tensor",
 ]
 for _s in _SCHEMAS:
@@ -418,3 +422,44 @@ def _swav_ce_cpu(scores, q, dscores, loss, temperature, scale):
 @_impl("row_normalize_")
 def _row_normalize_cpu(w):
     w.div_(w.norm(dim=1, keepdim=True).clamp_min(1e-12))
+
+
+@_impl("bn_fwd")
+def _bn_fwd_cpu(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, groups=1):
+    G = groups
+    xf = x.float().reshape(G, x.shape[0] // G, *x.shape[1:])
+    R = xf[0].numel() // xf.shape[2]
+    mean = xf.mean(dim=(1, 3, 4))                  # [G, C]
+    var = xf.var(dim=(1, 3, 4), unbiased=False)
+    rstd = torch.rsqrt(var + eps)
+    y = (xf - mean[:, None, :, None, None]) * (rstd * gamma)[:, None, :, None, None] + beta.view(1, 1, -1, 1, 1)
+    y = y.reshape(x.shape)
+    if res is not None:
+        y = y + res.float()
+    if relu:
+        y = y.clamp_min(0)
+    if running_mean is not None:
+        for k in range(G):
+            running_mean.mul_(1 - momentum).add_(mean[k], alpha=momentum)
+            running_var.mul_(1 - momentum).add_(var[k] * (R / max(R - 1, 1)), alpha=momentum)
+    return y.to(x.dtype).contiguous(memory_format=torch.channels_last), mean, rstd
+
+
+@_impl("bn_bwd")
+def _bn_bwd_cpu(dy, y, x, mean, rstd, gamma, relu, want_dres):
+    mean2 = mean.reshape(-1, x.shape[1])
+    rstd2 = rstd.reshape(-1, x.shape[1])
+    G = mean2.shape[0]
+    g = dy.float()
+    if relu:
+        g = torch.where(y.float() > 0, g, torch.zeros_like(g))
+    gg = g.reshape(G, x.shape[0] // G, *x.shape[1:])
+    xh = (x.float().reshape(gg.shape) - mean2[:, None, :, None, None]) * rstd2[:, None, :, None, None]
+    sb = gg.sum(dim=(1, 3, 4))                       # [G, C]
+    sgx = (gg * xh).sum(dim=(1, 3, 4))
+    R = gg[0].numel() // x.shape[1]
+    dx = (gamma * rstd2)[:, None, :, None, None] * (gg - (sb / R)[:, None, :, None, None]
+                                                    - xh * (sgx / R)[:, None, :, None, None])
+    cl = torch.channels_last
+    dres = g.to(x.dtype).contiguous(memory_format=cl) if want_dres else torch.empty(0, dtype=x.dtype)
+    return dx.reshape(x.shape).to(x.dtype).contiguous(memory_format=cl), dres, sgx.sum(0), sb.sum(0)

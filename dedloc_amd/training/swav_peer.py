@@ -115,7 +115,7 @@ class SwavPeer:
                                              image_size=int(dcfg.get("SYNTHETIC_IMAGE_SIZE", 256)), augment=aug,
                                              out_dtype=torch.bfloat16 if self.device.type == "cuda" else torch.float32)
         self.frozen = [(name, int(iters)) for name, iters in (mcfg.get("TEMP_FROZEN_PARAMS_ITER_MAP") or [])]
-        self.use_graph = bool(mcfg.get("CUDA_GRAPH", True)) and self.device.type == "cuda" and \
+        self.use_graph = bool(mcfg.get("CUDA_GRAPH", False)) and self.device.type == "cuda" and \
             not bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING)
         self.graph_warmup = int(mcfg.get("CUDA_GRAPH_WARMUP", 3))  # eager iterations first (MIOpen find)
         self._graphed = None
@@ -130,9 +130,9 @@ class SwavPeer:
     def _build_graph(self, crops):
         """Capture the trunk+head forward and backward as HIP graphs (torch make_graphed_callables).
 
-        A SwAV iteration launches ~8.7k kernels (8 trunk passes x 53 BN layers x 7 MIOpen BN kernels
-        + convs + elementwise); at b=64 that is CPU launch-bound (~55 % GPU idle measured with
-        rocprofv3).  The loss (Sinkhorn + CE, global-step-dependent queue), the collaborative step
+        Opt-in (MODEL.CUDA_GRAPH): with batched equal-resolution trunk passes and the fused BN
+        kernels the iteration is GPU-bound and replaying the graph measured slower than eager
+        (1462 vs 1689 samples/s, b=64) because of the static-input/grad copies.  The loss (Sinkhorn + CE, global-step-dependent queue), the collaborative step
         and the prototype normalisation stay eager.  Warm-up iterations run inside the capture
         helper, so grads and BN statistics are restored afterwards."""
 
