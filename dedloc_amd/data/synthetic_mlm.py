@@ -51,9 +51,9 @@ class SyntheticSOPStream:
         if self.length_mode == "full":
             lengths = torch.full((B,), S, device=dev)
         else:  # ~10 % short document tails (the last instance of each document)
+            lo = min(self.min_len, max(8, S // 2))  # short sequences: never below 8 tokens
             short = torch.rand(B, generator=self.gen, device=dev) < 0.1
-            lengths = torch.where(short, self._rand(B, high=S - self.min_len) + self.min_len,
-                                  torch.full((B,), S, device=dev))
+            lengths = torch.where(short, self._rand(B, high=max(1, S - lo)) + lo, torch.full((B,), S, device=dev))
         ids = self._rand(B, S, high=self.V - FIRST_REGULAR_ID) + FIRST_REGULAR_ID
         ar = torch.arange(S, device=dev)[None, :]
         # segment A ends at a random split (>= 1 token each side)

@@ -1,0 +1,32 @@
+"""Host-side sanitizer run of the native control-plane server.
+
+GPU sanitizers are not available on this pool, so the C++ runtime (csrc/runtime/dht_server.cpp) is
+compiled together with a concurrent stress client (tests/native/dht_server_test.cpp) under
+AddressSanitizer + UndefinedBehaviorSanitizer and run on the CPU.
+"""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("san", ["address,undefined", "thread"])
+def test_dht_server_under_sanitizers(tmp_path, san):
+    if shutil.which("g++") is None:
+        pytest.skip("no host compiler")
+    exe = tmp_path / "dht_server_test"
+    cmd = ["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={san}", "-fno-omit-frame-pointer", "-pthread",
+           os.path.join(ROOT, "dedloc_amd/csrc/runtime/dht_server.cpp"),
+           os.path.join(ROOT, "tests/native/dht_server_test.cpp"), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in (r.stderr + r.stdout):
+        pytest.skip(f"sanitizer runtime for {san} not installed")
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "dht_server_test OK" in r.stdout, r.stdout + r.stderr
