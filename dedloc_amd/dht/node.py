@@ -239,7 +239,7 @@ class DHT:
     def __init__(self, initial_peers: Sequence[str] = (), listen: bool = True, listen_on: str = "0.0.0.0:*",
                  endpoint: Optional[str] = None, start: bool = True,
                  record_validators: Iterable[RecordValidatorBase] = (), client_mode: Optional[bool] = None,
-                 rpc_timeout: float = 5.0, replica_refresh: float = 10.0, **_ignored):
+                 rpc_timeout: float = 5.0, replica_refresh: float = 10.0, authorizer=None, **_ignored):
         if client_mode is not None:
             listen = not client_mode
         self.initial_peers = [p for p in (initial_peers or []) if p]
@@ -248,6 +248,11 @@ class DHT:
         self.endpoint_host = None
         if endpoint:
             self.endpoint_host = parse_endpoint(endpoint.replace("*", "0"))[0]
+        record_validators = list(record_validators)
+        if authorizer is not None:  # token-based access control (dht/auth.py)
+            from .auth import AuthorizedRecordValidator
+
+            record_validators.append(AuthorizedRecordValidator(authorizer))
         self.validator = CompositeValidator(record_validators)
         self.rpc_timeout = rpc_timeout
         self.replica_refresh = replica_refresh

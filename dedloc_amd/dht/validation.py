@@ -22,6 +22,15 @@ import msgpack
 from .crypto import RSAPrivateKey, RSAPublicKey
 
 _SIG_RE = re.compile(rb"\[signature:([A-Za-z0-9+/=]+)\]$")
+_TOKEN_RE = re.compile(rb"\[token:([A-Za-z0-9+/=]+)\]")  # access-token marker (dht/auth.py)
+
+
+def strip_token(value: bytes) -> bytes:
+    """Remove the last ``[token:...]`` marker (appended by AuthorizedRecordValidator)."""
+    m = None
+    for m in _TOKEN_RE.finditer(value):
+        pass
+    return value if m is None else value[:m.start()] + value[m.end():]
 _OWNER_RE = re.compile(rb"\[owner:(rsa:[A-Za-z0-9+/=]+)\]")
 
 
@@ -119,7 +128,7 @@ class SchemaValidator(RecordValidatorBase):
         ftype = self.fields.get(key)
         if ftype is None:
             return self.allow_extra_keys
-        body = _split_sig(value)[0]
+        body = strip_token(_split_sig(value)[0])
         try:
             obj = msgpack.unpackb(body, raw=False)
         except Exception:  # noqa: BLE001

@@ -33,6 +33,7 @@ from ..metrics import LocalMetrics, make_validators
 from ..models.albert import AlbertConfig, AlbertForPreTraining
 from ..optim.collaborative import CollaborativeOptimizer
 from ..optim.lamb import FusedLamb, get_linear_schedule_with_warmup
+from ..utils.perf import PerfStats
 
 logger = logging.getLogger(__name__)
 
@@ -140,6 +141,7 @@ class AlbertPeer:
         self.hf_step = 0
         self.metrics_log = []
         self._flat = flat
+        self.perf = PerfStats(self.device, enabled=bool(getattr(training_args, "perf_timers", True)))
 
     # ------------------------------------------------------------------ one HF step
     def train_step(self):
@@ -147,12 +149,14 @@ class AlbertPeer:
         ga = a.gradient_accumulation_steps
         self.throttle.begin()
         for _ in range(ga):
-            batch = self.data.next_batch()
-            out = self.model(batch["input_ids"], batch["attention_mask"], batch["token_type_ids"],
-                             labels=batch.get("labels"), sentence_order_label=batch["sentence_order_label"],
-                             mlm_positions=batch.get("mlm_positions"), mlm_labels=batch.get("mlm_labels"))
-            loss = out["loss"] / ga if ga > 1 else out["loss"]
-            loss.backward()
+            with self.perf.phase("data"):
+                batch = self.data.next_batch()
+            with self.perf.phase("fwd_bwd"):
+                out = self.model(batch["input_ids"], batch["attention_mask"], batch["token_type_ids"],
+                                 labels=batch.get("labels"), sentence_order_label=batch["sentence_order_label"],
+                                 mlm_positions=batch.get("mlm_positions"), mlm_labels=batch.get("mlm_labels"))
+                loss = out["loss"] / ga if ga > 1 else out["loss"]
+                loss.backward()
             self._loss_sum += loss.detach()
         if self.impl == "eager":
             if a.max_grad_norm:
@@ -161,7 +165,8 @@ class AlbertPeer:
             torch.ops.dedloc.grad_norm_clip(self._flat.grad, float(a.max_grad_norm or 0.0), self._clip_part,
                                             self._clip_out)
             self._drop_if_nonfinite()
-        self.collab_opt.step(batch_size=self.batch_size_per_step)
+        with self.perf.phase("collab_step"):  # accumulate (+ averaging + optimizer on global steps)
+            self.collab_opt.step(batch_size=self.batch_size_per_step)
         self.opt.zero_grad()
         self.mini_steps += 1
         self.hf_step += 1
@@ -211,8 +216,11 @@ class AlbertPeer:
                 self.dht.store(co.prefix + "_metrics", stats.model_dump(),
                                expiration_time=get_dht_time() + self.statistics_expiration,
                                subkey=self.local_public_key, return_future=True)
+            lg = co.last_group or {}
             rec = dict(stats.model_dump(), time=time.time(), hf_step=self.hf_step,
-                       lr=self.opt.param_groups[0]["lr"], group=(co.last_group or {}).get("size"))
+                       lr=self.opt.param_groups[0]["lr"], group=lg.get("size"),
+                       matchmaking_s=lg.get("matchmaking_s"), allreduce_s=lg.get("allreduce_s"),
+                       parts=lg.get("parts"), **self.perf.report())
             self.metrics_log.append(rec)
             if self.args.metrics_file:
                 with open(self.args.metrics_file, "a") as f:

@@ -1,0 +1,62 @@
+"""Per-phase GPU timers on HIP events (vissl ``PerfTimer``/``PerfStats``, ``vissl/utils/perf_stats.py:12-250``,
+SURVEY.md §2.3 V20 / §5.1).
+
+``with stats.phase("fwd_bwd"):`` records a start/end event pair on the current stream without
+synchronising; ``stats.report()`` waits only for the last recorded event and returns the mean
+milliseconds per phase since the previous report (host wall time is used on CPU).
+"""
+from __future__ import annotations
+
+import time
+from collections import defaultdict
+from contextlib import contextmanager
+from typing import Dict, List, Tuple
+
+import torch
+
+
+class PerfStats:
+    def __init__(self, device=None, enabled: bool = True):
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.cuda = self.device.type == "cuda" and torch.cuda.is_available()
+        self.enabled = enabled
+        self._events: Dict[str, List[Tuple]] = defaultdict(list)
+
+    @contextmanager
+    def phase(self, name: str):
+        if not self.enabled:
+            yield
+            return
+        if self.cuda:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            try:
+                yield
+            finally:
+                e.record()
+                self._events[name].append((s, e))
+        else:
+            t0 = time.perf_counter()
+            try:
+                yield
+            finally:
+                self._events[name].append((t0, time.perf_counter()))
+
+    def report(self) -> Dict[str, float]:
+        """Mean ms per phase occurrence since the last report (and the number of occurrences)."""
+        out = {}
+        if self.cuda:
+            last = [ev[-1][1] for ev in self._events.values() if ev]
+            for e in last:
+                e.synchronize()
+        for name, evs in self._events.items():
+            if not evs:
+                continue
+            if self.cuda:
+                ms = [s.elapsed_time(e) for s, e in evs]
+            else:
+                ms = [(e - s) * 1e3 for s, e in evs]
+            out[f"{name}_ms"] = sum(ms) / len(ms)
+            out[f"{name}_n"] = len(ms)
+        self._events.clear()
+        return out

@@ -245,3 +245,45 @@ def test_reference_flag_surface_parses():
     (co,) = HfArgumentParser((CoordinatorArguments,)).parse_args_into_dataclasses(
         ["--experiment_prefix", "albert", "--refresh_period", "5"])
     assert co.refresh_period == 5 and co.save_checkpoint_step_interval == 5
+
+
+# ----------------------------------------------------------------------------- access tokens (D14/H10)
+def test_token_authorizer_and_authorized_records():
+    from datetime import datetime, timedelta
+
+    from dedloc_amd.dht.auth import (AccessToken, InvalidCredentialsError, LocalAuthority, LocalTokenAuthorizer,
+                                     NotInAllowlistError)
+
+    authority = LocalAuthority({"alice": "pw", "bob": "pw2"}, coordinator="127.0.0.1:4242", ttl=600)
+    alice = LocalTokenAuthorizer(authority, "alice", "pw", RSAPrivateKey(bits=1024))
+    tok = alice.get_token()
+    assert tok.username == "alice" and alice.is_token_valid(tok) and alice.coordinator_port == 4242
+    assert not alice.does_token_need_refreshing(tok)
+    forged = AccessToken("mallory", tok.public_key, tok.expiration_time, tok.signature)
+    assert not alice.is_token_valid(forged)
+    old = (datetime.utcnow() - timedelta(seconds=5)).isoformat()
+    expired = AccessToken("alice", tok.public_key, old)
+    import base64
+    expired.signature = base64.b64encode(authority.key.sign(expired.payload()))
+    assert not alice.is_token_valid(expired)
+    with pytest.raises(NotInAllowlistError):
+        LocalTokenAuthorizer(authority, "eve", "x").join_experiment()
+    with pytest.raises(InvalidCredentialsError):
+        LocalTokenAuthorizer(authority, "bob", "wrong").join_experiment()
+
+    # records written through an authorized DHT are visible to authorized readers; unauthorized
+    # writers (no token) are invisible to them
+    validators, pub = make_validators("auth")
+    d_alice = DHT(start=True, record_validators=validators,
+                  authorizer=LocalTokenAuthorizer(authority, "alice", "pw"))
+    d_anon = DHT(initial_peers=[d_alice.endpoint], start=True)
+    try:
+        m = LocalMetrics(step=1, samples_per_second=1.0, samples_accumulated=1, loss=1.0, mini_steps=1)
+        assert d_alice.store("auth_metrics", m.model_dump(), get_dht_time() + 30, subkey=pub)
+        assert d_alice.get("auth_metrics", latest=True).value[pub].value["step"] == 1
+        d_anon.store("plain_key", 7, get_dht_time() + 30)
+        assert d_anon.get("plain_key").value == 7          # no validators on the anonymous node
+        assert d_alice.get("plain_key") is None            # ... but the authorized node rejects it
+    finally:
+        d_anon.shutdown()
+        d_alice.shutdown()
