@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--compression", default="FLOAT16")
     ap.add_argument("--impl", default="dedloc", choices=["dedloc", "eager"],
                     help="eager = HF AlbertForPreTraining + per-tensor torch LAMB (the measured baseline)")
+    ap.add_argument("--cpu_test", default=None, metavar="CONFIG_DIR",
+                    help="plumbing test only: run on CPU/gloo with the tiny model config in CONFIG_DIR "
+                         "(exercises the multi-rank orchestration of this script; not a measurement)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -60,7 +63,11 @@ def main():
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     from dedloc_amd.parallel import init_world
 
-    rank, world, dev = init_world()
+    rank, world, dev = init_world(device=torch.device("cpu") if args.cpu_test else None)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     from dedloc_amd.cli.arguments import AlbertTrainingArguments, CollaborationArguments, DatasetArguments
@@ -75,7 +82,7 @@ def main():
     targs = AlbertTrainingArguments(per_device_train_batch_size=args.micro_batch,
                                     gradient_accumulation_steps=args.grad_accum, seq_length=args.seq_len,
                                     save_steps=0, output_dir=f"/tmp/dedloc_bench_{os.getpid()}", seed=1234)
-    dargs = DatasetArguments(config_path="albert-large-v2")
+    dargs = DatasetArguments(config_path=args.cpu_test or "albert-large-v2")
     cargs = CollaborationArguments(experiment_prefix="bench", initial_peers=[ep[0]], dht_listen_on="127.0.0.1:*",
                                    target_batch_size=args.target_batch_size, compression=args.compression,
                                    listen_on="127.0.0.1:*", averaging_expiration=5.0, averaging_timeout=60.0,
@@ -100,17 +107,17 @@ def main():
         dist.barrier()
     base = co.local_step
     run_until(base + args.warmup)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     ema_start = co.performance_ema.samples_per_second
     t0 = time.perf_counter()
     samples = run_until(base + args.warmup + args.steps)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     ema = co.performance_ema.samples_per_second
     stats = torch.tensor([samples, dt, ema], dtype=torch.float64, device=dev)

@@ -1,0 +1,43 @@
+"""bench.py driver contract, exercised on CPU/gloo with a tiny model (multi-rank orchestration:
+DHT root broadcast, state download, collaborative steps with averaging, barrier-bracketed timing,
+max-over-ranks time, ONE JSON line from rank 0 with the required keys)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.multiproc
+@pytest.mark.timeout(400)
+def test_bench_two_ranks_cpu_plumbing(tmp_path):
+    from dedloc_amd.models.albert import AlbertConfig
+
+    cfg = tmp_path / "cfg"
+    AlbertConfig.tiny(num_hidden_layers=2, max_position_embeddings=64).save_pretrained(str(cfg))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--cpu_test", str(cfg), "--micro_batch", "2", "--seq_len", "64", "--target_batch_size", "8"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=360, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert KEYS <= set(out)
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["value"] > 0 and out["higher_is_better"] is True
+    assert out["averaging_rounds"] >= 1  # the two peers averaged over the world communicator
