@@ -648,9 +648,132 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
           ws.narrow(0, 2 * G * C + C, C)};
 }
 
+// ------------------------------------------------------------------ implicit-GEMM convolution (NHWC, conv.hip)
+// Weights arrive as [Cout, Cin, R, S] tensors whose memory is KRSC (channels_last), which is how the
+// flat parameter buffer stores every conv weight; permute(0,2,3,1) is then a free view.
+inline at::Tensor krsc_view(const at::Tensor& w) {
+  at::Tensor k = w.permute({0, 2, 3, 1});
+  return k.is_contiguous() ? k : k.contiguous();
+}
+
+inline int64_t conv_out(int64_t n, int64_t k, int64_t stride, int64_t pad) { return (n + 2 * pad - k) / stride + 1; }
+
+// stem (Cin not a multiple of 64): explicit im2col matrix [N*P*Q, Kp], k = (r, s, c), zero padded
+inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t P,
+                              int64_t Q, int64_t Kp) {
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  auto col = at::empty({N * P * Q, Kp}, x.options());
+  check(dl_im2col(cbf(x), (int)N, (int)H, (int)W, (int)C, (int)R, (int)S, (int)stride, (int)pad, (int)P, (int)Q,
+                  (int)Kp, bf(col), cur_stream(x)),
+        "im2col");
+  return col;
+}
+
+inline DlConvGeom geom(const bf16_t* img, int64_t N, int64_t H, int64_t W, int64_t C, int64_t I, int64_t J,
+                       int64_t sh, int64_t sw, int64_t TR, int64_t TS, int64_t dh0, int64_t dhs, int64_t dw0,
+                       int64_t dws) {
+  return DlConvGeom{img, (int)N, (int)H, (int)W, (int)C, (int)I, (int)J, (int)sh, (int)sw,
+                    (int)TR, (int)TS, (int)dh0, (int)dhs, (int)dw0, (int)dws};
+}
+
+at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+  expect_nhwc(x, "x");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4, "w must be a bf16 [Cout,Cin,R,S] GPU tensor");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t K = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(1) == C, "conv2d_fwd: weight/input channel mismatch");
+  const int64_t P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
+  auto y = at::empty({N, K, P, Q}, x.options(), at::MemoryFormat::ChannelsLast);
+  const at::Tensor wk = krsc_view(w);
+  if (C % 64 == 0) {
+    check(dl_conv_fwd(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(wk), R * S * C,
+                      (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x)),
+          "conv2d_fwd");
+    return y;
+  }
+  // stem: im2col, then a 1x1 conv over the column matrix
+  const int64_t RSC = R * S * C, Kp = (RSC + 63) / 64 * 64, M = N * P * Q;
+  const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, Kp);
+  auto wp = at::zeros({K, Kp}, w.options());
+  wp.narrow(1, 0, RSC).copy_(wk.reshape({K, RSC}));
+  check(dl_conv_fwd(geom(cbf(col), M, 1, 1, Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(wp), Kp, (int)K, bf(y), 1, 1, 1, 1,
+                    0, 0, K, cur_stream(x)),
+        "conv2d_fwd(stem)");
+  return y;
+}
+
+// dX = conv^T(dY): for each output parity class (a, b) of the stride, a dense sub-convolution over
+// the taps r = r0, r0 + stride, ... that reach it (dY row = i + dh0 - tr), weights [Cin][tr][ts][Cout]
+at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t stride, int64_t pad, int64_t H,
+                        int64_t W) {
+  const at::Tensor dy = dy_in.is_contiguous(at::MemoryFormat::ChannelsLast)
+                            ? dy_in
+                            : dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  expect_nhwc(dy, "dy");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4, "w must be a bf16 [Cout,Cin,R,S] GPU tensor");
+  const int64_t N = dy.size(0), K = dy.size(1), P = dy.size(2), Q = dy.size(3);
+  const int64_t C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(0) == K, "conv2d_dgrad: weight/grad channel mismatch");
+  TORCH_CHECK(K % 64 == 0, "conv2d_dgrad needs Cout % 64 == 0");
+  auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  const at::Tensor wk = krsc_view(w);  // [K, R, S, C]
+  for (int64_t a = 0; a < stride; ++a) {
+    const int64_t I = (H - a + stride - 1) / stride;
+    const int64_t r0 = (a + pad) % stride, TR = r0 < R ? (R - 1 - r0) / stride + 1 : 0;
+    const int64_t dh0 = (a + pad - r0) / stride;
+    for (int64_t b = 0; b < stride; ++b) {
+      const int64_t J = (W - b + stride - 1) / stride;
+      const int64_t s0 = (b + pad) % stride, TS = s0 < S ? (S - 1 - s0) / stride + 1 : 0;
+      const int64_t dw0 = (b + pad - s0) / stride;
+      if (I <= 0 || J <= 0) continue;
+      at::Tensor wd;
+      if (TR > 0 && TS > 0)
+        wd = wk.slice(1, r0, R, stride).slice(2, s0, S, stride).permute({3, 1, 2, 0}).contiguous();  // [C, TR, TS, K]
+      else
+        wd = at::zeros({C, 8}, w.options());  // no contributing tap: the class is all zeros
+      check(dl_conv_fwd(geom(cbf(dy), N, P, Q, K, I, J, 1, 1, TR, TS, dh0, -1, dw0, -1), cbf(wd),
+                        std::max<int64_t>(8, TR * TS * K), (int)C, bf(dx), (int)H, (int)W, (int)stride, (int)stride,
+                        (int)a, (int)b, C, cur_stream(dy)),
+            "conv2d_dgrad");
+    }
+  }
+  return dx;
+}
+
+// dW (fp32 [Cout, Cin, R, S] with KRSC memory, e.g. the flat-buffer grad view) += conv wgrad
+void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, int64_t stride, int64_t pad) {
+  const at::Tensor dy = dy_in.is_contiguous(at::MemoryFormat::ChannelsLast)
+                            ? dy_in
+                            : dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  expect_nhwc(dy, "dy");
+  expect_nhwc(x, "x");
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.dim() == 4, "dw must be an fp32 4-D GPU tensor");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t K = dy.size(1), P = dy.size(2), Q = dy.size(3), R = dw.size(2), S = dw.size(3);
+  TORCH_CHECK(dw.size(0) == K && dw.size(1) == C, "conv2d_wgrad: dw shape mismatch");
+  at::Tensor dk = dw.permute({0, 2, 3, 1});  // [K, R, S, C]
+  const bool direct = dk.is_contiguous();
+  at::Tensor acc = direct ? dk : at::zeros({K, R, S, C}, dw.options());
+  int rc;
+  if (C % 8 == 0 && C >= 8 && C % 64 == 0) {
+    rc = dl_conv_wgrad(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(dy), K, (int)K,
+                       f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy));
+  } else {
+    const int64_t RSC = R * S * C, Kp = (RSC + 63) / 64 * 64, M = N * P * Q;
+    const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, Kp);
+    rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K, f32(acc), RSC,
+                       (int)RSC, cur_stream(dy));
+  }
+  check(rc, "conv2d_wgrad");
+  if (!direct) dk.add_(acc);
+}
+
 }  // namespace
 
 TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
+  m.impl("conv2d_fwd", &conv2d_fwd);
+  m.impl("conv2d_dgrad", &conv2d_dgrad);
+  m.impl("conv2d_wgrad", &conv2d_wgrad);
   m.impl("bn_fwd", &bn_fwd);
   m.impl("bn_bwd", &bn_bwd);
   m.impl("sinkhorn", &sinkhorn);

@@ -74,6 +74,24 @@ int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* m
               const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
               int G, int relu, hipStream_t st);
 
+// conv.hip — implicit-GEMM NHWC convolutions.  The gathered operand is an NHWC image
+// [Nimg, H, W, C]; GEMM rows m = (n, i, j) over [Nimg, I, J]; tap t = (tr < TR, ts < TS) reads
+// pixel (i*sh + dh0 + tr*dhs, j*sw + dw0 + ts*dws) (zero outside the image).
+struct DlConvGeom {
+  const bf16_t* img;
+  int Nimg, H, W, C;
+  int I, J, sh, sw;
+  int TR, TS, dh0, dhs, dw0, dws;
+};
+// out[(n, i*osh+oh0, j*osw+ow0), 0..N) (NHWC, row stride ldo) = sum_{t,c} img(pixel(m,t), c) * w[n][t*C + c]
+int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
+                int oh0, int ow0, long ldo, hipStream_t st);
+// dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols)
+int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,
+                  hipStream_t st);
+int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int P, int Q, int Kp,
+              bf16_t* col, hipStream_t st);
+
 // attention.hip
 int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, bf16_t* out, long ldo, float* lse,
                 int B, int H, int S, int D, float scale, hipStream_t st);

@@ -1,0 +1,445 @@
+// Implicit-GEMM convolutions on MFMA for the SwAV ResNet-50 trunk.
+//
+// Activations are NHWC bf16 (torch channels_last), weights KRSC (the flat fp32 master buffer stores
+// every conv weight channels-last, utils/flat.py), so one gathered-operand GEMM covers all three
+// passes with no im2col buffer and no layout transposes (the 3-channel stem is the one exception:
+// it is lowered to an explicit im2col matrix, then runs as a 1x1 conv over it):
+//
+//   forward  Y[m=(n,p,q), k]     = sum_{t=(r,s), c} X[n, p*st+r-pad, q*st+s-pad, c] * W[k, t, c]
+//   dgrad    dX[(n,h,w), c]      = same kernel over dY with the tap-transposed weights; a stride-2
+//                                  conv splits into stride^2 parity classes (h = i*st + a), each a
+//                                  dense stride-1 sub-convolution over only its contributing taps
+//   wgrad    dW[k, (t, c)]      += sum_m dY[m, k] * X[pixel(m, t), c]     (fp32, split-K atomics)
+//
+// A "geometry" (DlConvGeom) describes the gathered operand: an NHWC image [Nimg, H, W, C], a grid
+// of GEMM rows m = (n, i, j) over [Nimg, I, J], and a tap lattice t = (tr, ts) whose pixel is
+// (i*sh + dh0 + tr*dhs, j*sw + dw0 + ts*dws); out-of-image taps read as zero (padding).
+//
+// Tiling (cdna_hip_programming.md §5): 128x128x64 workgroup tile, 4 waves (2 x 2) of 64x64 =
+// 4x4 v_mfma_f32_16x16x32_bf16 tiles, register-staged double-buffered LDS (T14: tile t+1's global
+// loads are issued before tile t's MFMAs and written to the other buffer after them), XOR-swizzled
+// LDS images (K-inner rows read with ds_read_b128, K-outer rows with ds_read_b64_tr_b16), 64 KiB
+// LDS and <=256 VGPRs so two workgroups share a CU, XCD-aware tile order (T1).  All gathered loads
+// are unconditional 16-byte loads from a clamped address followed by a select, so the compiler never
+// branches around a load (§5 item 4(c)).  The forward kernel swaps the MFMA operand roles so each
+// lane owns 4 consecutive output channels of one pixel (8-byte NHWC stores).
+#include <algorithm>
+
+#include "dl_common.h"
+#include "dl_kernels.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef short s8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s4_t lds_s4;
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int NT = 256;
+constexpr int TILE = BM * BK * 2;  // 16 KiB per operand per stage
+constexpr int LDS_BYTES = 4 * TILE;
+
+// K-inner image [128 rows][64 k] (128-B rows, 8 chunks of 16 B): chunk c of row r at c ^ ((r>>1)&7)
+__device__ __forceinline__ int kin_off(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
+// K-outer image [64 k][128 rows] (256-B rows, 16 chunks): chunk c of k-row r at c ^ 2((r&3)|((r>>1)&4)),
+// so the four k-rows of one ds_read_b64_tr_b16 land on distinct bank groups
+__device__ __forceinline__ int kout_off(int krow, int c) {
+  return krow * 256 + ((c ^ (((krow & 3) | ((krow >> 1) & 4)) << 1)) << 4);
+}
+
+__device__ __forceinline__ floatx4 mfma16(bf16x8 a, bf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// 16 rows x 32 k fragment: lane l -> row r0 + (l&15), k = 8*(l>>4) + j  (either image kind)
+template <bool KOUTER>
+__device__ __forceinline__ bf16x8 load_frag(const uint8_t* img, int r0, int ksub, int lane) {
+  if constexpr (!KOUTER) {
+    return *reinterpret_cast<const bf16x8*>(img + kin_off(r0 + (lane & 15), 4 * ksub + (lane >> 4)));
+  } else {
+    const int g = lane >> 4, i = lane & 15;
+    const int krow = 32 * ksub + 8 * g + (i >> 2);
+    const int col = r0 + 4 * (i & 3);
+    const int o1 = kout_off(krow, col >> 3) + ((col & 7) << 1);
+    const int o2 = kout_off(krow + 4, col >> 3) + ((col & 7) << 1);
+    const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + o1));
+    const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + o2));
+    const s8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+struct Stage { uint4 v[4]; };
+
+// thread `tid`, slot u: K-inner tiles put chunk (tid&7) of row (tid>>3)+32u; K-outer tiles put
+// chunk (tid&15) of k-row (tid>>4)+16u
+__device__ __forceinline__ void st_kin(const Stage& s, uint8_t* img) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = threadIdx.x + NT * u;
+    *reinterpret_cast<uint4*>(img + kin_off(idx >> 3, idx & 7)) = s.v[u];
+  }
+}
+__device__ __forceinline__ void st_kout(const Stage& s, uint8_t* img) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = threadIdx.x + NT * u;
+    *reinterpret_cast<uint4*>(img + kout_off(idx >> 4, idx & 15)) = s.v[u];
+  }
+}
+
+__device__ __forceinline__ uint4 sel(bool ok, uint4 v) {
+  return ok ? v : uint4{0u, 0u, 0u, 0u};
+}
+
+// exact a / b for 0 <= a < 2^24 through one float reciprocal (+-1 correction)
+__device__ __forceinline__ int fdiv(int a, int b, float rb) {
+  int q = (int)((float)a * rb);
+  const int r = a - q * b;
+  q += (r >= b) - (r < 0);
+  return q;
+}
+
+// =============================================================================================
+// forward / dgrad:  out[pixel(m), n] = sum_k A(m, k) W[n, k],  A gathered K-inner
+// =============================================================================================
+struct FwdArgs {
+  DlConvGeom g;
+  const bf16_t* w;
+  long ldw;
+  int N;  // output channels
+  bf16_t* out;
+  int OH, OW, osh, osw, oh0, ow0;
+  long ldo;
+  int M, K;
+};
+
+__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const DlConvGeom& g = p.g;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int IJ = g.I * g.J;
+
+  // per-thread gathered rows (fixed over the K loop): image row base and pixel origin
+  int hb[4], wb[4], nb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int m = m0 + (tid >> 3) + 32 * u;
+    if (m < p.M) {
+      const int n = m / IJ, r = m - n * IJ;
+      const int i = r / g.J, j = r - i * g.J;
+      hb[u] = i * g.sh;
+      wb[u] = j * g.sw;
+      nb[u] = n * g.H;
+    } else {
+      hb[u] = -(1 << 29);  // never inside the image -> zero row
+      wb[u] = 0;
+      nb[u] = 0;
+    }
+  }
+  const int cofs = (tid & 7) * 8;
+  int brow[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) brow[u] = min(n0 + (tid >> 3) + 32 * u, p.N - 1);
+
+  auto load_a = [&](Stage& s, int k0) {
+    const int t = k0 / g.C, c0 = k0 - t * g.C;
+    const int tr = t / g.TS, ts = t - tr * g.TS;
+    const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int h = hb[u] + dh, w = wb[u] + dw;
+      const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const long off = ok ? ((long)(nb[u] + h) * g.W + w) * g.C + c0 + cofs : 0;
+      s.v[u] = sel(ok, *reinterpret_cast<const uint4*>(g.img + off));
+    }
+  };
+  auto load_b = [&](Stage& s, int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s.v[u] = *reinterpret_cast<const uint4*>(p.w + (long)brow[u] * p.ldw + k0 + cofs);
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  Stage sa, sb;
+  if (nk > 0) {
+    load_a(sa, 0);
+    load_b(sb, 0);
+    st_kin(sa, smem);
+    st_kin(sb, smem + TILE);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    const uint8_t* Ai = smem + cur * 2 * TILE;
+    const uint8_t* Bi = Ai + TILE;
+    if (t + 1 < nk) {
+      load_a(sa, (t + 1) * BK);
+      load_b(sb, (t + 1) * BK);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi] = load_frag<false>(Ai, wm * 64 + mi * 16, ks, lane);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const bf16x8 bfr = load_frag<false>(Bi, wn * 64 + ni * 16, ks, lane);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) acc[ni][mi] = mfma16(bfr, af[mi], acc[ni][mi]);
+      }
+    }
+    if (t + 1 < nk) {
+      uint8_t* An = smem + (cur ^ 1) * 2 * TILE;
+      st_kin(sa, An);
+      st_kin(sb, An + TILE);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[ni][mi][i] = out[pixel m0+wm*64+mi*16+(lane&15)][channel n0+wn*64+ni*16+4*(lane>>4)+i]
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + mi * 16 + (lane & 15);
+    if (m >= p.M) continue;
+    const int n = m / IJ, r = m - n * IJ;
+    const int i = r / g.J, j = r - i * g.J;
+    bf16_t* orow = p.out + ((long)(n * p.OH + i * p.osh + p.oh0) * p.OW + j * p.osw + p.ow0) * p.ldo;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int ch = n0 + wn * 64 + ni * 16 + 4 * (lane >> 4);
+      if (ch >= p.N) continue;
+      uint2 v;
+      v.x = (uint32_t)f2bf(acc[ni][mi][0]) | ((uint32_t)f2bf(acc[ni][mi][1]) << 16);
+      v.y = (uint32_t)f2bf(acc[ni][mi][2]) | ((uint32_t)f2bf(acc[ni][mi][3]) << 16);
+      *reinterpret_cast<uint2*>(orow + ch) = v;
+    }
+  }
+}
+
+// =============================================================================================
+// wgrad:  dW[k, col] += sum_m dY[m, k] * B(col, m),  col = (t, c), both operands K-outer
+// =============================================================================================
+struct WgradArgs {
+  DlConvGeom g;
+  const bf16_t* dy;
+  long ldy;
+  int Cout;
+  float* dw;
+  long lddw;
+  int Ncols;   // stored gradient columns (<= gathered rows)
+  int Brows;   // gathered operand extent TR*TS*C (load clamp)
+  int M;       // reduction extent Nimg*I*J
+  int m_per_split;
+  float rIJ, rJ;
+};
+
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const DlConvGeom& g = p.g;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int tiles_n = (p.Ncols + BN - 1) / BN;
+  const int tiles_m = (p.Cout + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int kbeg = blockIdx.z * p.m_per_split;
+  const int kend = min(p.M, kbeg + p.m_per_split);
+  if (kbeg >= kend) return;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int IJ = g.I * g.J;
+
+  const int chunk = tid & 15, krow0 = tid >> 4;
+  const int acol = min(m0 + chunk * 8, p.Cout - 8);
+  const int kk = min(n0 + chunk * 8, p.Brows - 8);
+  const int t = kk / g.C, c = kk - t * g.C;
+  const int tr = t / g.TS, ts = t - tr * g.TS;
+  const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
+
+  auto load_a = [&](Stage& s, int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = kbeg + k0 + krow0 + 16 * u;
+      const bool ok = m < kend;
+      s.v[u] = sel(ok, *reinterpret_cast<const uint4*>(p.dy + (long)(ok ? m : kbeg) * p.ldy + acol));
+    }
+  };
+  auto load_b = [&](Stage& s, int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = kbeg + k0 + krow0 + 16 * u;
+      const int n = fdiv(m, IJ, p.rIJ), r = m - n * IJ;
+      const int i = fdiv(r, g.J, p.rJ), j = r - i * g.J;
+      const int h = i * g.sh + dh, w = j * g.sw + dw;
+      const bool ok = m < kend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const long off = ok ? ((long)(n * g.H + h) * g.W + w) * g.C + c : 0;
+      s.v[u] = sel(ok, *reinterpret_cast<const uint4*>(g.img + off));
+    }
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  Stage sa, sb;
+  load_a(sa, 0);
+  load_b(sb, 0);
+  st_kout(sa, smem);
+  st_kout(sb, smem + TILE);
+  __syncthreads();
+  for (int s = 0; s < nk; ++s) {
+    const int cur = s & 1;
+    const uint8_t* Ai = smem + cur * 2 * TILE;
+    const uint8_t* Bi = Ai + TILE;
+    if (s + 1 < nk) {
+      load_a(sa, (s + 1) * BK);
+      load_b(sb, (s + 1) * BK);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = load_frag<true>(Bi, wn * 64 + ni * 16, ks, lane);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const bf16x8 af = load_frag<true>(Ai, wm * 64 + mi * 16, ks, lane);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(af, bfr[ni], acc[mi][ni]);
+      }
+    }
+    if (s + 1 < nk) {
+      uint8_t* An = smem + (cur ^ 1) * 2 * TILE;
+      st_kout(sa, An);
+      st_kout(sb, An + TILE);
+    }
+    __syncthreads();
+  }
+
+  // acc[mi][ni][i] = dW[channel m0+wm*64+mi*16+4*(lane>>4)+i][col n0+wn*64+ni*16+(lane&15)]
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = m0 + wm * 64 + mi * 16 + 4 * (lane >> 4) + i;
+      if (ch >= p.Cout) continue;
+      float* drow = p.dw + (long)ch * p.lddw;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + wn * 64 + ni * 16 + (lane & 15);
+        if (col >= p.Ncols) continue;
+        if (split) atomicAdd(drow + col, acc[mi][ni][i]);
+        else drow[col] += acc[mi][ni][i];
+      }
+    }
+  }
+}
+
+// =============================================================================================
+// explicit im2col for the 3-channel stem: col[m=(n,p,q)][k=(r,s,c)], zero padded to Kp columns
+// =============================================================================================
+__global__ void im2col_kernel(const bf16_t* __restrict__ x, int H, int W, int C, int R, int S, int stride, int pad,
+                              int P, int Q, int RSC, int Kp, bf16_t* __restrict__ col, long total) {
+  const int kchunks = Kp / 8;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const long m = idx / kchunks;
+    const int kc = (int)(idx - m * kchunks);
+    const int q = (int)(m % Q);
+    const long t = m / Q;
+    const int pp = (int)(t % P);
+    const long n = t / P;
+    uint32_t w32[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      uint32_t pair = 0;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int k = kc * 8 + e + h2;
+        bf16_t v = 0;
+        if (k < RSC) {
+          const int cc = k % C, rs = k / C;
+          const int s = rs % S, r = rs / S;
+          const int h = pp * stride - pad + r, w = q * stride - pad + s;
+          if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = x[((n * H + h) * W + w) * C + cc];
+        }
+        pair |= (uint32_t)v << (16 * h2);
+      }
+      w32[e / 2] = pair;
+    }
+    *reinterpret_cast<uint4*>(col + m * Kp + kc * 8) = uint4{w32[0], w32[1], w32[2], w32[3]};
+  }
+}
+
+template <typename Kern>
+void set_lds(Kern k) {
+  DL_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+}
+
+}  // namespace
+
+int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
+                int oh0, int ow0, long ldo, hipStream_t st) {
+  if (g.C % BK || N % 4 || ldw % 8 || ldo % 4 || g.I < 0 || g.J < 0) return -1;
+  const long M = (long)g.Nimg * g.I * g.J;
+  if (M >= (1L << 31)) return -1;
+  if (M == 0 || N == 0) return 0;
+  FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C};
+  static bool attr = false;
+  if (!attr) {
+    set_lds(conv_fwd_kernel);
+    attr = true;
+  }
+  const int tiles = (int)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  conv_fwd_kernel<<<dim3(tiles), NT, LDS_BYTES, st>>>(a);
+  return 0;
+}
+
+int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,
+                  hipStream_t st) {
+  const int Brows = g.TR * g.TS * g.C;
+  if (g.C % 8 || Cout % 8 || Cout < 8 || ldy % 8 || Brows < 8 || Ncols > Brows) return -1;
+  const long M = (long)g.Nimg * g.I * g.J;
+  if (M >= (1L << 24)) return -1;  // fdiv exactness bound
+  if (M == 0 || Ncols == 0) return 0;
+  const int tiles = ((Cout + BM - 1) / BM) * ((Ncols + BN - 1) / BN);
+  // split the (long) pixel reduction so that ~4 workgroups per CU exist; each split is a
+  // multiple of the 64-deep k-step and at least 8 k-steps long
+  const long ksteps = (M + BK - 1) / BK;
+  long splits = std::max(1L, std::min<long>((1024 + tiles - 1) / tiles, ksteps / 8));
+  const long steps_per = (ksteps + splits - 1) / splits;
+  splits = (ksteps + steps_per - 1) / steps_per;
+  WgradArgs a{g, dy, ldy, Cout, dw, lddw, Ncols, Brows, (int)M, (int)(steps_per * BK),
+              1.f / (float)(g.I * g.J), 1.f / (float)g.J};
+  static bool attr = false;
+  if (!attr) {
+    set_lds(conv_wgrad_kernel);
+    attr = true;
+  }
+  conv_wgrad_kernel<<<dim3(tiles, 1, (unsigned)splits), NT, LDS_BYTES, st>>>(a);
+  return 0;
+}
+
+int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int P, int Q, int Kp,
+              bf16_t* col, hipStream_t st) {
+  if (Kp % 8 || Kp < R * S * C) return -1;
+  const long total = (long)N * P * Q * (Kp / 8);
+  if (total == 0) return 0;
+  const int threads = 256;
+  const long blocks = std::min<long>((total + threads - 1) / threads, 256L * 64);
+  im2col_kernel<<<dim3((unsigned)blocks), threads, 0, st>>>(x, H, W, C, R, S, stride, pad, P, Q, R * S * C, Kp, col,
+                                                            total);
+  return 0;
+}

@@ -14,6 +14,7 @@ Parameter names match torchvision/vissl (``trunk.*``, ``heads.0.*``) for checkpo
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence
 
 import torch
@@ -40,6 +41,56 @@ class _BNAct(torch.autograd.Function):
         x, y, mean, rstd, gamma = ctx.saved_tensors
         dx, dres, dgamma, dbeta = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, gamma, ctx.relu, ctx.has_res)
         return dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None
+
+
+class _ConvNHWC(torch.autograd.Function):
+    """Conv2d (no bias, groups 1) on channels-last bf16 through the implicit-GEMM MFMA kernels
+    (csrc/kernels/conv.hip).  The weight gradient accumulates in fp32 straight into the parameter's
+    bound ``.grad`` (the flat gradient buffer, KRSC layout) when there is one, like the ALBERT layer."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad, module):
+        wb = weight.detach().to(torch.bfloat16)  # keeps the channels-last (KRSC) strides
+        ctx.save_for_backward(x, wb)
+        ctx.stride, ctx.pad, ctx.module = stride, pad, module
+        return torch.ops.dedloc.conv2d_fwd(x, wb, stride, pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3])
+        dw = None
+        if ctx.needs_input_grad[1]:
+            weight = ctx.module.weight
+            g = weight.grad
+            if g is not None and g.dtype == torch.float32 and g.permute(0, 2, 3, 1).is_contiguous():
+                torch.ops.dedloc.conv2d_wgrad(dy, x, g, ctx.stride, ctx.pad)  # in place, no AccumulateGrad
+            else:
+                dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device).contiguous(
+                    memory_format=torch.channels_last)
+                torch.ops.dedloc.conv2d_wgrad(dy, x, dw, ctx.stride, ctx.pad)
+                dw = dw.to(weight.dtype)
+        return dx, dw, None, None, None
+
+
+class ConvNHWC(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters / state-dict keys) whose GPU path on channels-last bf16
+    activations is the hand-written implicit-GEMM MFMA convolution (forward, dgrad, wgrad); other
+    inputs (CPU plumbing, fp32) take the stock module.  ``DEDLOC_CONV=miopen`` routes the GPU path
+    through MIOpen instead (A/B measurements only)."""
+
+    native = os.environ.get("DEDLOC_CONV", "hip") != "miopen"
+
+    def forward(self, x):
+        if (self.native and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+                and self.bias is None and self.groups == 1 and self.dilation == (1, 1)
+                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
+                and self.padding_mode == "zeros"):
+            return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self)
+        return super().forward(x)
 
 
 class BNAct(nn.BatchNorm2d):
@@ -79,11 +130,11 @@ class Bottleneck(nn.Module):
 
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
-        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.conv1 = ConvNHWC(inplanes, planes, 1, bias=False)
         self.bn1 = BNAct(planes, relu=True)
-        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)  # ResNet v1.5
+        self.conv2 = ConvNHWC(planes, planes, 3, stride=stride, padding=1, bias=False)  # ResNet v1.5
         self.bn2 = BNAct(planes, relu=True)
-        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.conv3 = ConvNHWC(planes, planes * 4, 1, bias=False)
         self.bn3 = BNAct(planes * 4, relu=True)  # relu(bn3(conv3) + identity), add fused
         self.downsample = downsample
 
@@ -98,7 +149,7 @@ class ResNet50Trunk(nn.Module):
     def __init__(self, layers=(3, 4, 6, 3), zero_init_residual=False, checkpoint_stages: bool = False):
         super().__init__()
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.conv1 = ConvNHWC(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = BNAct(64, relu=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make_layer(64, layers[0])
@@ -120,7 +171,7 @@ class ResNet50Trunk(nn.Module):
     def _make_layer(self, planes, blocks, stride=1):
         down = None
         if stride != 1 or self.inplanes != planes * 4:
-            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+            down = nn.Sequential(ConvNHWC(self.inplanes, planes * 4, 1, stride=stride, bias=False),
                                  BNAct(planes * 4))
         layers = [Bottleneck(self.inplanes, planes, stride, down)]
         self.inplanes = planes * 4

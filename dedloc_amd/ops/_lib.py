@@ -50,6 +50,9 @@ _SCHEMAS = [
     "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres) "
     "-> (Tensor, Tensor, Tensor, Tensor)",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias) -> Tensor",
+    "conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor",
+    "conv2d_dgrad(Tensor dy, Tensor w, int stride, int pad, int H, int W) -> Tensor",
+    "conv2d_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad) -> ()",
 ]
 for _s in _SCHEMAS:
     LIB.define(_s)
@@ -443,6 +446,24 @@ def _bn_fwd_cpu(x, res, gamma, beta, running_mean, running_var, eps, momentum, r
             running_mean.mul_(1 - momentum).add_(mean[k], alpha=momentum)
             running_var.mul_(1 - momentum).add_(var[k] * (R / max(R - 1, 1)), alpha=momentum)
     return y.to(x.dtype).contiguous(memory_format=torch.channels_last), mean, rstd
+
+
+@_impl("conv2d_fwd")
+def _conv2d_fwd_cpu(x, w, stride, pad):
+    y = F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
+    return y.to(x.dtype).contiguous(memory_format=torch.channels_last)
+
+
+@_impl("conv2d_dgrad")
+def _conv2d_dgrad_cpu(dy, w, stride, pad, H, W):
+    shape = (dy.shape[0], w.shape[1], H, W)
+    dx = torch.nn.grad.conv2d_input(shape, w.float(), dy.float(), stride=stride, padding=pad)
+    return dx.to(dy.dtype).contiguous(memory_format=torch.channels_last)
+
+
+@_impl("conv2d_wgrad")
+def _conv2d_wgrad_cpu(dy, x, dw, stride, pad):
+    dw.add_(torch.nn.grad.conv2d_weight(x.float(), dw.shape, dy.float(), stride=stride, padding=pad))
 
 
 @_impl("bn_bwd")

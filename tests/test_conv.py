@@ -1,0 +1,145 @@
+"""Implicit-GEMM NHWC convolution kernels (csrc/kernels/conv.hip) vs a plain PyTorch fp32 reference.
+
+Shapes cover every distinct conv of the SwAV ResNet-50 trunk: the 7x7/2
+3-channel stem (im2col path), 1x1 reduce/expand, 3x3 stride 1 and stride 2 (parity-class dgrad) and
+the 1x1 stride-2 downsample, at small batch and both crop resolutions' spatial sizes.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dedloc_amd.ops  # noqa: F401
+
+CL = torch.channels_last
+
+# (N, Cin, H, Cout, k, stride, pad)
+SHAPES = [
+    (2, 3, 32, 64, 7, 2, 3),        # stem (im2col)
+    (2, 64, 14, 64, 1, 1, 0),       # layer1 reduce
+    (2, 64, 14, 64, 3, 1, 1),       # layer1 3x3
+    (2, 64, 14, 256, 1, 1, 0),      # expand / downsample (stride 1)
+    (2, 256, 14, 128, 1, 1, 0),
+    (2, 128, 14, 128, 3, 2, 1),     # layer2 first block 3x3 stride 2
+    (2, 256, 14, 512, 1, 2, 0),     # downsample stride 2
+    (3, 512, 6, 512, 3, 2, 1),      # layer4 first block (96-crop spatial 6 -> 3)
+    (4, 512, 3, 512, 3, 1, 1),      # layer4 3x3 at 3x3 spatial
+    (1, 1024, 7, 2048, 1, 2, 0),    # odd spatial size with stride 2
+    (2, 128, 9, 192, 3, 1, 1),      # Cout not a multiple of the 128 tile
+]
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _data(dev, N, Cin, H, Cout, k, stride, pad, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(N, Cin, H, H, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).bfloat16().to(dev)
+    w = w.contiguous(memory_format=CL)
+    P = (H + 2 * pad - k) // stride + 1
+    dy = torch.randn(N, Cout, P, P, generator=g).bfloat16().to(dev).contiguous(memory_format=CL)
+    return x, w, dy
+
+
+def _reference(x, w, dy, stride, pad):
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    y = F.conv2d(xr, wr, stride=stride, padding=pad)
+    dx, dw = torch.autograd.grad(y, [xr, wr], dy.float())
+    return y.detach(), dx, dw
+
+
+def test_conv_ops_cpu_match_autograd():
+    x, w, dy = _data("cpu", 2, 8, 9, 16, 3, 2, 1)
+    y = torch.ops.dedloc.conv2d_fwd(x, w, 2, 1)
+    yr, dxr, dwr = _reference(x, w, dy, 2, 1)
+    assert _rel(y, yr) < 1e-2
+    dx = torch.ops.dedloc.conv2d_dgrad(dy, w, 2, 1, 9, 9)
+    assert _rel(dx, dxr) < 1e-2
+    dw = torch.zeros(16, 8, 3, 3)
+    torch.ops.dedloc.conv2d_wgrad(dy, x, dw, 2, 1)
+    assert _rel(dw, dwr) < 1e-5
+
+
+def test_conv_module_cpu_fallback_is_stock():
+    from dedloc_amd.models.resnet_swav import ConvNHWC
+
+    m = ConvNHWC(8, 16, 3, stride=2, padding=1, bias=False)
+    ref = torch.nn.Conv2d(8, 16, 3, stride=2, padding=1, bias=False)
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(2, 8, 9, 9)
+    assert torch.equal(m(x), ref(x))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_conv_fwd_gpu(cuda, shape):
+    N, Cin, H, Cout, k, stride, pad = shape
+    x, w, dy = _data(cuda, *shape)
+    y = torch.ops.dedloc.conv2d_fwd(x, w, stride, pad)
+    yr, _, _ = _reference(x, w, dy, stride, pad)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=CL)
+    assert _rel(y, yr) < 1e-2, _rel(y, yr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] % 64 == 0 and s[3] % 64 == 0],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv_dgrad_gpu(cuda, shape):
+    N, Cin, H, Cout, k, stride, pad = shape
+    x, w, dy = _data(cuda, *shape, seed=1)
+    dx = torch.ops.dedloc.conv2d_dgrad(dy, w, stride, pad, H, H)
+    _, dxr, _ = _reference(x, w, dy, stride, pad)
+    assert dx.shape == dxr.shape and dx.is_contiguous(memory_format=CL)
+    assert _rel(dx, dxr) < 1e-2, _rel(dx, dxr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_conv_wgrad_gpu(cuda, shape):
+    N, Cin, H, Cout, k, stride, pad = shape
+    x, w, dy = _data(cuda, *shape, seed=2)
+    _, _, dwr = _reference(x, w, dy, stride, pad)
+    base = torch.randn(Cout, Cin, k, k, device=cuda).contiguous(memory_format=CL)
+    dw = base.clone()
+    torch.ops.dedloc.conv2d_wgrad(dy, x, dw, stride, pad)  # accumulates into the KRSC fp32 buffer
+    assert _rel(dw - base, dwr) < 1e-3, _rel(dw - base, dwr)
+    dw2 = base.clone().contiguous()  # NCHW-contiguous destination goes through a temporary
+    torch.ops.dedloc.conv2d_wgrad(dy, x, dw2, stride, pad)
+    assert _rel(dw2 - base, dwr) < 1e-3
+
+
+@pytest.mark.gpu
+def test_conv_wgrad_large_reduction_split_k(cuda):
+    """224-crop stem at batch 4: 50k-pixel reduction split over many workgroups (fp32 atomics)."""
+    shape = (4, 3, 224, 64, 7, 2, 3)
+    x, w, dy = _data(cuda, *shape, seed=3)
+    _, _, dwr = _reference(x, w, dy, 2, 3)
+    dw = torch.zeros(64, 3, 7, 7, device=cuda).contiguous(memory_format=CL)
+    torch.ops.dedloc.conv2d_wgrad(dy, x, dw, 2, 3)
+    assert _rel(dw, dwr) < 1e-3
+
+
+@pytest.mark.gpu
+def test_conv_module_grads_land_in_flat_buffer(cuda):
+    """ConvNHWC inside FlatParams(autograd, channels_last): dgrad returned, wgrad accumulated in place."""
+    from dedloc_amd.models.resnet_swav import ConvNHWC
+    from dedloc_amd.utils.flat import FlatParams
+
+    torch.manual_seed(4)
+    m = ConvNHWC(64, 128, 3, stride=2, padding=1, bias=False).to(cuda)
+    w_ref = m.weight.detach().bfloat16().float().clone()
+    flat = FlatParams(m.named_parameters(), device=cuda, with_bf16=False, autograd=True, channels_last=True)
+    x = torch.randn(2, 64, 12, 12, device=cuda).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
+    for _ in range(2):  # two backward passes accumulate
+        y = m(x)
+        coef = torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)
+        (y.float() * coef).sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    wr = w_ref.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=2, padding=1)
+    (yr * coef).sum().backward()
+    assert _rel(y, yr) < 1e-2
+    assert _rel(flat.view(flat.grad, "weight"), 2 * wr.grad) < 1e-2
+    assert _rel(x.grad, 2 * xr.grad) < 1e-2
