@@ -46,6 +46,13 @@ def main():
 
         os.environ.pop("DEDLOC_GEMM", None)
         rec("current", lambda: O.gemm_acc_f32(dy, x, g, True, False))
+        for sp in (1, 2, 4, 8, 16, 32):  # direct hipBLASLt token-split into fp32 slabs, forced split count
+            os.environ["DEDLOC_WGRAD_SPLITS"] = str(sp)
+            rec(f"lt_split{sp}", lambda: O.gemm_acc_f32(dy, x, g, True, False))
+        os.environ.pop("DEDLOC_WGRAD_SPLITS", None)
+        if os.environ.get("WGRAD_QUICK"):
+            print(json.dumps(out), flush=True)
+            continue
         rec("aten_f32", lambda: torch.ops.aten.addmm.dtype_out(g, dy.t(), x, torch.float32, out=g))
         rec("aten_bf16+add", lambda: g.add_(torch.mm(dy.t(), x)))
         os.environ["DEDLOC_GEMM"] = "mfma"

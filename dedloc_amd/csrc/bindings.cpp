@@ -440,6 +440,11 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
 // 3072x1024: 244 -> ~200 us.  S = largest power of two <= min(8, 256 / #256x256-tiles).
 int wgrad_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) {  // measurement override (bench/wgrad_bench.py)
+    int s = std::max(1, std::atoi(e));
+    while (s > 1 && (K % (s * 64) || K / s < 256)) s /= 2;
+    return s;
+  }
   int s = 1;
   while (s < 8 && tiles * s * 2 <= 256 && K % (s * 2 * 64) == 0 && K / (s * 2) >= 1024) s *= 2;
   return s;

@@ -19,10 +19,11 @@
 // 4x4 v_mfma_f32_16x16x32_bf16 tiles, register-staged double-buffered LDS (T14: tile t+1's global
 // loads are issued before tile t's MFMAs and written to the other buffer after them), XOR-swizzled
 // LDS images (K-inner rows read with ds_read_b128, K-outer rows with ds_read_b64_tr_b16), 64 KiB
-// LDS and <=256 VGPRs so two workgroups share a CU, XCD-aware tile order (T1).  All gathered loads
-// are unconditional 16-byte loads from a clamped address followed by a select, so the compiler never
-// branches around a load (§5 item 4(c)).  The forward kernel swaps the MFMA operand roles so each
-// lane owns 4 consecutive output channels of one pixel (8-byte NHWC stores).
+// LDS and <=256 VGPRs so two workgroups share a CU, XCD-aware tile order (T1).  Gathered loads are
+// unconditional 16-byte buffer loads whose padding taps read zeros through the descriptor's range
+// check, so the compiler never branches around a load (§5 item 4(c)) and never waits early; two
+// register stage sets keep two k-tiles of loads in flight.  The forward kernel swaps the MFMA
+// operand roles so each lane owns 4 consecutive output channels of one pixel (8-byte NHWC stores).
 #include <algorithm>
 
 #include "dl_common.h"
@@ -89,8 +90,19 @@ __device__ __forceinline__ void st_kout(const Stage& s, uint8_t* img) {
   }
 }
 
-__device__ __forceinline__ uint4 sel(bool ok, uint4 v) {
-  return ok ? v : uint4{0u, 0u, 0u, 0u};
+// Gathered operands are read with raw buffer loads (SRSRC descriptor, 32-bit byte offsets): a padding
+// tap or a row past the end gets an offset beyond num_records and the hardware returns zeros, so no
+// select consumes the loaded value early (a select right after the load forces a vmcnt wait there and
+// serialises the prefetch pipeline).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned OOB = 0xFFFFFFF0u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  return uint4{v.x, v.y, v.z, v.w};
 }
 
 // exact a / b for 0 <= a < 2^24 through one float reciprocal (+-1 correction)
@@ -113,6 +125,7 @@ struct FwdArgs {
   int OH, OW, osh, osw, oh0, ow0;
   long ldo;
   int M, K;
+  unsigned img_bytes, w_bytes;
 };
 
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
@@ -148,6 +161,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) brow[u] = min(n0 + (tid >> 3) + 32 * u, p.N - 1);
 
+  const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, p.w_bytes);
   auto load_a = [&](Stage& s, int k0) {
     const int t = k0 / g.C, c0 = k0 - t * g.C;
     const int tr = t / g.TS, ts = t - tr * g.TS;
@@ -156,13 +171,13 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     for (int u = 0; u < 4; ++u) {
       const int h = hb[u] + dh, w = wb[u] + dw;
       const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const long off = ok ? ((long)(nb[u] + h) * g.W + w) * g.C + c0 + cofs : 0;
-      s.v[u] = sel(ok, *reinterpret_cast<const uint4*>(g.img + off));
+      const unsigned off = 2u * ((unsigned)((nb[u] + h) * g.W + w) * (unsigned)g.C + (unsigned)(c0 + cofs));
+      s.v[u] = bload(rimg, ok ? off : OOB);
     }
   };
   auto load_b = [&](Stage& s, int k0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s.v[u] = *reinterpret_cast<const uint4*>(p.w + (long)brow[u] * p.ldw + k0 + cofs);
+    for (int u = 0; u < 4; ++u) s.v[u] = bload(rw, 2u * ((unsigned)brow[u] * (unsigned)p.ldw + (unsigned)(k0 + cofs)));
   };
 
   floatx4 acc[4][4];
@@ -171,23 +186,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / BK;
-  Stage sa, sb;
-  if (nk > 0) {
-    load_a(sa, 0);
-    load_b(sb, 0);
-    st_kin(sa, smem);
-    st_kin(sb, smem + TILE);
-  }
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    const uint8_t* Ai = smem + cur * 2 * TILE;
+  auto compute = [&](const uint8_t* Ai) {
     const uint8_t* Bi = Ai + TILE;
-    if (t + 1 < nk) {
-      load_a(sa, (t + 1) * BK);
-      load_b(sb, (t + 1) * BK);
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[4];
@@ -200,11 +200,42 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
         for (int mi = 0; mi < 4; ++mi) acc[ni][mi] = mfma16(bfr, af[mi], acc[ni][mi]);
       }
     }
-    if (t + 1 < nk) {
-      uint8_t* An = smem + (cur ^ 1) * 2 * TILE;
-      st_kin(sa, An);
-      st_kin(sb, An + TILE);
-    }
+  };
+
+  // Two register stage sets (x: even tiles, y: odd tiles) keep the global loads of tiles t+1 AND
+  // t+2 in flight while tile t computes: the gathered loads' latency is several times one 128x128
+  // k-step of MFMA work, so a single prefetched tile leaves the CU waiting.
+  const int nk = p.K / BK;
+  uint8_t* buf0 = smem;
+  uint8_t* buf1 = smem + 2 * TILE;
+  Stage xa, xb, ya, yb;
+  // The loop body is branch-free around the memory operations (tile indices past the end are
+  // clamped to the last tile: loaded and staged but never computed), so the compiler's wait
+  // counting sees the true issue order and waits only for the set it is about to store.
+  const int last = max(nk - 1, 0) * BK;
+  if (nk > 0) {
+    load_a(xa, 0);
+    load_b(xb, 0);
+    load_a(ya, min(BK, last));
+    load_b(yb, min(BK, last));
+    st_kin(xa, buf0);
+    st_kin(xb, buf0 + TILE);
+    load_a(xa, min(2 * BK, last));
+    load_b(xb, min(2 * BK, last));
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; t += 2) {
+    compute(buf0);  // tile t
+    st_kin(ya, buf1);
+    st_kin(yb, buf1 + TILE);
+    load_a(ya, min((t + 3) * BK, last));
+    load_b(yb, min((t + 3) * BK, last));
+    __syncthreads();
+    if (t + 1 < nk) compute(buf1);  // tile t + 1
+    st_kin(xa, buf0);
+    st_kin(xb, buf0 + TILE);
+    load_a(xa, min((t + 4) * BK, last));
+    load_b(xb, min((t + 4) * BK, last));
     __syncthreads();
   }
 
@@ -243,6 +274,7 @@ struct WgradArgs {
   int M;       // reduction extent Nimg*I*J
   int m_per_split;
   float rIJ, rJ;
+  unsigned img_bytes, dy_bytes;
 };
 
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
@@ -267,12 +299,14 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
   const int tr = t / g.TS, ts = t - tr * g.TS;
   const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
 
+  const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, p.dy_bytes);
   auto load_a = [&](Stage& s, int k0) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int m = kbeg + k0 + krow0 + 16 * u;
-      const bool ok = m < kend;
-      s.v[u] = sel(ok, *reinterpret_cast<const uint4*>(p.dy + (long)(ok ? m : kbeg) * p.ldy + acol));
+      const unsigned off = 2u * ((unsigned)m * (unsigned)p.ldy + (unsigned)acol);
+      s.v[u] = bload(rdy, m < kend ? off : OOB);
     }
   };
   auto load_b = [&](Stage& s, int k0) {
@@ -283,8 +317,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
       const int i = fdiv(r, g.J, p.rJ), j = r - i * g.J;
       const int h = i * g.sh + dh, w = j * g.sw + dw;
       const bool ok = m < kend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const long off = ok ? ((long)(n * g.H + h) * g.W + w) * g.C + c : 0;
-      s.v[u] = sel(ok, *reinterpret_cast<const uint4*>(g.img + off));
+      const unsigned off = 2u * ((unsigned)((n * g.H + h) * g.W + w) * (unsigned)g.C + (unsigned)c);
+      s.v[u] = bload(rimg, ok ? off : OOB);
     }
   };
 
@@ -294,20 +328,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  Stage sa, sb;
-  load_a(sa, 0);
-  load_b(sb, 0);
-  st_kout(sa, smem);
-  st_kout(sb, smem + TILE);
-  __syncthreads();
-  for (int s = 0; s < nk; ++s) {
-    const int cur = s & 1;
-    const uint8_t* Ai = smem + cur * 2 * TILE;
+  auto compute = [&](const uint8_t* Ai) {
     const uint8_t* Bi = Ai + TILE;
-    if (s + 1 < nk) {
-      load_a(sa, (s + 1) * BK);
-      load_b(sb, (s + 1) * BK);
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 bfr[4];
@@ -320,11 +342,34 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(af, bfr[ni], acc[mi][ni]);
       }
     }
-    if (s + 1 < nk) {
-      uint8_t* An = smem + (cur ^ 1) * 2 * TILE;
-      st_kout(sa, An);
-      st_kout(sb, An + TILE);
-    }
+  };
+
+  // 2-deep register prefetch (see the forward kernel)
+  uint8_t* buf0 = smem;
+  uint8_t* buf1 = smem + 2 * TILE;
+  Stage xa, xb, ya, yb;
+  const int last = (nk - 1) * BK;  // branch-free loop body, clamped tile indices (forward kernel)
+  load_a(xa, 0);
+  load_b(xb, 0);
+  load_a(ya, min(BK, last));
+  load_b(yb, min(BK, last));
+  st_kout(xa, buf0);
+  st_kout(xb, buf0 + TILE);
+  load_a(xa, min(2 * BK, last));
+  load_b(xb, min(2 * BK, last));
+  __syncthreads();
+  for (int s = 0; s < nk; s += 2) {
+    compute(buf0);
+    st_kout(ya, buf1);
+    st_kout(yb, buf1 + TILE);
+    load_a(ya, min((s + 3) * BK, last));
+    load_b(yb, min((s + 3) * BK, last));
+    __syncthreads();
+    if (s + 1 < nk) compute(buf1);
+    st_kout(xa, buf0);
+    st_kout(xb, buf0 + TILE);
+    load_a(xa, min((s + 4) * BK, last));
+    load_b(xb, min((s + 4) * BK, last));
     __syncthreads();
   }
 
@@ -396,7 +441,10 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
   const long M = (long)g.Nimg * g.I * g.J;
   if (M >= (1L << 31)) return -1;
   if (M == 0 || N == 0) return 0;
-  FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C};
+  const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * ldw;
+  if (img_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
+  FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C,
+            (unsigned)img_bytes, (unsigned)w_bytes};
   static bool attr = false;
   if (!attr) {
     set_lds(conv_fwd_kernel);
@@ -421,8 +469,10 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
   long splits = std::max(1L, std::min<long>((1024 + tiles - 1) / tiles, ksteps / 8));
   const long steps_per = (ksteps + splits - 1) / splits;
   splits = (ksteps + steps_per - 1) / steps_per;
+  const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, dy_bytes = 2L * M * ldy;
+  if (img_bytes >= (1L << 31) || dy_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
   WgradArgs a{g, dy, ldy, Cout, dw, lddw, Ncols, Brows, (int)M, (int)(steps_per * BK),
-              1.f / (float)(g.I * g.J), 1.f / (float)g.J};
+              1.f / (float)(g.I * g.J), 1.f / (float)g.J, (unsigned)img_bytes, (unsigned)dy_bytes};
   static bool attr = false;
   if (!attr) {
     set_lds(conv_wgrad_kernel);

@@ -49,6 +49,7 @@ class AlbertConfig:
     initializer_range: float = 0.02
     layer_norm_eps: float = 1e-12
     classifier_dropout_prob: float = 0.1
+    num_labels: Optional[int] = None  # classification heads (HF writes it to config.json as well)
     pad_token_id: int = 0
     bos_token_id: int = 2
     eos_token_id: int = 3
@@ -151,27 +152,19 @@ class _AlbertLayerFn(torch.autograd.Function):
         return dh, None, None, None, None, None
 
 
-class AlbertForPreTraining(nn.Module):
-    """HF-key-compatible ALBERT pre-training model (fp32 master params, bf16 compute)."""
+class AlbertPreTrainedModel(nn.Module):
+    """Shared ALBERT trunk (embeddings, mapping-in, the shared layer group(s), optional pooler) with
+    HF-compatible parameter names, flat fp32/bf16 storage and the fused encoder forward.  Heads are
+    added by the subclasses (pre-training, sequence / token classification)."""
+
+    add_pooler = True
 
     def __init__(self, config: AlbertConfig):
         super().__init__()
         self.config = c = config
         self._p: Dict[str, nn.Parameter] = {}
         E, H, I, V = c.embedding_size, c.hidden_size, c.intermediate_size, c.vocab_size
-
-        def add(name, *shape, init="normal"):
-            t = torch.empty(*shape)
-            if init == "normal":
-                t.normal_(0.0, c.initializer_range)
-            elif init == "ones":
-                t.fill_(1.0)
-            else:
-                t.zero_()
-            p = nn.Parameter(t)
-            self._p[name] = p
-            self.register_parameter(name.replace(".", "__"), p)
-
+        add = self._add
         add("albert.embeddings.word_embeddings.weight", V, E)
         add("albert.embeddings.position_embeddings.weight", c.max_position_embeddings, E)
         add("albert.embeddings.token_type_embeddings.weight", c.type_vocab_size, E)
@@ -198,16 +191,26 @@ class AlbertForPreTraining(nn.Module):
                 add(pre + "ffn.bias", I, init="zeros")
                 add(pre + "ffn_output.weight", H, I)
                 add(pre + "ffn_output.bias", H, init="zeros")
-        add("albert.pooler.weight", H, H)
-        add("albert.pooler.bias", H, init="zeros")
-        add("predictions.bias", V, init="zeros")
-        add("predictions.dense.weight", E, H)
-        add("predictions.dense.bias", E, init="zeros")
-        add("predictions.LayerNorm.weight", E, init="ones")
-        add("predictions.LayerNorm.bias", E, init="zeros")
-        add("sop_classifier.classifier.weight", 2, H)
-        add("sop_classifier.classifier.bias", 2, init="zeros")
+        if self.add_pooler:
+            add("albert.pooler.weight", H, H)
+            add("albert.pooler.bias", H, init="zeros")
+        self._add_heads()
         self.flat: Optional[FlatParams] = None
+
+    def _add(self, name, *shape, init="normal"):
+        t = torch.empty(*shape)
+        if init == "normal":
+            t.normal_(0.0, self.config.initializer_range)
+        elif init == "ones":
+            t.fill_(1.0)
+        else:
+            t.zero_()
+        p = nn.Parameter(t)
+        self._p[name] = p
+        self.register_parameter(name.replace(".", "__"), p)
+
+    def _add_heads(self):
+        pass
 
     # ------------------------------------------------------------------ parameters / checkpoints
     def hf_named_parameters(self):
@@ -222,11 +225,8 @@ class AlbertForPreTraining(nn.Module):
         return self.flat
 
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
-        """state dict with exactly HF AlbertForPreTraining's keys (tied decoder included)."""
-        sd = {k: v.detach() for k, v in self._p.items()}
-        sd["predictions.decoder.weight"] = sd["albert.embeddings.word_embeddings.weight"]
-        sd["predictions.decoder.bias"] = sd["predictions.bias"]
-        return sd
+        """state dict with exactly the HF model class's keys."""
+        return {k: v.detach() for k, v in self._p.items()}
 
     @torch.no_grad()
     def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
@@ -242,14 +242,18 @@ class AlbertForPreTraining(nn.Module):
     def save_pretrained(self, directory: str):
         os.makedirs(directory, exist_ok=True)
         self.config.save_pretrained(directory)
-        sd = {k: v.detach().float().cpu().contiguous() for k, v in self.hf_state_dict().items()}
-        sd["predictions.decoder.weight"] = sd["predictions.decoder.weight"].clone()
-        sd["predictions.decoder.bias"] = sd["predictions.decoder.bias"].clone()
+        # tied entries are stored as separate tensors, as HF's torch.save of the state dict does
+        sd = {k: v.detach().float().cpu().contiguous().clone() for k, v in self.hf_state_dict().items()}
         torch.save(sd, os.path.join(directory, "pytorch_model.bin"))
 
     @classmethod
-    def from_pretrained(cls, directory: str) -> "AlbertForPreTraining":
+    def from_pretrained(cls, directory: str, strict: Optional[bool] = None, **config_overrides):
+        """Load a checkpoint directory.  Head classes loading a pre-training checkpoint keep their
+        freshly initialised head (HF behaviour), so ``strict`` defaults to True only for the class
+        that wrote it (keys must all be present)."""
         cfg = AlbertConfig.from_pretrained(directory)
+        for k, v in config_overrides.items():
+            setattr(cfg, k, v)
         model = cls(cfg)
         sd_path = os.path.join(directory, "pytorch_model.bin")
         if os.path.exists(sd_path):
@@ -258,7 +262,9 @@ class AlbertForPreTraining(nn.Module):
             from safetensors.torch import load_file
 
             sd = load_file(os.path.join(directory, "model.safetensors"))
-        model.load_hf_state_dict(sd)
+        if strict is None:
+            strict = all(k in sd for k in model._p if not k.startswith("albert."))
+        model.load_hf_state_dict(sd, strict=strict)
         return model
 
     def resize_token_embeddings(self, n: int):
@@ -268,6 +274,8 @@ class AlbertForPreTraining(nn.Module):
             return
         assert self.flat is None, "resize before materialize()"
         for key in ("albert.embeddings.word_embeddings.weight", "predictions.bias"):
+            if key not in self._p:
+                continue
             old = self._p[key].data
             new = torch.empty((n,) + tuple(old.shape[1:]))
             if key.endswith("weight"):
@@ -352,6 +360,32 @@ class AlbertForPreTraining(nn.Module):
                 h = self._albert_layer(h, views[g][i], mask, Sp)
         return h, Sp
 
+    def num_parameters(self) -> int:
+        return sum(p.numel() for p in self._p.values())
+
+
+class AlbertForPreTraining(AlbertPreTrainedModel):
+    """HF ``AlbertForPreTraining`` (MLM head with the decoder tied to the word embeddings + SOP head)."""
+
+    def _add_heads(self):
+        c = self.config
+        E, H, V = c.embedding_size, c.hidden_size, c.vocab_size
+        add = self._add
+        add("predictions.bias", V, init="zeros")
+        add("predictions.dense.weight", E, H)
+        add("predictions.dense.bias", E, init="zeros")
+        add("predictions.LayerNorm.weight", E, init="ones")
+        add("predictions.LayerNorm.bias", E, init="zeros")
+        add("sop_classifier.classifier.weight", 2, H)
+        add("sop_classifier.classifier.bias", 2, init="zeros")
+
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        """state dict with exactly HF AlbertForPreTraining's keys (tied decoder included)."""
+        sd = super().hf_state_dict()
+        sd["predictions.decoder.weight"] = sd["albert.embeddings.word_embeddings.weight"]
+        sd["predictions.decoder.bias"] = sd["predictions.bias"]
+        return sd
+
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, labels=None, sentence_order_label=None,
                 mlm_positions=None, mlm_labels=None, return_logits=False):
         """HF-compatible pre-training forward.
@@ -409,8 +443,71 @@ class AlbertForPreTraining(nn.Module):
         out["loss"] = loss
         return out
 
-    def num_parameters(self) -> int:
-        return sum(p.numel() for p in self._p.values())
+
+class AlbertForSequenceClassification(AlbertPreTrainedModel):
+    """HF ``AlbertForSequenceClassification``: pooler(tanh) on [CLS] -> dropout -> classifier.
+    Cross-entropy for ``num_labels > 1``, MSE for regression (``num_labels == 1``).  Used by the
+    sahajBERT NCC fine-tuning recipe (reference sahajbert/train_ncc.py)."""
+
+    def __init__(self, config: AlbertConfig, num_labels: Optional[int] = None):
+        self.num_labels = int(num_labels or config.num_labels or 2)
+        config.num_labels = self.num_labels
+        super().__init__(config)
+
+    def _add_heads(self):
+        self._add("classifier.weight", self.num_labels, self.config.hidden_size)
+        self._add("classifier.bias", self.num_labels, init="zeros")
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, labels=None):
+        c, f = self.config, self.flat
+        B = input_ids.shape[0]
+        h, Sp = self.encode(input_ids, attention_mask, token_type_ids)
+        cls = h.view(B, Sp, -1)[:, 0].contiguous()
+        pooled = ops.tanh(ops.linear(cls, f.w("albert.pooler.weight"), f.w("albert.pooler.bias"),
+                                     f.g("albert.pooler.weight"), f.g("albert.pooler.bias")))
+        if self.training and c.classifier_dropout_prob > 0:
+            pooled = F.dropout(pooled, c.classifier_dropout_prob, True)
+        logits = ops.linear(pooled, f.w("classifier.weight"), f.w("classifier.bias"), f.g("classifier.weight"),
+                            f.g("classifier.bias"))
+        out = {"logits": logits}
+        if labels is not None:
+            if self.num_labels == 1:
+                out["loss"] = F.mse_loss(logits.float().view(-1), labels.float().view(-1))
+            else:
+                out["loss"] = ops.cross_entropy(logits, labels)
+        return out
+
+
+class AlbertForTokenClassification(AlbertPreTrainedModel):
+    """HF ``AlbertForTokenClassification`` (no pooler): dropout -> per-token classifier, CE over the
+    positions whose label != -100.  Used by the sahajBERT NER recipe (reference sahajbert/train_ner.py)."""
+
+    add_pooler = False
+
+    def __init__(self, config: AlbertConfig, num_labels: Optional[int] = None):
+        self.num_labels = int(num_labels or config.num_labels or 2)
+        config.num_labels = self.num_labels
+        super().__init__(config)
+
+    def _add_heads(self):
+        self._add("classifier.weight", self.num_labels, self.config.hidden_size)
+        self._add("classifier.bias", self.num_labels, init="zeros")
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, labels=None):
+        c, f = self.config, self.flat
+        B, S = input_ids.shape
+        h, Sp = self.encode(input_ids, attention_mask, token_type_ids)
+        if self.training and c.classifier_dropout_prob > 0:
+            h = F.dropout(h, c.classifier_dropout_prob, True)
+        logits = ops.linear(h, f.w("classifier.weight"), f.w("classifier.bias"), f.g("classifier.weight"),
+                            f.g("classifier.bias"))
+        out = {"logits": logits.view(B, Sp, -1)[:, :S]}
+        if labels is not None:
+            lab = labels
+            if Sp != S:
+                lab = F.pad(labels, (0, Sp - S), value=-100)
+            out["loss"] = ops.cross_entropy(logits, lab.reshape(-1))
+        return out
 
 
 def flops_per_sample(config: AlbertConfig, seq_len: int, masked_per_seq: int) -> float:
