@@ -211,14 +211,18 @@ class DecentralizedAverager:
         self.dht.store(f"{self.prefix}_state_sharing", {"endpoint": self.state_server.endpoint, "step": int(step)},
                        get_dht_time() + self.metadata_expiration, subkey=self.peer_id, return_future=True)
 
-    def load_state_from_peers(self, timeout: float = 60.0):
-        """(metadata, tensors) from the freshest state-sharing peer, or None if nobody shares."""
+    def load_state_from_peers(self, timeout: float = 15.0, min_step: int = 0):
+        """(metadata, tensors) from the freshest state-sharing peer whose advertised step is at least
+        ``min_step``, or None if nobody qualifies (peers that are not ahead have nothing to give: a
+        fresh collaboration of peers all at step 0 starts at once instead of downloading in a circle)."""
         rec = self.dht.get(f"{self.prefix}_state_sharing", latest=True)
         if rec is None or not isinstance(rec.value, dict):
             return None
         donors = []
         for sub, v in rec.value.items():
             if sub == self.peer_id or not isinstance(v.value, dict):
+                continue
+            if int(v.value.get("step", 0)) < min_step:
                 continue
             donors.append((v.value.get("step", 0), v.value["endpoint"]))
         for step, ep in sorted(donors, reverse=True):

@@ -180,6 +180,7 @@ void launch_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const flo
 int dl_layernorm_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y,
                      bf16_t* s_out, float* mean, float* rstd, int rows, int D, float eps, hipStream_t st) {
   switch (D) {
+    case 64: launch_fwd<64>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
     case 128: launch_fwd<128>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
     case 256: launch_fwd<256>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
     case 512: launch_fwd<512>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st); break;
@@ -196,6 +197,7 @@ int dl_layernorm_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, cons
                      bf16_t* ds, float* dg_part, float* db_part, float* dsum, int rows, int D, int nparts,
                      hipStream_t st) {
   switch (D) {
+    case 64: launch_bwd<64>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
     case 128: launch_bwd<128>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
     case 256: launch_bwd<256>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
     case 512: launch_bwd<512>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;

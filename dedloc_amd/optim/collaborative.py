@@ -159,8 +159,11 @@ class CollaborativeOptimizer:
     def load_state_from_peers(self, **kwargs) -> bool:
         """Download params + optimizer state from the freshest donor (App. A.7)."""
         self._finish_param_round(apply=False)
+        # download WITHOUT holding lock_step: our own state server takes that lock to snapshot the
+        # state it serves, so two peers loading from each other would otherwise block each other
+        kwargs.setdefault("min_step", self.local_step + 1 if self.local_step > 0 or self.is_synchronized else 0)
+        res = self.averager.load_state_from_peers(**kwargs)
         with self.lock_step:
-            res = self.averager.load_state_from_peers(**kwargs)
             if res is None:
                 # nobody shares state: keep our parameters but adopt the collaboration's step, otherwise
                 # an out-of-sync peer would retry forever without contributing

@@ -9,7 +9,7 @@ step() {
   echo "rc=$rc $*"; grep -E '^\{|passed|failed' "$log" | tail -60 || tail -4 "$log"
   if [ $rc -ne 0 ]; then echo "stopping after rc=$rc"; tail -30 "$log"; exit $rc; fi
 }
-step gpurun_out/s3_conv_tests.log 300 python -u -m pytest tests/test_conv.py tests/test_finetune.py -x -q -m gpu --timeout 120 --timeout-method thread
+step gpurun_out/s3_conv_tests.log 300 python -u -m pytest tests/test_conv.py tests/test_finetune.py tests/test_kernels_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread
 step gpurun_out/s3_conv_bench.log 400 python bench/conv_bench.py
 step gpurun_out/s3_swav_hip.log 300 python bench/swav_step.py --batch 64 --iters 10
 WGRAD_QUICK=1 step gpurun_out/s3_wgrad.log 300 python bench/wgrad_bench.py

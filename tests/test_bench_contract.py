@@ -6,6 +6,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -24,20 +25,28 @@ def _port():
 
 @pytest.mark.multiproc
 @pytest.mark.timeout(400)
-def test_bench_two_ranks_cpu_plumbing(tmp_path):
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_multi_rank_cpu_plumbing(tmp_path, nproc):
     from dedloc_amd.models.albert import AlbertConfig
 
     cfg = tmp_path / "cfg"
     AlbertConfig.tiny(num_hidden_layers=2, max_position_embeddings=64).save_pretrained(str(cfg))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--cpu_test", str(cfg), "--micro_batch", "2", "--seq_len", "64", "--target_batch_size", "8"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc), "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(nproc), "--steps", "2", "--warmup", "1",
+           "--cpu_test", str(cfg), "--micro_batch", "2", "--seq_len", "64", "--target_batch_size", str(4 * nproc)]
     env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    t0 = time.time()
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=360, env=env)
+    wall = time.time() - t0
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert KEYS <= set(out)
-    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["value"] > 0 and out["higher_is_better"] is True
-    assert out["averaging_rounds"] >= 1  # the two peers averaged over the world communicator
+    assert out["n_gpus"] == nproc and out["steps"] == 2 and out["value"] > 0 and out["higher_is_better"] is True
+    # every global step (warm-up + timed) averaged over the world communicator with all peers
+    assert out["averaging_rounds"] >= 3 and out["averaging_failed"] == 0
+    assert out["last_group"]["size"] == nproc
+    # a fresh collaboration starts at once (no circular state downloads between step-0 peers) and
+    # no step waits out a matchmaking window
+    assert out["ms_per_step"] < 4000 and wall < 120, (out["ms_per_step"], wall)
