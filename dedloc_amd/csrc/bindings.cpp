@@ -663,13 +663,21 @@ inline at::Tensor krsc_view(const at::Tensor& w) {
 
 inline int64_t conv_out(int64_t n, int64_t k, int64_t stride, int64_t pad) { return (n + 2 * pad - k) / stride + 1; }
 
-// stem (Cin not a multiple of 64): explicit im2col matrix [N*P*Q, Kp], k = (r, s, c), zero padded
+// stem (Cin not a multiple of 64): explicit im2col matrix [N*P*Q, Kp], k = r*SCp + s*C + c (each
+// filter row padded from S*C to SCp = roundup(S*C, 8) columns), zero padded to Kp = roundup(R*SCp, 64)
+struct StemCols {
+  int64_t SCp, Kp;
+};
+inline StemCols stem_cols(int64_t R, int64_t S, int64_t C) {
+  const int64_t SCp = (S * C + 7) / 8 * 8;
+  return {SCp, (R * SCp + 63) / 64 * 64};
+}
 inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t P,
-                              int64_t Q, int64_t Kp) {
+                              int64_t Q, const StemCols& sc) {
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  auto col = at::empty({N * P * Q, Kp}, x.options());
+  auto col = at::empty({N * P * Q, sc.Kp}, x.options());
   check(dl_im2col(cbf(x), (int)N, (int)H, (int)W, (int)C, (int)R, (int)S, (int)stride, (int)pad, (int)P, (int)Q,
-                  (int)Kp, bf(col), cur_stream(x)),
+                  (int)sc.SCp, (int)sc.Kp, bf(col), cur_stream(x)),
         "im2col");
   return col;
 }
@@ -697,12 +705,13 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
     return y;
   }
   // stem: im2col, then a 1x1 conv over the column matrix
-  const int64_t RSC = R * S * C, Kp = (RSC + 63) / 64 * 64, M = N * P * Q;
-  const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, Kp);
-  auto wp = at::zeros({K, Kp}, w.options());
-  wp.narrow(1, 0, RSC).copy_(wk.reshape({K, RSC}));
-  check(dl_conv_fwd(geom(cbf(col), M, 1, 1, Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(wp), Kp, (int)K, bf(y), 1, 1, 1, 1,
-                    0, 0, K, cur_stream(x)),
+  const StemCols sc = stem_cols(R, S, C);
+  const int64_t M = N * P * Q;
+  const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
+  auto wp = at::zeros({K, sc.Kp}, w.options());
+  wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
+  check(dl_conv_fwd(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(wp), sc.Kp, (int)K, bf(y), 1, 1,
+                    1, 1, 0, 0, K, cur_stream(x)),
         "conv2d_fwd(stem)");
   return y;
 }
@@ -763,13 +772,18 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
   if (C % 8 == 0 && C >= 8 && C % 64 == 0) {
     rc = dl_conv_wgrad(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(dy), K, (int)K,
                        f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy));
+    check(rc, "conv2d_wgrad");
   } else {
-    const int64_t RSC = R * S * C, Kp = (RSC + 63) / 64 * 64, M = N * P * Q;
-    const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, Kp);
-    rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K, f32(acc), RSC,
-                       (int)RSC, cur_stream(dy));
+    // stem: wgrad over the padded column matrix into a [K, R, SCp] slab, then the real columns
+    const StemCols sc = stem_cols(R, S, C);
+    const int64_t M = N * P * Q;
+    const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
+    auto slab = at::zeros({K, R, sc.SCp}, dw.options());
+    rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K, f32(slab),
+                       R * sc.SCp, (int)(R * sc.SCp), cur_stream(dy));
+    check(rc, "conv2d_wgrad(stem)");
+    acc.view({K, R, S * C}).add_(slab.narrow(2, 0, S * C));
   }
-  check(rc, "conv2d_wgrad");
   if (!direct) dk.add_(acc);
 }
 

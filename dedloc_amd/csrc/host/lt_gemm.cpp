@@ -143,7 +143,9 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
   uint64_t wsz = s->ws_size;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz));
   const char* tune_env = std::getenv("DEDLOC_LT_TUNE");
-  const int want = (tune_env && tune_env[0] == '0') ? 1 : 16;
+  // candidates timed per shape (once, at the first call): DEDLOC_LT_TUNE=0 takes the heuristic's
+  // first choice, =N times the top N (default 64: the top 16 missed faster kernels on some shapes)
+  const int want = !tune_env ? 64 : std::max(1, std::atoi(tune_env));
   std::vector<hipblasLtMatmulHeuristicResult_t> res(want);
   int n = 0;
   const hipblasStatus_t hs =

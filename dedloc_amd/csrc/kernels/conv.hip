@@ -126,6 +126,7 @@ struct FwdArgs {
   long ldo;
   int M, K;
   unsigned img_bytes, w_bytes;
+  int tpw;  // output tiles per workgroup
 };
 
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
@@ -135,35 +136,49 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   const int wm = wv >> 1, wn = wv & 1;
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int ntiles = tiles_m * tiles_n;
+  // persistent over `tpw` consecutive output tiles (same pixel rows, successive channel blocks
+  // first): the load stream runs on across tile boundaries, so short-K convs (1x1 over 64-256
+  // channels: 1-4 k-steps per tile) keep loads in flight under the previous tile's MFMAs/epilogue
+  const int tile0 = xcd_remap(blockIdx.x, gridDim.x) * p.tpw;
+  const int mytiles = min(p.tpw, ntiles - tile0);
+  if (mytiles <= 0) return;
+  const int nk = p.K / BK;
   const int IJ = g.I * g.J;
-
-  // per-thread gathered rows (fixed over the K loop): image row base and pixel origin
-  int hb[4], wb[4], nb[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int m = m0 + (tid >> 3) + 32 * u;
-    if (m < p.M) {
-      const int n = m / IJ, r = m - n * IJ;
-      const int i = r / g.J, j = r - i * g.J;
-      hb[u] = i * g.sh;
-      wb[u] = j * g.sw;
-      nb[u] = n * g.H;
-    } else {
-      hb[u] = -(1 << 29);  // never inside the image -> zero row
-      wb[u] = 0;
-      nb[u] = 0;
-    }
-  }
   const int cofs = (tid & 7) * 8;
-  int brow[4];
+
+  // load cursor: per-thread decoded gathered rows of the tile being loaded
+  int dec_tile = -1;
+  int hb[4], wb[4], nb[4], brow[4];
+  auto decode = [&](int tile) {
+    dec_tile = tile;
+    const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) brow[u] = min(n0 + (tid >> 3) + 32 * u, p.N - 1);
+    for (int u = 0; u < 4; ++u) {
+      const int m = m0 + (tid >> 3) + 32 * u;
+      if (m < p.M) {
+        const int n = m / IJ, r = m - n * IJ;
+        const int i = r / g.J, j = r - i * g.J;
+        hb[u] = i * g.sh;
+        wb[u] = j * g.sw;
+        nb[u] = n * g.H;
+      } else {
+        hb[u] = -(1 << 29);  // never inside the image -> zero row
+        wb[u] = 0;
+        nb[u] = 0;
+      }
+      brow[u] = min(n0 + (tid >> 3) + 32 * u, p.N - 1);
+    }
+  };
 
   const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, p.w_bytes);
-  auto load_a = [&](Stage& s, int k0) {
+  const int nsteps = mytiles * nk;
+  // stage step s (clamped: steps past the end reload the last one; staged, never computed)
+  auto load_step = [&](Stage& sa, Stage& sb, int s) {
+    s = min(s, nsteps - 1);
+    const int tile = tile0 + s / nk, k0 = (s % nk) * BK;
+    if (tile != dec_tile) decode(tile);
     const int t = k0 / g.C, c0 = k0 - t * g.C;
     const int tr = t / g.TS, ts = t - tr * g.TS;
     const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
@@ -172,12 +187,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
       const int h = hb[u] + dh, w = wb[u] + dw;
       const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       const unsigned off = 2u * ((unsigned)((nb[u] + h) * g.W + w) * (unsigned)g.C + (unsigned)(c0 + cofs));
-      s.v[u] = bload(rimg, ok ? off : OOB);
+      sa.v[u] = bload(rimg, ok ? off : OOB);
     }
-  };
-  auto load_b = [&](Stage& s, int k0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s.v[u] = bload(rw, 2u * ((unsigned)brow[u] * (unsigned)p.ldw + (unsigned)(k0 + cofs)));
+    for (int u = 0; u < 4; ++u) sb.v[u] = bload(rw, 2u * ((unsigned)brow[u] * (unsigned)p.ldw + (unsigned)(k0 + cofs)));
   };
 
   floatx4 acc[4][4];
@@ -202,60 +215,77 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     }
   };
 
-  // Two register stage sets (x: even tiles, y: odd tiles) keep the global loads of tiles t+1 AND
-  // t+2 in flight while tile t computes: the gathered loads' latency is several times one 128x128
-  // k-step of MFMA work, so a single prefetched tile leaves the CU waiting.
-  const int nk = p.K / BK;
+  // acc[ni][mi][i] = out[pixel m0+wm*64+mi*16+(lane&15)][channel n0+wn*64+ni*16+4*(lane>>4)+i].
+  // The 128x128 bf16 tile is staged through the LDS buffer the pipeline is not using (`stage`,
+  // 32 KiB: [128 pixels][16 chunks of 16 B], chunk c of row r at c ^ (r & 15)) and written back as
+  // whole 256-byte pixel rows (16 B per lane), instead of 8-byte pieces scattered over 16 rows.
+  auto epilogue = [&](int tile, uint8_t* stage) {
+    const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int row = wm * 64 + mi * 16 + (lane & 15);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = wn * 64 + ni * 16 + 4 * (lane >> 4);  // channel within the tile
+        uint2 v;
+        v.x = (uint32_t)f2bf(acc[ni][mi][0]) | ((uint32_t)f2bf(acc[ni][mi][1]) << 16);
+        v.y = (uint32_t)f2bf(acc[ni][mi][2]) | ((uint32_t)f2bf(acc[ni][mi][3]) << 16);
+        *reinterpret_cast<uint2*>(stage + row * 256 + (((col >> 3) ^ (row & 15)) << 4) + ((col & 7) << 1)) = v;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = tid + NT * u, row = idx >> 4, c = idx & 15;
+      const int m = m0 + row, ch = n0 + c * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(stage + row * 256 + ((c ^ (row & 15)) << 4));
+      if (m < p.M && ch < p.N) {
+        const int n = m / IJ, r = m - n * IJ;
+        const int i = r / g.J, j = r - i * g.J;
+        bf16_t* orow = p.out + ((long)(n * p.OH + i * p.osh + p.oh0) * p.OW + j * p.osw + p.ow0) * p.ldo;
+        *reinterpret_cast<uint4*>(orow + ch) = v;
+      }
+    }
+    __syncthreads();  // the staging buffer is restaged by the pipeline right after
+  };
+
+  if (nk == 0) {  // no contributing tap (a dgrad parity class): the tiles are zero
+    for (int t = 0; t < mytiles; ++t) epilogue(tile0 + t, smem);
+    return;
+  }
+
+  // Two register stage sets (x: even steps, y: odd steps) keep the global loads of steps s+1 AND
+  // s+2 in flight while step s computes.  The loop body is branch-free around the loads and LDS
+  // stores, so the compiler's wait counting sees the true issue order and waits only for the set
+  // it is about to store.
   uint8_t* buf0 = smem;
   uint8_t* buf1 = smem + 2 * TILE;
   Stage xa, xb, ya, yb;
-  // The loop body is branch-free around the memory operations (tile indices past the end are
-  // clamped to the last tile: loaded and staged but never computed), so the compiler's wait
-  // counting sees the true issue order and waits only for the set it is about to store.
-  const int last = max(nk - 1, 0) * BK;
-  if (nk > 0) {
-    load_a(xa, 0);
-    load_b(xb, 0);
-    load_a(ya, min(BK, last));
-    load_b(yb, min(BK, last));
-    st_kin(xa, buf0);
-    st_kin(xb, buf0 + TILE);
-    load_a(xa, min(2 * BK, last));
-    load_b(xb, min(2 * BK, last));
-  }
+  load_step(xa, xb, 0);
+  load_step(ya, yb, 1);
+  st_kin(xa, buf0);
+  st_kin(xb, buf0 + TILE);
+  load_step(xa, xb, 2);
   __syncthreads();
-  for (int t = 0; t < nk; t += 2) {
-    compute(buf0);  // tile t
+  for (int s = 0; s < nsteps; s += 2) {
+    compute(buf0);  // step s
+    if (s % nk == nk - 1) epilogue(tile0 + s / nk, buf1);  // buf1: drained, not yet restaged
     st_kin(ya, buf1);
     st_kin(yb, buf1 + TILE);
-    load_a(ya, min((t + 3) * BK, last));
-    load_b(yb, min((t + 3) * BK, last));
+    load_step(ya, yb, s + 3);
     __syncthreads();
-    if (t + 1 < nk) compute(buf1);  // tile t + 1
+    if (s + 1 < nsteps) {
+      compute(buf1);  // step s + 1
+      if ((s + 1) % nk == nk - 1) epilogue(tile0 + (s + 1) / nk, buf0);
+    }
     st_kin(xa, buf0);
     st_kin(xb, buf0 + TILE);
-    load_a(xa, min((t + 4) * BK, last));
-    load_b(xb, min((t + 4) * BK, last));
+    load_step(xa, xb, s + 4);
     __syncthreads();
-  }
-
-  // epilogue: acc[ni][mi][i] = out[pixel m0+wm*64+mi*16+(lane&15)][channel n0+wn*64+ni*16+4*(lane>>4)+i]
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int m = m0 + wm * 64 + mi * 16 + (lane & 15);
-    if (m >= p.M) continue;
-    const int n = m / IJ, r = m - n * IJ;
-    const int i = r / g.J, j = r - i * g.J;
-    bf16_t* orow = p.out + ((long)(n * p.OH + i * p.osh + p.oh0) * p.OW + j * p.osw + p.ow0) * p.ldo;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int ch = n0 + wn * 64 + ni * 16 + 4 * (lane >> 4);
-      if (ch >= p.N) continue;
-      uint2 v;
-      v.x = (uint32_t)f2bf(acc[ni][mi][0]) | ((uint32_t)f2bf(acc[ni][mi][1]) << 16);
-      v.y = (uint32_t)f2bf(acc[ni][mi][2]) | ((uint32_t)f2bf(acc[ni][mi][3]) << 16);
-      *reinterpret_cast<uint2*>(orow + ch) = v;
-    }
   }
 }
 
@@ -394,37 +424,45 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
 }
 
 // =============================================================================================
-// explicit im2col for the 3-channel stem: col[m=(n,p,q)][k=(r,s,c)], zero padded to Kp columns
+// im2col for the 3-channel stem: col[m=(n,p,q)][r*SCp + s*C + c], each filter row (r) padded from
+// S*C (21) to SCp (24) columns so that one thread owns one (pixel, filter row) pair and writes it as
+// aligned 16-byte stores; columns [R*SCp, Kp) are zero (written by the r == 0 thread).
 // =============================================================================================
 __global__ void im2col_kernel(const bf16_t* __restrict__ x, int H, int W, int C, int R, int S, int stride, int pad,
-                              int P, int Q, int RSC, int Kp, bf16_t* __restrict__ col, long total) {
-  const int kchunks = Kp / 8;
+                              int P, int Q, int SCp, int Kp, bf16_t* __restrict__ col, long total) {
+  const int SC = S * C;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const long m = idx / kchunks;
-    const int kc = (int)(idx - m * kchunks);
+    const long m = idx / R;
+    const int r = (int)(idx - m * R);
     const int q = (int)(m % Q);
     const long t = m / Q;
     const int pp = (int)(t % P);
     const long n = t / P;
-    uint32_t w32[4];
+    const int h = pp * stride - pad + r;
+    const bool hok = (unsigned)h < (unsigned)H;
+    const int w0 = q * stride - pad;
+    const bf16_t* row = x + ((n * H + (hok ? h : 0)) * W) * (long)C;
+    bf16_t* dst = col + m * Kp + (long)r * SCp;
+    for (int c8 = 0; c8 < SCp; c8 += 8) {
+      uint32_t w32[4];
 #pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      uint32_t pair = 0;
+      for (int e = 0; e < 8; e += 2) {
+        uint32_t pair = 0;
 #pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int k = kc * 8 + e + h2;
-        bf16_t v = 0;
-        if (k < RSC) {
-          const int cc = k % C, rs = k / C;
-          const int s = rs % S, r = rs / S;
-          const int h = pp * stride - pad + r, w = q * stride - pad + s;
-          if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = x[((n * H + h) * W + w) * C + cc];
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int k = c8 + e + h2;
+          const int s = k / C, cc = k - s * C;
+          const int w = w0 + s;
+          bf16_t v = 0;
+          if (hok && k < SC && (unsigned)w < (unsigned)W) v = row[(long)w * C + cc];
+          pair |= (uint32_t)v << (16 * h2);
         }
-        pair |= (uint32_t)v << (16 * h2);
+        w32[e / 2] = pair;
       }
-      w32[e / 2] = pair;
+      *reinterpret_cast<uint4*>(dst + c8) = uint4{w32[0], w32[1], w32[2], w32[3]};
     }
-    *reinterpret_cast<uint4*>(col + m * Kp + kc * 8) = uint4{w32[0], w32[1], w32[2], w32[3]};
+    if (r == 0)
+      for (int c8 = R * SCp; c8 < Kp; c8 += 8) *reinterpret_cast<uint4*>(col + m * Kp + c8) = uint4{0u, 0u, 0u, 0u};
   }
 }
 
@@ -443,15 +481,17 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
   if (M == 0 || N == 0) return 0;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * ldw;
   if (img_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
+  const int tiles = (int)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
+  const int tpw = std::max(1, tiles / 1024);
   FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C,
-            (unsigned)img_bytes, (unsigned)w_bytes};
+            (unsigned)img_bytes, (unsigned)w_bytes, tpw};
   static bool attr = false;
   if (!attr) {
     set_lds(conv_fwd_kernel);
     attr = true;
   }
-  const int tiles = (int)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  conv_fwd_kernel<<<dim3(tiles), NT, LDS_BYTES, st>>>(a);
+  conv_fwd_kernel<<<dim3((tiles + tpw - 1) / tpw), NT, LDS_BYTES, st>>>(a);
   return 0;
 }
 
@@ -482,14 +522,13 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
   return 0;
 }
 
-int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int P, int Q, int Kp,
-              bf16_t* col, hipStream_t st) {
-  if (Kp % 8 || Kp < R * S * C) return -1;
-  const long total = (long)N * P * Q * (Kp / 8);
+int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int P, int Q, int SCp,
+              int Kp, bf16_t* col, hipStream_t st) {
+  if (SCp % 8 || SCp < S * C || Kp % 8 || Kp < R * SCp) return -1;
+  const long total = (long)N * P * Q * R;
   if (total == 0) return 0;
   const int threads = 256;
   const long blocks = std::min<long>((total + threads - 1) / threads, 256L * 64);
-  im2col_kernel<<<dim3((unsigned)blocks), threads, 0, st>>>(x, H, W, C, R, S, stride, pad, P, Q, R * S * C, Kp, col,
-                                                            total);
+  im2col_kernel<<<dim3((unsigned)blocks), threads, 0, st>>>(x, H, W, C, R, S, stride, pad, P, Q, SCp, Kp, col, total);
   return 0;
 }
