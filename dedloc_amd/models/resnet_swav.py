@@ -79,10 +79,14 @@ class _ConvNHWC(torch.autograd.Function):
 class ConvNHWC(nn.Conv2d):
     """``nn.Conv2d`` (same parameters / state-dict keys) whose GPU path on channels-last bf16
     activations is the hand-written implicit-GEMM MFMA convolution (forward, dgrad, wgrad); other
-    inputs (CPU plumbing, fp32) take the stock module.  ``DEDLOC_CONV=miopen`` routes the GPU path
-    through MIOpen instead (A/B measurements only)."""
+    inputs (CPU plumbing, fp32) take the stock module.
 
-    native = os.environ.get("DEDLOC_CONV", "hip") != "miopen"
+    Backend choice (``SwAVModel(conv_impl=...)``, config ``MODEL.CONV_IMPL``, env ``DEDLOC_CONV``):
+    measured on MI355X (profiles/conv_bench_*.jsonl) MIOpen's NHWC kernels are still 1.1-1.6x faster
+    in total over the SwAV trunk shapes (the hand-written kernels win on 25 of the 138 (shape, pass)
+    pairs), so ``miopen`` is the default and ``hip`` selects the implicit-GEMM kernels."""
+
+    native = os.environ.get("DEDLOC_CONV", "miopen") == "hip"
 
     def forward(self, x):
         if (self.native and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
@@ -210,11 +214,17 @@ class SwAVPrototypesHead(nn.Module):
 
 class SwAVModel(nn.Module):
     def __init__(self, num_prototypes: int = 3000, single_pass_every_crop: bool = True,
-                 checkpoint_stages: bool = False):
+                 checkpoint_stages: bool = False, conv_impl: str | None = None):
         super().__init__()
         self.trunk = ResNet50Trunk(checkpoint_stages=checkpoint_stages)
         self.heads = nn.ModuleList([SwAVPrototypesHead(num_prototypes=num_prototypes)])
         self.single_pass_every_crop = single_pass_every_crop
+        if conv_impl is not None:
+            if conv_impl not in ("hip", "miopen"):
+                raise ValueError(f"conv_impl must be 'hip' or 'miopen', got {conv_impl!r}")
+            for m in self.trunk.modules():
+                if isinstance(m, ConvNHWC):
+                    m.native = conv_impl == "hip"
 
     def set_bn_stat_groups(self, g: int):
         for m in self.trunk.modules():

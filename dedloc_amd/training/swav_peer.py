@@ -65,7 +65,8 @@ class SwavPeer:
         self.batch_size = int(dcfg.BATCHSIZE_PER_REPLICA)
         self.model = SwAVModel(num_prototypes=int(mcfg.HEAD.num_clusters),
                                single_pass_every_crop=bool(mcfg.SINGLE_PASS_EVERY_CROP),
-                               checkpoint_stages=bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING))
+                               checkpoint_stages=bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING),
+                               conv_impl=mcfg.get("CONV_IMPL") or None)
         self.model.to(self.device).train()
         self.flat = FlatParams(self.model.named_parameters(), device=self.device, with_bf16=False, autograd=True,
                                channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
