@@ -26,6 +26,7 @@ from typing import Dict, Optional
 
 import torch
 
+from ..data.sop_dataset import DiskSOPStream, is_sop_dataset
 from ..data.synthetic_mlm import SyntheticSOPStream, peer_seed
 from ..dht import DHT, get_dht_time
 from ..emulation import ChurnController, StepThrottle, parse_churn_schedule, profile_for_rank
@@ -103,6 +104,10 @@ class AlbertPeer:
             self.scheduler = get_linear_schedule_with_warmup(self.opt, a.warmup_steps, a.max_steps)
         else:
             self.model = get_model(training_args, config)
+            disk = getattr(dataset_args, "dataset_path", None)
+            if is_sop_dataset(disk):  # run_trainer.py: model.resize_token_embeddings(len(tokenizer))
+                with open(os.path.join(disk, "sop_meta.json")) as f:
+                    self.model.resize_token_embeddings(int(json.load(f)["vocab_size"]))
             self.model.materialize(self.device)
             self.model.train()
             self.opt, self.scheduler = build_optimizer(self.model, training_args)
@@ -126,10 +131,16 @@ class AlbertPeer:
             emulate_transfer_delay=getattr(ca, "emulate_transfer_delay", False))
         self.statistics_expiration = ca.statistics_expiration
         seed = peer_seed(self.local_public_key, training_args.seed)
-        self.data = SyntheticSOPStream(training_args.per_device_train_batch_size, training_args.seq_length,
-                                       self.model.config.vocab_size, seed=seed, device=self.device,
-                                       mask_mode=getattr(dataset_args, "mask_mode", "fixed"),
-                                       length_mode=getattr(dataset_args, "length_mode", "full"))
+        if is_sop_dataset(getattr(dataset_args, "dataset_path", None)):
+            # a tokenized corpus built by data/sop_dataset.py (the reference's albert_tokenized_wikitext)
+            logger.info(f"training on the tokenized dataset at {dataset_args.dataset_path}")
+            self.data = DiskSOPStream(dataset_args.dataset_path, training_args.per_device_train_batch_size,
+                                      seed=seed, device=self.device)
+        else:
+            self.data = SyntheticSOPStream(training_args.per_device_train_batch_size, training_args.seq_length,
+                                           self.model.config.vocab_size, seed=seed, device=self.device,
+                                           mask_mode=getattr(dataset_args, "mask_mode", "fixed"),
+                                           length_mode=getattr(dataset_args, "length_mode", "full"))
         flat = self.model.flat
         self._clip_part = torch.zeros(256, device=self.device)
         self._clip_out = torch.zeros(2, device=self.device)
