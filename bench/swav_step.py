@@ -28,10 +28,11 @@ def main():
     ap.add_argument("--grouped", action="store_true", help="one trunk pass per crop resolution")
     ap.add_argument("--queue", action="store_true", help="queue active (3840 rows in Sinkhorn)")
     ap.add_argument("--graph", action="store_true", help="capture trunk+head fwd/bwd as HIP graphs")
+    ap.add_argument("--no_find", action="store_true", help="MIOpen immediate mode (cudnn.benchmark=False)")
     ap.add_argument("--conv", default=None, choices=["hip", "miopen"], help="conv backend (default: config)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = not args.no_find
     ov = [f"config.DATA.TRAIN.BATCHSIZE_PER_REPLICA={args.batch}", f"config.OPTIMIZER.batch_size_for_tracking={args.batch}",
           "config.OPTIMIZER.target_batch_size=100000000", f"config.MODEL.SINGLE_PASS_EVERY_CROP={not args.grouped}",
           f"config.LOSS.swav_loss.queue.start_iter={0 if args.queue else 10**9}", "config.CHECKPOINT.DIR=/tmp/swav_bench", f"config.MODEL.CUDA_GRAPH={args.graph}"] + ([f"config.MODEL.CONV_IMPL={args.conv}"] if args.conv else [])
@@ -39,9 +40,11 @@ def main():
     dht = DHT(start=True)
     peer = SwavPeer(cfg, dev, dht=dht)
     try:
-        for _ in range(args.warmup):
+        for i in range(args.warmup):  # progress lines: MIOpen's first-call search can take minutes
+            t0 = time.perf_counter()
             peer.train_step()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            print(f"warmup {i}: {time.perf_counter() - t0:.2f}s", file=sys.stderr, flush=True)
         t = time.perf_counter()
         for _ in range(args.iters):
             peer.train_step()
@@ -60,7 +63,7 @@ def main():
         print(json.dumps({"metric": "swav_rn50_local_samples_per_sec_per_gpu", "value": args.batch / dt,
                           "ms_per_iter": dt * 1e3, "data_ms": data_ms, "larc_sgd_step_ms": opt_ms,
                           "batch": args.batch, "crops": "2x224+6x96", "grouped": args.grouped, "queue": args.queue, "hip_graph": args.graph,
-                          "conv": peer.cfg.MODEL.get("CONV_IMPL"),
+                          "conv": peer.cfg.MODEL.get("CONV_IMPL"), "miopen_find": not args.no_find,
                           "peak_mem_gb": torch.cuda.max_memory_allocated() / 2**30}))
     finally:
         peer.shutdown()

@@ -61,6 +61,9 @@ class DatasetArguments:
     vocab_size: Optional[int] = field(default=None, metadata={"help": "Override the vocabulary size (sahajBERT: 31995)"})
     length_mode: str = field(default="full", metadata={"help": "synthetic instance lengths: full (all 512) or wikitext (10% short tails)"})
     mask_mode: str = field(default="fixed", metadata={"help": "fixed (max_predictions_per_seq form) or hf (Bernoulli 15%)"})
+    stream_sources: Optional[str] = field(default=None, metadata={
+        "help": "sahajBERT streaming corpus over local text: 'path_a:0.23,path_b:0.77' (tokenized on the fly "
+                "with --tokenizer_path, 10^4-document shuffle buffer, per-peer seed)"})
 
 
 @dataclass

@@ -147,32 +147,107 @@ class DiskSOPStream:
 
     @torch.no_grad()
     def next_batch(self) -> Dict[str, torch.Tensor]:
-        rows = self.ds[self._next_indices()]
-        L = max(len(r) for r in rows["input_ids"])
-        B = self.B
-        pad = self.meta["pad"]
-        ids = torch.full((B, L), pad, dtype=torch.long)
-        tt = torch.zeros((B, L), dtype=torch.long)
-        am = torch.zeros((B, L), dtype=torch.long)
-        special = torch.ones((B, L), dtype=torch.bool)
-        for i in range(B):
-            n = len(rows["input_ids"][i])
-            ids[i, :n] = torch.tensor(rows["input_ids"][i])
-            tt[i, :n] = torch.tensor(rows["token_type_ids"][i])
-            am[i, :n] = 1
-            special[i, :n] = torch.tensor(rows["special_tokens_mask"][i], dtype=torch.bool)
-        prob = torch.full((B, L), self.p)
-        prob.masked_fill_(special, 0.0)
-        picked = torch.bernoulli(prob, generator=self.gen).bool()
-        labels = torch.where(picked, ids, torch.full_like(ids, -100))
-        to_mask = torch.bernoulli(torch.full((B, L), 0.8), generator=self.gen).bool() & picked
-        ids = torch.where(to_mask, torch.full_like(ids, self.meta["mask"]), ids)
-        to_rand = torch.bernoulli(torch.full((B, L), 0.5), generator=self.gen).bool() & picked & ~to_mask
-        rand_tok = torch.randint(self.meta["vocab_size"], (B, L), generator=self.gen)
-        ids = torch.where(to_rand, rand_tok, ids)
-        batch = {"input_ids": ids, "token_type_ids": tt, "attention_mask": am, "labels": labels,
-                 "sentence_order_label": torch.tensor(rows["sentence_order_label"], dtype=torch.long)}
-        return {k: v.to(self.device, non_blocking=True) for k, v in batch.items()}
+        return collate_mlm(self.ds[self._next_indices()], self.meta, self.gen, self.p, self.device)
+
+
+@torch.no_grad()
+def collate_mlm(rows: Dict[str, List], meta: Dict[str, int], gen: torch.Generator, p: float = 0.15,
+                device=None) -> Dict[str, torch.Tensor]:
+    """``DataCollatorForLanguageModeling`` semantics over columnar SOP rows: pad to the longest row,
+    select p of the non-special tokens; 80 % -> [MASK], 10 % -> random token, 10 % kept."""
+    B = len(rows["input_ids"])
+    L = max(len(r) for r in rows["input_ids"])
+    ids = torch.full((B, L), meta["pad"], dtype=torch.long)
+    tt = torch.zeros((B, L), dtype=torch.long)
+    am = torch.zeros((B, L), dtype=torch.long)
+    special = torch.ones((B, L), dtype=torch.bool)
+    for i in range(B):
+        n = len(rows["input_ids"][i])
+        ids[i, :n] = torch.tensor(rows["input_ids"][i])
+        tt[i, :n] = torch.tensor(rows["token_type_ids"][i])
+        am[i, :n] = 1
+        special[i, :n] = torch.tensor(rows["special_tokens_mask"][i], dtype=torch.bool)
+    prob = torch.full((B, L), p)
+    prob.masked_fill_(special, 0.0)
+    picked = torch.bernoulli(prob, generator=gen).bool()
+    labels = torch.where(picked, ids, torch.full_like(ids, -100))
+    to_mask = torch.bernoulli(torch.full((B, L), 0.8), generator=gen).bool() & picked
+    ids = torch.where(to_mask, torch.full_like(ids, meta["mask"]), ids)
+    to_rand = torch.bernoulli(torch.full((B, L), 0.5), generator=gen).bool() & picked & ~to_mask
+    ids = torch.where(to_rand, torch.randint(meta["vocab_size"], (B, L), generator=gen), ids)
+    batch = {"input_ids": ids, "token_type_ids": tt, "attention_mask": am, "labels": labels,
+             "sentence_order_label": torch.tensor(rows["sentence_order_label"], dtype=torch.long)}
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    return {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
+
+
+class StreamingSOPStream:
+    """sahajBERT's streaming corpus (reference ``sahajbert/dataset_streaming.py``: Wikipedia-bn and
+    OSCAR-bn merged with probabilities 0.23 / 0.77, a 10^4-document shuffle buffer seeded per peer,
+    SOP instances tokenized on the fly, an endless stream) over local text sources.
+
+    ``sources``: [(path, probability)], each path a text file or directory (``read_documents``);
+    every source restarts when exhausted, so the stream never ends."""
+
+    def __init__(self, sources, tokenizer, batch_size: int, seed: int = 0, device="cpu", max_seq_length: int = 512,
+                 shuffle_buffer: int = 10_000, mlm_probability: float = 0.15):
+        if not sources:
+            raise ValueError("no streaming sources")
+        total = float(sum(p for _, p in sources))
+        self.paths = [s for s, _ in sources]
+        self.cum = []
+        acc = 0.0
+        for _, p in sources:
+            acc += p / total
+            self.cum.append(acc)
+        self.rng = random.Random(seed)
+        self.builder = SOPInstanceBuilder(tokenizer, max_seq_length, seed=seed + 1)
+        self.meta = special_ids(tokenizer)
+        self.B, self.p, self.device = batch_size, mlm_probability, torch.device(device)
+        self.gen = torch.Generator().manual_seed(int(seed) % (2 ** 63))
+        self.iters = [self._cycle(p) for p in self.paths]
+        self.buffer: List[str] = []
+        self.shuffle_buffer = max(1, shuffle_buffer)
+        self.pending: List[Dict[str, List[int]]] = []
+        self.source_counts = [0] * len(self.paths)
+
+    @staticmethod
+    def _cycle(path):
+        while True:
+            n = 0
+            for doc in read_documents(path):
+                n += 1
+                yield doc
+            if n == 0:
+                raise ValueError(f"source {path} holds no document")
+
+    def _draw_document(self) -> str:
+        while len(self.buffer) < self.shuffle_buffer:  # fill / refill the shuffle buffer from the mixture
+            u = self.rng.random()
+            k = next(i for i, c in enumerate(self.cum) if u <= c or i == len(self.cum) - 1)
+            self.source_counts[k] += 1
+            self.buffer.append(next(self.iters[k]))
+        j = self.rng.randrange(len(self.buffer))
+        self.buffer[j], self.buffer[-1] = self.buffer[-1], self.buffer[j]
+        return self.buffer.pop()
+
+    def next_batch(self) -> Dict[str, torch.Tensor]:
+        while len(self.pending) < self.B:
+            self.pending.extend(self.builder.from_document(self._draw_document()))
+        rows, self.pending = self.pending[:self.B], self.pending[self.B:]
+        cols = {k: [r[k] for r in rows] for k in rows[0]}
+        return collate_mlm(cols, self.meta, self.gen, self.p, self.device)
+
+
+def parse_sources(spec: str):
+    """``"path_a:0.23,path_b:0.77"`` -> [(path_a, 0.23), (path_b, 0.77)] (probability defaults to 1)."""
+    out = []
+    for item in filter(None, (s.strip() for s in spec.split(","))):
+        path, _, prob = item.rpartition(":")
+        if not path or not prob.replace(".", "", 1).isdigit():
+            path, prob = item, "1"
+        out.append((path, float(prob)))
+    return out
 
 
 def main(argv=None):

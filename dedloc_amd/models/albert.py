@@ -72,7 +72,10 @@ class AlbertConfig:
         return cls(**base)
 
     def to_dict(self) -> Dict:
-        return asdict(self)
+        d = asdict(self)
+        if d.get("num_labels") is None:  # HF's PretrainedConfig rejects num_labels=None
+            d.pop("num_labels", None)
+        return d
 
     @classmethod
     def from_dict(cls, d: Dict) -> "AlbertConfig":

@@ -81,12 +81,13 @@ class ConvNHWC(nn.Conv2d):
     activations is the hand-written implicit-GEMM MFMA convolution (forward, dgrad, wgrad); other
     inputs (CPU plumbing, fp32) take the stock module.
 
-    Backend choice (``SwAVModel(conv_impl=...)``, config ``MODEL.CONV_IMPL``, env ``DEDLOC_CONV``):
-    measured on MI355X (profiles/conv_bench_*.jsonl) MIOpen's NHWC kernels are still 1.1-1.6x faster
-    in total over the SwAV trunk shapes (the hand-written kernels win on 25 of the 138 (shape, pass)
-    pairs), so ``miopen`` is the default and ``hip`` selects the implicit-GEMM kernels."""
+    Backend choice (``SwAVModel(conv_impl=...)``, config ``MODEL.CONV_IMPL``, env ``DEDLOC_CONV``),
+    measured on MI355X for the SwAV b=64 iteration (profiles/README.md): ``hip`` (default) 1518-1531
+    samples/s, first iteration ~15 s; MIOpen immediate mode 1405 samples/s, first iteration ~49 s;
+    MIOpen with exhaustive find (cudnn.benchmark) 1700 samples/s once its per-shape search is done, but
+    that search took from ~1 to >3 minutes per fresh process on the pool's boxes."""
 
-    native = os.environ.get("DEDLOC_CONV", "miopen") == "hip"
+    native = os.environ.get("DEDLOC_CONV", "hip") == "hip"
 
     def forward(self, x):
         if (self.native and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)

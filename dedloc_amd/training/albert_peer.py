@@ -26,7 +26,7 @@ from typing import Dict, Optional
 
 import torch
 
-from ..data.sop_dataset import DiskSOPStream, is_sop_dataset
+from ..data.sop_dataset import DiskSOPStream, StreamingSOPStream, is_sop_dataset, parse_sources
 from ..data.synthetic_mlm import SyntheticSOPStream, peer_seed
 from ..dht import DHT, get_dht_time
 from ..emulation import ChurnController, StepThrottle, parse_churn_schedule, profile_for_rank
@@ -105,7 +105,13 @@ class AlbertPeer:
         else:
             self.model = get_model(training_args, config)
             disk = getattr(dataset_args, "dataset_path", None)
-            if is_sop_dataset(disk):  # run_trainer.py: model.resize_token_embeddings(len(tokenizer))
+            self._stream_tokenizer = None
+            if getattr(dataset_args, "stream_sources", None):
+                from transformers import AutoTokenizer
+
+                self._stream_tokenizer = AutoTokenizer.from_pretrained(dataset_args.tokenizer_path)
+                self.model.resize_token_embeddings(len(self._stream_tokenizer))
+            elif is_sop_dataset(disk):  # run_trainer.py: model.resize_token_embeddings(len(tokenizer))
                 with open(os.path.join(disk, "sop_meta.json")) as f:
                     self.model.resize_token_embeddings(int(json.load(f)["vocab_size"]))
             self.model.materialize(self.device)
@@ -131,7 +137,13 @@ class AlbertPeer:
             emulate_transfer_delay=getattr(ca, "emulate_transfer_delay", False))
         self.statistics_expiration = ca.statistics_expiration
         seed = peer_seed(self.local_public_key, training_args.seed)
-        if is_sop_dataset(getattr(dataset_args, "dataset_path", None)):
+        if getattr(self, "_stream_tokenizer", None) is not None:
+            # sahajBERT: lazily merged text sources, shuffle buffer and tokenization seeded per peer
+            logger.info(f"streaming SOP instances from {dataset_args.stream_sources}")
+            self.data = StreamingSOPStream(parse_sources(dataset_args.stream_sources), self._stream_tokenizer,
+                                           training_args.per_device_train_batch_size, seed=seed % (2 ** 31),
+                                           device=self.device, max_seq_length=training_args.seq_length)
+        elif is_sop_dataset(getattr(dataset_args, "dataset_path", None)):
             # a tokenized corpus built by data/sop_dataset.py (the reference's albert_tokenized_wikitext)
             logger.info(f"training on the tokenized dataset at {dataset_args.dataset_path}")
             self.data = DiskSOPStream(dataset_args.dataset_path, training_args.per_device_train_batch_size,

@@ -149,3 +149,73 @@ def test_run_trainer_on_tokenized_dataset(tokenizer, tmp_path):
         assert max(rec["step"] for rec in recs) >= 2 and all(torch.isfinite(torch.tensor(rec["loss"])) for rec in recs)
     finally:
         root.shutdown()
+
+
+def test_parse_sources():
+    from dedloc_amd.data.sop_dataset import parse_sources
+
+    assert parse_sources("a/wiki:0.23, b/oscar:0.77") == [("a/wiki", 0.23), ("b/oscar", 0.77)]
+    assert parse_sources("corpus.txt") == [("corpus.txt", 1.0)]
+    assert parse_sources("c:/x/y.txt:2,") == [("c:/x/y.txt", 2.0)]
+
+
+def test_streaming_mixture_and_endless(tokenizer, tmp_path):
+    """sahajBERT streaming semantics: sources mixed by probability through a shuffle buffer, each
+    source restarting when exhausted (the stream never ends), deterministic per seed."""
+    from dedloc_amd.data.sop_dataset import StreamingSOPStream
+
+    tok, _ = tokenizer
+    (tmp_path / "a.txt").write_text("\n\n".join(_corpus(5, seed=2)) + "\n")
+    (tmp_path / "b.txt").write_text("\n\n".join(_corpus(7, seed=3)) + "\n")
+    srcs = [(str(tmp_path / "a.txt"), 0.23), (str(tmp_path / "b.txt"), 0.77)]
+
+    def make(seed):
+        return StreamingSOPStream(srcs, tok, batch_size=4, seed=seed, max_seq_length=48, shuffle_buffer=16)
+
+    s = make(3)
+    batches = [s.next_batch() for _ in range(60)]  # far more instances than the 12 documents hold
+    for b in batches:
+        assert b["input_ids"].shape[0] == 4 and b["input_ids"].shape[1] <= 48
+        assert set(b["sentence_order_label"].tolist()) <= {0, 1}
+        assert ((b["labels"] == -100) | b["attention_mask"].bool()).all()
+    frac = s.source_counts[0] / sum(s.source_counts)
+    assert sum(s.source_counts) > 24 and 0.1 < frac < 0.38
+    again = make(3)
+    assert all(torch.equal(again.next_batch()["input_ids"], batches[i]["input_ids"]) for i in range(5))
+    other = make(4)
+    assert not all(torch.equal(other.next_batch()["input_ids"], batches[i]["input_ids"]) for i in range(5))
+
+
+@pytest.mark.timeout(300)
+def test_run_trainer_streaming_sources(tokenizer, tmp_path):
+    """run_trainer --stream_sources: the sahajBERT streaming path (tokenizer from --tokenizer_path,
+    embeddings resized to it) trains a peer for two collaborative steps."""
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.models.albert import AlbertConfig
+
+    tok, tok_dir = tokenizer
+    (tmp_path / "w.txt").write_text("\n\n".join(_corpus(20, seed=4)) + "\n")
+    (tmp_path / "o.txt").write_text("\n\n".join(_corpus(30, seed=5)) + "\n")
+    cfgdir = tmp_path / "cfg"
+    AlbertConfig.tiny(num_hidden_layers=2, max_position_embeddings=64).save_pretrained(str(cfgdir))
+    root = DHT(listen_on="127.0.0.1:*")
+    try:
+        metrics = tmp_path / "m.jsonl"
+        cmd = [sys.executable, "-m", "dedloc_amd.cli.run_trainer", "--experiment_prefix", "stream",
+               "--initial_peers", root.endpoint, "--device", "cpu", "--config_path", str(cfgdir),
+               "--stream_sources", f"{tmp_path / 'w.txt'}:0.23,{tmp_path / 'o.txt'}:0.77",
+               "--tokenizer_path", tok_dir, "--seq_length", "64", "--per_device_train_batch_size", "2",
+               "--gradient_accumulation_steps", "1", "--target_batch_size", "4", "--stop_after_global_steps", "2",
+               "--save_steps", "0", "--output_dir", str(tmp_path / "out"), "--min_refresh_period", "0.05",
+               "--default_refresh_period", "0.1", "--dht_listen_on", "127.0.0.1:*", "--listen_on", "127.0.0.1:*",
+               "--metrics_file", str(metrics)]
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        env.pop("RANK", None)
+        env.pop("WORLD_SIZE", None)
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "streaming SOP instances" in r.stderr
+        recs = [json.loads(x) for x in metrics.read_text().splitlines()]
+        assert max(rec["step"] for rec in recs) >= 2 and all(torch.isfinite(torch.tensor(rec["loss"])) for rec in recs)
+    finally:
+        root.shutdown()

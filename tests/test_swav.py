@@ -390,7 +390,9 @@ def test_swav_single_pass_semantics_fused_gpu(cuda):
     from dedloc_amd.models.resnet_swav import SwAVModel
 
     torch.manual_seed(12)
-    m1 = SwAVModel(num_prototypes=64, single_pass_every_crop=True).to(cuda).train()
+    # hand-written convs: per-pixel results do not depend on the batch size, so the comparison isolates
+    # the BN statistics groups (MIOpen may pick a different algorithm for the 3x larger batch)
+    m1 = SwAVModel(num_prototypes=64, single_pass_every_crop=True, conv_impl="hip").to(cuda).train()
     m2 = copy.deepcopy(m1)
     cl = torch.channels_last
     crops = [torch.randn(4, 3, 64, 64, device=cuda).bfloat16().contiguous(memory_format=cl) for _ in range(3)]
