@@ -438,7 +438,7 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
 // batched hipBLASLt GEMM into fp32 partial slabs, then add the slabs into the fp32 gradient:
 // measured at T=32768 (bench/wgrad_bench.py) 1024x1024: 174 -> ~80 us, 4096x1024: 307 -> ~280 us,
 // 3072x1024: 244 -> ~200 us.  S = largest power of two <= min(8, 256 / #256x256-tiles).
-int wgrad_splits(int64_t M, int64_t N, int64_t K) {
+int wgrad_splits(int64_t M, int64_t N, int64_t K, int max_splits = 8) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) {  // measurement override (bench/wgrad_bench.py)
     int s = std::max(1, std::atoi(e));
@@ -446,11 +446,12 @@ int wgrad_splits(int64_t M, int64_t N, int64_t K) {
     return s;
   }
   int s = 1;
-  while (s < 8 && tiles * s * 2 <= 256 && K % (s * 2 * 64) == 0 && K / (s * 2) >= 1024) s *= 2;
+  while (s < max_splits && tiles * s * 2 <= 256 && K % (s * 2 * 64) == 0 && K / (s * 2) >= 1024) s *= 2;
   return s;
 }
 
-void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b) {
+void gemm_acc_f32_split(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b,
+                        int max_splits) {
   expect(c, at::kFloat, "c");
   const Mat Av = a_view(a, trans_a), Bv = b_view(b, trans_b);
   const int64_t ntiles = ((Av.rows + 255) / 256) * ((Bv.rows + 255) / 256);
@@ -468,7 +469,7 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
   }
   if (lt_ok(a, b) && c.stride(1) == 1) {
     DlLtArgs l = lt_args(a, b, trans_a, trans_b);
-    const int S = (trans_a && !trans_b && c.is_contiguous()) ? wgrad_splits(l.M, l.N, l.K) : 1;
+    const int S = (trans_a && !trans_b && c.is_contiguous()) ? wgrad_splits(l.M, l.N, l.K, max_splits) : 1;
     if (S > 1) {  // token-split batched GEMM into fp32 slabs + slab sum
       auto slabs = at::empty({S, l.M, l.N}, c.options());
       const long kslice = l.K / S;
@@ -502,6 +503,10 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
   const at::Tensor A = trans_a ? a.t() : a;
   const at::Tensor B = trans_b ? b.t() : b;
   at::_ops::addmm_dtype_out::call(c, A, B, at::kFloat, 1, 1, c);
+}
+
+void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b) {
+  gemm_acc_f32_split(a, b, c, trans_a, trans_b, 8);
 }
 
 // fused FFN-up: H = x W^T + b (pre-activation, kept for backward), G = gelu_new(H)
@@ -682,6 +687,30 @@ inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t
   return col;
 }
 
+// Convolutions that are plain GEMMs go to hipBLASLt: 1x1 stride-1 unpadded convs over NHWC tensors
+// (x[N*H*W, C] x W[K, C]^T, dgrad dY[N*H*W, K] x W, wgrad dY^T x X with the token-split fp32 slabs of
+// gemm_acc_f32) and the stem's column-matrix GEMM.  Measured on the SwAV b=64 shapes
+// (profiles/conv_bench_*.jsonl) the implicit-GEMM kernel runs these short-K / N=64 GEMMs at 40-50% of
+// the library's speed.  DEDLOC_CONV_GEMM=hip forces conv.hip everywhere (kernel tests).
+bool conv_lt() {
+  const char* e = std::getenv("DEDLOC_CONV_GEMM");
+  return use_lt() && !(e && e[0] == 'h');
+}
+inline bool is_pointwise(int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  return R == 1 && S == 1 && stride == 1 && pad == 0;
+}
+inline at::Tensor rows2d(const at::Tensor& t) {  // channels-last [N, C, H, W] -> [N*H*W, C] view
+  return t.permute({0, 2, 3, 1}).reshape({-1, t.size(1)});
+}
+// D[M, N] (bf16, row stride ldd) = A[M, K] . B[N, K]^T or A . B (trans_b false: B is [K, N])
+bool lt_plain(const at::Tensor& a, const at::Tensor& b, bool trans_b, void* d, int64_t ldd, hipStream_t st) {
+  if (!lt_ok(a, b)) return false;
+  DlLtArgs l = lt_args(a, b, false, trans_b);
+  l.D = d;
+  l.ldd = ldd;
+  return dl_lt_matmul(l, st) == 0;
+}
+
 inline DlConvGeom geom(const bf16_t* img, int64_t N, int64_t H, int64_t W, int64_t C, int64_t I, int64_t J,
                        int64_t sh, int64_t sw, int64_t TR, int64_t TS, int64_t dh0, int64_t dhs, int64_t dw0,
                        int64_t dws) {
@@ -698,6 +727,9 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   const int64_t P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
   auto y = at::empty({N, K, P, Q}, x.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);
+  if (is_pointwise(R, S, stride, pad) && conv_lt() &&
+      lt_plain(rows2d(x), wk.view({K, C}), true, y.data_ptr(), K, cur_stream(x)))
+    return y;
   if (C % 64 == 0) {
     check(dl_conv_fwd(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(wk), R * S * C,
                       (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x)),
@@ -710,6 +742,7 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
   auto wp = at::zeros({K, sc.Kp}, w.options());
   wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
+  if (conv_lt() && lt_plain(col, wp, true, y.data_ptr(), K, cur_stream(x))) return y;
   check(dl_conv_fwd(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(wp), sc.Kp, (int)K, bf(y), 1, 1,
                     1, 1, 0, 0, K, cur_stream(x)),
         "conv2d_fwd(stem)");
@@ -731,6 +764,9 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
   TORCH_CHECK(K % 64 == 0, "conv2d_dgrad needs Cout % 64 == 0");
   auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);  // [K, R, S, C]
+  if (is_pointwise(R, S, stride, pad) && H == P && W == Q && conv_lt() &&
+      lt_plain(rows2d(dy), wk.view({K, C}), false, dx.data_ptr(), C, cur_stream(dy)))
+    return dx;
   for (int64_t a = 0; a < stride; ++a) {
     const int64_t I = (H - a + stride - 1) / stride;
     const int64_t r0 = (a + pad) % stride, TR = r0 < R ? (R - 1 - r0) / stride + 1 : 0;
@@ -769,7 +805,9 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
   const bool direct = dk.is_contiguous();
   at::Tensor acc = direct ? dk : at::zeros({K, R, S, C}, dw.options());
   int rc;
-  if (C % 8 == 0 && C >= 8 && C % 64 == 0) {
+  if (is_pointwise(R, S, stride, pad) && conv_lt()) {
+    gemm_acc_f32_split(rows2d(dy), rows2d(x), acc.view({K, C}), true, false, 32);
+  } else if (C % 8 == 0 && C >= 8 && C % 64 == 0) {
     rc = dl_conv_wgrad(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(dy), K, (int)K,
                        f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy));
     check(rc, "conv2d_wgrad");
@@ -778,11 +816,17 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
     const StemCols sc = stem_cols(R, S, C);
     const int64_t M = N * P * Q;
     const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
-    auto slab = at::zeros({K, R, sc.SCp}, dw.options());
-    rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K, f32(slab),
-                       R * sc.SCp, (int)(R * sc.SCp), cur_stream(dy));
-    check(rc, "conv2d_wgrad(stem)");
-    acc.view({K, R, S * C}).add_(slab.narrow(2, 0, S * C));
+    if (conv_lt()) {
+      auto slab = at::zeros({K, sc.Kp}, dw.options());
+      gemm_acc_f32_split(rows2d(dy), col, slab, true, false, 32);
+      acc.view({K, R, S * C}).add_(slab.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C));
+    } else {
+      auto slab = at::zeros({K, R, sc.SCp}, dw.options());
+      rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K,
+                         f32(slab), R * sc.SCp, (int)(R * sc.SCp), cur_stream(dy));
+      check(rc, "conv2d_wgrad(stem)");
+      acc.view({K, R, S * C}).add_(slab.narrow(2, 0, S * C));
+    }
   }
   if (!direct) dk.add_(acc);
 }

@@ -28,6 +28,16 @@ SHAPES = [
 ]
 
 
+# 1x1 stride-1 convs and the stem's column GEMM route to hipBLASLt by default (bindings.cpp conv_lt)
+LT_SHAPES = [s for s in SHAPES if s[1] == 3 or (s[4] == 1 and s[5] == 1)]
+
+
+@pytest.fixture
+def hip_kernels(monkeypatch):
+    """Force conv.hip for every shape (the library route would otherwise take the GEMM-shaped ones)."""
+    monkeypatch.setenv("DEDLOC_CONV_GEMM", "hip")
+
+
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
@@ -74,7 +84,7 @@ def test_conv_module_cpu_fallback_is_stock():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_conv_fwd_gpu(cuda, shape):
+def test_conv_fwd_gpu(cuda, hip_kernels, shape):
     N, Cin, H, Cout, k, stride, pad = shape
     x, w, dy = _data(cuda, *shape)
     y = torch.ops.dedloc.conv2d_fwd(x, w, stride, pad)
@@ -86,7 +96,7 @@ def test_conv_fwd_gpu(cuda, shape):
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] % 64 == 0 and s[3] % 64 == 0],
                          ids=lambda s: "x".join(map(str, s)))
-def test_conv_dgrad_gpu(cuda, shape):
+def test_conv_dgrad_gpu(cuda, hip_kernels, shape):
     N, Cin, H, Cout, k, stride, pad = shape
     x, w, dy = _data(cuda, *shape, seed=1)
     dx = torch.ops.dedloc.conv2d_dgrad(dy, w, stride, pad, H, H)
@@ -97,7 +107,7 @@ def test_conv_dgrad_gpu(cuda, shape):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
-def test_conv_wgrad_gpu(cuda, shape):
+def test_conv_wgrad_gpu(cuda, hip_kernels, shape):
     N, Cin, H, Cout, k, stride, pad = shape
     x, w, dy = _data(cuda, *shape, seed=2)
     _, _, dwr = _reference(x, w, dy, stride, pad)
@@ -111,7 +121,7 @@ def test_conv_wgrad_gpu(cuda, shape):
 
 
 @pytest.mark.gpu
-def test_conv_wgrad_large_reduction_split_k(cuda):
+def test_conv_wgrad_large_reduction_split_k(cuda, hip_kernels):
     """224-crop stem at batch 4: 50k-pixel reduction split over many workgroups (fp32 atomics)."""
     shape = (4, 3, 224, 64, 7, 2, 3)
     x, w, dy = _data(cuda, *shape, seed=3)
@@ -119,6 +129,26 @@ def test_conv_wgrad_large_reduction_split_k(cuda):
     dw = torch.zeros(64, 3, 7, 7, device=cuda).contiguous(memory_format=CL)
     torch.ops.dedloc.conv2d_wgrad(dy, x, dw, 2, 3)
     assert _rel(dw, dwr) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", LT_SHAPES + [(4, 3, 224, 64, 7, 2, 3)], ids=lambda s: "x".join(map(str, s)))
+def test_conv_library_gemm_route_gpu(cuda, shape, monkeypatch):
+    """Default routing: pointwise convs and the stem GEMM through hipBLASLt (fwd, dgrad, fp32 wgrad
+    accumulated with token-split slabs)."""
+    monkeypatch.delenv("DEDLOC_CONV_GEMM", raising=False)
+    N, Cin, H, Cout, k, stride, pad = shape
+    x, w, dy = _data(cuda, *shape, seed=4)
+    yr, dxr, dwr = _reference(x, w, dy, stride, pad)
+    y = torch.ops.dedloc.conv2d_fwd(x, w, stride, pad)
+    assert y.is_contiguous(memory_format=CL) and _rel(y, yr) < 1e-2, _rel(y, yr)
+    if Cout % 64 == 0 and Cin % 64 == 0:
+        dx = torch.ops.dedloc.conv2d_dgrad(dy, w, stride, pad, H, H)
+        assert dx.is_contiguous(memory_format=CL) and _rel(dx, dxr) < 1e-2, _rel(dx, dxr)
+    base = torch.randn(Cout, Cin, k, k, device=cuda).contiguous(memory_format=CL)
+    dw = base.clone()
+    torch.ops.dedloc.conv2d_wgrad(dy, x, dw, stride, pad)
+    assert _rel(dw - base, dwr) < 1e-3, _rel(dw - base, dwr)
 
 
 @pytest.mark.gpu
