@@ -605,6 +605,25 @@ void row_normalize_(at::Tensor w) {
   check(dl_row_normalize(f32(w), (int)w.size(0), (int)w.size(1), cur_stream(w)), "row_normalize");
 }
 
+at::Tensor multicrop(const at::Tensor& pool, const at::Tensor& params, int64_t size, int64_t rad,
+                     at::ArrayRef<double> mean, at::ArrayRef<double> std) {
+  expect(pool, at::kFloat, "pool");
+  expect(params, at::kFloat, "params");
+  TORCH_CHECK(pool.dim() == 4 && pool.size(1) == 3, "pool must be [P, 3, H, W]");
+  TORCH_CHECK(params.dim() == 2 && params.size(1) == 20, "params must be [nb, 20]");
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "mean/std need 3 channels");
+  const int64_t nb = params.size(0), S = size;
+  auto out = at::empty({nb, 3, S, S}, pool.options().dtype(at::kBFloat16), at::MemoryFormat::ChannelsLast);
+  if (nb == 0) return out;
+  auto ws = at::empty({2 * nb * 3 * S * S + nb}, pool.options());
+  const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  const float sd[3] = {(float)std[0], (float)std[1], (float)std[2]};
+  check(dl_multicrop(f32(pool), (int)pool.size(0), (int)pool.size(2), (int)pool.size(3), f32(params), (int)nb, (int)S, (int)rad, m, sd,
+                     f32(ws), bf(out), cur_stream(pool)),
+        "multicrop (blur radius must be < crop size and <= 16)");
+  return out;
+}
+
 // ------------------------------------------------------------------ BatchNorm (channels-last, fused act)
 inline void expect_nhwc(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -842,6 +861,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("sinkhorn", &sinkhorn);
   m.impl("swav_ce", &swav_ce);
   m.impl("row_normalize_", &row_normalize_);
+  m.impl("multicrop", &multicrop);
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);
   m.impl("gelu_fwd", &gelu_fwd);

@@ -67,6 +67,10 @@ int dl_sinkhorn(const float* scores, float* P, float* Q, float* ws, int n, int K
 int dl_swav_ce(const void* scores, int scores_bf16, const float* q, float* dscores, float* loss, int rows, int K,
                float temperature, float scale, hipStream_t st);
 int dl_row_normalize(float* w, int rows, int d, hipStream_t st);
+// SwAV multi-crop augmentation (augment.hip): pool [P, 3, Hp, Wp] fp32, params [nb, 20] fp32,
+// ws >= 2 * nb*3*S*S + nb floats, out [nb, S, S, 3] bf16 (channels-last [nb, 3, S, S])
+int dl_multicrop(const float* pool, int P, int Hp, int Wp, const float* params, int nb, int S, int rad, const float* mean,
+                 const float* stdv, float* ws, bf16_t* out, hipStream_t st);
 int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta, float* sums,
               float* mean, float* rstd, float* run_mean, float* run_var, long R, int C, int G, float eps,
               float momentum, int relu, hipStream_t st);

@@ -45,6 +45,7 @@ _SCHEMAS = [
     "sinkhorn(Tensor scores, int bs, float eps, int iters) -> Tensor",
     "swav_ce(Tensor scores, Tensor q, Tensor(a!) dscores, Tensor(b!) loss, float temperature, float scale) -> ()",
     "row_normalize_(Tensor(a!) w) -> ()",
+    "multicrop(Tensor pool, Tensor params, int size, int rad, float[] mean, float[] std) -> Tensor",
     "bn_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
     "float eps, float momentum, bool relu, int groups=1) -> (Tensor, Tensor, Tensor)",
     "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres) "
@@ -425,6 +426,13 @@ def _swav_ce_cpu(scores, q, dscores, loss, temperature, scale):
 @_impl("row_normalize_")
 def _row_normalize_cpu(w):
     w.div_(w.norm(dim=1, keepdim=True).clamp_min(1e-12))
+
+
+@_impl("multicrop")
+def _multicrop_cpu(pool, params, size, rad, mean, std):
+    from dedloc_amd.data.multicrop import augment_reference
+
+    return augment_reference(pool, params, size, rad, mean, std)
 
 
 @_impl("bn_fwd")

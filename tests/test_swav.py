@@ -154,6 +154,43 @@ def test_multicrop_shapes_cpu():
     assert [tuple(c.shape) for c in crops] == [(3, 3, 32, 32)] * 2 + [(3, 3, 16, 16)] * 3
     assert all(torch.isfinite(c).all() for c in crops)
     assert crops[0].is_contiguous(memory_format=torch.channels_last)
+    again = SyntheticMultiCropStream(3, "cpu", seed=1, pool_size=4, image_size=48, augment=aug,
+                                     out_dtype=torch.float32).next_batch()
+    assert all(torch.equal(a, b) for a, b in zip(crops, again))  # per-peer seed fixes every draw
+
+
+def test_multicrop_params_cover_the_reference_transforms():
+    """Parameter table statistics match the vissl transform probabilities (flip 0.5, colour 0.8,
+    grayscale 0.2, blur 0.5) and RandomResizedCrop's area range."""
+    from dedloc_amd.data.multicrop import MultiCropAugment
+
+    aug = MultiCropAugment()
+    gen = torch.Generator().manual_seed(0)
+    p = aug.sample_params(torch.zeros(20000, dtype=torch.long), (0.05, 0.14), gen)
+    assert abs((p[:, 1] < 0).float().mean() - 0.5) < 0.02
+    assert abs(p[:, 8].mean() - 0.8) < 0.02 and abs(p[:, 9].mean() - 0.2) < 0.02
+    assert abs((p[:, 19] > 0).float().mean() - 0.5) < 0.02
+    area = p[:, 1].abs() * p[:, 3]
+    assert area.min() >= 0.05 - 1e-4 and area.max() <= 0.14 + 1e-4
+    M = p[0, 10:19].view(3, 3)
+    assert torch.allclose(M.sum(1), torch.ones(3), atol=1e-4)  # a hue rotation keeps greys grey
+
+
+@pytest.mark.gpu
+def test_multicrop_kernels_match_reference(cuda):
+    """augment.hip (sample / colour / blur / normalize) vs the tensor-op reference on the same table."""
+    from dedloc_amd.data.multicrop import MultiCropAugment, _smooth_images, augment_reference
+
+    pool = _smooth_images(6, 64, torch.Generator(device=cuda).manual_seed(0), cuda)
+    aug = MultiCropAugment()
+    gen = torch.Generator().manual_seed(3)
+    for size, scale in ((40, (0.14, 1.0)), (16, (0.05, 0.14))):
+        params = aug.sample_params(torch.randint(0, 6, (24,), generator=gen), scale, gen)
+        out = torch.ops.dedloc.multicrop(pool, params.to(cuda), size, aug.rad, list(aug.mean), list(aug.std))
+        ref = augment_reference(pool.cpu(), params, size, aug.rad, aug.mean, aug.std)
+        assert out.dtype == torch.bfloat16 and out.is_contiguous(memory_format=torch.channels_last)
+        err = (out.cpu().float() - ref.float()).abs()
+        assert err.max() < 0.05 and err.mean() < 2e-3, (err.max(), err.mean())
 
 
 def _tiny_cfg(extra=()):
