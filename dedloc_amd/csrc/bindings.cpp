@@ -692,9 +692,9 @@ inline int64_t conv_out(int64_t n, int64_t k, int64_t stride, int64_t pad) { ret
 struct StemCols {
   int64_t SCp, Kp;
 };
-inline StemCols stem_cols(int64_t R, int64_t S, int64_t C) {
-  const int64_t SCp = (S * C + 7) / 8 * 8;
-  return {SCp, (R * SCp + 63) / 64 * 64};
+inline StemCols stem_cols(int64_t R, int64_t S, int64_t C, bool lt) {
+  const int64_t SCp = (S * C + 7) / 8 * 8;  // hipBLASLt needs 16-byte rows only; conv.hip a multiple of BK
+  return {SCp, lt ? R * SCp : (R * SCp + 63) / 64 * 64};
 }
 inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t P,
                               int64_t Q, const StemCols& sc) {
@@ -755,16 +755,22 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
           "conv2d_fwd");
     return y;
   }
-  // stem: im2col, then a 1x1 conv over the column matrix
-  const StemCols sc = stem_cols(R, S, C);
+  // stem: im2col, then a GEMM (hipBLASLt) or a 1x1 conv (conv.hip) over the column matrix
   const int64_t M = N * P * Q;
-  const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
-  auto wp = at::zeros({K, sc.Kp}, w.options());
-  wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
-  if (conv_lt() && lt_plain(col, wp, true, y.data_ptr(), K, cur_stream(x))) return y;
-  check(dl_conv_fwd(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(wp), sc.Kp, (int)K, bf(y), 1, 1,
-                    1, 1, 0, 0, K, cur_stream(x)),
-        "conv2d_fwd(stem)");
+  for (const bool lt : {true, false}) {
+    if (lt && !conv_lt()) continue;
+    const StemCols sc = stem_cols(R, S, C, lt);
+    const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
+    auto wp = at::zeros({K, sc.Kp}, w.options());
+    wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
+    if (lt) {
+      if (lt_plain(col, wp, true, y.data_ptr(), K, cur_stream(x))) return y;
+      continue;
+    }
+    check(dl_conv_fwd(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(wp), sc.Kp, (int)K, bf(y), 1,
+                      1, 1, 1, 0, 0, K, cur_stream(x)),
+          "conv2d_fwd(stem)");
+  }
   return y;
 }
 
@@ -832,7 +838,7 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
     check(rc, "conv2d_wgrad");
   } else {
     // stem: wgrad over the padded column matrix into a [K, R, SCp] slab, then the real columns
-    const StemCols sc = stem_cols(R, S, C);
+    const StemCols sc = stem_cols(R, S, C, conv_lt());
     const int64_t M = N * P * Q;
     const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
     if (conv_lt()) {
