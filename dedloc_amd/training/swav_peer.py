@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import json
 import logging
+import math
 import time
 from pathlib import Path
 from typing import Optional
@@ -33,6 +34,7 @@ from ..models.swav_loss import SwAVLoss
 from ..optim.collaborative import CollaborativeOptimizer
 from ..optim.lamb import FusedLarcSGD, LinearWarmupCosineAnnealingLR
 from ..utils.flat import FlatParams
+from ..utils.perf import PerfStats
 
 logger = logging.getLogger(__name__)
 
@@ -68,6 +70,11 @@ class SwavPeer:
                                checkpoint_stages=bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING),
                                conv_impl=mcfg.get("CONV_IMPL") or None)
         self.model.to(self.device).train()
+        hooks = cfg.get("HOOKS") or {}
+        self.check_nan = bool(hooks.get("CHECK_NAN", True))
+        self.log_frequency = max(1, int(cfg.get("LOG_FREQUENCY", 10)))
+        # vissl PerfTimer/LogPerfTimeMetricsHook (V20): HIP-event phase timers, reported per global step
+        self.perf = PerfStats(self.device, enabled=bool(hooks.get("PERF_STATS", True)))
         self.flat = FlatParams(self.model.named_parameters(), device=self.device, with_bf16=False, autograd=True,
                                channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
         self.model.normalize_prototypes()
@@ -167,17 +174,24 @@ class SwavPeer:
             return self.model(crops)
 
     def train_step(self, crops=None):
-        crops = crops if crops is not None else self.data.next_batch()
-        emb, scores = self._forward(crops)
-        proto = self.model.heads[0].prototypes0.weight
-        loss = self.loss_fn(emb.float(), scores, proto, training_iterations=int(self.collab_opt.local_step))
-        loss.backward()
+        with self.perf.phase("data"):
+            crops = crops if crops is not None else self.data.next_batch()
+        with self.perf.phase("fwd"):
+            emb, scores = self._forward(crops)
+        with self.perf.phase("loss_bwd"):
+            proto = self.model.heads[0].prototypes0.weight
+            loss = self.loss_fn(emb.float(), scores, proto, training_iterations=int(self.collab_opt.local_step))
+            loss.backward()
         for name, iters in self.frozen:  # FreezeParametersHook (state_update_hooks.py:235-280)
             if self.iteration < iters:
                 name = name[len("module."):] if name.startswith("module.") else name
                 self.flat.view(self.flat.grad, name).zero_()
         self._loss_sum += loss.detach()
-        self.collab_opt.step(batch_size=self.batch_size)
+        if self.check_nan and (self.iteration + 1) % self.log_frequency == 0 and \
+                not bool(torch.isfinite(self._loss_sum)):  # before the step: NaN grads never reach the averaging
+            self._nan_dump(float(self._loss_sum))
+        with self.perf.phase("collab_step"):
+            self.collab_opt.step(batch_size=self.batch_size)
         self.opt.zero_grad()
         self.model.normalize_prototypes()  # NormalizePrototypesHook.on_update (swav_hooks.py:63-92)
         self.iteration += 1
@@ -191,13 +205,15 @@ class SwavPeer:
             return
         self.last_reported_step = co.local_step
         loss = float(self._loss_sum.item())
+        if self.check_nan and not math.isfinite(loss):
+            self._nan_dump(loss)
         stats = LocalMetrics(step=int(co.local_step), samples_per_second=float(co.performance_ema.samples_per_second),
                              samples_accumulated=int(co.local_samples_accumulated), loss=loss,
                              mini_steps=int(self.mini_steps))
         self.dht.store(co.prefix + "_metrics", stats.model_dump(), expiration_time=get_dht_time() + 600,
                        subkey=self.local_public_key, return_future=True)
         rec = dict(stats.model_dump(), time=time.time(), iteration=self.iteration, lr=self.opt.param_groups[0]["lr"],
-                   queue=bool(self.loss_fn.use_queue))
+                   queue=bool(self.loss_fn.use_queue), **self.perf.report())
         self.metrics_log.append(rec)
         if self.cfg.get("METRICS_FILE"):
             with open(self.cfg.METRICS_FILE, "a") as f:
@@ -206,6 +222,20 @@ class SwavPeer:
                     f"lr {self.opt.param_groups[0]['lr']:.4g}")
         self._loss_sum.zero_()
         self.mini_steps = 0
+
+    def _nan_dump(self, loss: float):
+        """vissl CheckNanLossHook (``state_update_hooks.py:207-233``) / the SwAV loss's NaN dump: save
+        the model, optimizer and loss state next to the checkpoints, then stop this peer.  Checked every
+        LOG_FREQUENCY iterations (one host sync per check, before the collaborative step) and at every
+        global-step report, where the loss is read anyway."""
+        d = Path(self.cfg.CHECKPOINT.DIR)
+        d.mkdir(parents=True, exist_ok=True)
+        path = d / f"nan_dump_iteration{self.iteration}.torch"
+        state = self.state_dict()
+        state["loss_sum"] = loss
+        torch.save(state, path)
+        logger.error(f"non-finite SwAV loss ({loss}) at iteration {self.iteration}; state dumped to {path}")
+        raise FloatingPointError(f"non-finite SwAV loss at iteration {self.iteration} (dump: {path})")
 
     # ------------------------------------------------------------------ checkpoints (V19)
     def state_dict(self):

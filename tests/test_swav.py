@@ -447,3 +447,31 @@ def test_swav_single_pass_semantics_fused_gpu(cuda):
     bn1, bn2 = m1.trunk.layer1[0].bn1, m2.trunk.layer1[0].bn1
     assert torch.allclose(bn1.running_mean, bn2.running_mean, atol=2e-3)
     assert int(bn1.num_batches_tracked) == int(bn2.num_batches_tracked) == 3
+
+
+def test_swav_nan_loss_dumps_state_and_stops(tmp_path):
+    """CheckNanLossHook semantics: a non-finite loss is caught at the next global-step report, the
+    peer state is dumped to the checkpoint dir and the peer stops; phase timers land in the metrics."""
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.training.swav_peer import SwavPeer
+
+    cfg = _tiny_cfg([f"config.CHECKPOINT.DIR={tmp_path}", "config.LOG_FREQUENCY=2"])
+    dht = DHT(start=True)
+    peer = SwavPeer(cfg, "cpu", dht=dht)
+    try:
+        for _ in range(4):
+            peer.train_step()
+        rec = peer.metrics_log[-1]
+        assert rec["fwd_ms"] > 0 and rec["loss_bwd_ms"] > 0 and rec["data_n"] >= 1
+        with torch.no_grad():
+            peer.model.trunk.conv1.weight.fill_(float("nan"))
+        with pytest.raises(FloatingPointError):
+            for _ in range(4):
+                peer.train_step()
+        dumps = list(tmp_path.glob("nan_dump_iteration*.torch"))
+        assert len(dumps) == 1
+        sd = torch.load(dumps[0], map_location="cpu", weights_only=True)
+        assert not math.isfinite(sd["loss_sum"]) and "model" in sd
+    finally:
+        peer.shutdown()
+        dht.shutdown()
