@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu_test", default=None, metavar="CONFIG_DIR",
                     help="plumbing test only: run on CPU/gloo with the tiny model config in CONFIG_DIR "
                          "(exercises the multi-rank orchestration of this script; not a measurement)")
+    ap.add_argument("--throttle", type=float, default=0.0,
+                    help="emulation only: idle seconds added after every micro-step (with --cpu_test, stands in "
+                         "for GPU compute time when studying the collaboration protocol's overheads)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -86,7 +89,8 @@ def main():
         dist.broadcast_object_list(ep, src=0)
     targs = AlbertTrainingArguments(per_device_train_batch_size=args.micro_batch,
                                     gradient_accumulation_steps=args.grad_accum, seq_length=args.seq_len,
-                                    save_steps=0, output_dir=f"/tmp/dedloc_bench_{os.getpid()}", seed=1234)
+                                    save_steps=0, output_dir=f"/tmp/dedloc_bench_{os.getpid()}", seed=1234,
+                                    throttle=args.throttle)
     dargs = DatasetArguments(config_path=args.cpu_test or "albert-large-v2")
     cargs = CollaborationArguments(experiment_prefix="bench", initial_peers=[ep[0]], dht_listen_on="127.0.0.1:*",
                                    target_batch_size=args.target_batch_size, compression=args.compression,
