@@ -39,7 +39,20 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __rest
   sums += (long)blockIdx.y * 2 * C;
   const long r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (long r = r0 + rsub; r < r1; r += rpi) {
+  long r = r0 + rsub;
+  for (; r + 3 * rpi < r1; r += 4 * rpi) {  // four 16-byte loads in flight per thread
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ld8(x + (r + u * rpi) * C + cv * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += v[u][j];
+        q[j] = fmaf(v[u][j], v[u][j], q[j]);
+      }
+  }
+  for (; r < r1; r += rpi) {
     float v[8];
     ld8(x + r * C + cv * 8, v);
 #pragma unroll
@@ -106,8 +119,31 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
   x += base;
   y += base;
   if (res != nullptr) res += base;
-  for (long i = blockIdx.x * (long)kThreads + threadIdx.x; i < nvec; i += (long)gridDim.x * kThreads) {
-    const int c0 = (int)(i % CV) * 8;
+  // CV is a power of two (bn_shape_ok), so the channel of vector i is i & (CV - 1); two vectors per
+  // iteration keep two independent load chains in flight per thread
+  const long stride = (long)gridDim.x * kThreads;
+  long i = blockIdx.x * (long)kThreads + threadIdx.x;
+  for (; i + stride < nvec; i += 2 * stride) {
+    float v[2][8], rr[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ld8(x + (i + u * stride) * 8, v[u]);
+      if (res != nullptr) ld8(res + (i + u * stride) * 8, rr[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c0 = ((int)(i + u * stride) & (CV - 1)) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float o = fmaf(v[u][j], sc[c0 + j], sh[c0 + j]);
+        if (res != nullptr) o += rr[u][j];
+        v[u][j] = relu ? fmaxf(o, 0.f) : o;
+      }
+      store_bf16<8>(y + (i + u * stride) * 8, v[u]);
+    }
+  }
+  for (; i < nvec; i += stride) {
+    const int c0 = ((int)i & (CV - 1)) * 8;
     float v[8];
     ld8(x + i * 8, v);
     float rr[8];
@@ -147,7 +183,26 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
     rs[j] = rstd[cv * 8 + j];
   }
   float sg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sgx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (long r = r0 + rsub; r < r1; r += rpi) {
+  long r = r0 + rsub;
+  for (; r + rpi < r1; r += 2 * rpi) {  // two rows (up to six 16-byte loads) in flight per thread
+    float g[2][8], xv[2][8], yv[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long off = (r + u * rpi) * C + cv * 8;
+      ld8(dy + off, g[u]);
+      ld8(x + off, xv[u]);
+      if (relu) ld8(y + off, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gg = (!relu || yv[u][j] > 0.f) ? g[u][j] : 0.f;
+        sg[j] += gg;
+        sgx[j] = fmaf(gg, (xv[u][j] - mu[j]) * rs[j], sgx[j]);
+      }
+  }
+  for (; r < r1; r += rpi) {
     const long off = r * C + cv * 8;
     float g[8], xv[8];
     ld8(dy + off, g);
@@ -217,8 +272,37 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
   if (dres != nullptr) dres += base;
   const int CV = C >> 3;
   const long nvec = R * CV;
-  for (long i = blockIdx.x * (long)kThreads + threadIdx.x; i < nvec; i += (long)gridDim.x * kThreads) {
-    const int c0 = (int)(i % CV) * 8;
+  const long stride = (long)gridDim.x * kThreads;
+  long i = blockIdx.x * (long)kThreads + threadIdx.x;
+  for (; i + stride < nvec; i += 2 * stride) {
+    float g[2][8], xv[2][8], yv[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ld8(dy + (i + u * stride) * 8, g[u]);
+      ld8(x + (i + u * stride) * 8, xv[u]);
+      if (relu) ld8(y + (i + u * stride) * 8, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long iv = i + u * stride;
+      const int c0 = ((int)iv & (CV - 1)) * 8;
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[u][j] = yv[u][j] > 0.f ? g[u][j] : 0.f;
+      }
+      if (dres != nullptr) store_bf16<8>(dres + iv * 8, g[u]);
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        const float xh = (xv[u][j] - mu_s[c]) * rs_s[c];
+        o[j] = k1[c] * (g[u][j] - mg[c] - xh * mgx[c]);
+      }
+      store_bf16<8>(dx + iv * 8, o);
+    }
+  }
+  for (; i < nvec; i += stride) {
+    const int c0 = ((int)i & (CV - 1)) * 8;
     float g[8], xv[8];
     ld8(dy + i * 8, g);
     ld8(x + i * 8, xv);
@@ -246,8 +330,12 @@ inline bool bn_shape_ok(int C) {
   return (kThreads % CV) == 0;
 }
 
-inline int stats_blocks(long R, long& rpb) {
-  long nb = (R + 63) / 64;
+// Rows per block: enough for ~8 row-iterations per thread (a block covers rpi = 256 / (C/8) rows per
+// iteration), at most 1024 blocks per statistics group.  Sizing by rows alone gave the 2048-channel
+// layers (rpi = 1) 64 serial iterations per thread on fewer blocks than CUs (profiles/README.md).
+inline int stats_blocks(long R, int C, long& rpb) {
+  const long rpi = kThreads / (C / 8);
+  long nb = (R + 8 * rpi - 1) / (8 * rpi);
   if (nb > 1024) nb = 1024;
   if (nb < 1) nb = 1;
   rpb = (R + nb - 1) / nb;
@@ -269,7 +357,7 @@ int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
   if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
   DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
   long rpb;
-  const int nb = stats_blocks(R, rpb);
+  const int nb = stats_blocks(R, C, rpb);
   bn_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(x, sums, R, C, rpb);
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
   bn_apply_kernel<<<dim3(na, G), kThreads, 0, st>>>(x, res, y, sums, gamma, beta, mean, rstd, run_mean, run_var, R, C,
@@ -283,7 +371,7 @@ int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* m
   if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
   DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
   long rpb;
-  const int nb = stats_blocks(R, rpb);
+  const int nb = stats_blocks(R, C, rpb);
   bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu);
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
   bn_bwd_dx_kernel<<<dim3(na, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
