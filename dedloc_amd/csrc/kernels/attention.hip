@@ -16,6 +16,8 @@
 // One LDS image per 64x64 bf16 tile serves both the row reads and the transposed reads: 16-byte
 // chunk c of row r lives at chunk c ^ f((r>>1)&7), f(x) = x ^ ((x&1)<<2) — conflict-free for the
 // ds_read_b128 lane groups and for the 4-row tr-read blocks (derivation in docs/KERNELS.md).
+#include <cstdlib>
+
 #include "dl_common.h"
 #include "dl_kernels.h"
 
@@ -113,6 +115,22 @@ __device__ __forceinline__ void store4(bf16_t* p, float a, float b, float c, flo
 // 2^RESCALE_THR (cdna_hip_programming.md T13: P <= 2^8 is exact enough in bf16 for P.V; the
 // rescale decision precedes the tile's exponentiation, so nothing is ever scaled twice).
 constexpr float RESCALE_THR = 8.f;
+
+// XCD-aware block order (T1): the hardware deals consecutive workgroups round-robin to the 8 XCDs,
+// which would put the S/128 query (or key) blocks of one head on different XCDs, each re-reading
+// that head's K/V (Q/dO) into its own L2.  Renumber so each XCD gets a contiguous run of logical
+// blocks: all blocks of a head then share one L2.
+struct BlockId {
+  int x, h, b;
+};
+__device__ __forceinline__ BlockId block_id(int xcd) {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int n = gx * gy * gridDim.z;
+  int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if (xcd && (n & 7) == 0) p = (p & 7) * (n >> 3) + (p >> 3);
+  return BlockId{p % gx, (p / gx) % gy, p / (gx * gy)};
+}
+
 
 __device__ __forceinline__ int kv_end_of(const int* kvinfo, int B, int b, int S, bool& use_len) {
   use_len = false;
@@ -237,9 +255,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
                                                           const float* __restrict__ mbias,
                                                           const int* __restrict__ kvinfo, bf16_t* __restrict__ out,
                                                           long ldo, float* __restrict__ lse, int B, int H, int S,
-                                                          float sl2) {
+                                                          float sl2, int xcd) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
-  const int b = blockIdx.z, h = blockIdx.y;
+  const BlockId bid = block_id(xcd);
+  const int b = bid.b, h = bid.h;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
   const long rb = (long)b * S;
   const bf16_t* Qg = qkv + rb * ld + h * HD;
@@ -255,7 +274,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   c.smem = smem;
   c.mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
 
-  const int q = blockIdx.x * 128 + w * 32 + r;
+  const int q = bid.x * 128 + w * 32 + r;
   const int qc = min(q, S - 1);
   bf16x8 qf[4];
 #pragma unroll
@@ -306,9 +325,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
                                                              const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
                                                              long ldo, const float* __restrict__ lse,
                                                              float* __restrict__ delta, bf16_t* __restrict__ dqkv,
-                                                             int B, int H, int S, float sl2, float scale) {
+                                                             int B, int H, int S, float sl2, float scale, int xcd) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
-  const int b = blockIdx.z, h = blockIdx.y;
+  const BlockId bid = block_id(xcd);
+  const int b = bid.b, h = bid.h;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
   const long rb = (long)b * S;
   const bf16_t* Qg = qkv + rb * ld + h * HD;
@@ -319,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
   const float* mb_g = (!use_len && mbias) ? mbias + rb : nullptr;
   float* mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
 
-  const int q = blockIdx.x * 128 + w * 32 + r;
+  const int q = bid.x * 128 + w * 32 + r;
   const int qc = min(q, S - 1);
   bf16x8 qf[4], df[4];
   float dl = 0.f;
@@ -422,9 +442,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
                                                                const float* __restrict__ lse,
                                                                const float* __restrict__ delta,
                                                                bf16_t* __restrict__ dqkv, int B, int H, int S,
-                                                               float sl2, float scale) {
+                                                               float sl2, float scale, int xcd) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 2 * 64 * 4];
-  const int b = blockIdx.z, h = blockIdx.y;
+  const BlockId bid = block_id(xcd);
+  const int b = bid.b, h = bid.h;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
   const long rb = (long)b * S;
   const bf16_t* Qg = qkv + rb * ld + h * HD;
@@ -435,11 +456,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
   const float* del_g = delta + ((long)b * H + h) * S;
   float* rowv = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);  // [2 buf][lse 64 | delta 64]
 
-  const int k = blockIdx.x * 128 + w * 32 + r;
+  const int k = bid.x * 128 + w * 32 + r;
   const int kc = min(k, S - 1);
   bool use_len;
   const int kv_end = kv_end_of(kvinfo, B, b, S, use_len);
-  if (use_len && blockIdx.x * 128 >= kv_end) {  // every key of this block is padding: dK = dV = 0
+  if (use_len && bid.x * 128 >= kv_end) {  // every key of this block is padding: dK = dV = 0
     if (k < S) {
       bf16_t* dkp = dqkv + (rb + k) * ld + (long)H * HD + h * HD;
       bf16_t* dvp = dqkv + (rb + k) * ld + 2L * H * HD + h * HD;
@@ -538,6 +559,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
   }
 }
 
+// DEDLOC_ATTN_XCD=0 restores the hardware block order (A/B measurement)
+int attn_xcd() {
+  static const int v = [] {
+    const char* e = std::getenv("DEDLOC_ATTN_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
 }  // namespace
 
 int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, bf16_t* out, long ldo, float* lse,
@@ -545,7 +575,7 @@ int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid((S + 127) / 128, H, B);
-  attn_fwd_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2);
+  attn_fwd_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
   return 0;
 }
 
@@ -556,7 +586,8 @@ int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid((S + 127) / 128, H, B);
   attn_bwd_dq_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, B, H, S, sl2,
-                                           scale);
-  attn_bwd_dkdv_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2, scale);
+                                           scale, attn_xcd());
+  attn_bwd_dkdv_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2, scale,
+                                             attn_xcd());
   return 0;
 }
