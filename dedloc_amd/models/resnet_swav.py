@@ -85,7 +85,9 @@ class ConvNHWC(nn.Conv2d):
     measured on MI355X for the SwAV b=64 iteration (profiles/README.md): ``hip`` (default) 1518-1531
     samples/s, first iteration ~15 s; MIOpen immediate mode 1405 samples/s, first iteration ~49 s;
     MIOpen with exhaustive find (cudnn.benchmark) 1700 samples/s once its per-shape search is done, but
-    that search took from ~1 to >3 minutes per fresh process on the pool's boxes."""
+    that search took from ~1 to >3 minutes per fresh process on the pool's boxes.  The 3-channel stem
+    alone defaults to MIOpen (``MODEL.STEM_CONV_IMPL``): its direct kernels beat im2col + GEMM 2.7x and
+    the search for two shapes takes ~13 s (1979.6 vs 1905.5 samples/s)."""
 
     native = os.environ.get("DEDLOC_CONV", "hip") == "hip"
 
@@ -215,17 +217,20 @@ class SwAVPrototypesHead(nn.Module):
 
 class SwAVModel(nn.Module):
     def __init__(self, num_prototypes: int = 3000, single_pass_every_crop: bool = True,
-                 checkpoint_stages: bool = False, conv_impl: str | None = None):
+                 checkpoint_stages: bool = False, conv_impl: str | None = None, stem_conv_impl: str | None = None):
         super().__init__()
         self.trunk = ResNet50Trunk(checkpoint_stages=checkpoint_stages)
         self.heads = nn.ModuleList([SwAVPrototypesHead(num_prototypes=num_prototypes)])
         self.single_pass_every_crop = single_pass_every_crop
+        for impl in (conv_impl, stem_conv_impl):
+            if impl is not None and impl not in ("hip", "miopen"):
+                raise ValueError(f"conv backend must be 'hip' or 'miopen', got {impl!r}")
         if conv_impl is not None:
-            if conv_impl not in ("hip", "miopen"):
-                raise ValueError(f"conv_impl must be 'hip' or 'miopen', got {conv_impl!r}")
             for m in self.trunk.modules():
                 if isinstance(m, ConvNHWC):
                     m.native = conv_impl == "hip"
+        if stem_conv_impl is not None:  # the 3-channel 7x7 stem alone (MODEL.STEM_CONV_IMPL)
+            self.trunk.conv1.native = stem_conv_impl == "hip"
 
     def set_bn_stat_groups(self, g: int):
         for m in self.trunk.modules():
