@@ -66,7 +66,8 @@ class _ConvNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             weight = ctx.module.weight
             g = weight.grad
-            if g is not None and g.dtype == torch.float32 and g.permute(0, 2, 3, 1).is_contiguous():
+            if (g is not None and ctx.module.inplace_wgrad and g.dtype == torch.float32
+                    and g.permute(0, 2, 3, 1).is_contiguous()):
                 torch.ops.dedloc.conv2d_wgrad(dy, x, g, ctx.stride, ctx.pad)  # in place, no AccumulateGrad
             else:
                 dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device).contiguous(
@@ -90,6 +91,9 @@ class ConvNHWC(nn.Conv2d):
     the search for two shapes takes ~13 s (1979.6 vs 1905.5 samples/s)."""
 
     native = os.environ.get("DEDLOC_CONV", "hip") == "hip"
+    # False: return the weight gradient through autograd instead of adding it into the bound .grad
+    # (HIP-graph capture via make_graphed_callables needs every parameter to receive an autograd grad)
+    inplace_wgrad = True
 
     def forward(self, x):
         if (self.native and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)

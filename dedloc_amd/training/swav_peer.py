@@ -143,7 +143,8 @@ class SwavPeer:
 
         Opt-in (MODEL.CUDA_GRAPH): with batched equal-resolution trunk passes and the fused BN
         kernels the iteration is GPU-bound and replaying the graph measured slower than eager
-        (1462 vs 1689 samples/s, b=64) because of the static-input/grad copies.  The loss (Sinkhorn + CE, global-step-dependent queue), the collaborative step
+        (1462 vs 1689 samples/s, b=64; with the HIP convs 1685 vs 1976) because of the static-input/grad
+        copies.  The loss (Sinkhorn + CE, global-step-dependent queue), the collaborative step
         and the prototype normalisation stay eager.  Warm-up iterations run inside the capture
         helper, so grads and BN statistics are restored afterwards."""
 
@@ -155,6 +156,11 @@ class SwavPeer:
             def forward(self, *xs):
                 return self.m(list(xs))
 
+        from ..models.resnet_swav import ConvNHWC
+
+        for m in self.model.modules():  # captured backward must hand every weight grad to autograd
+            if isinstance(m, ConvNHWC):
+                m.inplace_wgrad = False
         grads = self.flat.grad.clone()
         bufs = {k: v.clone() for k, v in self.model.named_buffers()}
         sample = tuple(c.detach().clone() for c in crops)

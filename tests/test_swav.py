@@ -298,7 +298,10 @@ def test_swav_loss_gpu_matches_cpu(cuda):
 
 
 @pytest.mark.gpu
-def test_swav_peer_gpu_step(cuda, tmp_path):
+@pytest.mark.parametrize("graph", [False, True])
+def test_swav_peer_gpu_step(cuda, tmp_path, graph):
+    """Eager and HIP-graph (MODEL.CUDA_GRAPH: forward/backward replayed after 3 eager iterations;
+    the hand-written convs then return their weight grads through autograd) peer iterations."""
     from dedloc_amd.dht import DHT
     from dedloc_amd.training.swav_peer import SwavPeer
 
@@ -306,11 +309,13 @@ def test_swav_peer_gpu_step(cuda, tmp_path):
         "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=8", "config.DATA.TRAIN.SYNTHETIC_POOL_SIZE=16",
         "config.LOSS.swav_loss.queue.start_iter=0", "config.LOSS.swav_loss.queue.queue_length=64",
         "config.OPTIMIZER.target_batch_size=16", "config.OPTIMIZER.batch_size_for_tracking=8",
-        f"config.CHECKPOINT.DIR={tmp_path}"])
+        f"config.CHECKPOINT.DIR={tmp_path}", f"config.MODEL.CUDA_GRAPH={graph}"])
     dht = DHT(start=True)
     peer = SwavPeer(cfg, cuda, dht=dht)
     try:
-        losses = [float(peer.train_step()) for _ in range(3)]
+        losses = [float(peer.train_step()) for _ in range(5 if graph else 3)]
+        if graph:
+            assert peer._graphed is not None
         assert all(math.isfinite(x) for x in losses), losses
         w = peer.model.heads[0].prototypes0.weight
         assert torch.allclose(w.norm(dim=1), torch.ones(w.shape[0], device=cuda), atol=1e-4)
