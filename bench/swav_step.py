@@ -29,8 +29,8 @@ def main():
     ap.add_argument("--queue", action="store_true", help="queue active (3840 rows in Sinkhorn)")
     ap.add_argument("--graph", action="store_true", help="capture trunk+head fwd/bwd as HIP graphs")
     ap.add_argument("--no_find", action="store_true", help="MIOpen immediate mode (cudnn.benchmark=False)")
-    ap.add_argument("--conv", default=None, choices=["hip", "miopen"], help="conv backend (default: config)")
-    ap.add_argument("--stem", default=None, choices=["hip", "miopen"], help="stem conv backend (default: config)")
+    ap.add_argument("--conv", default=None, choices=["hip", "miopen", "auto"], help="conv backend (default: config)")
+    ap.add_argument("--stem", default=None, choices=["hip", "miopen", "null"], help="stem conv backend (default: config)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     ov = [f"config.DATA.TRAIN.BATCHSIZE_PER_REPLICA={args.batch}", f"config.OPTIMIZER.batch_size_for_tracking={args.batch}",

@@ -227,14 +227,22 @@ class SwAVModel(nn.Module):
         self.heads = nn.ModuleList([SwAVPrototypesHead(num_prototypes=num_prototypes)])
         self.single_pass_every_crop = single_pass_every_crop
         for impl in (conv_impl, stem_conv_impl):
-            if impl is not None and impl not in ("hip", "miopen"):
-                raise ValueError(f"conv backend must be 'hip' or 'miopen', got {impl!r}")
+            if impl is not None and impl not in ("hip", "miopen", "auto"):
+                raise ValueError(f"conv backend must be 'hip', 'miopen' or 'auto', got {impl!r}")
         if conv_impl is not None:
             for m in self.trunk.modules():
                 if isinstance(m, ConvNHWC):
-                    m.native = conv_impl == "hip"
+                    m.native = conv_impl == "hip" or (conv_impl == "auto" and not self._miopen_wins(m))
         if stem_conv_impl is not None:  # the 3-channel 7x7 stem alone (MODEL.STEM_CONV_IMPL)
             self.trunk.conv1.native = stem_conv_impl == "hip"
+
+    @staticmethod
+    def _miopen_wins(m: "ConvNHWC") -> bool:
+        """Shape classes where MIOpen's kernels measured clearly faster than conv.hip on the SwAV b=64
+        shapes (profiles/conv_bench_v6_*.jsonl): the 3-channel stem (2.7x) and the 64-output-channel
+        3x3 convs (fwd 2x: a 128-wide output tile is half idle at N=64).  Only these shapes pay
+        MIOpen's one-time solver search."""
+        return m.in_channels == 3 or (m.kernel_size == (3, 3) and m.out_channels == 64)
 
     def set_bn_stat_groups(self, g: int):
         for m in self.trunk.modules():
