@@ -86,9 +86,10 @@ class ConvNHWC(nn.Conv2d):
     measured on MI355X for the SwAV b=64 iteration (profiles/README.md): ``hip`` (default) 1518-1531
     samples/s, first iteration ~15 s; MIOpen immediate mode 1405 samples/s, first iteration ~49 s;
     MIOpen with exhaustive find (cudnn.benchmark) 1700 samples/s once its per-shape search is done, but
-    that search took from ~1 to >3 minutes per fresh process on the pool's boxes.  The 3-channel stem
-    alone defaults to MIOpen (``MODEL.STEM_CONV_IMPL``): its direct kernels beat im2col + GEMM 2.7x and
-    the search for two shapes takes ~13 s (1979.6 vs 1905.5 samples/s)."""
+    that search took from ~1 to >3 minutes per fresh process on the pool's boxes.  ``auto`` (the
+    config default) keeps MIOpen only where it clearly wins — the 3-channel stem (2.7x over
+    im2col + GEMM) and the 64-output-channel 3x3 convs (2x forward) — so the search covers four
+    shapes (~20 s once): 1982.1 samples/s vs 1953.9 for hip + MIOpen stem and 1905.5 for all-hip."""
 
     native = os.environ.get("DEDLOC_CONV", "hip") == "hip"
     # False: return the weight gradient through autograd instead of adding it into the bound .grad
