@@ -23,3 +23,14 @@ def cuda():
 
     assert ops.native_loaded(), "gfx950 kernel library must be loaded on a GPU box"
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _isolate_miopen_find():
+    """SwavPeer turns on cudnn.benchmark (MIOpen solver search, MODEL.MIOPEN_FIND); restore it after
+    every test so later MIOpen reference computations use the same (immediate-mode) solvers."""
+    import torch
+
+    saved = torch.backends.cudnn.benchmark
+    yield
+    torch.backends.cudnn.benchmark = saved
