@@ -73,7 +73,11 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Te
   expect(dgamma, at::kFloat, "dgamma");
   expect(dbeta, at::kFloat, "dbeta");
   const int64_t D = dy.size(-1), rows = dy.numel() / D;
-  const int nparts = (int)std::min<int64_t>(512, std::max<int64_t>(1, rows / 32));
+  static const int64_t max_parts = [] {  // DEDLOC_LN_PARTS: measurement override of the grid cap
+    const char* e = std::getenv("DEDLOC_LN_PARTS");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(512);
+  }();
+  const int nparts = (int)std::min<int64_t>(max_parts, std::max<int64_t>(1, rows / 32));
   auto ds = at::empty_like(dy);
   if (!accumulate) {
     dgamma.zero_();
