@@ -38,3 +38,12 @@ def test_contributor_cli_dry_run_subprocess():
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["micro_batch"] == 8 and "--per_device_train_batch_size" in out["run_trainer"]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_micro_batch_sizing_gpu(cuda):
+    mb = micro_batch_for_device("cuda")
+    assert 1 <= mb <= 256 and mb & (mb - 1) == 0  # a power of two up to the measured plateau
