@@ -1,22 +1,35 @@
-"""Butterfly all-reduce over the RCCL (GPU) / gloo (CPU) world communicator.
+"""Butterfly all-reduce over a group communicator (RCCL on GPUs, gloo on CPU).
 
 A matchmade group (any subset of the world) averages a list of flat fp32 tensors:
 
-  1. pack   : wire = compress(x * w_me)                    (one HIP pack kernel per tensor)
-  2. scatter: member j receives part j of everyone's wire  (grouped isend/irecv, all pairs at once —
+  1. pack   : wire = compress(x)                             (one HIP pack kernel per tensor)
+  2. scatter: member j receives part j of everyone's wire    (grouped isend/irecv, all pairs at once —
               on an 8-GPU xGMI mesh every GPU drives its 7 links concurrently instead of the one
               link per hop of a ring)
-  3. reduce : avg_j = sum_k wire_k[j] / sum_k w_k          (HIP reduce kernel, fp32 accumulation)
-  4. gather : every member receives every averaged part    (grouped isend/irecv)
-  5. unpack : x = decompress(avg)  or the delta rule  x += decompress(avg) - snapshot
+  3. reduce : avg_j = sum_k w_k wire_k[j] / sum_k w_k in fp32, and for every sender k the delta
+              d_k[j] = compress(avg_j - decompress(wire_k[j]))     (one HIP reduce_delta kernel)
+  4. return : member j sends d_k[j] back to sender k          (grouped isend/irecv)
+  5. unpack : x += decompress(d)                              (fp32, on the live tensor)
+
+Returning averaged-part *deltas* (hivemind 0.9.x's ``averaged_part - tensor_part`` rule) instead of
+the average keeps each peer's fp32 master tensor: the peer adds (average - what it sent), so the
+compression residual of its own contribution stays in its fp32 tensor and parameter updates below
+half a FLOAT16 ulp survive averaging (replacing the tensor by the decoded average would round the
+master parameters to fp16 every global step).  When all peers hold the same tensor the deltas are
+exactly zero.
 
 Part sizes come from the load-balancing LP; client-mode members own no part (they only send and
-receive), auxiliary members contribute no tensor (weight 0) but reduce a part.  Because only the
-group's ranks post operations, subsets need no extra communicators.
+receive), auxiliary members contribute no tensor (weight 0) but reduce a part.
+
+Timeouts: completion is polled on the host against a deadline (an RCCL ``Work.wait`` only orders
+streams, it never times out); on expiry the round raises ``AllreduceException`` and the caller must
+abort the communicator (``parallel.GroupCommunicators.invalidate``) so the operations still posted
+on it cannot be matched by a later round.
 """
 from __future__ import annotations
 
 import datetime
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -33,7 +46,7 @@ class AllreduceException(RuntimeError):
 
 @dataclass
 class GroupSpec:
-    ranks: List[int]            # process-group rank of each member, in group order
+    ranks: List[int]            # world rank of each member, in group order
     part_sizes: List[int]       # elements of the averaged vector owned by each member
     weights: List[float]        # averaging weight of each member (0 for auxiliary peers)
     contributes: List[bool]     # False for auxiliary peers (they send no tensor)
@@ -44,14 +57,42 @@ class GroupSpec:
         return len(self.ranks)
 
 
+def _run_p2p(p2p, deadline: Optional[float], pg=None):
+    """Post one batch of grouped P2P operations and wait for all of them, at most until ``deadline``
+    (``time.monotonic()`` seconds)."""
+    if not p2p:
+        return
+    works = dist.batch_isend_irecv(p2p)
+    if dist.get_backend(pg) == "gloo":
+        # gloo send/recv works only complete inside wait(), which honours a timeout
+        for w in works:
+            left = None if deadline is None else max(1e-3, deadline - time.monotonic())
+            try:
+                ok = w.wait(timeout=datetime.timedelta(seconds=left)) if left is not None else w.wait()
+            except RuntimeError as e:
+                raise AllreduceException(f"all-reduce failed: {e}") from e
+            if ok is False:
+                raise AllreduceException("all-reduce timed out")
+        return
+    pending = list(works)
+    while pending:
+        pending = [w for w in pending if not w.is_completed()]
+        if not pending:
+            break
+        if deadline is not None and time.monotonic() > deadline:
+            raise AllreduceException("all-reduce timed out")
+        time.sleep(2e-4)
+    for w in works:  # surfaces a backend error; orders the current stream after the transfer
+        w.wait()
+
+
 def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compression: str = "FLOAT16",
-                        pg=None, timeout: Optional[float] = 30.0, snapshots: Optional[Sequence[torch.Tensor]] = None,
-                        sources: Optional[Sequence[torch.Tensor]] = None):
+                        pg=None, timeout: Optional[float] = 30.0, sources: Optional[Sequence[torch.Tensor]] = None):
     """Average ``tensors`` in place across the group described by ``spec``.
 
-    ``sources``: pack these instead of ``tensors`` (same shapes) — used by delayed parameter
-    averaging, which averages a snapshot while the live parameters keep training.
-    ``snapshots``: delta rule on unpack (``t += avg - snapshot``)."""
+    ``sources``: pack these instead of ``tensors`` (same shapes) and add the averaging deltas to
+    ``tensors`` — delayed parameter averaging packs a snapshot and collects the delta in a zeroed
+    buffer while the live parameters keep training.  Returns the group's total weight."""
     ops = torch.ops.dedloc
     wire = WIRE_DTYPES[compression]
     dev = tensors[0].device
@@ -64,33 +105,24 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
         starts.append(starts[-1] + p)
     my_lo, my_hi = starts[me], starts[me + 1]
     P = my_hi - my_lo
-    total_w = float(sum(w for w, c in zip(spec.weights, spec.contributes) if c))
+    contrib_idx = [j for j in range(spec.size) if spec.contributes[j]]
+    total_w = float(sum(spec.weights[j] for j in contrib_idx))
     if total_w <= 0:
         raise AllreduceException("group has no contributing weight")
+    deadline = time.monotonic() + timeout if timeout else None
+    i_contribute = spec.contributes[me]
 
-    # 1. pack (weight-scaled, compressed) into one contiguous wire buffer
-    send = torch.empty(V, dtype=wire, device=dev)
-    if spec.contributes[me]:
+    # 1. pack (compressed, unweighted: the reducer applies the weights in fp32)
+    send = torch.empty(V if i_contribute else 0, dtype=wire, device=dev)
+    if i_contribute:
         o = 0
         for t, n in zip(sources if sources is not None else tensors, sizes):
-            ops.pack(t.reshape(-1), send[o:o + n], float(spec.weights[me]))
+            ops.pack(t.reshape(-1), send[o:o + n], 1.0)
             o += n
-    contrib_idx = [j for j in range(spec.size) if spec.contributes[j]]
-    recv = torch.empty((max(1, len(contrib_idx)), max(P, 1)), dtype=wire, device=dev)
+    nc = len(contrib_idx)
+    recv = torch.empty((max(1, nc), max(P, 1)), dtype=wire, device=dev)
 
-    def _run(p2p):
-        if not p2p:
-            return
-        works = dist.batch_isend_irecv(p2p)
-        td = datetime.timedelta(seconds=timeout) if timeout else None
-        for w in works:
-            if td is not None:
-                if not w.wait(timeout=td):
-                    raise AllreduceException("all-reduce timed out")
-            else:
-                w.wait()
-
-    # 2. reduce-scatter
+    # 2. reduce-scatter: part j of every contributor's wire goes to member j
     p2p = []
     for slot, j in enumerate(contrib_idx):
         if j == me:
@@ -99,35 +131,40 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
             continue
         if P:
             p2p.append(dist.P2POp(dist.irecv, recv[slot, :P], spec.ranks[j], group=pg))
-    if spec.contributes[me]:
+    if i_contribute:
         for j in range(spec.size):
             if j != me and spec.part_sizes[j] > 0:
                 p2p.append(dist.P2POp(dist.isend, send[starts[j]:starts[j + 1]], spec.ranks[j], group=pg))
-    _run(p2p)
+    _run_p2p(p2p, deadline, pg)
 
-    # 3. reduce my part (fp32 accumulation, weighted mean), result in wire dtype
-    gathered = send  # reuse: everyone's averaged parts land here
+    # 3. weighted fp32 average of my part and one delta row per contributor
+    deltas = None
     if P:
-        avg = torch.empty(P, dtype=wire, device=dev)
-        part_view = recv[:, :P].contiguous() if recv.shape[1] != P else recv
-        ops.reduce_parts(part_view, len(contrib_idx), avg, 1.0 / total_w)
-        gathered[my_lo:my_hi].copy_(avg)
+        parts = recv if recv.shape[1] == P else recv[:, :P].contiguous()
+        w = torch.tensor([float(spec.weights[j]) for j in contrib_idx], dtype=torch.float32, device=dev)
+        deltas = torch.empty_like(parts)
+        ops.reduce_delta(parts, w, deltas)
 
-    # 4. all-gather of the averaged parts
+    # 4. every contributor receives its deltas for every part
+    dbuf = torch.empty(V if i_contribute else 0, dtype=wire, device=dev)
     p2p = []
-    for j in range(spec.size):
+    for slot, j in enumerate(contrib_idx):
         if j == me:
+            if P:
+                dbuf[my_lo:my_hi].copy_(deltas[slot])
             continue
         if P:
-            p2p.append(dist.P2POp(dist.isend, gathered[my_lo:my_hi], spec.ranks[j], group=pg))
-        if spec.part_sizes[j] > 0:
-            p2p.append(dist.P2POp(dist.irecv, gathered[starts[j]:starts[j + 1]], spec.ranks[j], group=pg))
-    _run(p2p)
+            p2p.append(dist.P2POp(dist.isend, deltas[slot], spec.ranks[j], group=pg))
+    if i_contribute:
+        for j in range(spec.size):
+            if j != me and spec.part_sizes[j] > 0:
+                p2p.append(dist.P2POp(dist.irecv, dbuf[starts[j]:starts[j + 1]], spec.ranks[j], group=pg))
+    _run_p2p(p2p, deadline, pg)
 
-    # 5. unpack (auxiliary peers keep their buffers untouched unless they hold tensors)
-    o = 0
-    for k, (t, n) in enumerate(zip(tensors, sizes)):
-        snap = None if snapshots is None else snapshots[k].reshape(-1)
-        ops.unpack(gathered[o:o + n], t.reshape(-1), snap)
-        o += n
+    # 5. unpack: x += delta (auxiliary peers hold no averaged tensor)
+    if i_contribute:
+        o = 0
+        for t, n in zip(tensors, sizes):
+            ops.unpack(dbuf[o:o + n], t.reshape(-1), None, True)
+            o += n
     return total_w

@@ -4,8 +4,12 @@ In-process design (no helper processes, no host staging of the averaged tensors)
   * matchmaking through the control-plane DHT (``DHT.join_group``): a group closes at
     ``target_group_size``, when every live peer of the collaboration has joined, or when the
     ``averaging_expiration`` window of its first member ends;
-  * the data plane is the butterfly all-reduce over the world RCCL communicator
-    (``allreduce.butterfly_allreduce``) with LP-balanced parts and FLOAT16/BFLOAT16 wire compression;
+  * the data plane is the butterfly all-reduce (``allreduce.butterfly_allreduce``) with LP-balanced
+    parts and FLOAT16/BFLOAT16 wire compression, on a group communicator keyed by (member set,
+    data-plane epoch) (``parallel.GroupCommunicators``).  Every member announces its epoch in its
+    matchmaking info and the group runs on epoch max(announced), so all members pick the same
+    communicator; a failed round aborts that communicator and the member moves to epoch + 1, which
+    forces a fresh communicator the next time it averages with any of those peers;
   * state sharing: every peer with ``allow_state_sharing`` runs a small TCP state server
     (``listen_on``) and advertises it under ``{prefix}_state_sharing``; ``load_state_from_peers``
     downloads (metadata, tensors) from the freshest donor.
@@ -130,6 +134,12 @@ class DecentralizedAverager:
         self.allow_state_sharing = allow_state_sharing and not auxiliary
         self.metadata_expiration = metadata_expiration
         self.pg = pg
+        self.epoch = 0
+        self.comms = None
+        if pg is None:
+            from ..parallel import GroupCommunicators
+
+            self.comms = GroupCommunicators(timeout_s=max(60.0, 2 * averaging_timeout))
         self.rank = rank if rank is not None else (dist.get_rank() if dist.is_available() and dist.is_initialized() else 0)
         self.lock_averaged_tensors = threading.RLock()
         self.last_group: Optional[Dict] = None
@@ -153,7 +163,8 @@ class DecentralizedAverager:
             return None
         weight = 0.0 if self.auxiliary else float(weight)
         bw = 0.0 if self.client_mode else (self.throughput if self.throughput is not None else 1.0)
-        info = {"rank": self.rank, "bandwidth": bw, "weight": weight, "aux": self.auxiliary, "gather": gather or {}}
+        info = {"rank": self.rank, "bandwidth": bw, "weight": weight, "aux": self.auxiliary, "gather": gather or {},
+                "epoch": self.epoch}
         window = self.averaging_expiration
         t_join = time.perf_counter()
         try:
@@ -176,13 +187,21 @@ class DecentralizedAverager:
                          my_index=my_index)
         if sum(w for w, c in zip(spec.weights, spec.contributes) if c) <= 0:
             return None
+        epoch = max(int(i.get("epoch", 0)) for i in infos)
+        self.epoch = max(self.epoch, epoch)
         t0 = time.perf_counter()
         try:
+            pg = self.pg if self.pg is not None else self.comms.get(spec.ranks, epoch)
             with self.lock_averaged_tensors:
-                butterfly_allreduce(tensors, spec, self.compression, pg=self.pg,
+                butterfly_allreduce(tensors, spec, self.compression, pg=pg,
                                     timeout=timeout or self.averaging_timeout, sources=sources)
         except (AllreduceException, RuntimeError) as e:
-            logger.warning(f"all-reduce failed ({e}); skipping this round")
+            # the communicator may still hold posted operations: abort it and move to a new epoch
+            # so no later round can be matched against them
+            logger.warning(f"all-reduce failed ({e}); skipping this round (data-plane epoch {epoch} -> {epoch + 1})")
+            if self.comms is not None:
+                self.comms.invalidate(spec.ranks, epoch)
+            self.epoch = max(self.epoch, epoch + 1)
             return None
         if self.emulate_transfer_delay and bw > 0:  # emulate the volunteer's link (AWS_runner wondershaper caps)
             from ..emulation.heterogeneity import emulated_transfer_seconds
@@ -237,3 +256,5 @@ class DecentralizedAverager:
     def shutdown(self):
         if self.state_server is not None:
             self.state_server.shutdown()
+        if self.comms is not None:
+            self.comms.close()

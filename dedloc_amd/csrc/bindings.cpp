@@ -216,15 +216,29 @@ void reduce_parts(const at::Tensor& parts, int64_t nparts, at::Tensor out, doubl
         "reduce_parts");
 }
 
-void unpack(const at::Tensor& src, at::Tensor dst, const c10::optional<at::Tensor>& snap) {
+void reduce_delta(const at::Tensor& parts, const at::Tensor& weights, at::Tensor deltas) {
+  TORCH_CHECK(parts.is_cuda() && parts.is_contiguous() && parts.dim() == 2, "parts must be a contiguous [n, P] GPU tensor");
+  TORCH_CHECK(deltas.is_cuda() && deltas.is_contiguous() && deltas.sizes() == parts.sizes() &&
+                  deltas.scalar_type() == parts.scalar_type(),
+              "deltas must match parts");
+  expect(weights, at::kFloat, "weights");
+  const int64_t nparts = parts.size(0), n = parts.size(1);
+  TORCH_CHECK(weights.numel() == nparts, "one weight per part");
+  check(dl_reduce_delta(parts.data_ptr(), deltas.data_ptr(), dtype_code(parts), n, (int)nparts, f32(weights), n,
+                        cur_stream(parts)),
+        "reduce_delta");
+}
+
+void unpack(const at::Tensor& src, at::Tensor dst, const c10::optional<at::Tensor>& snap, bool add) {
   expect(dst, at::kFloat, "dst");
   TORCH_CHECK(src.is_cuda() && src.is_contiguous() && src.numel() == dst.numel(), "unpack src mismatch");
   const float* sp = nullptr;
   if (snap.has_value()) {
+    TORCH_CHECK(!add, "unpack: snap and add are exclusive");
     expect(*snap, at::kFloat, "snap");
     sp = f32(*snap);
   }
-  check(dl_unpack(src.data_ptr(), dtype_code(src), f32(dst), sp, dst.numel(), cur_stream(dst)), "unpack");
+  check(dl_unpack(src.data_ptr(), dtype_code(src), f32(dst), sp, add ? 1 : 0, dst.numel(), cur_stream(dst)), "unpack");
 }
 
 // ------------------------------------------------------------------ embeddings / loss
@@ -887,6 +901,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("pack", &pack);
   m.impl("reduce_parts", &reduce_parts);
   m.impl("unpack", &unpack);
+  m.impl("reduce_delta", &reduce_delta);
   m.impl("embed_ln_fwd", &embed_ln_fwd);
   m.impl("embed_bwd", &embed_bwd);
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);

@@ -43,7 +43,9 @@ int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st
 int dl_pack(const float* src, void* dst, int dst_dt, size_t n, float weight, hipStream_t st);
 int dl_reduce_parts(const void* parts, int part_dt, size_t part_stride, int nparts, void* out, int out_dt, size_t n,
                     float inv_total, hipStream_t st);
-int dl_unpack(const void* src, int src_dt, float* dst, const float* snap, size_t n, hipStream_t st);
+int dl_unpack(const void* src, int src_dt, float* dst, const float* snap, int add, size_t n, hipStream_t st);
+int dl_reduce_delta(const void* parts, void* deltas, int dt, size_t part_stride, int nparts, const float* weights,
+                    size_t n, hipStream_t st);
 
 // embedding.hip
 int dl_embed_ln_fwd(const long* ids, const long* tt, const float* wemb, const float* pemb, const float* temb,

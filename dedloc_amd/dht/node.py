@@ -387,7 +387,7 @@ class DHT:
         """Store ``value`` (msgpack-serialisable) under key[/subkey] until ``expiration_time``."""
         kb, sb = _b(key), (None if subkey is None else _b(subkey))
         vb = msgpack.packb(value, use_bin_type=True)
-        vb = self.validator.sign_value(kb, sb, vb)
+        vb = self.validator.sign_value(kb, sb, vb, expiration_time)
         if not self.validator.validate(kb, sb, vb, expiration_time):
             fut: cf.Future = cf.Future()
             fut.set_result(False)

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import base64
 import re
+import struct
 import typing
 from typing import Any, Dict, Iterable, List, Optional
 
@@ -86,14 +87,18 @@ class RSASignatureValidator(RecordValidatorBase):
         return None
 
     @staticmethod
-    def _payload(key, subkey, value):
-        return b"|".join((key, subkey or b"", value))
+    def _payload(key, subkey, value, expiration):
+        # the expiration is signed in its exact wire form (the float64 the server stores), so a
+        # replayed record cannot be given a later expiration to pin a stale owner's state
+        return b"|".join((key, subkey or b"", value, struct.pack("<d", float(expiration))))
 
     def sign_value(self, key, subkey, value, expiration=None):
         owner = self._owner(key, subkey)
         if owner is None or owner != self._pub:
             return value
-        sig = self._key.sign(self._payload(key, subkey, value))
+        if expiration is None:
+            raise ValueError("signing an owned record needs its expiration time")
+        sig = self._key.sign(self._payload(key, subkey, value, expiration))
         return value + b"[signature:" + base64.b64encode(sig) + b"]"
 
     def strip_value(self, key, subkey, value):
@@ -107,7 +112,7 @@ class RSASignatureValidator(RecordValidatorBase):
         if sig is None:
             return False
         try:
-            return RSAPublicKey.from_bytes(owner).verify(self._payload(key, subkey, body), sig)
+            return RSAPublicKey.from_bytes(owner).verify(self._payload(key, subkey, body, expiration), sig)
         except Exception:  # noqa: BLE001
             return False
 

@@ -32,7 +32,8 @@ _SCHEMAS = [
     "axpby(Tensor(a!) y, Tensor x, float a, float b, Tensor? flag=None) -> ()",
     "pack(Tensor src, Tensor(a!) dst, float weight) -> ()",
     "reduce_parts(Tensor parts, int nparts, Tensor(a!) out, float inv_total) -> ()",
-    "unpack(Tensor src, Tensor(a!) dst, Tensor? snap) -> ()",
+    "unpack(Tensor src, Tensor(a!) dst, Tensor? snap, bool add=False) -> ()",
+    "reduce_delta(Tensor parts, Tensor weights, Tensor(a!) deltas) -> ()",
     "embed_ln_fwd(Tensor ids, Tensor? tt, Tensor wemb, Tensor pemb, Tensor temb, Tensor gamma, Tensor beta, int S, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
     "embed_bwd(Tensor ds, Tensor ids, Tensor? tt, Tensor(a!) dwemb, Tensor(b!) dpemb, Tensor(c!) dtemb, int S) -> ()",
     "xent_fwd_bwd(Tensor logits, Tensor labels, bool inplace, int ignore_index) -> (Tensor, Tensor)",
@@ -271,9 +272,23 @@ def _reduce_cpu(parts, nparts, out, inv_total):
     out.copy_(s.to(out.dtype))
 
 
+@_impl("reduce_delta")
+def _reduce_delta_cpu(parts, weights, deltas):
+    x = parts.float()
+    w = weights.float()
+    tot = float(w.sum())
+    avg = x[0] + (w[1:, None] * (x[1:] - x[0])).sum(0) * (1.0 / tot if tot > 0 else 0.0)
+    d = avg[None, :] - x
+    if deltas.dtype == torch.float16:
+        d = d.clamp(-65504.0, 65504.0)
+    deltas.copy_(d.to(deltas.dtype))
+
+
 @_impl("unpack")
-def _unpack_cpu(src, dst, snap):
-    if snap is None:
+def _unpack_cpu(src, dst, snap, add=False):
+    if add:
+        dst.add_(src.float())
+    elif snap is None:
         dst.copy_(src.float())
     else:
         dst.add_(src.float() - snap)

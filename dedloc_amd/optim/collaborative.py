@@ -120,7 +120,7 @@ class CollaborativeOptimizer:
         self._param_done_event = None
         if delay_param_averaging:
             self._param_snapshot = torch.empty_like(self.flat.fp32)
-            self._param_avg = torch.empty_like(self.flat.fp32)
+            self._param_delta = torch.empty_like(self.flat.fp32)
             self._side_stream = torch.cuda.Stream(self.flat.fp32.device) if self.flat.fp32.is_cuda else None
 
         self.lock_collaboration_state = threading.Lock()
@@ -336,6 +336,7 @@ class CollaborativeOptimizer:
     # ------------------------------------------------------------------ delayed parameter averaging
     def _start_param_round(self, weight: float, expected_group_size: int):
         self._param_snapshot.copy_(self.flat.fp32)
+        self._param_delta.zero_()
         ready = None
         if self._side_stream is not None:
             ready = torch.cuda.Event()
@@ -348,12 +349,12 @@ class CollaborativeOptimizer:
                     with torch.cuda.stream(self._side_stream):
                         self._side_stream.wait_event(ready)
                         res = self.averager.step(weight=weight, timeout=self.averaging_timeout,
-                                                 expected_group_size=expected_group_size, tensors=[self._param_avg],
+                                                 expected_group_size=expected_group_size, tensors=[self._param_delta],
                                                  sources=[self._param_snapshot], key_suffix="_params")
                         self._param_done_event.record(self._side_stream)
                 else:
                     res = self.averager.step(weight=weight, timeout=self.averaging_timeout,
-                                             expected_group_size=expected_group_size, tensors=[self._param_avg],
+                                             expected_group_size=expected_group_size, tensors=[self._param_delta],
                                              sources=[self._param_snapshot], key_suffix="_params")
             except Exception as e:  # noqa: BLE001
                 logger.warning(f"delayed parameter averaging failed: {e}")
@@ -377,8 +378,7 @@ class CollaborativeOptimizer:
             return
         ops = torch.ops.dedloc
         with self.lock_step:
-            ops.axpby(self.flat.fp32, self._param_avg, 1.0, 1.0)       # p += avg(snapshot)
-            ops.axpby(self.flat.fp32, self._param_snapshot, 1.0, -1.0)  # p -= snapshot
+            ops.axpby(self.flat.fp32, self._param_delta, 1.0, 1.0)  # p += avg(snapshot) - snapshot
             self.flat.refresh_bf16()
         self.stats["param_rounds"] = self.stats.get("param_rounds", 0) + 1
 

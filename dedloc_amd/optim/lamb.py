@@ -60,7 +60,9 @@ class FusedLamb(_FlatOptimizer):
         self.step_count += 1
         t = self.step_count
         bc = math.sqrt(1 - b2 ** t) / (1 - b1 ** t) if grp["debias"] else 1.0
-        clamp = 1e30 if grp["adam"] else grp["clamp_value"]
+        # adam mode (torch_optimizer.Lamb(adam=True)): trust ratio 1.  The kernel's trust is
+        # min(||p||, clamp) / ||u|| with "1 when the clamped weight norm is 0", so clamp 0 is exactly that
+        clamp = 0.0 if grp["adam"] else grp["clamp_value"]
         ct, cs, cl, twd = self.tables
         torch.ops.dedloc.lamb_step(self.flat.fp32, g, self.exp_avg, self.exp_avg_sq, ct, cs, cl, twd, self.norms,
                                    b1, b2, grp["eps"], grp["lr"] * bc, clamp, grad_scale)
@@ -69,29 +71,52 @@ class FusedLamb(_FlatOptimizer):
     def state_tensors(self) -> List[torch.Tensor]:
         return [self.exp_avg, self.exp_avg_sq]
 
+    def _groups(self) -> List[List[int]]:
+        """Flat indices of the reference's parameter groups, in its order: decayed first, then the
+        no-decay group (albert/run_trainer.py:74-84); inside a group, model (flat) order."""
+        return [[i for i, n in enumerate(self.flat.names) if self.weight_decay_of[n] == wd_val]
+                for wd_val in sorted(set(self.weight_decay_of.values()), reverse=True)]
+
     def state_dict(self) -> Dict:
         m, v = self._per_param(self.exp_avg), self._per_param(self.exp_avg_sq)
         state = {i: {"step": self.step_count, "exp_avg": m[i], "exp_avg_sq": v[i]} for i in m}
         groups = []
-        for wd_val in sorted(set(self.weight_decay_of.values()), reverse=True):
+        for idx in self._groups():
             g = {k: v for k, v in self.param_groups[0].items() if k != "params"}
-            g["weight_decay"] = wd_val
-            g["params"] = [i for i, n in enumerate(self.flat.names) if self.weight_decay_of[n] == wd_val]
+            g["weight_decay"] = self.weight_decay_of[self.flat.names[idx[0]]]
+            g["params"] = idx
             groups.append(g)
         return {"state": state, "param_groups": groups}
 
     @torch.no_grad()
     def load_state_dict(self, sd: Dict):
+        """Accepts this class's own state dicts and torch-format ones (torch.optim / torch_optimizer /
+        HF Trainer ``optimizer.pt``), whose ids number the parameters group by group: like
+        ``torch.optim.Optimizer.load_state_dict`` the saved ``param_groups[k]['params']`` ids are
+        zipped with this optimizer's k-th group."""
         st = sd.get("state", {})
-        for i, n in enumerate(self.flat.names):
-            s = st.get(i) or st.get(str(i))
-            if not s:
+        saved_groups = sd.get("param_groups") or []
+        ours = self._groups()
+        if saved_groups and [len(g["params"]) for g in saved_groups] == [len(g) for g in ours]:
+            id_map = {int(sid): fi for g, idx in zip(saved_groups, ours) for sid, fi in zip(g["params"], idx)}
+        elif saved_groups:
+            raise ValueError(f"optimizer state has groups of sizes {[len(g['params']) for g in saved_groups]}, "
+                             f"this optimizer {[len(g) for g in ours]}")
+        else:
+            id_map = {i: i for i in range(len(self.flat.names))}
+        for sid, s in st.items():
+            fi = id_map.get(int(sid))
+            if fi is None or not s:
                 continue
-            self.flat.view(self.exp_avg, n).copy_(s["exp_avg"])
-            self.flat.view(self.exp_avg_sq, n).copy_(s["exp_avg_sq"])
+            n = self.flat.names[fi]
+            dst_m, dst_v = self.flat.view(self.exp_avg, n), self.flat.view(self.exp_avg_sq, n)
+            if tuple(s["exp_avg"].shape) != tuple(dst_m.shape):
+                raise ValueError(f"state {sid} has shape {tuple(s['exp_avg'].shape)}, parameter {n} {tuple(dst_m.shape)}")
+            dst_m.copy_(s["exp_avg"])
+            dst_v.copy_(s["exp_avg_sq"])
             self.step_count = int(s.get("step", self.step_count))
-        if sd.get("param_groups"):
-            self.param_groups[0]["lr"] = sd["param_groups"][0].get("lr", self.param_groups[0]["lr"])
+        if saved_groups:
+            self.param_groups[0]["lr"] = saved_groups[0].get("lr", self.param_groups[0]["lr"])
 
 
 class FusedLarcSGD(_FlatOptimizer):

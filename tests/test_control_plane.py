@@ -111,15 +111,44 @@ def test_rsa_sign_verify_roundtrip():
 def test_signature_validator_owner_only():
     owner = RSASignatureValidator(RSAPrivateKey(bits=1024))
     intruder = RSASignatureValidator(RSAPrivateKey(bits=1024))
-    key, sub, val = b"exp_metrics", owner.local_public_key, b"payload"
-    signed = owner.sign_value(key, sub, val)
-    assert owner.validate(key, sub, signed, 0) and intruder.validate(key, sub, signed, 0)
-    forged = intruder.sign_value(key, sub, val)  # intruder cannot sign for someone else's subkey
-    assert forged == val and not owner.validate(key, sub, forged, 0)
+    key, sub, val, exp = b"exp_metrics", owner.local_public_key, b"payload", 1234.5
+    signed = owner.sign_value(key, sub, val, exp)
+    assert owner.validate(key, sub, signed, exp) and intruder.validate(key, sub, signed, exp)
+    forged = intruder.sign_value(key, sub, val, exp)  # intruder cannot sign for someone else's subkey
+    assert forged == val and not owner.validate(key, sub, forged, exp)
     tampered = signed.replace(b"payload", b"paylaod")
-    assert not owner.validate(key, sub, tampered, 0)
+    assert not owner.validate(key, sub, tampered, exp)
     assert owner.strip_value(key, sub, signed) == val
     assert owner.validate(b"public_key", None, b"anything", 0)  # unowned records are not signature-checked
+    # the signature covers the expiration: a replayed record with a later expiration is rejected
+    assert not owner.validate(key, sub, signed, exp + 1e6)
+    assert not owner.validate(key, sub, signed, exp + 1e-9 * exp)
+
+
+def test_replayed_record_with_extended_expiration_is_rejected_by_dht():
+    """replaying an owner's signed record with a far-future expiration must not pin it."""
+    from dedloc_amd.dht import DHT, get_dht_time
+    from dedloc_amd.dht.node import _b
+
+    owner_v = RSASignatureValidator(RSAPrivateKey(bits=1024))
+    root = DHT(listen_on="127.0.0.1:*", record_validators=[owner_v])
+    try:
+        sub = owner_v.local_public_key
+        exp = get_dht_time() + 30
+        assert root.store("exp_progress", {"step": 1}, exp, subkey=sub)
+        got = root.get("exp_progress", latest=True)
+        assert got is not None and got.value[sub].value == {"step": 1}
+        # an attacker copies the signed bytes and re-stores them directly with a later expiration
+        kb, sb = _b("exp_progress"), _b(sub)
+        import msgpack
+
+        body = owner_v.sign_value(kb, sb, msgpack.packb({"step": 0}, use_bin_type=True), exp - 10)
+        root._raw_store_all(kb, sb, body, get_dht_time() + 1e6)  # replay of an older record, expiration bumped
+        got = root.get("exp_progress", latest=True)
+        # the replay wins the latest-expiration merge on the server but fails validation on read
+        assert got is None or sub not in got.value or got.value[sub].value != {"step": 0}
+    finally:
+        root.shutdown()
 
 
 def test_schema_validator_metrics_records():

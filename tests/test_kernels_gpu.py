@@ -312,6 +312,34 @@ def test_pack_reduce_unpack(cuda, wire):
     assert rel(loc, ref + 1.0) < tol * 3
 
 
+@pytest.mark.parametrize("wire", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("k", [3, 20])  # 20 > the kernel's 16 register slots
+def test_reduce_delta_and_unpack_add(cuda, wire, k):
+    """The averaging path: per-sender deltas of the fp32 weighted mean, added to the fp32 master."""
+    n = 10007
+    torch.manual_seed(0)
+    masters = [torch.randn(n, device=cuda) + 4.0 for _ in range(k)]
+    ws = torch.rand(k, device=cuda) + 0.25
+    parts = torch.empty(k, n, dtype=wire, device=cuda)
+    for i in range(k):
+        OPS.pack(masters[i], parts[i], 1.0)
+    deltas = torch.empty_like(parts)
+    OPS.reduce_delta(parts, ws, deltas)
+    pf = parts.float()
+    avg = (pf * ws[:, None]).sum(0) / ws.sum()
+    ref = avg[None, :] - pf  # fp32 reference of the same op
+    tol = 1e-6 if wire == torch.float32 else (2e-3 if wire == torch.float16 else 1e-2)
+    assert (deltas.float() - ref).abs().max().item() <= tol * ref.abs().max().item() + 1e-6
+    for i in range(k):
+        m = masters[i].clone()
+        OPS.unpack(deltas[i], m, None, True)
+        torch.testing.assert_close(m, masters[i] + deltas[i].float())
+    # identical contributions: deltas are exactly zero, the fp32 master is untouched
+    same = parts[0:1].expand(k, n).contiguous()
+    OPS.reduce_delta(same, ws, deltas)
+    assert deltas.float().abs().max().item() == 0.0
+
+
 def test_gemm_paths(cuda):
     a = torch.randn(300, 128, device=cuda).bfloat16()
     w = torch.randn(200, 128, device=cuda).bfloat16()

@@ -1,0 +1,83 @@
+"""FusedLamb semantics on CPU: torch_optimizer's adam mode and torch-format optimizer state dicts."""
+import math
+
+import torch
+
+import dedloc_amd.ops  # noqa: F401
+from dedloc_amd.optim.lamb import FusedLamb
+from dedloc_amd.utils.flat import FlatParams
+
+# ALBERT-like naming: no-decay parameters interleave with decayed ones in model order
+NAMES = [("emb.weight", (7, 5)), ("emb.LayerNorm.weight", (5,)), ("dense.weight", (3, 5)), ("dense.bias", (3,)),
+         ("out.weight", (4, 3))]
+NO_DECAY = {"emb.LayerNorm.weight", "dense.bias"}
+
+
+def _params(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return [(n, torch.nn.Parameter(torch.randn(*s, generator=g))) for n, s in NAMES]
+
+
+def test_lamb_adam_mode_has_unit_trust_ratio():
+    named = _params()
+    ref = {n: p.detach().clone() for n, p in named}
+    flat = FlatParams(named, with_bf16=False)
+    lr, wd, eps, (b1, b2) = 1e-2, 0.01, 1e-6, (0.9, 0.999)
+    opt = FusedLamb(flat, lr=lr, weight_decay=wd, eps=eps, betas=(b1, b2), clamp_value=10.0, adam=True,
+                    no_decay=NO_DECAY)
+    m = {n: torch.zeros_like(p) for n, p in ref.items()}
+    v = {n: torch.zeros_like(p) for n, p in ref.items()}
+    g = torch.Generator().manual_seed(1)
+    for t in range(1, 4):
+        grads = {n: torch.randn(p.shape, generator=g) for n, p in ref.items()}
+        for n in flat.names:
+            flat.g(n).copy_(grads[n])
+        opt.step()
+        bc = math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+        for n, p in ref.items():  # torch_optimizer.Lamb(adam=True, debias=True): trust_ratio = 1
+            m[n].mul_(b1).add_(grads[n], alpha=1 - b1)
+            v[n].mul_(b2).addcmul_(grads[n], grads[n], value=1 - b2)
+            u = m[n] / (v[n].sqrt() + eps) + (0.0 if n in NO_DECAY else wd) * p
+            p.add_(u, alpha=-lr * bc)
+    for n, p in ref.items():
+        torch.testing.assert_close(flat.p(n), p, rtol=1e-5, atol=1e-6)
+
+
+def test_lamb_loads_torch_format_state_dict():
+    # a torch optimizer with the reference's two groups (decayed first, then no-decay) numbers its
+    # state group by group: ids 0..2 decayed, 3..4 no-decay — not the model order
+    named_t = _params()
+    decay = [p for n, p in named_t if n not in NO_DECAY]
+    no_decay = [p for n, p in named_t if n in NO_DECAY]
+    topt = torch.optim.Adam([{"params": decay, "weight_decay": 0.01}, {"params": no_decay, "weight_decay": 0.0}],
+                            lr=3e-3)
+    for _, p in named_t:
+        p.grad = torch.randn_like(p)
+    topt.step()
+    sd = topt.state_dict()
+    assert sd["param_groups"][1]["params"] == [3, 4]
+
+    flat = FlatParams(_params(), with_bf16=False)
+    opt = FusedLamb(flat, lr=1e-3, weight_decay=0.01, no_decay=NO_DECAY)
+    opt.load_state_dict(sd)
+    by_name = {n: topt.state[p] for n, p in named_t}
+    for n in flat.names:
+        torch.testing.assert_close(flat.view(opt.exp_avg, n), by_name[n]["exp_avg"])
+        torch.testing.assert_close(flat.view(opt.exp_avg_sq, n), by_name[n]["exp_avg_sq"])
+    assert opt.step_count == 1 and opt.lr == 3e-3
+
+    # ... and our state dict loads back into a torch optimizer with the same groups
+    ours = opt.state_dict()
+    named_2 = _params()
+    topt2 = torch.optim.Adam([{"params": [p for n, p in named_2 if n not in NO_DECAY], "weight_decay": 0.01},
+                              {"params": [p for n, p in named_2 if n in NO_DECAY], "weight_decay": 0.0}], lr=1.0)
+    ours["state"] = {k: dict(s, step=torch.tensor(float(s["step"]))) for k, s in ours["state"].items()}
+    topt2.load_state_dict(ours)
+    for (n, p2) in named_2:
+        torch.testing.assert_close(topt2.state[p2]["exp_avg"], by_name[n]["exp_avg"])
+
+    # our own round trip
+    flat3 = FlatParams(_params(), with_bf16=False)
+    opt3 = FusedLamb(flat3, lr=1e-3, weight_decay=0.01, no_decay=NO_DECAY)
+    opt3.load_state_dict(opt.state_dict())
+    assert torch.equal(opt3.exp_avg, opt.exp_avg) and torch.equal(opt3.exp_avg_sq, opt.exp_avg_sq)
