@@ -1,7 +1,18 @@
-"""ALBERT-large layer GEMMs: dedloc MFMA kernel vs hipBLASLt (same random bf16 data, one process,
-interleaved rounds — cdna_hip_programming.md §5.4 rules 24/25)."""
+"""ALBERT-large layer GEMMs: the hand-written MFMA kernels vs hipBLASLt (same random bf16 data, one
+process, interleaved rounds — cdna_hip_programming.md §5.4 rules 24/25).
+
+Variants per GEMM (the dispatch policy is read per call, so one process times them all):
+  gemm8 : csrc/kernels/gemm8.hip (LDS-DMA 8-phase pipeline)         DEDLOC_GEMM=mfma
+  gemm1 : csrc/kernels/gemm.hip (register-staged)                   DEDLOC_GEMM=mfma1
+  lt    : direct hipBLASLt (autotuned) + separate epilogue kernels  DEDLOC_GEMM=lib
+Fused epilogues are timed as the op the model calls (gemm_gelu: bias + GELU; gemm_dgelu: GELU'
++ bias-gradient column sums), so "lt" includes its separate elementwise kernel.
+
+usage: T=131072 python bench/gemm_bench.py [--check]
+"""
 import json
 import os
+import sys
 import time
 
 import torch
@@ -9,9 +20,10 @@ import torch
 import dedloc_amd.ops  # noqa: F401
 
 O = torch.ops.dedloc
+VARIANTS = {"gemm8": "mfma", "gemm1": "mfma1", "lt": "lib"}
 
 
-def timeit(fn, iters=20):
+def timeit(fn, iters=10):
     fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -21,33 +33,70 @@ def timeit(fn, iters=20):
     return (time.perf_counter() - t0) / iters
 
 
+def with_policy(pol, fn):
+    def run():
+        os.environ["DEDLOC_GEMM"] = pol
+        return fn()
+    return run
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
 def main():
     T = int(os.environ.get("T", 32768))
+    check = "--check" in sys.argv
+    variants = os.environ.get("VARIANTS", "gemm8,lt").split(",")
     dev = torch.device("cuda")
     H, I = 1024, 4096
+    torch.manual_seed(0)
     res = []
-    shapes = [("qkv_fwd", H, 3 * H), ("o_fwd", H, H), ("ffn1_fwd", H, I), ("ffn2_fwd", I, H)]
+    shapes = [("qkv", H, 3 * H), ("o", H, H), ("ffn1", H, I), ("ffn2", I, H)]
     for name, K, N in shapes:
-        x = torch.randn(T, K, device=dev).bfloat16()
-        w = torch.randn(N, K, device=dev).bfloat16()
-        dy = torch.randn(T, N, device=dev).bfloat16()
+        x = (torch.rand(T, K, device=dev) * 2 - 1).bfloat16()
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.05).bfloat16()
+        b = torch.randn(N, device=dev)
+        dy = (torch.rand(T, N, device=dev) * 2 - 1).bfloat16()
         g = torch.zeros(N, K, device=dev)
+        db = torch.zeros(N, device=dev)
         fl = 2.0 * T * N * K
-        for kind, fn_ours, fn_lib in [
-            ("fwd", lambda: O.gemm(x, w, None, None, False, True, 0), lambda: torch.mm(x, w.t())),
-            ("dgrad", lambda: O.gemm(dy, w, None, None, False, False, 0), lambda: torch.mm(dy, w)),
-            ("wgrad", lambda: O.gemm_acc_f32(dy, x, g, True, False),
-             lambda: torch.ops.aten.addmm.dtype_out(g, dy.t(), x, torch.float32, out=g)),
-        ]:
-            ts = {"ours": [], "lib": []}
+        kinds = [("fwd", lambda: O.gemm(x, w, b, None, False, True, 0)),
+                 ("dgrad", lambda: O.gemm(dy, w, None, None, False, False, 0)),
+                 ("wgrad", lambda: O.gemm_acc_f32(dy, x, g, True, False))]
+        if name == "ffn1":
+            kinds.append(("fwd_gelu", lambda: O.gemm_gelu(x, w, b)))
+        if name == "ffn2":
+            f = (torch.randn(T, K, device=dev)).bfloat16()
+            kinds.append(("dgrad_dgelu", lambda: O.gemm_dgelu(dy, w, f, db)))
+        for kind, fn in kinds:
+            if check:
+                outs = {}
+                for v in variants:
+                    os.environ["DEDLOC_GEMM"] = VARIANTS[v]
+                    g.zero_()
+                    db.zero_()
+                    o = fn()
+                    o = g.clone() if kind == "wgrad" else (o[1] if isinstance(o, (tuple, list)) else o).clone()
+                    outs[v] = (o, db.clone())
+                base = outs[variants[-1]]
+                for v in variants[:-1]:
+                    print(json.dumps({"check": f"{name}:{kind}", "variant": v, "rel_vs_" + variants[-1]: rel(outs[v][0], base[0]),
+                                      "dbias_rel": rel(outs[v][1], base[1]) if kind == "dgrad_dgelu" else None}),
+                          flush=True)
+            ts = {v: [] for v in variants}
             for _ in range(3):
-                ts["ours"].append(timeit(fn_ours))
-                ts["lib"].append(timeit(fn_lib))
-            t_o, t_l = min(ts["ours"]), min(ts["lib"])
-            res.append({"gemm": f"{name}:{kind}", "M": T, "N": N, "K": K, "ours_us": round(t_o * 1e6, 1),
-                        "lib_us": round(t_l * 1e6, 1), "ours_tflops": round(fl / t_o / 1e12, 1),
-                        "lib_tflops": round(fl / t_l / 1e12, 1)})
-            print(json.dumps(res[-1]), flush=True)
+                for v in variants:
+                    ts[v].append(timeit(with_policy(VARIANTS[v], fn)))
+            row = {"gemm": f"{name}:{kind}", "M": T, "N": N, "K": K}
+            for v in variants:
+                t = min(ts[v])
+                row[f"{v}_us"] = round(t * 1e6, 1)
+                row[f"{v}_tflops"] = round(fl / t / 1e12, 1)
+            res.append(row)
+            print(json.dumps(row), flush=True)
+    os.environ.pop("DEDLOC_GEMM", None)
 
 
 if __name__ == "__main__":

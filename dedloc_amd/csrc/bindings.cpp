@@ -8,6 +8,8 @@
 #include <torch/library.h>
 #include <c10/hip/HIPStream.h>
 
+#include <cstring>
+
 #include "dl_kernels.h"
 #include "dl_lt.h"
 
@@ -343,12 +345,15 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
 //     1.1-1.5 PF/s on these shapes vs ~0.6-0.95 for gemm.hip's register-staged loop).
 // DEDLOC_GEMM=mfma forces gemm.hip everywhere (correctness tests), =lib forces the library;
 // DEDLOC_LT=0 routes the library path through ATen instead of the direct hipBLASLt calls.
-int gemm_policy() {  // 0 auto, 1 mfma, 2 lib  (read per call: tests flip it at run time)
+int gemm_policy() {  // 0 auto, 1 mfma, 2 lib, 3 mfma with the register-staged gemm.hip only
   const char* e = std::getenv("DEDLOC_GEMM");
-  return !e ? 0 : (e[0] == 'm' ? 1 : (e[0] == 'l' ? 2 : 0));
+  if (!e) return 0;
+  if (!std::strcmp(e, "mfma1")) return 3;
+  return e[0] == 'm' ? 1 : (e[0] == 'l' ? 2 : 0);
 }
+bool use_gemm8() { return gemm_policy() != 3; }
 bool use_mfma_gemm() { return gemm_policy() != 2; }
-bool force_mfma_gemm() { return gemm_policy() == 1; }
+bool force_mfma_gemm() { const int g = gemm_policy(); return g == 1 || g == 3; }
 bool use_lt() {
   const char* e = std::getenv("DEDLOC_LT");
   return !(e && e[0] == '0');
@@ -400,6 +405,38 @@ inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias) {
   return bias->scalar_type() == at::kFloat ? bias->contiguous() : bias->to(at::kFloat).contiguous();
 }
 
+// The hand-written kernels: gemm8.hip (LDS-DMA 8-phase pipeline) where its contract holds,
+// gemm.hip (register-staged) otherwise.  Returns 0 on success.
+int own_gemm(int akout, int bkout, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
+             bf16_t* C, long ldc, float* Cf, long ldcf, const float* bias, const bf16_t* R, long ldr, bf16_t* H,
+             long ldh, float* dbias, hipStream_t st) {
+  if (use_gemm8() && dl_gemm8(akout, bkout, epi, A, lda, B, ldb, M, N, K, C, ldc, Cf, ldcf, 0, epi == 3 ? 1 : 0,
+                              bias, R, ldr, H, ldh, dbias, 1, st) == 0)
+    return 0;
+  return dl_gemm(akout, bkout, epi, A, lda, B, ldb, M, N, K, C, ldc, Cf, ldcf, bias, R, ldr, H, ldh, dbias, 1, st);
+}
+
+// fp32-accumulating weight gradient c += op(a) op(b) through gemm8: the token (reduction) dimension
+// is split into S slices written as fp32 slabs and summed into c (no atomics); -1 if unsupported.
+int own_wgrad(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, at::Tensor c, hipStream_t st) {
+  if (!use_gemm8() || !c.is_contiguous()) return -1;
+  const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
+  int S = 1;
+  if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) S = std::max(1, std::atoi(e));
+  else
+    while (S < 16 && tiles * S * 2 <= 512 && A.k % (S * 2 * 64) == 0 && A.k / (S * 2) >= 1024) S *= 2;
+  while (S > 1 && A.k % (S * 64)) S /= 2;
+  if (S == 1)
+    return dl_gemm8(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, nullptr, 0,
+                    f32(c), c.stride(0), 0, 1, nullptr, nullptr, 0, nullptr, 0, nullptr, 1, st);
+  auto slabs = at::empty({S, A.rows, B.rows}, c.options());
+  const int rc = dl_gemm8(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
+                          nullptr, 0, f32(slabs), B.rows, A.rows * B.rows, 0, nullptr, nullptr, 0, nullptr, 0, nullptr,
+                          S, st);
+  if (rc != 0) return rc;
+  return dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), st);
+}
+
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& residual, bool trans_a, bool trans_b, int64_t epilogue) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm operands must be GPU tensors");
@@ -408,10 +445,10 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
     TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
     auto c = at::empty({A.rows, B.rows}, a.options());
     const at::Tensor bias32 = f32_bias(bias);
-    const int rc = dl_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
-                           bf(c), B.rows, nullptr, 0, bias32.defined() ? f32(bias32) : nullptr,
-                           residual.has_value() ? cbf(*residual) : nullptr, B.rows, nullptr, 0, nullptr, 1,
-                           cur_stream(a));
+    const int rc = own_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
+                            bf(c), B.rows, nullptr, 0, bias32.defined() ? f32(bias32) : nullptr,
+                            residual.has_value() ? cbf(*residual) : nullptr, B.rows, nullptr, 0, nullptr,
+                            cur_stream(a));
     if (rc == 0) return c;
   }
   if (lt_ok(a, b) && (!residual.has_value() || (residual->is_contiguous() && residual->scalar_type() == at::kBFloat16))) {
@@ -476,6 +513,7 @@ void gemm_acc_f32_split(const at::Tensor& a, const at::Tensor& b, at::Tensor c, 
   if (force_mfma_gemm() && mfma_ok(a, b)) {
     const Mat A = Av, B = Bv;
     TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
+    if (own_wgrad(A, B, a, b, c, cur_stream(a)) == 0) return;
     // split the reduction so that at least ~2 workgroups per CU exist (wgrad: few output tiles,
     // very long token reduction); splits accumulate with fp32 atomics
     const int64_t tiles = ntiles;
@@ -533,9 +571,9 @@ std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tens
   auto G = at::empty_like(H);
   if (force_mfma_gemm() && mfma_ok(x, w)) {
     const at::Tensor bias32 = f32_bias(bias);
-    const int rc = dl_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0),
-                           (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1), nullptr,
-                           1, cur_stream(x));
+    const int rc = own_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0),
+                            (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1),
+                            nullptr, cur_stream(x));
     if (rc == 0) return {H, G};
   }
   // hipBLASLt on ROCm 7.2 has no gfx950 solution for GELU_AUX_BIAS (scripts/lt_debug.py), so the
@@ -563,9 +601,9 @@ at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tenso
   expect(dbias, at::kFloat, "dbias");
   if (force_mfma_gemm() && mfma_ok(dy, w)) {
     auto C = at::empty({dy.size(0), w.size(1)}, dy.options());
-    const int rc = dl_gemm(0, 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0), (int)w.size(1),
-                           (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0,
-                           f32(dbias), 1, cur_stream(dy));
+    const int rc = own_gemm(0, 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0), (int)w.size(1),
+                            (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0,
+                            f32(dbias), cur_stream(dy));
     if (rc == 0) return C;
   }
   // (hipBLASLt's DGELU_BGRAD epilogue returns wrong results for this layout on ROCm 7.2 —

@@ -63,6 +63,12 @@ int dl_gemm(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, cons
             int K, bf16_t* C, long ldc, float* Cf, long ldcf, const float* bias, const bf16_t* R, long ldr, bf16_t* H,
             long ldh, float* dbias, int splits, hipStream_t st);
 
+// gemm8.hip (LDS-DMA 8-phase MFMA GEMM; epi as dl_gemm; EPI 3 writes fp32 slab blockIdx.y of
+// Cf (+= when accumulate); splits > 1 only for EPI 3)
+int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N,
+             int K, bf16_t* C, long ldc, float* Cf, long ldcf, long slab, int accumulate, const float* bias,
+             const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st);
+
 // swav.hip
 int dl_sinkhorn(const float* scores, float* P, float* Q, float* ws, int n, int K, int bs, float eps, int iters,
                 hipStream_t st);

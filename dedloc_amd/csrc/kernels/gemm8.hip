@@ -1,0 +1,427 @@
+// bf16 GEMM on MFMA with LDS-DMA staging and an 8-phase K loop (the
+// structure of cdna_hip_programming.md §5 "The 256² 8-phase template", written for this repo).
+//
+//   C[M,N] = sum_k A(m,k) B(n,k)      fp32 accumulation, v_mfma_f32_16x16x32_bf16
+//
+// Operand storage (template flags), as in gemm.hip:
+//   K-inner : element (r, k) at p[r * ld + k]   (activations, forward weights [out][in])
+//   K-outer : element (r, k) at p[k * ld + r]   (dgrad weights, wgrad operands)
+//
+// Tile 256 x 256 x 64, 512 threads = 8 waves as 2 (M) x 4 (N), 128 x 64 outputs per wave held as
+// four 64 x 32 quadrants.  Each operand tile is staged as two half-tiles of 128 rows x 64 k (16 KiB)
+// by global_load_lds (16 B per lane, two instructions per thread per half-tile, no VGPR staging):
+// A half h holds the tile rows with bit 6 == h, B half h the columns with bit 5 == h, so quadrant
+// (qm, qn) of every wave reads exactly half-tiles A_qm and B_qn.  The K loop runs 4 phases per K-tile,
+// one quadrant each, in the order (0,0) (0,1) (1,1) (1,0):
+//
+//   phase: ds_read this quadrant's new fragments | issue one half-tile of prefetch (2 glds) |
+//          s_barrier | 16 MFMA (setprio 1) | s_barrier
+//
+// Waves 4-7 run one barrier behind waves 0-3 (stagger), so on each SIMD one wave computes while its
+// partner reads and prefetches.  Prefetch runs 6 half-tiles (1.5 K-tiles) ahead: each half-tile
+// of the double buffer is restaged two phases after its last read — safe for the lagging group
+// too — and the only vmcnt wait is a counted vmcnt(4) in the last phase of each K-tile (two
+// half-tiles stay in flight across the barriers; never vmcnt(0) in steady state).  All LDS is one __shared__ array and
+// every barrier is a raw s_barrier, so no compiler-inserted vmcnt(0) drains the pipeline.
+//
+// LDS images (bank-conflict free, checked by simulation of the gfx950 lane groups):
+//   K-inner half-tile: [128 rows][8 x 16 B], chunk c of row r at c ^ ((r >> 1) & 7)  -> ds_read_b128
+//   K-outer half-tile: [64 k][16 x 16 B],   chunk c of k-row k at c ^ (((k&3)<<2)|((k>>2)&3))
+//                      -> ds_read_b64_tr_b16 (hardware transpose to the MFMA operand layout)
+// LDS-DMA writes each 1 KiB piece lane-linearly; the swizzle is applied on the per-lane global
+// source address and on the read (both sides, cdna_hip_programming.md rule 21).
+//
+// Epilogues (staged through LDS as fp32, 64 rows per round, written as 16-B row chunks):
+//   EPI_STORE  C = acc (+ bias[n]) (+ R[m,n])                                 bf16
+//   EPI_GELU   H = bf16(acc + bias); C = gelu_new(H)                          bf16 x2
+//   EPI_DGELU  C = bf16(acc) * gelu_new'(R[m,n]); dbias[n] += sum_m C         bf16 (+ fp32 atomics)
+//   EPI_F32    Cf[z][m,n] = acc  or  += acc (split z = blockIdx.y)            fp32
+#include "dl_common.h"
+#include "dl_kernels.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4_t lds_s4;
+typedef __attribute__((address_space(3))) void lds_void;
+
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3 };
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int HALF = 16384;     // one half-tile image
+constexpr int BUF = 4 * HALF;   // slots in stage order: 0 = A0, 1 = B1, 2 = A1, 3 = B0
+constexpr int SMEM = 2 * BUF;   // double buffer: 128 KiB
+
+__device__ __forceinline__ int kin_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int kout_swz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+
+// Tile row / column of local index l (0..127) of half-tile h: A halves interleave 64-row blocks
+// (bit 6 of the tile row), B halves 32-column blocks (bit 5), matching the waves' quadrants.
+template <bool ISB>
+__device__ __forceinline__ int half_to_tile(int l, int h) {
+  return ISB ? ((l >> 5) << 6) + (h << 5) + (l & 31) : ((l >> 6) << 7) + (h << 6) + (l & 63);
+}
+
+// Issue the two LDS-DMA pieces of this thread for one half-tile.
+template <bool KO, bool ISB>
+__device__ __forceinline__ void stage_half(const bf16_t* __restrict__ g, long ld, int r0, int rows_valid, int k0,
+                                           int half, uint8_t* slot, int w, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int region = j * 8 + w;  // 1 KiB piece of the 16 KiB image
+    const bf16_t* src;
+    if constexpr (!KO) {
+      const int lrow = region * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ kin_swz(lrow);
+      const int trow = half_to_tile<ISB>(lrow, half);
+      const int grow = min(r0 + trow, rows_valid - 1);  // M tail: clamp (rows are masked on store)
+      src = g + (long)grow * ld + k0 + c * 8;
+    } else {
+      const int k = region * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ kout_swz(k);
+      const int tcol = half_to_tile<ISB>(c * 8, half);  // 8-column chunks never straddle a block
+      src = g + (long)(k0 + k) * ld + r0 + tcol;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(slot + region * 1024), 16, 0, 0);
+  }
+}
+
+// MFMA operand fragment: 16 rows (r0..) x 32 k (k-step ks) of a half-tile image; lane l holds
+// (row r0 + (l & 15), k = 32 ks + 8 (l >> 4) + j), j = 0..7.
+template <bool KO>
+__device__ __forceinline__ bf16x8 frag(const uint8_t* img, int r0, int ks, int lane) {
+  if constexpr (!KO) {
+    const int row = r0 + (lane & 15), c = 4 * ks + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((c ^ kin_swz(row)) << 4));
+  } else {
+    const int g = lane >> 4, i = lane & 15;
+    const int kr = 32 * ks + 8 * g + (i >> 2);
+    const int col = r0 + 4 * (i & 3);
+    const int o1 = kr * 256 + (((col >> 3) ^ kout_swz(kr)) << 4) + ((col & 7) << 1);
+    const int o2 = (kr + 4) * 256 + (((col >> 3) ^ kout_swz(kr + 4)) << 4) + ((col & 7) << 1);
+    const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + o1));
+    const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + o2));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+// f32 -> bf16 by the hardware converter (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN kept), no branches
+__device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
+  const __bf16 x = (__bf16)a, y = (__bf16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+__device__ __forceinline__ float round_bf16(float a) { return (float)(__bf16)a; }
+__device__ __forceinline__ void store8_bf16(bf16_t* dst, const float* v) {
+  *reinterpret_cast<uint4*>(dst) = uint4{pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]), pack2_bf16(v[4], v[5]),
+                                         pack2_bf16(v[6], v[7])};
+}
+
+struct Args {
+  const bf16_t* A; long lda;
+  const bf16_t* B; long ldb;
+  int M, N, K;                   // K per split
+  bf16_t* C; long ldc;
+  float* Cf; long ldcf; long slab; int accumulate;
+  const float* bias;
+  const bf16_t* R; long ldr;     // residual (STORE) or pre-activation (DGELU)
+  bf16_t* H; long ldh;           // pre-activation out (GELU)
+  float* dbias;                  // column sums out (DGELU)
+};
+
+#define DL_MFMA_QUAD(QM, QN)                                                          \
+  do {                                                                                \
+    __builtin_amdgcn_s_setprio(1);                                                    \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                  \
+      _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                \
+        _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                              \
+          acc[QM][QN][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(              \
+              af[mi][ks], bfr[ni][ks], acc[QM][QN][mi][ni], 0, 0, 0);                 \
+    __builtin_amdgcn_s_setprio(0);                                                    \
+  } while (0)
+
+template <bool AKO, bool BKO, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int tiles_n = p.N / BN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int kbase = blockIdx.y * p.K;
+  const int nk = p.K / BK;
+
+  floatx4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) acc[a][b][c][d] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile h = 4 t + k of the stream: k = 0 A0, 1 B1, 2 A1, 3 B0 -> slot k of buffer t & 1
+#define DL_STAGE(T, KSLOT)                                                                          \
+  do {                                                                                              \
+    uint8_t* slot_ = smem + ((T) & 1) * BUF + (KSLOT) * HALF;                                       \
+    const int k0_ = kbase + (T) * BK;                                                               \
+    if ((KSLOT) == 0) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 0, slot_, w, lane);          \
+    else if ((KSLOT) == 1) stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 1, slot_, w, lane);      \
+    else if ((KSLOT) == 2) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 1, slot_, w, lane);     \
+    else stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 0, slot_, w, lane);                        \
+  } while (0)
+
+#ifdef GEMM8_PROBE_DESYNC  // measurement build only: offset the first wave of workgroups in time
+  if (blockIdx.x < 256) {
+    const int d = ((blockIdx.x >> 3) & 3) * GEMM8_PROBE_DESYNC;
+    for (int i = 0; i < d; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
+  // prologue: tile 0 and the first two half-tiles (A0, B1) of tile 1
+  DL_STAGE(0, 0); DL_STAGE(0, 1); DL_STAGE(0, 2); DL_STAGE(0, 3);
+  if (nk > 1) {
+    DL_STAGE(1, 0); DL_STAGE(1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  // Stagger (cdna_hip_programming.md §5 template, MI355X_MICROARCH.md "Two waves per SIMD"): waves
+  // 4-7 (the M half wm = 1; wave w and w + 4 share a SIMD) run one barrier behind waves 0-3, so on
+  // every SIMD one wave issues its 16 MFMAs while its partner reads fragments and issues the
+  // prefetch.  Every half-tile is restaged two phases after its last read, so even the lagging
+  // group's reads (retired by the lgkmcnt wait in front of its MFMAs) are done before the leading
+  // group's LDS-DMA into that region is issued.
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+  const int ra = wm * 64;  // this wave's rows inside an A half-tile image
+  const int cb = wn * 32;  // this wave's columns inside a B half-tile image
+  bf16x8 af[4][2], bfr[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* buf = smem + (t & 1) * BUF;
+    const uint8_t* iA0 = buf;
+    const uint8_t* iB1 = buf + HALF;
+    const uint8_t* iA1 = buf + 2 * HALF;
+    const uint8_t* iB0 = buf + 3 * HALF;
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+
+    // ---- phase 0: quadrant (0,0); prefetch A1 of tile t+1
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA0, ra + mi * 16, ks, lane);
+    if (more1) DL_STAGE(t + 1, 2);
+    __builtin_amdgcn_s_barrier();
+    DL_MFMA_QUAD(0, 0);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 1: quadrant (0,1); prefetch B0 of tile t+1
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB1, cb + ni * 16, ks, lane);
+    if (more1) DL_STAGE(t + 1, 3);
+    __builtin_amdgcn_s_barrier();
+    DL_MFMA_QUAD(0, 1);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 2: quadrant (1,1); prefetch A0 of tile t+2
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA1, ra + mi * 16, ks, lane);
+    if (more2) DL_STAGE(t + 2, 0);
+    __builtin_amdgcn_s_barrier();
+    DL_MFMA_QUAD(1, 1);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 3: quadrant (1,0); prefetch B1 of tile t+2; retire tile t+1
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+    if (more2) {
+      DL_STAGE(t + 2, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    DL_MFMA_QUAD(1, 0);
+    __builtin_amdgcn_s_barrier();
+  }
+#undef DL_STAGE
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: every wave passes the same barriers
+  __builtin_amdgcn_s_barrier();               // all fragment reads done before the epilogue reuses LDS
+
+#ifdef GEMM8_PROBE_NO_EPILOGUE  // measurement build only: keep the accumulators live, write nothing
+  if (p.M < 0) {
+    float z = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int d = 0; d < 2; ++d) z += acc[a][b][c][d][0] + acc[a][b][c][d][3];
+    p.Cf[threadIdx.x] = z;
+  }
+  return;
+#endif
+  // ---------------------------------------------------------------- epilogue
+  // Each wave stages 64 x 64 fp32 per round (quadrant row qm) in its own 16 KiB LDS region:
+  // row r at r * 256 B, 16-B chunk q of it at q ^ (r & 1) (conflict-free row reads).
+  uint8_t* ep = smem + w * 16384;
+  const int crow = 4 * (lane >> 4), ccol = lane & 15;
+  float bias_v[2][2];
+#pragma unroll
+  for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      bias_v[qn][ni] = 0.f;
+      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
+        if (p.bias) bias_v[qn][ni] = p.bias[n0 + wn * 64 + qn * 32 + ni * 16 + ccol];
+    }
+  float colsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
+  const int rch = lane & 7;   // 8-column chunk handled in the row phase
+  const int rr = lane >> 3;   // row within a pass of 8 rows
+
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm) {
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = mi * 16 + crow + i;
+            const int c = qn * 32 + ni * 16 + ccol;
+            const int q = (c >> 2) ^ (r & 1);
+            *reinterpret_cast<float*>(ep + r * 256 + q * 16 + (c & 3) * 4) = acc[qm][qn][mi][ni][i] + bias_v[qn][ni];
+          }
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int r = pass * 8 + rr;
+      const float4 lo = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch) ^ (r & 1)) << 4));
+      const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const int gm = m0 + wm * 128 + qm * 64 + r;
+      const int gn = n0 + wn * 64 + rch * 8;
+#ifdef GEMM8_PROBE_NO_STORE  // measurement build only (bench/gemm8_probe.hip): skip the output writes
+      if (gm < 0) {
+#else
+      if (gm < p.M) {
+#endif
+        if constexpr (EPI == EPI_STORE) {
+          if (p.R) {
+            float rv[8];
+            load_bf16<8>(p.R + (long)gm * p.ldr + gn, rv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += rv[j];
+          }
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v);
+        } else if constexpr (EPI == EPI_GELU) {
+          float h[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
+          store8_bf16(p.H + (long)gm * p.ldh + gn, h);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = gelu_tanh(h[j]);
+          store8_bf16(p.C + (long)gm * p.ldc + gn, h);
+        } else if constexpr (EPI == EPI_DGELU) {
+          float f[8];
+          load_bf16<8>(p.R + (long)gm * p.ldr + gn, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad(f[j]));
+            colsum[j] += v[j];
+          }
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v);
+        } else {
+          float* dst = p.Cf + (long)blockIdx.y * p.slab + (long)gm * p.ldcf + gn;
+          if (p.accumulate) {
+            const float4 o0 = *reinterpret_cast<const float4*>(dst);
+            const float4 o1 = *reinterpret_cast<const float4*>(dst + 4);
+            v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
+            v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+          }
+          *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<float4*>(dst + 4) = float4{v[4], v[5], v[6], v[7]};
+        }
+      }
+    }
+  }
+  if constexpr (EPI == EPI_DGELU) {
+    if (p.dbias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float s = colsum[j];
+        s += __shfl_xor(s, 8, 64);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        colsum[j] = s;
+      }
+      if (lane < 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + wn * 64 + lane * 8 + j], colsum[j]);
+      }
+    }
+  }
+}
+#undef DL_MFMA_QUAD
+
+template <bool AKO, bool BKO, int EPI>
+int launch8(const Args& a, int splits, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
+  gemm8_kernel<AKO, BKO, EPI><<<dim3(tiles, splits), NT, 0, st>>>(a);
+  return 0;
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+// Returns -1 when the shape is outside the kernel's contract: N % 256 == 0, K % (64 * splits) == 0,
+// a K-outer A needs M % 256 == 0, every leading dimension a multiple of 8 elements and every base
+// pointer 16-byte aligned.
+int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N,
+             int K, bf16_t* C, long ldc, float* Cf, long ldcf, long slab, int accumulate, const float* bias,
+             const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return -1;
+  if (N % BN || K % (BK * splits)) return -1;
+  if (a_kouter && M % BM) return -1;
+  if (lda % 8 || ldb % 8 || !aligned16(A) || !aligned16(B)) return -1;
+  if (epi == EPI_F32) {
+    if (!Cf || ldcf % 4 || !aligned16(Cf) || slab % 4) return -1;
+  } else {
+    if (!C || ldc % 8 || !aligned16(C)) return -1;
+    if (R && (ldr % 8 || !aligned16(R))) return -1;
+    if (epi == EPI_GELU && (!H || ldh % 8 || !aligned16(H))) return -1;
+    if (epi == EPI_DGELU && !R) return -1;
+    if (splits != 1) return -1;
+  }
+  Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias};
+#define DL_GEMM8_CASE(AK, BK_, E) \
+  if (a_kouter == AK && b_kouter == BK_ && epi == E) return launch8<AK, BK_, E>(a, splits, st);
+  DL_GEMM8_CASE(0, 0, EPI_STORE)
+  DL_GEMM8_CASE(0, 0, EPI_GELU)
+  DL_GEMM8_CASE(0, 1, EPI_STORE)
+  DL_GEMM8_CASE(0, 1, EPI_DGELU)
+  DL_GEMM8_CASE(1, 1, EPI_F32)
+  DL_GEMM8_CASE(0, 0, EPI_F32)
+#undef DL_GEMM8_CASE
+  return -1;
+}

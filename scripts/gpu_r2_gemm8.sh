@@ -1,0 +1,14 @@
+#!/bin/bash
+# gemm8 bring-up: GEMM numerics tier, then gemm8 vs hipBLASLt on the ALBERT layer shapes.
+mkdir -p gpurun_out
+export PYTHONPATH=$PWD
+step() {
+  local log=$1; shift
+  timeout -k 10 "$@" > "$log" 2>&1
+  local rc=$?
+  echo "rc=$rc $*"; grep -E '^\{|passed|failed|Error|error' "$log" | tail -40 | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "stopping after rc=$rc"; tail -30 "$log"; exit $rc; fi
+}
+step gpurun_out/g8_pytest.log 300 python -u -m pytest tests/test_kernels_gpu.py -q -x -k "gemm" --timeout 120 --timeout-method thread
+T=32768 VARIANTS=gemm8,gemm1,lt step gpurun_out/g8_bench32k.log 300 python -u bench/gemm_bench.py --check
+T=131072 step gpurun_out/g8_bench131k.log 300 python -u bench/gemm_bench.py
