@@ -49,6 +49,9 @@ class CollaborationArguments(AveragerArguments, CollaborativeOptimizerArguments,
     peer_bandwidths: Optional[str] = field(default=None, metadata={"help": "per-rank emulated bandwidth list (Mbps), e.g. 200,100,100,50"})
     peer_client_mode: Optional[str] = field(default=None, metadata={"help": "per-rank client-mode flags, e.g. 0,0,0,1"})
     emulate_transfer_delay: bool = field(default=False, metadata={"help": "also delay each all-reduce to the emulated bandwidth's transfer time"})
+    eta_slack: float = field(default=0.5, metadata={
+        "help": "begin the global step when the collaboration's ETA falls within this fraction of one local step "
+                "from now (0 = hivemind's rule: only once the ETA has passed)"})
 
 
 @dataclass

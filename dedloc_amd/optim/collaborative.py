@@ -77,7 +77,7 @@ class CollaborativeOptimizer:
                  auxiliary: bool = False, allow_state_sharing: bool = True, verbose: bool = False, start: bool = True,
                  compression_type: str = "FLOAT16", compression: Optional[str] = None, throughput: Optional[float] = None,
                  peer_id: Optional[bytes] = None, max_grad_norm: Optional[float] = None,
-                 delay_param_averaging: bool = False, **averager_kwargs):
+                 delay_param_averaging: bool = False, eta_slack: float = 0.0, **averager_kwargs):
         self.opt, self.dht, self.prefix = opt, dht, prefix
         self.flat = opt.flat
         self.scheduler = scheduler
@@ -114,6 +114,7 @@ class CollaborativeOptimizer:
             averaging_timeout=self.averaging_timeout, **averager_kwargs)
         self.averager.get_current_state = self._get_current_state
 
+        self.eta_slack = float(eta_slack)
         self.delay_param_averaging = delay_param_averaging
         self._param_round: Optional[threading.Thread] = None
         self._param_round_result = None
@@ -226,7 +227,7 @@ class CollaborativeOptimizer:
 
         if self._param_round is not None and not self._param_round.is_alive():
             self._finish_param_round()
-        if not self.collaboration_state.ready_for_step:
+        if not (self.collaboration_state.ready_for_step or self._ready_within_slack(batch_size)):
             return None
 
         logger.log(self.status_loglevel, f"beginning global optimizer step #{self.collaboration_state.optimizer_step}")
@@ -270,6 +271,21 @@ class CollaborativeOptimizer:
         self.last_step_time = get_dht_time()
         logger.log(self.status_loglevel, f"optimizer step #{self.local_step} done")
         return group
+
+    def _ready_within_slack(self, batch_size: int) -> bool:
+        """ETA slack (``eta_slack`` > 0, not in hivemind 0.9.x): start the global step now when the
+        collaboration's predicted ETA lies less than ``eta_slack`` of one local step ahead.  With the
+        reference rule every peer enters averaging at the first step boundary AFTER the ETA, so the
+        group waits for the peer whose boundary falls last (close to a whole local step with many
+        peers); entering at the boundary nearest to the ETA halves that wait, and the global batch
+        stays the target on average (the weights use each peer's actual sample count)."""
+        if self.eta_slack <= 0 or self.performance_ema.samples_per_second <= 0:
+            return False
+        cs = self.collaboration_state
+        if cs.num_peers < 2 or cs.optimizer_step > self.local_step:
+            return False
+        step_time = batch_size / self.performance_ema.samples_per_second
+        return get_dht_time() + self.eta_slack * step_time >= cs.eta_next_step
 
     def step_aux(self, **kwargs):
         """Auxiliary peer: join the averaging rounds as a reducer only (run_aux.py:260-262).

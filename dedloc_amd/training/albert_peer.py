@@ -134,7 +134,7 @@ class AlbertPeer:
             expected_drift_rate=ca.expected_drift_rate, performance_ema_alpha=ca.performance_ema_alpha,
             target_group_size=ca.target_group_size, metadata_expiration=ca.metadata_expiration, pg=pg, rank=rank,
             delay_param_averaging=getattr(ca, "delay_param_averaging", False),
-            emulate_transfer_delay=getattr(ca, "emulate_transfer_delay", False))
+            emulate_transfer_delay=getattr(ca, "emulate_transfer_delay", False), eta_slack=getattr(ca, "eta_slack", 0.0))
         self.statistics_expiration = ca.statistics_expiration
         seed = peer_seed(self.local_public_key, training_args.seed)
         if getattr(self, "_stream_tokenizer", None) is not None:

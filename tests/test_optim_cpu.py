@@ -81,3 +81,35 @@ def test_lamb_loads_torch_format_state_dict():
     opt3 = FusedLamb(flat3, lr=1e-3, weight_decay=0.01, no_decay=NO_DECAY)
     opt3.load_state_dict(opt.state_dict())
     assert torch.equal(opt3.exp_avg, opt.exp_avg) and torch.equal(opt3.exp_avg_sq, opt.exp_avg_sq)
+
+
+def test_eta_slack_readiness_rule():
+    """CollaborativeOptimizer's ETA slack: begin the global step at the local step boundary nearest
+    to the collaboration's ETA instead of the first one after it (0 = hivemind's rule)."""
+
+    from dedloc_amd.dht import DHT, get_dht_time
+    from dedloc_amd.optim.collaborative import CollaborationState, CollaborativeOptimizer
+
+    dht = DHT(listen_on="127.0.0.1:*")
+    try:
+        flat = FlatParams(_params(), with_bf16=False)
+        opt = FusedLamb(flat, lr=1e-3)
+        co = CollaborativeOptimizer(opt, dht=dht, prefix="slack", target_batch_size=64, batch_size_per_step=4,
+                                    start=False, eta_slack=0.5, allow_state_sharing=False)
+        co.performance_ema.samples_per_second = 40.0  # one local step of 4 samples = 0.1 s
+        now = get_dht_time()
+        co.collaboration_state = CollaborationState(0, 40, 64, num_peers=4, num_clients=0, eta_next_step=now + 0.04,
+                                                    next_fetch_time=now + 10)
+        assert not co.collaboration_state.ready_for_step      # hivemind's rule would run one more step
+        assert co._ready_within_slack(4)                       # the ETA is closer than half a step
+        co.collaboration_state.eta_next_step = now + 0.2
+        assert not co._ready_within_slack(4)                   # two local steps away: keep accumulating
+        co.eta_slack = 0.0
+        co.collaboration_state.eta_next_step = now + 0.04
+        assert not co._ready_within_slack(4)
+        co.eta_slack = 0.5
+        co.collaboration_state.num_peers = 1                   # alone: nobody to wait for
+        assert not co._ready_within_slack(4)
+        co.shutdown()
+    finally:
+        dht.shutdown()
