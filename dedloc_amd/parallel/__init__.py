@@ -30,11 +30,12 @@ def env_rank_world():
     return rank, world, local
 
 
-def init_world(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[torch.device] = None):
+def init_world(backend: Optional[str] = None, timeout_s: float = 600.0, device: Optional[torch.device] = None,
+               force: bool = False):
     """Initialise (or reuse) the world process group from torchrun-style env variables.
 
-    Returns (rank, world_size, device).  A single process without MASTER_ADDR runs without a
-    process group (world size 1; averaging is then skipped, as in the reference's 1-peer case).
+    Returns (rank, world_size, device).  A single process runs without a process group (world
+    size 1; averaging is then skipped, as in the reference's 1-peer case) unless ``force``.
     """
     rank, world, local = env_rank_world()
     if device is None:
@@ -44,13 +45,15 @@ def init_world(backend: Optional[str] = None, timeout_s: float = 600.0, device: 
             device = torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = backend or ("nccl" if device.type == "cuda" else "gloo")
-        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
-        if backend == "nccl":
-            kw["device_id"] = device
-        dist.init_process_group(**kw)
+        # no device_id: a world communicator bound to a device makes torch create every later group
+        # with ncclCommSplit, a collective over ALL world ranks, which member-only group creation
+        # (GroupCommunicators) would hang in; unbound, each group gets its own ncclCommInitRank
+        # among its members (the current device is set above)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
         # the first P2P batch must not be the first collective on the communicator
         t = torch.zeros(1, device=device)
         dist.all_reduce(t)
@@ -121,8 +124,11 @@ def _new_member_group(ranks, name: str, timeout: datetime.timedelta):
     backend, store = c10d._world.pg_map[default_pg]
     me = dist.get_rank()
     assert me in ranks, "only members create a group communicator"
+    if default_pg.bound_device_id is not None:
+        raise RuntimeError("the world process group is bound to a device: group communicators would be created by "
+                           "ncclCommSplit over all world ranks (init the world with parallel.init_world)")
     pg, _ = c10d._new_process_group_helper(len(ranks), ranks.index(me), ranks, backend, store, name, timeout=timeout,
-                                           device_id=default_pg.bound_device_id, group_desc=name)
+                                           group_desc=name)
     c10d._world.pg_group_ranks[pg] = {g: i for i, g in enumerate(ranks)}
     # RCCL: the first operation on a communicator must include every member (lazy init); the
     # all-reduce also proves every member has created its end before any P2P traffic is posted

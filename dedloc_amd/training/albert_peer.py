@@ -193,11 +193,26 @@ class AlbertPeer:
         self.opt.zero_grad()
         self.mini_steps += 1
         self.hf_step += 1
+        self._pace()
         self.throttle.end()
         self.on_step_end()
         ev = self.churn.due(self.collab_opt.local_step, time.time())
         if ev is not None:
             self.drop_out(ev.duration, restart=ev.mode == "restart")
+
+    def _pace(self):
+        """Keep the host at most one micro-step ahead of the GPU: wait for the PREVIOUS step's end
+        event (the queue still holds this step, so the GPU never idles).  Progress reports and the
+        PerformanceEMA then count samples the device has actually processed, which the
+        collaboration's ETA (and so the moment every peer enters averaging) depends on — the
+        reference gets the same effect from its per-step host syncs (params_are_finite)."""
+        if self.device.type != "cuda":
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        prev, self._step_event = getattr(self, "_step_event", None), ev
+        if prev is not None:
+            prev.synchronize()
 
     # ------------------------------------------------------------------ churn (emulation/churn.py)
     def drop_out(self, duration: float, restart: bool = False):
