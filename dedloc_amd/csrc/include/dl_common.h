@@ -39,6 +39,17 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return (bf16_t)(u >> 16);
 }
 
+// Hardware f32 -> bf16 (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN), branch-free:
+// same results as f2bf for every input except the NaN payload bits.
+__device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
+  const __bf16 x = (__bf16)a, y = (__bf16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+__device__ __forceinline__ float round_bf16(float a) { return (float)(__bf16)a; }
+__device__ __forceinline__ uint4 pack8_bf16(const float* v) {
+  return uint4{pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]), pack2_bf16(v[4], v[5]), pack2_bf16(v[6], v[7])};
+}
+
 // fp16 (IEEE half) conversions for the FLOAT16 wire format.
 __device__ __forceinline__ uint16_t f2h(float f) {
   _Float16 h = (_Float16)f;

@@ -2,6 +2,8 @@
 // fp32<->bf16 casts of the flat parameter buffer, tanh for the SOP pooler.
 // All bf16 traffic is 16 B per lane (Guideline 13); grids are capped at 256 CUs x 8 blocks and
 // grid-strided (Guideline 11).
+#include <cstdlib>
+
 #include "dl_common.h"
 #include "dl_kernels.h"
 
@@ -24,6 +26,39 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
+// v2 (default): no grid stride — each thread owns VPT vectors of a 1024-vector block chunk and
+// issues all their loads before any math (LayerNorm's access shape, which streams at ~6.3 TB/s),
+// branch-free hardware bf16 conversion: 498 -> 389 us at T=131072 x 4096 (4.3 -> 5.5 TB/s,
+// bench/ew_bench.py, bitwise equal).  DEDLOC_EW=1 selects the grid-strided v1 (A/B).  The same
+// change to the GELU-backward column-sum kernel (8 rows in flight) measured no gain (640 vs 649 us).
+constexpr int VPT = 4;
+__global__ __launch_bounds__(256) void gelu_fwd_v2_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ y,
+                                                          size_t nvec) {
+  const size_t base = (size_t)blockIdx.x * (256 * VPT) + threadIdx.x;
+  uint4 raw[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const size_t i = base + (size_t)k * 256;
+    if (i < nvec) raw[k] = reinterpret_cast<const uint4*>(h)[i];
+  }
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const size_t i = base + (size_t)k * 256;
+    if (i < nvec) {
+      float v[8];
+      load_bf16<8>(reinterpret_cast<const bf16_t*>(&raw[k]), v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
+      reinterpret_cast<uint4*>(y)[i] = pack8_bf16(v);
+    }
+  }
+}
+
+bool ew_v1() {
+  const char* e = std::getenv("DEDLOC_EW");
+  return e && e[0] == '1';
+}
+
 __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
                                                        bf16_t* __restrict__ dh, size_t nvec) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
@@ -41,7 +76,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict_
 // 512 columns x rpb rows; wave w takes rows w, w+4, ... with 4 rows of 16-byte loads in flight per
 // lane.  The 4 wave partials meet in LDS and leave as lane-contiguous fp32 atomics (256 B per wave
 // instruction, Guideline 12) — one atomic per column per block.
-template <bool GELU>
+template <bool GELU, int RU = 4>
 __global__ __launch_bounds__(256) void colsum_tile_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ h,
                                                           bf16_t* __restrict__ dh, float* __restrict__ out, int rows,
                                                           int N, int rpb) {
@@ -54,15 +89,15 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const bf16_t* __restri
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (active) {
     int r = r0 + w;
-    for (; r + 12 < r1; r += 16) {
-      uint4 xr[4], hr[4];
+    for (; r + 4 * (RU - 1) < r1; r += 4 * RU) {
+      uint4 xr[RU], hr[RU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RU; ++u) {
         xr[u] = *reinterpret_cast<const uint4*>(x + (size_t)(r + 4 * u) * N + c0);
         if (GELU) hr[u] = *reinterpret_cast<const uint4*>(h + (size_t)(r + 4 * u) * N + c0);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RU; ++u) {
         float g[8];
         load_bf16<8>(reinterpret_cast<const bf16_t*>(&xr[u]), g);
         if (GELU) {
@@ -188,7 +223,12 @@ __global__ __launch_bounds__(256) void add_bf16_to_f32_kernel(const bf16_t* __re
 
 int dl_gelu_fwd(const bf16_t* h, bf16_t* y, size_t n, hipStream_t st) {
   if (n % 8) return -1;
-  gelu_fwd_kernel<<<grid_for(n / 8, 256), 256, 0, st>>>(h, y, n / 8);
+  if (ew_v1()) {
+    gelu_fwd_kernel<<<grid_for(n / 8, 256), 256, 0, st>>>(h, y, n / 8);
+    return 0;
+  }
+  const size_t nvec = n / 8;
+  gelu_fwd_v2_kernel<<<(unsigned)((nvec + 256 * VPT - 1) / (256 * VPT)), 256, 0, st>>>(h, y, nvec);
   return 0;
 }
 
@@ -202,7 +242,7 @@ int dl_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* h, bf16_t* dh, float* dbi
   if (N % 8) return -1;
   const int rpb = 256;
   dim3 grid((N + 511) / 512, (rows + rpb - 1) / rpb);
-  colsum_tile_kernel<true><<<grid, 256, 0, st>>>(dy, h, dh, dbias, rows, N, rpb);
+  colsum_tile_kernel<true, 4><<<grid, 256, 0, st>>>(dy, h, dh, dbias, rows, N, rpb);
   return 0;
 }
 
@@ -225,7 +265,7 @@ int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hi
   }
   const int rpb2 = 256;
   dim3 grid((N + 511) / 512, (rows + rpb2 - 1) / rpb2);
-  colsum_tile_kernel<false><<<grid, 256, 0, st>>>(x, nullptr, nullptr, part, rows, N, rpb2);
+  colsum_tile_kernel<false, 4><<<grid, 256, 0, st>>>(x, nullptr, nullptr, part, rows, N, rpb2);
   (void)rpb;
   return 0;
 }

@@ -106,15 +106,8 @@ __device__ __forceinline__ bf16x8 frag(const uint8_t* img, int r0, int ks, int l
   }
 }
 
-// f32 -> bf16 by the hardware converter (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN kept), no branches
-__device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
-  const __bf16 x = (__bf16)a, y = (__bf16)b;
-  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
-}
-__device__ __forceinline__ float round_bf16(float a) { return (float)(__bf16)a; }
 __device__ __forceinline__ void store8_bf16(bf16_t* dst, const float* v) {
-  *reinterpret_cast<uint4*>(dst) = uint4{pack2_bf16(v[0], v[1]), pack2_bf16(v[2], v[3]), pack2_bf16(v[4], v[5]),
-                                         pack2_bf16(v[6], v[7])};
+  *reinterpret_cast<uint4*>(dst) = pack8_bf16(v);
 }
 
 struct Args {
