@@ -34,10 +34,13 @@ def main():
     g = torch.rand(1024, device=dev) + 0.5
     b = torch.randn(1024, device=dev)
     nb = h.numel() * 2
+    _, _, mean, rstd = O.layernorm_fwd(x, r, g, b, 1e-12)
+    dgam, dbet, dsum = torch.zeros(1024, device=dev), torch.zeros(1024, device=dev), torch.zeros(1024, device=dev)
     cases = [("gelu_fwd", lambda: O.gelu_fwd(h), 2 * nb),
              ("gelu_bwd_colsum", lambda: O.gelu_bwd(dy, h, db), 3 * nb),
              ("bias_grad_3072", lambda: O.bias_grad(dq, dbq, True), dq.numel() * 2),
-             ("ln_fwd_res", lambda: O.layernorm_fwd(x, r, g, b, 1e-12), 4 * x.numel() * 2)]
+             ("ln_fwd_res", lambda: O.layernorm_fwd(x, r, g, b, 1e-12), 4 * x.numel() * 2),
+             ("ln_bwd", lambda: O.layernorm_bwd(x, r, g, mean, rstd, dgam, dbet, True, dsum), 3 * x.numel() * 2)]
     # numerics: v2 must equal v1 bit for bit on the bf16 outputs
     os.environ["DEDLOC_EW"] = "1"
     y1 = O.gelu_fwd(h)
