@@ -45,8 +45,19 @@ def main():
     def bwd():
         return O.attn_bwd(qkv, mbias, out, dout, lse, H, S, scale, kvinfo)
 
+    dbias = torch.zeros(3 * H * D, device=dev)
+
+    def bwd_fused_bias():  # the model's call: QKV bias gradient inside the backward
+        return O.attn_bwd(qkv, mbias, out, dout, lse, H, S, scale, kvinfo, dbias)
+
+    def bwd_then_colsum():  # the previous form: backward, then a column-sum pass over dqkv
+        g = O.attn_bwd(qkv, mbias, out, dout, lse, H, S, scale, kvinfo)
+        O.bias_grad(g, dbias, True)
+        return g
+
     res = {}
-    for name, fn, flop_mult in (("fwd", fwd, 4), ("bwd", bwd, 10)):
+    for name, fn, flop_mult in (("fwd", fwd, 4), ("bwd", bwd, 10), ("bwd_fused_bias", bwd_fused_bias, 10),
+                                ("bwd_then_colsum", bwd_then_colsum, 10)):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()

@@ -317,7 +317,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& qkv, const c10::op
 
 at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbias, const at::Tensor& out,
                     const at::Tensor& dout, const at::Tensor& lse, int64_t H, int64_t S, double scale,
-                    const c10::optional<at::Tensor>& kvinfo) {
+                    const c10::optional<at::Tensor>& kvinfo, const c10::optional<at::Tensor>& dbias) {
   expect(qkv, at::kBFloat16, "qkv");
   expect(out, at::kBFloat16, "out");
   expect(dout, at::kBFloat16, "dout");
@@ -325,8 +325,14 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
   auto dqkv = at::empty_like(qkv);
   auto delta = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
   const float* mb = mbias.has_value() ? f32(*mbias) : nullptr;
+  float* dbp = nullptr;
+  if (dbias.has_value()) {
+    expect(*dbias, at::kFloat, "dbias");
+    TORCH_CHECK(dbias->numel() == ld, "dbias must have 3*H*D elements");
+    dbp = f32(*dbias);
+  }
   check(dl_attn_bwd(cbf(qkv), ld, mb, kvinfo_ptr(kvinfo, B), cbf(out), cbf(dout), H * D, f32(lse), f32(delta),
-                    bf(dqkv), (int)B, (int)H, (int)S, (int)D, (float)scale, cur_stream(qkv)),
+                    bf(dqkv), dbp, (int)B, (int)H, (int)S, (int)D, (float)scale, cur_stream(qkv)),
         "attn_bwd");
   return dqkv;
 }

@@ -108,6 +108,8 @@ int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int str
 // attention.hip
 int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, bf16_t* out, long ldo, float* lse,
                 int B, int H, int S, int D, float scale, hipStream_t st);
+// dbias (optional, fp32 [3 H D], accumulated): the QKV projection's bias gradient (query: column
+// sums of dQ; key: zero; value: column sums of dout)
 int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, const bf16_t* out,
-                const bf16_t* dout, long ldo, const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D,
-                float scale, hipStream_t st);
+                const bf16_t* dout, long ldo, const float* lse, float* delta, bf16_t* dqkv, float* dbias, int B, int H,
+                int S, int D, float scale, hipStream_t st);

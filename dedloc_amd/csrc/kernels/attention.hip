@@ -325,8 +325,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
                                                              const bf16_t* __restrict__ out, const bf16_t* __restrict__ dout,
                                                              long ldo, const float* __restrict__ lse,
                                                              float* __restrict__ delta, bf16_t* __restrict__ dqkv,
-                                                             int B, int H, int S, float sl2, float scale, int xcd) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
+                                                             float* __restrict__ dbias, int B, int H, int S, float sl2,
+                                                             float scale, int xcd) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 4 * 64 * 4];  // tail: mask bias / bias-grad partials
   const BlockId bid = block_id(xcd);
   const int b = bid.b, h = bid.h;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
@@ -431,6 +432,61 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
       for (int u = 0; u < 4; ++u)
         store4(dp_ + 32 * t + 8 * u + 4 * hh, dq[t][4 * u] * scale, dq[t][4 * u + 1] * scale,
                dq[t][4 * u + 2] * scale, dq[t][4 * u + 3] * scale);
+  }
+  if (dbias) {
+    // Fused bias gradient of the QKV projection (replaces a [T, 3H*64] column-sum pass):
+    //   query bias: column sums of the dQ just stored (bf16-rounded, as stored);
+    //   value bias: sum_k dV[k] = sum_q dO[q] (softmax rows sum to one), from the dO this block loaded;
+    //   key bias:   sum_k dK[k] = 0 exactly (sum_k dS[q,k] = delta - delta), so nothing is added.
+    // Column sums through LDS (cross-lane shuffles of 64 values per lane cost more than the
+    // column-sum pass they replace): each wave writes its [32 queries][64 columns] fp32 block
+    // (16-B chunk c of row r at c ^ (r & 15): conflict-free writes and column reads), then thread
+    // (wave w', column c) sums the 32 rows of wave w' and the four partials meet in the last 1 KiB.
+    float* red = reinterpret_cast<float*>(smem);          // [4 waves][32 rows][64 columns]
+    float* part = red + 4 * 32 * 64;                       // [4 waves][64 columns]
+    const bool live = q < S;
+    auto chunk_addr = [&](int row, int ch) { return red + (w * 32 + row) * 64 + ((ch ^ (row & 15)) << 2); };
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+      if (which == 0) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {  // dQ columns 32 t + 8 u + 4 hh + (0..3), as stored above
+            float4 v = float4{0.f, 0.f, 0.f, 0.f};
+            if (live)
+              v = float4{round_bf16(dq[t][4 * u] * scale), round_bf16(dq[t][4 * u + 1] * scale),
+                         round_bf16(dq[t][4 * u + 2] * scale), round_bf16(dq[t][4 * u + 3] * scale)};
+            *reinterpret_cast<float4*>(chunk_addr(r, 8 * t + 2 * u + hh)) = v;
+          }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {  // dO columns 16 ks + 8 hh + 4 g + (0..3), as loaded above
+            float4 v = float4{0.f, 0.f, 0.f, 0.f};
+            if (live)
+              v = float4{(float)df[ks][4 * g], (float)df[ks][4 * g + 1], (float)df[ks][4 * g + 2],
+                         (float)df[ks][4 * g + 3]};
+            *reinterpret_cast<float4*>(chunk_addr(r, 4 * ks + 2 * hh + g)) = v;
+          }
+      }
+      __syncthreads();
+      {
+        const int c = lane;  // this thread: column c of wave w's 32 rows
+        float sum = 0.f;
+#pragma unroll 8
+        for (int row = 0; row < 32; ++row) sum += red[(w * 32 + row) * 64 + (((c >> 2) ^ (row & 15)) << 2) + (c & 3)];
+        part[w * 64 + c] = sum;
+      }
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        const int c = threadIdx.x;
+        atomicAdd(&dbias[(which ? 2L * H * HD : 0L) + h * HD + c],
+                  part[c] + part[64 + c] + part[128 + c] + part[192 + c]);
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -580,13 +636,13 @@ int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
 }
 
 int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, const bf16_t* out,
-                const bf16_t* dout, long ldo, const float* lse, float* delta, bf16_t* dqkv, int B, int H, int S, int D,
-                float scale, hipStream_t st) {
+                const bf16_t* dout, long ldo, const float* lse, float* delta, bf16_t* dqkv, float* dbias, int B, int H,
+                int S, int D, float scale, hipStream_t st) {
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid((S + 127) / 128, H, B);
-  attn_bwd_dq_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, B, H, S, sl2,
-                                           scale, attn_xcd());
+  attn_bwd_dq_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, dbias, B, H, S,
+                                           sl2, scale, attn_xcd());
   attn_bwd_dkdv_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2, scale,
                                              attn_xcd());
   return 0;

@@ -147,10 +147,11 @@ class _AlbertLayerFn(torch.autograd.Function):
         O.gemm_acc_f32(ds1, att, lv["gwo"], True, False)
         datt = O.gemm(ds1, lv["wo"], None, None, False, False, 0)
         H = ctx.H
+        # the QKV bias gradient rides in the attention backward (query: colsum dQ, value: colsum
+        # datt, key: exactly zero — softmax is shift invariant), no separate column-sum pass
         dqkv = O.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
-                          ctx.mask[1])
+                          ctx.mask[1], lv["gbqkv"])
         O.gemm_acc_f32(dqkv, h, lv["gwqkv"], True, False)
-        O.bias_grad(dqkv, lv["gbqkv"], True)
         dh = O.gemm(dqkv, lv["wqkv"], None, ds1, False, False, 0)
         return dh, None, None, None, None, None
 

@@ -39,7 +39,7 @@ _SCHEMAS = [
     "xent_fwd_bwd(Tensor logits, Tensor labels, bool inplace, int ignore_index) -> (Tensor, Tensor)",
     "attn_fwd(Tensor qkv, Tensor? mbias, int H, int S, float scale, Tensor? kvinfo=None) -> (Tensor, Tensor)",
     "attn_bwd(Tensor qkv, Tensor? mbias, Tensor out, Tensor dout, Tensor lse, int H, int S, float scale, "
-    "Tensor? kvinfo=None) -> Tensor",
+    "Tensor? kvinfo=None, Tensor(a!)? dbias=None) -> Tensor",
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
     "gemm_gelu(Tensor x, Tensor w, Tensor bias) -> (Tensor, Tensor)",
@@ -362,7 +362,7 @@ def _attn_fwd_cpu(qkv, mbias, H, S, scale, kvinfo=None):
 
 
 @_impl("attn_bwd")
-def _attn_bwd_cpu(qkv, mbias, out, dout, lse, H, S, scale, kvinfo=None):
+def _attn_bwd_cpu(qkv, mbias, out, dout, lse, H, S, scale, kvinfo=None, dbias=None):
     q, k, v, s = _attn_probs(qkv, mbias, H, S, scale)
     B, _, _, D = q.shape
     p = torch.softmax(s, -1)
@@ -375,8 +375,12 @@ def _attn_bwd_cpu(qkv, mbias, out, dout, lse, H, S, scale, kvinfo=None):
     dq = torch.matmul(ds, k) * scale
     dk = torch.matmul(ds.transpose(-1, -2), q) * scale
     g = torch.stack([dq, dk, dv], dim=2)  # B,H,3,S,D
-    g = g.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H * D)
-    return _bf(g)
+    g = _bf(g.permute(0, 3, 2, 1, 4).reshape(B * S, 3 * H * D))
+    if dbias is not None:  # query: colsum(dQ); key: 0 (softmax shift invariance); value: colsum(dout)
+        HD = H * D
+        dbias[:HD] += g[:, :HD].float().sum(0)
+        dbias[2 * HD:] += dout.float().reshape(-1, HD).sum(0)
+    return g
 
 
 @_impl("gemm")

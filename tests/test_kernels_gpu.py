@@ -83,11 +83,21 @@ def test_attention(cuda, B, H, S):
     ref = _attn_ref(qkv_r, mask, H, S)
     assert rel(out, ref) < 1.5e-2, rel(out, ref)
     dout = torch.randn_like(out)
-    dqkv = OPS.attn_bwd(qkv, mbias, out, dout, lse, H, S, 1 / math.sqrt(D))
+    dbias = torch.full((3 * H * D,), 0.25, device=cuda)
+    dqkv = OPS.attn_bwd(qkv, mbias, out, dout, lse, H, S, 1 / math.sqrt(D), None, dbias)
     g_ref = torch.autograd.grad(ref, qkv_r, dout.float())[0]
     for part in range(3):
         sl = slice(part * H * D, (part + 1) * H * D)
         assert rel(dqkv[:, sl], g_ref[:, sl]) < 3e-2, (part, rel(dqkv[:, sl], g_ref[:, sl]))
+    # fused QKV bias gradient (accumulated): query = colsum(dQ), key = 0 exactly (softmax shift
+    # invariance: the reference's colsum(dK) is rounding noise around 0), value = colsum(dout)
+    HD = H * D
+    bref = g_ref.sum(0)
+    assert rel(dbias[:HD] - 0.25, dqkv[:, :HD].float().sum(0)) < 1e-4
+    assert rel(dbias[:HD] - 0.25, bref[:HD]) < 3e-2
+    assert torch.equal(dbias[HD:2 * HD], torch.full_like(dbias[HD:2 * HD], 0.25))
+    assert bref[HD:2 * HD].abs().max().item() < 1e-3 * bref[:HD].abs().max().item() + 1e-3
+    assert rel(dbias[2 * HD:] - 0.25, bref[2 * HD:]) < 1e-2
 
 
 def test_attention_large_logits(cuda):
