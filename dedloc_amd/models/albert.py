@@ -105,6 +105,10 @@ def _layer_prefix(g: int, i: int) -> str:
     return f"albert.encoder.albert_layer_groups.{g}.albert_layers.{i}."
 
 
+# DEDLOC_RESIDUAL=ln keeps the residual add inside the LayerNorm kernel (A/B measurement)
+_RESIDUAL_IN_GEMM = os.environ.get("DEDLOC_RESIDUAL", "gemm") != "ln"
+
+
 class _AlbertLayerFn(torch.autograd.Function):
     """One application of the shared ALBERT transformer layer with a hand-scheduled backward.
 
@@ -121,11 +125,20 @@ class _AlbertLayerFn(torch.autograd.Function):
         mbias, kvinfo = mask
         qkv = O.gemm(h, lv["wqkv"], lv["bqkv32"], None, False, True, 0)
         att, lse = O.attn_fwd(qkv, mbias, H, S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)), kvinfo)
-        a = O.gemm(att, lv["wo"], lv["bo32"], None, False, True, 0)
-        h1, s1, m1, r1 = O.layernorm_fwd(a, h, lv["ln1g"], lv["ln1b"], eps)
-        f, g = O.gemm_gelu(h1, lv["w1"], lv["b132"])  # bias + gelu_new fused in the GEMM epilogue
-        f2 = O.gemm(g, lv["w2"], lv["b232"], None, False, True, 0)
-        out, s2, m2, r2 = O.layernorm_fwd(f2, h1, lv["ln2g"], lv["ln2b"], eps)
+        if _RESIDUAL_IN_GEMM:
+            # residual sums ride in the GEMM epilogues (C = h, beta = 1): the LayerNorms then read one
+            # tensor and write one (s is the GEMM output itself) — 2 of 4 LN HBM passes removed
+            s1 = O.gemm(att, lv["wo"], lv["bo32"], h, False, True, 0)
+            h1, _, m1, r1 = O.layernorm_fwd(s1, None, lv["ln1g"], lv["ln1b"], eps)
+            f, g = O.gemm_gelu(h1, lv["w1"], lv["b132"])  # bias + gelu_new fused in the GEMM epilogue
+            s2 = O.gemm(g, lv["w2"], lv["b232"], h1, False, True, 0)
+            out, _, m2, r2 = O.layernorm_fwd(s2, None, lv["ln2g"], lv["ln2b"], eps)
+        else:
+            a = O.gemm(att, lv["wo"], lv["bo32"], None, False, True, 0)
+            h1, s1, m1, r1 = O.layernorm_fwd(a, h, lv["ln1g"], lv["ln1b"], eps)
+            f, g = O.gemm_gelu(h1, lv["w1"], lv["b132"])
+            f2 = O.gemm(g, lv["w2"], lv["b232"], None, False, True, 0)
+            out, s2, m2, r2 = O.layernorm_fwd(f2, h1, lv["ln2g"], lv["ln2b"], eps)
         ctx.save_for_backward(h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2)
         ctx.lv, ctx.mask, ctx.H, ctx.S = lv, mask, H, S
         return out
