@@ -45,6 +45,8 @@ def _peer(rank, world, port, dht_ep, out_q, cfg, mode=""):
                                    min_refresh_period=0.05, default_refresh_period=0.2, metadata_expiration=20,
                                    listen_on="127.0.0.1:*", bandwidth=100.0 + 50 * rank)
     late = rank == world - 1 and world == 3 and not aux and mode == ""
+    if mode == "kill":
+        aux = False
     if mode == "delay":
         cargs.delay_param_averaging = True
     elif mode == "hetero":
@@ -53,9 +55,12 @@ def _peer(rank, world, port, dht_ep, out_q, cfg, mode=""):
     elif mode == "churn":
         targs.peer_churn = ";;restart@2:2"  # rank 2 is preempted after global step 2 and respawned 2 s later
         targs.throttle = 0.1  # keep the survivors training (and serving state) while rank 2 is away
+    elif mode == "kill":
+        cargs.metadata_expiration = 6.0  # the dead peer drops out of the collaboration quickly
+        cargs.averaging_timeout = 4.0
     if late:
         targs.throttle = 0.0
-    else:
+    elif mode != "churn":
         targs.throttle = 0.05 if world == 3 else 0.0  # keep the early peers busy long enough to overlap
     peer = None
     if late:
@@ -72,6 +77,12 @@ def _peer(rank, world, port, dht_ep, out_q, cfg, mode=""):
             steps = 3 if world == 2 else (6 if late else 12)
             if mode == "churn":
                 steps = 8 if rank == 2 else 20
+            if mode == "kill" and rank == 2:
+                # a real process death (no clean-up, no tombstone) in the middle of training
+                peer.train(max_steps=600, stop_after_global_steps=2, max_seconds=60)
+                os.kill(os.getpid(), 9)
+            if mode == "kill":
+                steps = 8
             peer.train(max_steps=600, stop_after_global_steps=steps, max_seconds=60 if mode != "churn" else 90)
             peer.collab_opt._finish_param_round()
         res["local_step"] = peer.collab_opt.local_step
@@ -101,7 +112,7 @@ def _tiny_cfg(tmp_path):
     return str(d)
 
 
-def _run(world, tmp_path, mode=""):
+def _run(world, tmp_path, mode="", expect=None):
     from dedloc_amd.dht import DHT
 
     root = DHT(listen_on="127.0.0.1:*")
@@ -112,9 +123,11 @@ def _run(world, tmp_path, mode=""):
     procs = [ctx.Process(target=_peer, args=(r, world, port, root.endpoint, q, cfg, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=180) for _ in range(world)]
+    results = [q.get(timeout=180) for _ in range(world if expect is None else expect)]
     for p in procs:
         p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
     root.shutdown()
     return sorted(results, key=lambda r: r["rank"])
 
@@ -175,3 +188,20 @@ def test_churn_restart_rejoins_through_state_download(tmp_path):
     assert churned["state_loads"] >= 1  # lost its state -> downloaded it from a live peer
     assert churned["local_step"] >= 8 and survivor["local_step"] >= 8
     assert survivor["stats"]["global_steps"] >= 8  # the others kept training while it was away
+
+
+@pytest.mark.timeout(300)
+def test_peer_process_death_survivors_continue(tmp_path):
+    """A peer process is SIGKILLed mid-training (no tombstone, group communicator left dangling):
+    the survivors' round with it fails, they abort that communicator, move to a new data-plane
+    epoch and keep making global steps — averaging with each other once the dead peer's progress
+    record expires."""
+    res = _run(3, tmp_path, mode="kill", expect=2)
+    assert [r["rank"] for r in res] == [0, 1]
+    for r in res:
+        assert r["local_step"] >= 8, r
+    # after the death the two survivors averaged together again (group of 2 on a fresh epoch)
+    assert all(r["stats"]["averaging_rounds"] - r["stats"]["averaging_failed"] >= 3 for r in res), \
+        [r["stats"] for r in res]
+    d = (res[0]["params"] - res[1]["params"]).abs().max().item()
+    assert d < 5e-2, d
