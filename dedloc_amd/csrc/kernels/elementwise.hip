@@ -133,6 +133,59 @@ __global__ __launch_bounds__(256) void colsum_tile_kernel(const bf16_t* __restri
   }
 }
 
+// v2 of the fused GELU backward + bias-gradient column sums: straight-line per wave (no row loop):
+// each of the 8 waves of a block issues the loads of its 8 rows x 8 columns-per-lane at once, then
+// computes and stores them, so no row's loads queue behind another row's stores in the in-order
+// vmcnt (the v1 row loop waits for its own previous stores every iteration).  Block = 512 columns
+// x 64 rows; the 8 wave partials meet in LDS, one fp32 atomic per column per block.
+template <bool GELU>
+__global__ __launch_bounds__(512) void colsum_rows_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ h,
+                                                          bf16_t* __restrict__ dh, float* __restrict__ out, int rows,
+                                                          int N) {
+  constexpr int RW = 8;  // rows per wave
+  __shared__ float red[8][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int cb = blockIdx.x * 512;
+  const int c0 = cb + lane * 8;
+  const bool active = c0 < N;
+  const int rbase = blockIdx.y * (8 * RW) + w * RW;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    uint4 xr[RW], hr[RW];
+#pragma unroll
+    for (int u = 0; u < RW; ++u) {
+      const int r = min(rbase + u, rows - 1);
+      xr[u] = *reinterpret_cast<const uint4*>(x + (size_t)r * N + c0);
+      if (GELU) hr[u] = *reinterpret_cast<const uint4*>(h + (size_t)r * N + c0);
+    }
+#pragma unroll
+    for (int u = 0; u < RW; ++u) {
+      if (rbase + u >= rows) break;
+      float g[8];
+      load_bf16<8>(reinterpret_cast<const bf16_t*>(&xr[u]), g);
+      if (GELU) {
+        float v[8];
+        load_bf16<8>(reinterpret_cast<const bf16_t*>(&hr[u]), v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
+        store_bf16<8>(dh + (size_t)(rbase + u) * N + c0, g);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += g[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = acc[j];
+  __syncthreads();
+  const int c = threadIdx.x;  // 512 threads = 512 columns
+  if (cb + c < N) {
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += red[k][c];
+    atomicAdd(&out[cb + c], sum);
+  }
+}
+
 __global__ __launch_bounds__(256) void tanh_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     y[i] = f2bf(tanhf(bf2f(x[i])));
@@ -240,9 +293,14 @@ int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStre
 
 int dl_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* h, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st) {
   if (N % 8) return -1;
-  const int rpb = 256;
-  dim3 grid((N + 511) / 512, (rows + rpb - 1) / rpb);
-  colsum_tile_kernel<true, 4><<<grid, 256, 0, st>>>(dy, h, dh, dbias, rows, N, rpb);
+  if (ew_v1()) {
+    const int rpb = 256;
+    dim3 grid((N + 511) / 512, (rows + rpb - 1) / rpb);
+    colsum_tile_kernel<true, 4><<<grid, 256, 0, st>>>(dy, h, dh, dbias, rows, N, rpb);
+    return 0;
+  }
+  dim3 grid((N + 511) / 512, (rows + 63) / 64);
+  colsum_rows_kernel<true><<<grid, 512, 0, st>>>(dy, h, dh, dbias, rows, N);
   return 0;
 }
 
@@ -263,9 +321,14 @@ int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hi
     colsum_bf16_scalar_kernel<<<dim3((N + 255) / 256, nparts), 256, 0, st>>>(x, part, rows, N, rpb);
     return 0;
   }
-  const int rpb2 = 256;
-  dim3 grid((N + 511) / 512, (rows + rpb2 - 1) / rpb2);
-  colsum_tile_kernel<false, 4><<<grid, 256, 0, st>>>(x, nullptr, nullptr, part, rows, N, rpb2);
+  if (ew_v1()) {
+    const int rpb2 = 256;
+    dim3 grid((N + 511) / 512, (rows + rpb2 - 1) / rpb2);
+    colsum_tile_kernel<false, 4><<<grid, 256, 0, st>>>(x, nullptr, nullptr, part, rows, N, rpb2);
+    return 0;
+  }
+  dim3 grid((N + 511) / 512, (rows + 63) / 64);
+  colsum_rows_kernel<false><<<grid, 512, 0, st>>>(x, nullptr, nullptr, part, rows, N);
   (void)rpb;
   return 0;
 }
