@@ -52,6 +52,7 @@ def main():
     db.zero_()
     d2 = O.gelu_bwd(dy, h, db)
     print(json.dumps({"check": "v2_vs_v1", "gelu_fwd_equal": bool(torch.equal(y1, y2)),
+                      "gelu_fwd_rel": float((y1.float() - y2.float()).norm() / y1.float().norm()),
                       "gelu_bwd_equal": bool(torch.equal(d1, d2)),
                       "dbias_rel": float((db - s1).norm() / s1.norm())}), flush=True)
     for name, fn, nbytes in cases:

@@ -32,11 +32,11 @@ __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
 
+// f32 -> bf16, round-to-nearest-even, by the hardware converter (v_cvt_pk_bf16_f32): bit-identical
+// to torch's cast for every finite value and infinity, NaN stays NaN, and branch-free — the integer
+// rounding sequence with its NaN test cost VALU-bound kernels up to ~25% (bench/ew_bench.py).
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+  return __builtin_bit_cast(bf16_t, (__bf16)f);
 }
 
 // Hardware f32 -> bf16 (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN), branch-free:
@@ -106,6 +106,25 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   float t = fast_tanh(u);
   float du = k0 * (1.f + 3.f * k1 * x2);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+}
+
+// gelu_new(x) = x * sigma(2u) = x / (1 + 2^(-2 u log2 e)): one exp2 + one rcp
+__device__ __forceinline__ float gelu_tanh_sig(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * x * fmaf(k1, x * x, 1.f);
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
+}
+
+// gelu_new'(x) in the sigmoid form: gelu_new(x) = x * sigma(2u), u = k0 (x + k1 x^3), so
+// gelu_new'(x) = s + 2 x s (1 - s) u',  s = sigma(2u) = 1 / (1 + 2^(-2 u log2 e)):
+// one exp2 + one rcp and ~10 FMAs (the tanh form above needs ~15); same value to ~1e-7 relative.
+__device__ __forceinline__ float gelu_tanh_grad_sig(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = k0 * x * fmaf(k1, x2, 1.f);
+  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
+  const float du2 = (2.f * k0) * fmaf(3.f * k1, x2, 1.f);
+  return fmaf(x * du2, s - s * s, s);
 }
 
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, T1):

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict_
 // v2 (default): no grid stride — each thread owns VPT vectors of a 1024-vector block chunk and
 // issues all their loads before any math (LayerNorm's access shape, which streams at ~6.3 TB/s),
 // branch-free hardware bf16 conversion: 498 -> 389 us at T=131072 x 4096 (4.3 -> 5.5 TB/s,
-// bench/ew_bench.py, bitwise equal).  DEDLOC_EW=1 selects the grid-strided v1 (A/B).  The same
+// bench/ew_bench.py), sigmoid-form GELU (one exp2 + one rcp).  DEDLOC_EW=1 selects the grid-strided v1 (A/B).  The same
 // change to the GELU-backward column-sum kernel (8 rows in flight) measured no gain (640 vs 649 us).
 constexpr int VPT = 4;
 __global__ __launch_bounds__(256) void gelu_fwd_v2_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ y,
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_v2_kernel(const bf16_t* __restri
       float v[8];
       load_bf16<8>(reinterpret_cast<const bf16_t*>(&raw[k]), v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
+      for (int j = 0; j < 8; ++j) v[j] = gelu_tanh_sig(v[j]);
       reinterpret_cast<uint4*>(y)[i] = pack8_bf16(v);
     }
   }
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(512) void colsum_rows_kernel(const bf16_t* __restri
         float v[8];
         load_bf16<8>(reinterpret_cast<const bf16_t*>(&hr[u]), v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
+        for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad_sig(v[j])));
         store_bf16<8>(dh + (size_t)(rbase + u) * N + c0, g);
       }
 #pragma unroll
