@@ -2,6 +2,7 @@
 interleaved rounds in ONE process; box-to-box spread on this pool is up to ~10%).
 
     python bench/ab_step.py --batch 256 --ab residual     # residual add in GEMM epilogue vs in LayerNorm
+    python bench/ab_step.py --batch 256 --ab dgradwt      # dgrad GEMMs on transposed weight copies
 """
 import argparse
 import json
@@ -20,6 +21,8 @@ from bench.model_step import synthetic  # noqa: E402
 def set_variant(ab, v):
     if ab == "residual":
         albert._RESIDUAL_IN_GEMM = v == "B"
+    elif ab == "dgradwt":  # dgrad GEMMs against transposed weight copies (B) vs the plain weights (A)
+        albert._DGRAD_WT = v == "B"
     elif ab == "ew":
         os.environ["DEDLOC_EW"] = "1" if v == "A" else "2"
     else:

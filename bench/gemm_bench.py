@@ -65,6 +65,9 @@ def main():
         kinds = [("fwd", lambda: O.gemm(x, w, b, None, False, True, 0)),
                  ("dgrad", lambda: O.gemm(dy, w, None, None, False, False, 0)),
                  ("wgrad", lambda: O.gemm_acc_f32(dy, x, g, True, False))]
+        if os.environ.get("DGRAD_T"):  # dgrad against a transposed weight copy: the forward's layout
+            wt = w.t().contiguous()
+            kinds.insert(2, ("dgrad_wT", lambda: O.gemm(dy, wt, None, None, False, True, 0)))
         if name == "ffn1":
             kinds.append(("fwd_gelu", lambda: O.gemm_gelu(x, w, b)))
         if name == "ffn2":

@@ -601,22 +601,25 @@ std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tens
   return {H, G};
 }
 
-// fused FFN dgrad: C = (dy W) * gelu_new'(F), dbias += colsum(C)
-at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& F, at::Tensor dbias) {
+// fused FFN dgrad: C = (dy W) * gelu_new'(F), dbias += colsum(C).  trans_w: w holds W^T (the
+// forward-layout copy; hipBLASLt runs that "NT" form 13% faster than "NN" on the ALBERT shapes)
+at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& F, at::Tensor dbias,
+                      bool trans_w) {
   expect(F, at::kBFloat16, "F");
   expect(dbias, at::kFloat, "dbias");
+  const int64_t nout = trans_w ? w.size(0) : w.size(1);
   if (force_mfma_gemm() && mfma_ok(dy, w)) {
-    auto C = at::empty({dy.size(0), w.size(1)}, dy.options());
-    const int rc = own_gemm(0, 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0), (int)w.size(1),
-                            (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0,
-                            f32(dbias), cur_stream(dy));
+    auto C = at::empty({dy.size(0), nout}, dy.options());
+    const int rc = own_gemm(0, trans_w ? 0 : 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0),
+                            (int)nout, (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1),
+                            nullptr, 0, f32(dbias), cur_stream(dy));
     if (rc == 0) return C;
   }
   // (hipBLASLt's DGELU_BGRAD epilogue returns wrong results for this layout on ROCm 7.2 —
   // scripts/lt_debug.py — so the dgrad is a plain GEMM followed by the fused gelu'/bias-grad kernel)
   if (lt_ok(dy, w)) {
-    auto dg = at::empty({dy.size(0), w.size(1)}, dy.options());
-    DlLtArgs l = lt_args(dy, w, false, false);
+    auto dg = at::empty({dy.size(0), nout}, dy.options());
+    DlLtArgs l = lt_args(dy, w, false, trans_w);
     l.D = dg.data_ptr();
     l.ldd = dg.size(1);
     if (dl_lt_matmul(l, cur_stream(dy)) == 0) {
@@ -627,7 +630,7 @@ at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tenso
       return dh;
     }
   }
-  auto dg = at::mm(dy, w).contiguous();
+  auto dg = at::mm(dy, trans_w ? w.t() : w).contiguous();
   auto dh = at::empty_like(dg);
   check(dl_gelu_bwd_colsum(cbf(dg), cbf(F), bf(dh), f32(dbias), (int)dg.size(0), (int)dg.size(1), cur_stream(dg)),
         "gelu_bwd");

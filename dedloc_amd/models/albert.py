@@ -107,6 +107,10 @@ def _layer_prefix(g: int, i: int) -> str:
 
 # DEDLOC_RESIDUAL=ln keeps the residual add inside the LayerNorm kernel (A/B measurement)
 _RESIDUAL_IN_GEMM = os.environ.get("DEDLOC_RESIDUAL", "gemm") != "ln"
+# The backward's data-gradient GEMMs (dX = dY W) run against transposed weight copies made once per
+# encoder call (the 24 layers share them): hipBLASLt's "NT" kernels (the forward's layout) beat the
+# "NN" ones by 10-15% on these shapes (profiles/README.md).  DEDLOC_DGRAD_WT=0: plain weights.
+_DGRAD_WT = os.environ.get("DEDLOC_DGRAD_WT", "1") != "0"
 
 
 class _AlbertLayerFn(torch.autograd.Function):
@@ -152,21 +156,38 @@ class _AlbertLayerFn(torch.autograd.Function):
         # LN backward also accumulates colsum(ds) = the bias grad of the Linear that fed it
         ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True, lv["gb2"])
         O.gemm_acc_f32(ds2, g, lv["gw2"], True, False)
-        df = O.gemm_dgelu(ds2, lv["w2"], f, lv["gb1"])  # dgrad * gelu'(f) + ffn bias grad, one kernel
+        wt = "w2t" in lv  # transposed weight copies present (see _DGRAD_WT)
+        # dgrad * gelu'(f) + ffn bias grad, one kernel
+        df = O.gemm_dgelu(ds2, lv["w2t"], f, lv["gb1"], True) if wt else O.gemm_dgelu(ds2, lv["w2"], f, lv["gb1"])
         O.gemm_acc_f32(df, h1, lv["gw1"], True, False)
-        dh1 = O.gemm(df, lv["w1"], None, ds2, False, False, 0)  # residual branch folded in
+        dh1 = _dgrad(O, df, lv, "w1", ds2)  # residual branch folded in
         del df
         ds1 = O.layernorm_bwd(dh1, s1, lv["ln1g"], m1, r1, lv["gln1g"], lv["gln1b"], True, lv["gbo"])
         O.gemm_acc_f32(ds1, att, lv["gwo"], True, False)
-        datt = O.gemm(ds1, lv["wo"], None, None, False, False, 0)
+        datt = _dgrad(O, ds1, lv, "wo", None)
         H = ctx.H
         # the QKV bias gradient rides in the attention backward (query: colsum dQ, value: colsum
         # datt, key: exactly zero — softmax is shift invariant), no separate column-sum pass
         dqkv = O.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
                           ctx.mask[1], lv["gbqkv"])
         O.gemm_acc_f32(dqkv, h, lv["gwqkv"], True, False)
-        dh = O.gemm(dqkv, lv["wqkv"], None, ds1, False, False, 0)
+        dh = _dgrad(O, dqkv, lv, "wqkv", ds1)
         return dh, None, None, None, None, None
+
+
+def _dgrad(O, dy, lv, name, residual):
+    """dX = dY W (+ residual), against W^T's forward-layout copy when the layer views carry one."""
+    if name + "t" in lv:
+        return O.gemm(dy, lv[name + "t"], None, residual, False, True, 0)
+    return O.gemm(dy, lv[name], None, residual, False, False, 0)
+
+
+@torch.no_grad()
+def _with_transposed_weights(lv: Dict) -> Dict:
+    lv = dict(lv)
+    for name in ("wqkv", "wo", "w1", "w2"):
+        lv[name + "t"] = lv[name].t().contiguous()
+    return lv
 
 
 class AlbertPreTrainedModel(nn.Module):
@@ -370,6 +391,8 @@ class AlbertPreTrainedModel(nn.Module):
         m = "albert.encoder.embedding_hidden_mapping_in."
         h = ops.linear(x, f.w(m + "weight"), f.w(m + "bias"), f.g(m + "weight"), f.g(m + "bias"))
         views = [[self._layer_views(g, i) for i in range(c.inner_group_num)] for g in range(c.num_hidden_groups)]
+        if _DGRAD_WT and torch.is_grad_enabled():
+            views = [[_with_transposed_weights(lv) for lv in row] for row in views]
         per_group = c.num_hidden_layers // c.num_hidden_groups
         for layer in range(c.num_hidden_layers):
             g = int(layer / per_group)

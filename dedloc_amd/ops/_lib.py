@@ -51,7 +51,7 @@ _SCHEMAS = [
     "float eps, float momentum, bool relu, int groups=1) -> (Tensor, Tensor, Tensor)",
     "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres) "
     "-> (Tensor, Tensor, Tensor, Tensor)",
-    "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias) -> Tensor",
+    "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
     "conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor",
     "conv2d_dgrad(Tensor dy, Tensor w, int stride, int pad, int H, int W) -> Tensor",
     "conv2d_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad) -> ()",
@@ -404,8 +404,8 @@ def _gemm_gelu_cpu(x, w, bias):
 
 
 @_impl("gemm_dgelu")
-def _gemm_dgelu_cpu(dy, w, F, dbias):
-    dg = _bf(dy.float() @ w.float())
+def _gemm_dgelu_cpu(dy, w, F, dbias, trans_w=False):
+    dg = _bf(dy.float() @ (w.float().t() if trans_w else w.float()))
     return _gelu_bwd_cpu(dg, F, dbias)
 
 

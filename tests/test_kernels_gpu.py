@@ -467,6 +467,46 @@ def test_mfma_gemm_gelu_epilogues(cuda, force_mfma):
     assert rel(db, df.float().sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("policy", ["mfma", "lib"])
+def test_gemm_dgelu_transposed_weight(cuda, monkeypatch, policy):
+    """gemm_dgelu(trans_w=True) against W^T's forward-layout copy equals the plain-weight form."""
+    monkeypatch.setenv("DEDLOC_GEMM", policy)
+    torch.manual_seed(17)
+    M, H, I = 2048, 256, 1024
+    w2 = (torch.randn(H, I, device=cuda) * 0.1).bfloat16()
+    ds = torch.randn(M, H, device=cuda).bfloat16()
+    f = torch.randn(M, I, device=cuda).bfloat16()
+    db, dbt = torch.zeros(I, device=cuda), torch.zeros(I, device=cuda)
+    df = OPS.gemm_dgelu(ds, w2, f, db)
+    dft = OPS.gemm_dgelu(ds, w2.t().contiguous(), f, dbt, True)
+    fr = f.float().requires_grad_(True)
+    dref = torch.autograd.grad(F.gelu(fr, approximate="tanh"), fr, ds.float() @ w2.float())[0]
+    assert dft.shape == (M, I)
+    assert rel(dft, dref) < 2e-2 and rel(dft, df) < 1e-2
+    assert rel(dbt, dft.float().sum(0)) < 1e-3 and rel(dbt, db) < 1e-2
+
+
+def test_albert_layer_dgrad_transposed_weights(cuda):
+    """The ALBERT layer backward on transposed weight copies matches the plain-weight backward."""
+    from dedloc_amd.models import albert as A
+
+    cfg = A.AlbertConfig.tiny(hidden_size=256, intermediate_size=1024, num_attention_heads=4, num_hidden_layers=2)
+    torch.manual_seed(18)
+    model = A.AlbertForPreTraining(cfg)
+    model.materialize(cuda)
+    ids = torch.randint(5, cfg.vocab_size, (4, 128), device=cuda)
+    grads = {}
+    for wt in (False, True):
+        A._DGRAD_WT = wt
+        model.flat.grad.zero_()
+        h, _ = model.encode(ids)
+        h.float().pow(2).mean().backward()
+        grads[wt] = model.flat.grad.clone()
+    A._DGRAD_WT = True
+    assert torch.isfinite(grads[True]).all()
+    assert rel(grads[True], grads[False]) < 2e-2
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 192), (777, 1024, 320), (2048, 256, 4096)])
 def test_gemm8_pipeline_depths(cuda, force_mfma, M, N, K):
     """gemm8.hip: K-tile counts 1, 3, 5 and 64 exercise the prologue, the odd-tile buffer parity and
