@@ -97,6 +97,79 @@ __device__ __forceinline__ void tile_store(const TileRegs& t, uint8_t* tile) {
   *reinterpret_cast<uint4*>(tile + chunk_off(i1 >> 3, i1 & 7)) = t.b;
 }
 
+// ---- LDS-DMA staging ring (RING kernels) ---------------------------------------------------------
+// Each pipeline stage holds the two 64x64 tiles of one key (or query) block plus 64-128 floats of
+// per-row data, written by global_load_lds (no VGPR round trip, no ds_write).  NBUF stages: the
+// loads of stage s + NBUF - 1 are issued while stage s computes, and a counted vmcnt waits for
+// stage s only (PMC on the register-staged form: 26-43% of wave cycles parked in s_waitcnt /
+// barrier, scripts/gpu_r2_pmc.sh).  LDS-DMA writes lane-linearly (lane i -> base + 16 i), so the
+// XOR swizzle of chunk_off is applied to the SOURCE: lane i of 1-KiB piece p loads row 8p + i/8,
+// chunk (i & 7) ^ swz(row).
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int NBUF = 4;
+constexpr int STAGE = 2 * TILE_BYTES + 512;
+
+// The DMA instructions are issued from inline asm.  With __builtin_amdgcn_global_load_lds the
+// compiler's wait-count pass, which cannot tell ring slots apart, puts s_waitcnt vmcnt(0) in front
+// of the first LDS read after any in-flight DMA (seen in the ISA: before the V tr-reads), which
+// drains the whole prefetch every tile.  Hidden in asm, the DMAs are covered by the ring's own
+// counted waits; the compiler's waits for its own loads stay correct (they only get stricter).
+// M0 (the LDS base of the DMA) is written here and used by nothing else in these kernels.
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(const lds_void*)p);
+}
+__device__ __forceinline__ void dma16(const void* g, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g) : "memory", "m0");
+}
+__device__ __forceinline__ void dma4(const void* g, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(lds), "v"(g) : "memory", "m0");
+}
+
+// Prologue order in the RING kernels: issue the first NBUF-1 stages, THEN the block's compiler-visible
+// register loads (Q / dO / K / V rows, lse ...), then this real s_waitcnt vmcnt(0) (the builtin, so
+// the compiler's wait-count pass sees it): the asm DMAs are invisible to that pass, and a
+// compiler-placed partial vmcnt for those register loads inside the tile loop would drain the ring.
+// (the empty asm keeps the scheduler from sinking those loads below the wait; loads from const
+// __restrict__ arguments may still move, so values the tile loop reads are also passed through
+// `settle`, which makes the compiler complete the load before the asm and treat the register as
+// the asm's output)
+__device__ __forceinline__ void wait_vm_all() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+}
+template <typename T>
+__device__ __forceinline__ void settle(T& v) { asm volatile("" : "+v"(v)); }
+
+// this wave's two 1-KiB pieces (p = w, w + 4) of a 64-row tile starting at global row row0
+__device__ __forceinline__ void dma_tile(const bf16_t* g, long ld, int row0, uint8_t* tile, int w, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = w + 4 * j;
+    const int row = 8 * p + (lane >> 3);
+    const int c = (lane & 7) ^ swzf((row >> 1) & 7);
+    dma16(g + (long)(row0 + row) * ld + c * 8, lds_u32(tile + p * 1024));
+  }
+}
+
+// 64 consecutive floats -> 256 B of LDS (one dword per lane)
+__device__ __forceinline__ void dma_f32x64(const float* g, uint8_t* dst, int lane) {
+  dma4(g + lane, lds_u32(dst));
+}
+
+// Wait until this wave's pieces of the oldest in-flight stage have landed, leaving `ahead` later
+// stages (0..NBUF-2) in flight; npw = vector-memory ops this wave issues per stage (4 or 5).
+__device__ __forceinline__ void wait_stages(int ahead, bool five) {
+  if (five) {
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 // store 4 consecutive bf16 (8 bytes)
 __device__ __forceinline__ void store4(bf16_t* p, float a, float b, float c, float d) {
   uint2 v;
@@ -149,6 +222,21 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
   return r;
 }
 
+// Cross-half (lane L <-> L ^ 32) max / sum through v_permlane32_swap (a VALU op; __shfl_xor(x, 32)
+// is an LDS round trip on the softmax's critical path, T12).  After the swap r[0] holds, in lanes
+// 32..63, the value of lane L - 32 and r[1], in lanes 0..31, the value of lane L + 32, so one op
+// over r[0], r[1] combines the pair in every lane.
+__device__ __forceinline__ float half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  float m;
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
+  return m;
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // Forward tile loop over key tiles [kt0, kt1) of nt, with the next tile's K/V (and per-key bias)
 // prefetched through registers while this tile computes (T14).  Tile kt0 must already be staged.
 // LEAN: unmasked tiles — raw scores, the softmax scale rides in the exp FMA, no bias reads.
@@ -164,99 +252,157 @@ struct FwdCtx {
   float sl2;
   uint8_t* smem;
   float* mbs;
+  int w, lane;
+  // RING: issue stage s (key tile s) into ring slot s % NBUF
+  __device__ __forceinline__ void issue(int s) const {
+    uint8_t* slot = smem + (s % NBUF) * STAGE;
+    dma_tile(Kg, ld, s * 64, slot, w, lane);
+    dma_tile(Vg, ld, s * 64, slot + TILE_BYTES, w, lane);
+    if (mb_g) dma_f32x64(mb_g + s * 64, slot + 2 * TILE_BYTES, lane);
+  }
 };
 
 __device__ __forceinline__ float key_bias(const FwdCtx& c, int key) {
   return c.mb_g ? c.mb_g[key] : (key < c.kv_end ? 0.f : NEG_BIG);
 }
 
-template <bool LEAN>
-__device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int nt, const bf16x8 (&qf)[4],
-                                          floatx16 (&o)[2], float& m, float& l, int r, int hh, int lane) {
+// QS = 32-row query sub-blocks per wave (1 or 2).  With QS = 2 every K fragment (row reads) and V
+// fragment (tr-reads) read from LDS feeds two MFMAs, and each wave carries two independent softmax
+// chains the scheduler can interleave (the loop is latency-bound: PMC, profiles/README.md).
+template <bool LEAN, bool RING, int QS>
+__device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int nt, const bf16x8 (&qf)[QS][4],
+                                          floatx16 (&o)[QS][2], float (&m)[QS], float (&l)[QS], int r, int hh,
+                                          int lane) {
   TileRegs kr, vr;
   float mbr = 0.f;
   for (int kt = kt0; kt < kt1; ++kt) {
-    const int cur = kt & 1;
-    const uint8_t* Ks = c.smem + cur * 2 * TILE_BYTES;
+    const uint8_t* Ks;
+    const float* mb;
+    bool more = false;
+    if constexpr (RING) {
+      // stage kt landed (this wave) -> barrier: every wave's pieces landed and every wave is done
+      // with slot (kt - 1) % NBUF, which the stage issued next overwrites
+      wait_stages(min(nt - 1 - kt, NBUF - 2), c.mb_g != nullptr);
+      __syncthreads();
+      if (kt + NBUF - 1 < nt) c.issue(kt + NBUF - 1);
+      Ks = c.smem + (kt % NBUF) * STAGE;
+      mb = reinterpret_cast<const float*>(Ks + 2 * TILE_BYTES);
+    } else {
+      const int cur = kt & 1;
+      Ks = c.smem + cur * 2 * TILE_BYTES;
+      mb = c.mbs + cur * 64;
+      more = kt + 1 < nt;
+      if (more) {  // issue next tile's loads early; they land under the MFMAs below
+        tile_load(kr, c.Kg, c.ld, (kt + 1) * 64, c.S);
+        tile_load(vr, c.Vg, c.ld, (kt + 1) * 64, c.S);
+        if (threadIdx.x < 64) mbr = key_bias(c, (kt + 1) * 64 + threadIdx.x);
+      }
+    }
     const uint8_t* Vs = Ks + TILE_BYTES;
-    const float* mb = c.mbs + cur * 64;
-    const bool more = kt + 1 < nt;
-    if (more) {  // issue next tile's loads early; they land under the MFMAs below
-      tile_load(kr, c.Kg, c.ld, (kt + 1) * 64, c.S);
-      tile_load(vr, c.Vg, c.ld, (kt + 1) * 64, c.S);
-      if (threadIdx.x < 64) mbr = key_bias(c, (kt + 1) * 64 + threadIdx.x);
-    }
-    floatx16 s[2];
+    floatx16 s[QS][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[j][i] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) s[j] = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], s[j]);
-    }
-    if (!LEAN) {
+    for (int u = 0; u < QS; ++u)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[j][i] = fmaf(s[j][i], c.sl2, mb[32 * j + crow(i, hh)]);
-    }
-    float mx = vmax3(s[0][0], s[0][1], s[0][2]);
-#pragma unroll
-    for (int i = 3; i < 15; i += 2) mx = vmax3(mx, s[0][i], s[0][i + 1]);
-    mx = vmax3(mx, s[0][15], s[1][0]);
-#pragma unroll
-    for (int i = 1; i < 15; i += 2) mx = vmax3(mx, s[1][i], s[1][i + 1]);
-    mx = fmaxf(mx, s[1][15]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (LEAN) mx *= c.sl2;
-    const bool grow = mx > m + RESCALE_THR;
-    if (__ballot(grow) != 0) {  // rare after the first tile: rescale O and l to the new max
-      const float mn = grow ? mx : m;
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      l *= alpha;
-      m = mn;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[t][i] *= alpha;
-    }
-    const float nm = -m;
-    float rsa[4] = {0.f, 0.f, 0.f, 0.f};  // 4 independent add chains (latency, not issue, bound)
+        for (int i = 0; i < 16; ++i) s[u][j][i] = 0.f;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(LEAN ? fmaf(s[j][i], c.sl2, nm) : s[j][i] + nm);
-        s[j][i] = p;
-        rsa[i & 3] += p;
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 kfr = lds_row_frag(Ks, 32 * j + r, 2 * ks + hh);
+#pragma unroll
+        for (int u = 0; u < QS; ++u) s[u][j] = mfma32(kfr, qf[u][ks], s[u][j]);
       }
-    float rs = (rsa[0] + rsa[1]) + (rsa[2] + rsa[3]);
-    rs += __shfl_xor(rs, 32, 64);
-    l += rs;
+#pragma unroll
+    for (int u = 0; u < QS; ++u) {
+      if (!LEAN) {
+        if (!RING || c.mb_g) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s[u][j][i] = fmaf(s[u][j][i], c.sl2, mb[32 * j + crow(i, hh)]);
+        } else {  // RING stages carry the generic additive bias only; the length mask is computed here
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              s[u][j][i] = fmaf(s[u][j][i], c.sl2, kt * 64 + 32 * j + crow(i, hh) < c.kv_end ? 0.f : NEG_BIG);
+        }
+      }
+      // row max as four independent max3 chains of 8 scores (depth 6 instead of 16), then the halves
+      float mc[4];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const floatx16& sv = s[u][q4 >> 1];
+        const int o8 = (q4 & 1) * 8;
+        float v = vmax3(sv[o8], sv[o8 + 1], sv[o8 + 2]);
+        v = vmax3(v, sv[o8 + 3], sv[o8 + 4]);
+        v = vmax3(v, sv[o8 + 5], sv[o8 + 6]);
+        mc[q4] = v;
+      }
+      float mx = vmax3(vmax3(mc[0], mc[1], s[u][0][7]), vmax3(mc[2], mc[3], s[u][0][15]),
+                       vmax3(s[u][1][7], s[u][1][15], mc[0]));
+      mx = half_max(mx);
+      if (LEAN) mx *= c.sl2;
+      const bool grow = mx > m[u] + RESCALE_THR;
+      if (__ballot(grow) != 0) {  // rare after the first tile: rescale O and l to the new max
+        const float mn = grow ? mx : m[u];
+        const float alpha = __builtin_amdgcn_exp2f(m[u] - mn);
+        l[u] *= alpha;
+        m[u] = mn;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[u][t][i] *= alpha;
+      }
+      const float nm = -m[u];
+      float rsa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent add chains (latency bound)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float pv = __builtin_amdgcn_exp2f(LEAN ? fmaf(s[u][j][i], c.sl2, nm) : s[u][j][i] + nm);
+          s[u][j][i] = pv;
+          rsa[i & 7] += pv;
+        }
+      float rs = ((rsa[0] + rsa[1]) + (rsa[2] + rsa[3])) + ((rsa[4] + rsa[5]) + (rsa[6] + rsa[7]));
+      l[u] += half_sum(rs);
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack_acc(s[j], ss);
+        bf16x8 pb[QS];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) o[t] = mfma32(tr_operand(Vs, 32 * j + 16 * ss, hh, t, lane), pb, o[t]);
+        for (int u = 0; u < QS; ++u) pb[u] = pack_acc(s[u][j], ss);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 vfr = tr_operand(Vs, 32 * j + 16 * ss, hh, t, lane);
+#pragma unroll
+          for (int u = 0; u < QS; ++u) o[u][t] = mfma32(vfr, pb[u], o[u][t]);
+        }
       }
-    if (more) {
-      uint8_t* Kn = c.smem + (cur ^ 1) * 2 * TILE_BYTES;
-      tile_store(kr, Kn);
-      tile_store(vr, Kn + TILE_BYTES);
-      if (threadIdx.x < 64) c.mbs[(cur ^ 1) * 64 + threadIdx.x] = mbr;
+    if constexpr (!RING) {
+      if (more) {
+        uint8_t* Kn = c.smem + ((kt & 1) ^ 1) * 2 * TILE_BYTES;
+        tile_store(kr, Kn);
+        tile_store(vr, Kn + TILE_BYTES);
+        if (threadIdx.x < 64) c.mbs[((kt & 1) ^ 1) * 64 + threadIdx.x] = mbr;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
+// Block = 4 waves x QS x 32 query rows of one (batch, head).
+template <bool RING, int QS>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                           const float* __restrict__ mbias,
                                                           const int* __restrict__ kvinfo, bf16_t* __restrict__ out,
                                                           long ldo, float* __restrict__ lse, int B, int H, int S,
                                                           float sl2, int xcd) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[RING ? NBUF * STAGE : 4 * TILE_BYTES + 2 * 64 * 4];
   const BlockId bid = block_id(xcd);
   const int b = bid.b, h = bid.h;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
@@ -273,22 +419,42 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   c.sl2 = sl2;
   c.smem = smem;
   c.mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
-
-  const int q = bid.x * 128 + w * 32 + r;
-  const int qc = min(q, S - 1);
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) qf[ks] = gload8(Qg + (long)qc * ld + ks * 16 + 8 * hh);
-
-  floatx16 o[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
-  float m = NEG_BIG, l = 0.f;
+  c.w = w;
+  c.lane = lane;
 
   const int nt = (c.kv_end + 63) / 64;
-  {
+  if constexpr (RING) {
+    for (int s0 = 0; s0 < NBUF - 1 && s0 < nt; ++s0) c.issue(s0);
+  }
+  int q[QS];
+  bf16x8 qf[QS][4];
+#pragma unroll
+  for (int u = 0; u < QS; ++u) {
+    q[u] = bid.x * (128 * QS) + w * (32 * QS) + 32 * u + r;
+    const int qc = min(q[u], S - 1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[u][ks] = gload8(Qg + (long)qc * ld + ks * 16 + 8 * hh);
+    if constexpr (RING) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) settle(qf[u][ks]);
+    }
+  }
+
+  floatx16 o[QS][2];
+  float m[QS], l[QS];
+#pragma unroll
+  for (int u = 0; u < QS; ++u) {
+    m[u] = NEG_BIG;
+    l[u] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[u][t][i] = 0.f;
+  }
+
+  if constexpr (RING) {
+    wait_vm_all();
+  } else {
     TileRegs kr, vr;
     tile_load(kr, c.Kg, ld, 0, S);
     tile_load(vr, c.Vg, ld, 0, S);
@@ -296,29 +462,33 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     tile_store(kr, smem);
     tile_store(vr, smem + TILE_BYTES);
     if (threadIdx.x < 64) c.mbs[threadIdx.x] = mbr;
+    __syncthreads();
   }
-  __syncthreads();
   // lean tiles first (every tile when there is no mask), then the masked remainder: the boundary
   // tile of a length mask, or all tiles of a generic additive mask
   const int nlean = c.mb_g ? 0 : c.kv_end / 64;
-  fwd_tiles<true>(c, 0, nlean, nt, qf, o, m, l, r, hh, lane);
-  fwd_tiles<false>(c, nlean, nt, nt, qf, o, m, l, r, hh, lane);
+  fwd_tiles<true, RING, QS>(c, 0, nlean, nt, qf, o, m, l, r, hh, lane);
+  fwd_tiles<false, RING, QS>(c, nlean, nt, nt, qf, o, m, l, r, hh, lane);
 
-  if (q < S) {
-    const float inv = 1.f / l;
-    bf16_t* op = out + (rb + q) * ldo + h * HD;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+  for (int u = 0; u < QS; ++u) {
+    if (q[u] < S) {
+      const float inv = 1.f / l[u];
+      bf16_t* op = out + (rb + q[u]) * ldo + h * HD;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        store4(op + 32 * t + 8 * u + 4 * hh, o[t][4 * u] * inv, o[t][4 * u + 1] * inv, o[t][4 * u + 2] * inv,
-               o[t][4 * u + 3] * inv);
-    if (hh == 0) lse[((long)b * H + h) * S + q] = m + log2f(l);
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          store4(op + 32 * t + 8 * v + 4 * hh, o[u][t][4 * v] * inv, o[u][t][4 * v + 1] * inv,
+                 o[u][t][4 * v + 2] * inv, o[u][t][4 * v + 3] * inv);
+      if (hh == 0) lse[((long)b * H + h) * S + q[u]] = m[u] + log2f(l[u]);
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------ bwd dq
 // Also computes delta = rowsum(dO * O) for its queries and publishes it for the dkdv kernel.
+template <bool RING>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                              const float* __restrict__ mbias,
                                                              const int* __restrict__ kvinfo,
@@ -327,7 +497,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
                                                              float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                              float* __restrict__ dbias, int B, int H, int S, float sl2,
                                                              float scale, int xcd) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 4 * 64 * 4];  // tail: mask bias / bias-grad partials
+  // tail: mask bias / bias-grad partials (the epilogue reuses the first 33 KiB for its column sums)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[RING ? NBUF * STAGE : 4 * TILE_BYTES + 4 * 64 * 4];
   const BlockId bid = block_id(xcd);
   const int b = bid.b, h = bid.h;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
@@ -339,6 +510,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
   const int kv_end = kv_end_of(kvinfo, B, b, S, use_len);
   const float* mb_g = (!use_len && mbias) ? mbias + rb : nullptr;
   float* mbs = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);
+  const int nt = (kv_end + 63) / 64;
+  auto issue = [&](int st) {  // RING: key tile st -> slot st % NBUF
+    uint8_t* slot = smem + (st % NBUF) * STAGE;
+    dma_tile(Kg, ld, st * 64, slot, w, lane);
+    dma_tile(Vg, ld, st * 64, slot + TILE_BYTES, w, lane);
+    if (mb_g) dma_f32x64(mb_g + st * 64, slot + 2 * TILE_BYTES, lane);
+  };
+  if constexpr (RING) {
+    for (int s0 = 0; s0 < NBUF - 1 && s0 < nt; ++s0) issue(s0);
+  }
 
   const int q = bid.x * 128 + w * 32 + r;
   const int qc = min(q, S - 1);
@@ -354,8 +535,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
     for (int e = 0; e < 8; ++e) dl += (float)df[ks][e] * (float)of[e];
   }
   dl += __shfl_xor(dl, 32, 64);
-  const float l2 = lse[((long)b * H + h) * S + qc];
-  if (q < S && hh == 0) delta[((long)b * H + h) * S + q] = dl;
+  float l2 = lse[((long)b * H + h) * S + qc];
+  if constexpr (RING) {
+    settle(l2);
+    settle(dl);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      settle(qf[ks]);
+      settle(df[ks]);
+    }
+  }
+  // (delta is stored after the tile loop: a store issued here would sit in the vmcnt queue ahead of
+  // the ring's loads, and CDNA4 counts stores in vmcnt too)
 
   floatx16 dq[2];
 #pragma unroll
@@ -363,27 +554,39 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
 
-  const int nt = (kv_end + 63) / 64;
   TileRegs kr, vr;
   float mbr = 0.f;
-  tile_load(kr, Kg, ld, 0, S);
-  tile_load(vr, Vg, ld, 0, S);
-  if (threadIdx.x < 64) mbr = mb_g ? mb_g[threadIdx.x] : 0.f;
-  tile_store(kr, smem);
-  tile_store(vr, smem + TILE_BYTES);
-  if (threadIdx.x < 64) mbs[threadIdx.x] = mbr;
-  __syncthreads();
+  if constexpr (RING) {
+    wait_vm_all();
+  } else {
+    tile_load(kr, Kg, ld, 0, S);
+    tile_load(vr, Vg, ld, 0, S);
+    if (threadIdx.x < 64) mbr = mb_g ? mb_g[threadIdx.x] : 0.f;
+    tile_store(kr, smem);
+    tile_store(vr, smem + TILE_BYTES);
+    if (threadIdx.x < 64) mbs[threadIdx.x] = mbr;
+    __syncthreads();
+  }
 
   for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
-    const uint8_t* Ks = smem + cur * 2 * TILE_BYTES;
-    const uint8_t* Vs = Ks + TILE_BYTES;
-    const float* mb = mbs + cur * 64;
-    if (kt + 1 < nt) {
-      tile_load(kr, Kg, ld, (kt + 1) * 64, S);
-      tile_load(vr, Vg, ld, (kt + 1) * 64, S);
-      if (threadIdx.x < 64) mbr = mb_g ? mb_g[(kt + 1) * 64 + threadIdx.x] : 0.f;
+    const uint8_t* Ks;
+    const float* mb;
+    if constexpr (RING) {
+      wait_stages(min(nt - 1 - kt, NBUF - 2), mb_g != nullptr);
+      __syncthreads();
+      if (kt + NBUF - 1 < nt) issue(kt + NBUF - 1);
+      Ks = smem + (kt % NBUF) * STAGE;
+      mb = reinterpret_cast<const float*>(Ks + 2 * TILE_BYTES);
+    } else {
+      Ks = smem + (kt & 1) * 2 * TILE_BYTES;
+      mb = mbs + (kt & 1) * 64;
+      if (kt + 1 < nt) {
+        tile_load(kr, Kg, ld, (kt + 1) * 64, S);
+        tile_load(vr, Vg, ld, (kt + 1) * 64, S);
+        if (threadIdx.x < 64) mbr = mb_g ? mb_g[(kt + 1) * 64 + threadIdx.x] : 0.f;
+      }
     }
+    const uint8_t* Vs = Ks + TILE_BYTES;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       floatx16 st, dp;
@@ -416,14 +619,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
         for (int t = 0; t < 2; ++t) dq[t] = mfma32(tr_operand(Ks, 32 * j + 16 * ss, hh, t, lane), pb, dq[t]);
       }
     }
-    if (kt + 1 < nt) {
-      uint8_t* Kn = smem + (cur ^ 1) * 2 * TILE_BYTES;
-      tile_store(kr, Kn);
-      tile_store(vr, Kn + TILE_BYTES);
-      if (threadIdx.x < 64) mbs[(cur ^ 1) * 64 + threadIdx.x] = mbr;
+    if constexpr (!RING) {
+      if (kt + 1 < nt) {
+        uint8_t* Kn = smem + ((kt & 1) ^ 1) * 2 * TILE_BYTES;
+        tile_store(kr, Kn);
+        tile_store(vr, Kn + TILE_BYTES);
+        if (threadIdx.x < 64) mbs[((kt & 1) ^ 1) * 64 + threadIdx.x] = mbr;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
+  if constexpr (RING) __syncthreads();  // every wave is done with the ring before the epilogue reuses it
+  if (q < S && hh == 0) delta[((long)b * H + h) * S + q] = dl;
   if (q < S) {
     bf16_t* dp_ = dqkv + (rb + q) * ld + h * HD;
 #pragma unroll
@@ -491,6 +698,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
 }
 
 // ------------------------------------------------------------------------------------------ bwd dkdv
+template <bool RING>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                                const float* __restrict__ mbias,
                                                                const int* __restrict__ kvinfo,
@@ -499,7 +707,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
                                                                const float* __restrict__ delta,
                                                                bf16_t* __restrict__ dqkv, int B, int H, int S,
                                                                float sl2, float scale, int xcd) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * TILE_BYTES + 2 * 2 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[RING ? NBUF * STAGE : 4 * TILE_BYTES + 2 * 2 * 64 * 4];
   const BlockId bid = block_id(xcd);
   const int b = bid.b, h = bid.h;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, hh = lane >> 5;
@@ -528,13 +736,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     }
     return;
   }
+  const int nt = S / 64;
+  auto issue = [&](int st) {  // RING: query tile st -> slot st % NBUF; waves 0-1 fetch lse, 2-3 delta
+    uint8_t* slot = smem + (st % NBUF) * STAGE;
+    dma_tile(Qg, ld, st * 64, slot, w, lane);
+    dma_tile(dOg, ldo, st * 64, slot + TILE_BYTES, w, lane);
+    dma_f32x64((w < 2 ? lse_g : del_g) + st * 64, slot + 2 * TILE_BYTES + (w < 2 ? 0 : 256), lane);
+  };
+  if constexpr (RING) {
+    for (int s0 = 0; s0 < NBUF - 1 && s0 < nt; ++s0) issue(s0);
+  }
   bf16x8 kf[4], vf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     kf[ks] = gload8(Kg + (long)kc * ld + ks * 16 + 8 * hh);
     vf[ks] = gload8(Vg + (long)kc * ld + ks * 16 + 8 * hh);
   }
-  const float mbk = use_len ? (k < kv_end ? 0.f : NEG_BIG) : (mbias ? mbias[rb + kc] : 0.f);
+  float mbk = use_len ? (k < kv_end ? 0.f : NEG_BIG) : (mbias ? mbias[rb + kc] : 0.f);
+  if constexpr (RING) {
+    settle(mbk);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      settle(kf[ks]);
+      settle(vf[ks]);
+    }
+  }
 
   floatx16 dk[2], dv[2];
 #pragma unroll
@@ -542,29 +768,41 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
 #pragma unroll
     for (int i = 0; i < 16; ++i) { dk[t][i] = 0.f; dv[t][i] = 0.f; }
 
-  const int nt = S / 64;
   TileRegs qr, dr;
   float rv = 0.f;
-  tile_load(qr, Qg, ld, 0, S);
-  tile_load(dr, dOg, ldo, 0, S);
-  if (threadIdx.x < 128) rv = threadIdx.x < 64 ? lse_g[threadIdx.x] : del_g[threadIdx.x - 64];
-  tile_store(qr, smem);
-  tile_store(dr, smem + TILE_BYTES);
-  if (threadIdx.x < 128) rowv[threadIdx.x] = rv;
-  __syncthreads();
+  if constexpr (RING) {
+    wait_vm_all();
+  } else {
+    tile_load(qr, Qg, ld, 0, S);
+    tile_load(dr, dOg, ldo, 0, S);
+    if (threadIdx.x < 128) rv = threadIdx.x < 64 ? lse_g[threadIdx.x] : del_g[threadIdx.x - 64];
+    tile_store(qr, smem);
+    tile_store(dr, smem + TILE_BYTES);
+    if (threadIdx.x < 128) rowv[threadIdx.x] = rv;
+    __syncthreads();
+  }
 
   for (int qt = 0; qt < nt; ++qt) {
-    const int cur = qt & 1;
-    const uint8_t* Qs = smem + cur * 2 * TILE_BYTES;
-    const uint8_t* Ds = Qs + TILE_BYTES;
-    const float* lse_s = rowv + cur * 128;
-    const float* del_s = lse_s + 64;
-    if (qt + 1 < nt) {
-      tile_load(qr, Qg, ld, (qt + 1) * 64, S);
-      tile_load(dr, dOg, ldo, (qt + 1) * 64, S);
-      if (threadIdx.x < 128)
-        rv = threadIdx.x < 64 ? lse_g[(qt + 1) * 64 + threadIdx.x] : del_g[(qt + 1) * 64 + threadIdx.x - 64];
+    const uint8_t* Qs;
+    const float* lse_s;
+    if constexpr (RING) {
+      wait_stages(min(nt - 1 - qt, NBUF - 2), true);
+      __syncthreads();
+      if (qt + NBUF - 1 < nt) issue(qt + NBUF - 1);
+      Qs = smem + (qt % NBUF) * STAGE;
+      lse_s = reinterpret_cast<const float*>(Qs + 2 * TILE_BYTES);
+    } else {
+      Qs = smem + (qt & 1) * 2 * TILE_BYTES;
+      lse_s = rowv + (qt & 1) * 128;
+      if (qt + 1 < nt) {
+        tile_load(qr, Qg, ld, (qt + 1) * 64, S);
+        tile_load(dr, dOg, ldo, (qt + 1) * 64, S);
+        if (threadIdx.x < 128)
+          rv = threadIdx.x < 64 ? lse_g[(qt + 1) * 64 + threadIdx.x] : del_g[(qt + 1) * 64 + threadIdx.x - 64];
+      }
     }
+    const uint8_t* Ds = Qs + TILE_BYTES;
+    const float* del_s = lse_s + 64;
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2) {
       floatx16 s, dp;
@@ -593,13 +831,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
         }
       }
     }
-    if (qt + 1 < nt) {
-      uint8_t* Qn = smem + (cur ^ 1) * 2 * TILE_BYTES;
-      tile_store(qr, Qn);
-      tile_store(dr, Qn + TILE_BYTES);
-      if (threadIdx.x < 128) rowv[(cur ^ 1) * 128 + threadIdx.x] = rv;
+    if constexpr (!RING) {
+      if (qt + 1 < nt) {
+        uint8_t* Qn = smem + ((qt & 1) ^ 1) * 2 * TILE_BYTES;
+        tile_store(qr, Qn);
+        tile_store(dr, Qn + TILE_BYTES);
+        if (threadIdx.x < 128) rowv[((qt & 1) ^ 1) * 128 + threadIdx.x] = rv;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   if (k < S) {
     bf16_t* dkp = dqkv + (rb + k) * ld + (long)H * HD + h * HD;
@@ -613,6 +853,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
         store4(dvp + 32 * t + 8 * u + 4 * hh, dv[t][4 * u], dv[t][4 * u + 1], dv[t][4 * u + 2], dv[t][4 * u + 3]);
       }
   }
+}
+
+// DEDLOC_ATTN_RING=1/0 selects the LDS-DMA ring / the register-staged pipeline.  Default: the ring
+// for the 2-sub-block forward (it frees the 16 staging VGPRs that sub-block needs), registers for the
+// backward (measured equal at B=256 and 2-5% faster with padding: those loops are latency-bound).
+bool attn_ring(bool dflt) {
+  const char* e = std::getenv("DEDLOC_ATTN_RING");
+  return e ? e[0] == '1' : dflt;
+}
+
+// DEDLOC_ATTN_QS = query sub-blocks of 32 rows per wave in the forward (1 or 2; default 2)
+int attn_fwd_qs() {
+  const char* e = std::getenv("DEDLOC_ATTN_QS");
+  return (e && e[0] == '1') ? 1 : 2;
 }
 
 // DEDLOC_ATTN_XCD=0 restores the hardware block order (A/B measurement)
@@ -630,8 +884,19 @@ int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
                 int B, int H, int S, int D, float scale, hipStream_t st) {
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
-  dim3 grid((S + 127) / 128, H, B);
-  attn_fwd_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
+  const int qs = attn_fwd_qs();
+  dim3 grid((S + 128 * qs - 1) / (128 * qs), H, B);
+  if (attn_ring(qs == 2)) {
+    if (qs == 2)
+      attn_fwd_kernel<true, 2><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
+    else
+      attn_fwd_kernel<true, 1><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
+  } else {
+    if (qs == 2)
+      attn_fwd_kernel<false, 2><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
+    else
+      attn_fwd_kernel<false, 1><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
+  }
   return 0;
 }
 
@@ -641,9 +906,16 @@ int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid((S + 127) / 128, H, B);
-  attn_bwd_dq_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, dbias, B, H, S,
-                                           sl2, scale, attn_xcd());
-  attn_bwd_dkdv_kernel<<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2, scale,
-                                             attn_xcd());
+  if (attn_ring(false)) {
+    attn_bwd_dq_kernel<true><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, dbias, B,
+                                                   H, S, sl2, scale, attn_xcd());
+    attn_bwd_dkdv_kernel<true><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2,
+                                                     scale, attn_xcd());
+  } else {
+    attn_bwd_dq_kernel<false><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, dbias,
+                                                    B, H, S, sl2, scale, attn_xcd());
+    attn_bwd_dkdv_kernel<false><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S,
+                                                      sl2, scale, attn_xcd());
+  }
   return 0;
 }

@@ -7,6 +7,8 @@
 //
 // fwd:  s = x (+ r);  y = (s - mean) * rstd * gamma + beta;  saves mean/rstd (fp32) and s (bf16)
 // bwd:  ds = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)),  dgamma/dbeta column partials
+#include <cstdlib>
+
 #include "dl_common.h"
 #include "dl_kernels.h"
 
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 
 // Each block handles a contiguous chunk of rows (one wave per row, grid-strided inside the
 // block) and writes one fp32 partial row of dgamma/dbeta; dl_colsum_f32 reduces the partials.
-template <int D>
+template <int D, int R>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ ds,
@@ -97,34 +99,63 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       db[i * C::VW + j] = 0.f;
       dx[i * C::VW + j] = 0.f;
     }
-  for (int row = r0 + wid; row < r1; row += nw) {
-    const size_t base = (size_t)row * D;
-    float gy[C::EPL], xh[C::EPL];
+  // R rows per wave iteration, all R rows' loads issued before any is used: with one row in flight
+  // per wave (2 waves/SIMD) the kernel is bound by loads in flight, not by bandwidth.  (Prefetching
+  // row i+1 behind row i's stores measured slower: the stores sit ahead of the prefetch in the
+  // in-order vmcnt queue.)
+  for (int row = r0 + wid; row < r1; row += R * nw) {
+    int rr[R];
+    bool live[R];
 #pragma unroll
-    for (int i = 0; i < C::NV; ++i) {
-      load_bf16<C::VW>(dy + base + col_of<D>(lane, i), gy + i * C::VW);
-      load_bf16<C::VW>(s + base + col_of<D>(lane, i), xh + i * C::VW);
+    for (int u = 0; u < R; ++u) {
+      live[u] = row + u * nw < r1;
+      rr[u] = live[u] ? row + u * nw : row;
     }
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float a = 0.f, b = 0.f;
+    float gy[R][C::EPL], xh[R][C::EPL];
 #pragma unroll
-    for (int i = 0; i < C::EPL; ++i) {
-      xh[i] = (xh[i] - mean) * rstd;
-      dg[i] += gy[i] * xh[i];
-      db[i] += gy[i];
-      gy[i] *= g[i];
-      a += gy[i];
-      b += gy[i] * xh[i];
+    for (int u = 0; u < R; ++u) {
+      const size_t base = (size_t)rr[u] * D;
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) {
+        load_bf16<C::VW>(dy + base + col_of<D>(lane, i), gy[u] + i * C::VW);
+        load_bf16<C::VW>(s + base + col_of<D>(lane, i), xh[u] + i * C::VW);
+      }
     }
-    a = wave_sum(a) * (1.f / D);
-    b = wave_sum(b) * (1.f / D);
+    float a[R], b[R];
 #pragma unroll
-    for (int i = 0; i < C::EPL; ++i) {
-      gy[i] = bf2f(f2bf(rstd * (gy[i] - a - xh[i] * b)));
-      dx[i] += gy[i];
+    for (int u = 0; u < R; ++u) {
+      const float mean = mean_in[rr[u]], rstd = rstd_in[rr[u]];
+      const float keep = live[u] ? 1.f : 0.f;  // a duplicated row adds nothing to the column sums
+      a[u] = 0.f;
+      b[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < C::EPL; ++i) {
+        xh[u][i] = (xh[u][i] - mean) * rstd;
+        dg[i] += keep * gy[u][i] * xh[u][i];
+        db[i] += keep * gy[u][i];
+        gy[u][i] *= g[i];
+        a[u] += gy[u][i];
+        b[u] += gy[u][i] * xh[u][i];
+      }
     }
 #pragma unroll
-    for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(ds + base + col_of<D>(lane, i), gy + i * C::VW);
+    for (int u = 0; u < R; ++u) {
+      a[u] = wave_sum(a[u]) * (1.f / D);
+      b[u] = wave_sum(b[u]) * (1.f / D);
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (!live[u]) break;
+      const float rstd = rstd_in[rr[u]];
+#pragma unroll
+      for (int i = 0; i < C::EPL; ++i) {
+        gy[u][i] = bf2f(f2bf(rstd * (gy[u][i] - a[u] - xh[u][i] * b[u])));
+        dx[i] += gy[u][i];
+      }
+      const size_t base = (size_t)rr[u] * D;
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(ds + base + col_of<D>(lane, i), gy[u] + i * C::VW);
+    }
   }
   // reduce the per-wave column partials through LDS: 3 x nw x D floats
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -172,7 +203,17 @@ void launch_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const flo
   const int wpb = 4;
   const int rpb = (rows + nparts - 1) / nparts;
   size_t lds = (size_t)3 * wpb * D * sizeof(float);
-  ln_bwd_kernel<D><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
+  // DEDLOC_LN_ROWS=1|2|4: rows in flight per wave (A/B measurement); default 2
+  static const int R = [] {
+    const char* e = std::getenv("DEDLOC_LN_ROWS");
+    return e ? std::atoi(e) : 2;
+  }();
+  if (R == 4)
+    ln_bwd_kernel<D, 4><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
+  else if (R == 1)
+    ln_bwd_kernel<D, 1><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
+  else
+    ln_bwd_kernel<D, 2><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
 }
 
 }  // namespace

@@ -1,0 +1,14 @@
+#!/bin/bash
+mkdir -p gpurun_out
+export PYTHONPATH=$PWD
+step() {
+  local log=$1; shift
+  timeout -k 10 "$@" > "$log" 2>&1
+  local rc=$?
+  echo "rc=$rc $*"; grep -E '^\{|passed|failed|Error' "$log" | tail -12 | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "stopping after rc=$rc"; tail -40 "$log"; exit $rc; fi
+}
+step gpurun_out/swap_pytest.log 300 python -u -m pytest tests/test_kernels_gpu.py -q -m gpu -x -k "attn or attention" --timeout 120 --timeout-method thread
+step gpurun_out/swap_bench.log 300 python -u bench/attn_bench.py --batch 256
+DEDLOC_ATTN_RING=1 step gpurun_out/swap_bench_ring.log 300 python -u bench/attn_bench.py --batch 256
+step gpurun_out/swap_benchp.log 300 python -u bench/attn_bench.py --batch 256 --pad 0.3
