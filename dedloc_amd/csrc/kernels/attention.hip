@@ -488,7 +488,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
 
 // ------------------------------------------------------------------------------------------ bwd dq
 // Also computes delta = rowsum(dO * O) for its queries and publishes it for the dkdv kernel.
-template <bool RING>
+// QS = 32-row query sub-blocks per wave (as in the forward: every K / V fragment read from LDS
+// feeds QS MFMAs, and each wave carries QS independent chains).
+template <bool RING, int QS>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                              const float* __restrict__ mbias,
                                                              const int* __restrict__ kvinfo,
@@ -521,38 +523,45 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
     for (int s0 = 0; s0 < NBUF - 1 && s0 < nt; ++s0) issue(s0);
   }
 
-  const int q = bid.x * 128 + w * 32 + r;
-  const int qc = min(q, S - 1);
-  bf16x8 qf[4], df[4];
-  float dl = 0.f;
+  int q[QS];
+  bf16x8 qf[QS][4], df[QS][4];
+  float dl[QS], l2[QS];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    qf[ks] = gload8(Qg + (long)qc * ld + ks * 16 + 8 * hh);
-    const long oo = (rb + qc) * ldo + h * HD + ks * 16 + 8 * hh;
-    df[ks] = gload8(dout + oo);
-    const bf16x8 of = gload8(out + oo);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dl += (float)df[ks][e] * (float)of[e];
-  }
-  dl += __shfl_xor(dl, 32, 64);
-  float l2 = lse[((long)b * H + h) * S + qc];
-  if constexpr (RING) {
-    settle(l2);
-    settle(dl);
+  for (int u = 0; u < QS; ++u) {
+    q[u] = bid.x * (128 * QS) + w * (32 * QS) + 32 * u + r;
+    const int qc = min(q[u], S - 1);
+    dl[u] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      settle(qf[ks]);
-      settle(df[ks]);
+      qf[u][ks] = gload8(Qg + (long)qc * ld + ks * 16 + 8 * hh);
+      const long oo = (rb + qc) * ldo + h * HD + ks * 16 + 8 * hh;
+      df[u][ks] = gload8(dout + oo);
+      const bf16x8 of = gload8(out + oo);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dl[u] += (float)df[u][ks][e] * (float)of[e];
+    }
+    dl[u] += __shfl_xor(dl[u], 32, 64);
+    l2[u] = lse[((long)b * H + h) * S + qc];
+    if constexpr (RING) {
+      settle(l2[u]);
+      settle(dl[u]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        settle(qf[u][ks]);
+        settle(df[u][ks]);
+      }
     }
   }
   // (delta is stored after the tile loop: a store issued here would sit in the vmcnt queue ahead of
   // the ring's loads, and CDNA4 counts stores in vmcnt too)
 
-  floatx16 dq[2];
+  floatx16 dq[QS][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int u = 0; u < QS; ++u)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dq[u][t][i] = 0.f;
 
   TileRegs kr, vr;
   float mbr = 0.f;
@@ -587,36 +596,53 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
       }
     }
     const uint8_t* Vs = Ks + TILE_BYTES;
+    const bool interior = mb_g == nullptr && (kt + 1) * 64 <= kv_end;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      floatx16 st, dp;
+      floatx16 st[QS], dp[QS];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { st[i] = 0.f; dp[i] = 0.f; }
+      for (int u = 0; u < QS; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { st[u][i] = 0.f; dp[u][i] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        st = mfma32(lds_row_frag(Ks, 32 * j + r, 2 * ks + hh), qf[ks], st);
-        dp = mfma32(lds_row_frag(Vs, 32 * j + r, 2 * ks + hh), df[ks], dp);
-      }
-      if (mb_g == nullptr && (kt + 1) * 64 <= kv_end) {  // interior tile: no mask
+        const bf16x8 kfr = lds_row_frag(Ks, 32 * j + r, 2 * ks + hh);
+        const bf16x8 vfr = lds_row_frag(Vs, 32 * j + r, 2 * ks + hh);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(st[i], sl2, -l2));
-          st[i] = p * (dp[i] - dl);
+        for (int u = 0; u < QS; ++u) {
+          st[u] = mfma32(kfr, qf[u][ks], st[u]);
+          dp[u] = mfma32(vfr, df[u][ks], dp[u]);
         }
-      } else {
+      }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = kt * 64 + 32 * j + crow(i, hh);
-          const float bias = mb_g ? mb[32 * j + crow(i, hh)] : (key < kv_end ? 0.f : NEG_BIG);
-          const float p = __builtin_amdgcn_exp2f(st[i] * sl2 + bias - l2);
-          st[i] = p * (dp[i] - dl);
+      for (int u = 0; u < QS; ++u) {
+        if (interior) {  // interior tile: no mask
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(st[u][i], sl2, -l2[u]));
+            st[u][i] = p * (dp[u][i] - dl[u]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kt * 64 + 32 * j + crow(i, hh);
+            const float bias = mb_g ? mb[32 * j + crow(i, hh)] : (key < kv_end ? 0.f : NEG_BIG);
+            const float p = __builtin_amdgcn_exp2f(st[u][i] * sl2 + bias - l2[u]);
+            st[u][i] = p * (dp[u][i] - dl[u]);
+          }
         }
       }
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack_acc(st, ss);
+        bf16x8 pb[QS];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) dq[t] = mfma32(tr_operand(Ks, 32 * j + 16 * ss, hh, t, lane), pb, dq[t]);
+        for (int u = 0; u < QS; ++u) pb[u] = pack_acc(st[u], ss);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 ktr = tr_operand(Ks, 32 * j + 16 * ss, hh, t, lane);
+#pragma unroll
+          for (int u = 0; u < QS; ++u) dq[u][t] = mfma32(ktr, pb[u], dq[u][t]);
+        }
       }
     }
     if constexpr (!RING) {
@@ -630,15 +656,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
     }
   }
   if constexpr (RING) __syncthreads();  // every wave is done with the ring before the epilogue reuses it
-  if (q < S && hh == 0) delta[((long)b * H + h) * S + q] = dl;
-  if (q < S) {
-    bf16_t* dp_ = dqkv + (rb + q) * ld + h * HD;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+  for (int u = 0; u < QS; ++u) {
+    if (q[u] < S && hh == 0) delta[((long)b * H + h) * S + q[u]] = dl[u];
+    if (q[u] < S) {
+      bf16_t* dp_ = dqkv + (rb + q[u]) * ld + h * HD;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        store4(dp_ + 32 * t + 8 * u + 4 * hh, dq[t][4 * u] * scale, dq[t][4 * u + 1] * scale,
-               dq[t][4 * u + 2] * scale, dq[t][4 * u + 3] * scale);
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          store4(dp_ + 32 * t + 8 * v + 4 * hh, dq[u][t][4 * v] * scale, dq[u][t][4 * v + 1] * scale,
+                 dq[u][t][4 * v + 2] * scale, dq[u][t][4 * v + 3] * scale);
+    }
   }
   if (dbias) {
     // Fused bias gradient of the QKV projection (replaces a [T, 3H*64] column-sum pass):
@@ -646,53 +675,58 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
     //   value bias: sum_k dV[k] = sum_q dO[q] (softmax rows sum to one), from the dO this block loaded;
     //   key bias:   sum_k dK[k] = 0 exactly (sum_k dS[q,k] = delta - delta), so nothing is added.
     // Column sums through LDS (cross-lane shuffles of 64 values per lane cost more than the
-    // column-sum pass they replace): each wave writes its [32 queries][64 columns] fp32 block
-    // (16-B chunk c of row r at c ^ (r & 15): conflict-free writes and column reads), then thread
-    // (wave w', column c) sums the 32 rows of wave w' and the four partials meet in the last 1 KiB.
+    // column-sum pass they replace): per sub-block, each wave writes its [32 queries][64 columns]
+    // fp32 block (16-B chunk c of row r at c ^ (r & 15): conflict-free writes and column reads),
+    // then thread (wave w', column c) sums the 32 rows of wave w' and the four partials meet in
+    // the last 1 KiB.
     float* red = reinterpret_cast<float*>(smem);          // [4 waves][32 rows][64 columns]
     float* part = red + 4 * 32 * 64;                       // [4 waves][64 columns]
-    const bool live = q < S;
     auto chunk_addr = [&](int row, int ch) { return red + (w * 32 + row) * 64 + ((ch ^ (row & 15)) << 2); };
 #pragma unroll
-    for (int which = 0; which < 2; ++which) {
-      if (which == 0) {
+    for (int u = 0; u < QS; ++u) {
+      const bool live = q[u] < S;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+      for (int which = 0; which < 2; ++which) {
+        if (which == 0) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {  // dQ columns 32 t + 8 u + 4 hh + (0..3), as stored above
-            float4 v = float4{0.f, 0.f, 0.f, 0.f};
-            if (live)
-              v = float4{round_bf16(dq[t][4 * u] * scale), round_bf16(dq[t][4 * u + 1] * scale),
-                         round_bf16(dq[t][4 * u + 2] * scale), round_bf16(dq[t][4 * u + 3] * scale)};
-            *reinterpret_cast<float4*>(chunk_addr(r, 8 * t + 2 * u + hh)) = v;
-          }
-      } else {
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
+            for (int v4 = 0; v4 < 4; ++v4) {  // dQ columns 32 t + 8 v4 + 4 hh + (0..3), as stored above
+              float4 v = float4{0.f, 0.f, 0.f, 0.f};
+              if (live)
+                v = float4{round_bf16(dq[u][t][4 * v4] * scale), round_bf16(dq[u][t][4 * v4 + 1] * scale),
+                           round_bf16(dq[u][t][4 * v4 + 2] * scale), round_bf16(dq[u][t][4 * v4 + 3] * scale)};
+              *reinterpret_cast<float4*>(chunk_addr(r, 8 * t + 2 * v4 + hh)) = v;
+            }
+        } else {
 #pragma unroll
-          for (int g = 0; g < 2; ++g) {  // dO columns 16 ks + 8 hh + 4 g + (0..3), as loaded above
-            float4 v = float4{0.f, 0.f, 0.f, 0.f};
-            if (live)
-              v = float4{(float)df[ks][4 * g], (float)df[ks][4 * g + 1], (float)df[ks][4 * g + 2],
-                         (float)df[ks][4 * g + 3]};
-            *reinterpret_cast<float4*>(chunk_addr(r, 4 * ks + 2 * hh + g)) = v;
-          }
-      }
-      __syncthreads();
-      {
-        const int c = lane;  // this thread: column c of wave w's 32 rows
-        float sum = 0.f;
+          for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {  // dO columns 16 ks + 8 hh + 4 g + (0..3), as loaded above
+              float4 v = float4{0.f, 0.f, 0.f, 0.f};
+              if (live)
+                v = float4{(float)df[u][ks][4 * g], (float)df[u][ks][4 * g + 1], (float)df[u][ks][4 * g + 2],
+                           (float)df[u][ks][4 * g + 3]};
+              *reinterpret_cast<float4*>(chunk_addr(r, 4 * ks + 2 * hh + g)) = v;
+            }
+        }
+        __syncthreads();
+        {
+          const int c = lane;  // this thread: column c of wave w's 32 rows
+          float sum = 0.f;
 #pragma unroll 8
-        for (int row = 0; row < 32; ++row) sum += red[(w * 32 + row) * 64 + (((c >> 2) ^ (row & 15)) << 2) + (c & 3)];
-        part[w * 64 + c] = sum;
+          for (int row = 0; row < 32; ++row)
+            sum += red[(w * 32 + row) * 64 + (((c >> 2) ^ (row & 15)) << 2) + (c & 3)];
+          part[w * 64 + c] = sum;
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+          const int c = threadIdx.x;
+          atomicAdd(&dbias[(which ? 2L * H * HD : 0L) + h * HD + c],
+                    part[c] + part[64 + c] + part[128 + c] + part[192 + c]);
+        }
+        __syncthreads();
       }
-      __syncthreads();
-      if (threadIdx.x < 64) {
-        const int c = threadIdx.x;
-        atomicAdd(&dbias[(which ? 2L * H * HD : 0L) + h * HD + c],
-                  part[c] + part[64 + c] + part[128 + c] + part[192 + c]);
-      }
-      __syncthreads();
     }
   }
 }
@@ -869,6 +903,12 @@ int attn_fwd_qs() {
   return (e && e[0] == '1') ? 1 : 2;
 }
 
+// DEDLOC_ATTN_DQ_QS = query sub-blocks per wave in the dQ backward kernel (1 or 2; default 2)
+int attn_dq_qs() {
+  const char* e = std::getenv("DEDLOC_ATTN_DQ_QS");
+  return (e && e[0] == '1') ? 1 : 2;
+}
+
 // DEDLOC_ATTN_XCD=0 restores the hardware block order (A/B measurement)
 int attn_xcd() {
   static const int v = [] {
@@ -906,16 +946,26 @@ int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid((S + 127) / 128, H, B);
-  if (attn_ring(false)) {
-    attn_bwd_dq_kernel<true><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, dbias, B,
-                                                   H, S, sl2, scale, attn_xcd());
+  const int qs = attn_dq_qs();
+  dim3 grid_dq((S + 128 * qs - 1) / (128 * qs), H, B);
+  const bool ring_dq = attn_ring(qs == 2);
+  if (qs == 2 && ring_dq)
+    attn_bwd_dq_kernel<true, 2><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
+                                                         dbias, B, H, S, sl2, scale, attn_xcd());
+  else if (qs == 2)
+    attn_bwd_dq_kernel<false, 2><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
+                                                          dbias, B, H, S, sl2, scale, attn_xcd());
+  else if (ring_dq)
+    attn_bwd_dq_kernel<true, 1><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
+                                                         dbias, B, H, S, sl2, scale, attn_xcd());
+  else
+    attn_bwd_dq_kernel<false, 1><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
+                                                          dbias, B, H, S, sl2, scale, attn_xcd());
+  if (attn_ring(false))
     attn_bwd_dkdv_kernel<true><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2,
                                                      scale, attn_xcd());
-  } else {
-    attn_bwd_dq_kernel<false><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv, dbias,
-                                                    B, H, S, sl2, scale, attn_xcd());
+  else
     attn_bwd_dkdv_kernel<false><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S,
                                                       sl2, scale, attn_xcd());
-  }
   return 0;
 }
