@@ -179,6 +179,47 @@ def test_attention_deferred_rescale_ramp(cuda):
     assert rel(dqkv, g_ref) < 3e-2
 
 
+VARIANTS = [  # (forward sub-blocks, dQ sub-blocks, staging) — every kernel form the dispatcher can pick
+    {"DEDLOC_ATTN_QS": "1", "DEDLOC_ATTN_DQ_QS": "1", "DEDLOC_ATTN_RING": "0"},
+    {"DEDLOC_ATTN_QS": "1", "DEDLOC_ATTN_DQ_QS": "1", "DEDLOC_ATTN_RING": "1"},
+    {"DEDLOC_ATTN_QS": "2", "DEDLOC_ATTN_DQ_QS": "2", "DEDLOC_ATTN_RING": "0"},
+    {"DEDLOC_ATTN_QS": "2", "DEDLOC_ATTN_DQ_QS": "2"},  # default staging per kernel
+]
+
+
+@pytest.mark.parametrize("variant", range(len(VARIANTS)))
+@pytest.mark.parametrize("S,lens,generic", [(192, (192, 100, 64), False), (512, (512, 300, 17), False),
+                                             (256, (256, 130, 200), True)])
+def test_attention_kernel_variants(cuda, monkeypatch, variant, S, lens, generic):
+    """Register-staged vs LDS-DMA ring staging and one vs two query sub-blocks per wave, forward and
+    backward (incl. the fused QKV bias gradient), on length masks and on the generic additive bias;
+    S = 192 leaves the last 256-query block of the two-sub-block kernels partly empty."""
+    torch.manual_seed(11)
+    B, H, D = len(lens), 2, 64
+    qkv = (torch.randn(B * S, 3 * H * D, device=cuda) * 1.5).bfloat16()
+    mask = (torch.arange(S, device=cuda)[None, :] < torch.tensor(lens, device=cuda)[:, None]).long()
+    if generic:
+        mask[0, 5:9] = 0  # a hole: not a prefix mask -> the additive-bias path
+    mbias = torch.where(mask.bool(), 0.0, -1e30).float()
+    kvinfo = _kvinfo(mask)
+    for k, v in VARIANTS[variant].items():
+        monkeypatch.setenv(k, v)
+    out, lse = OPS.attn_fwd(qkv, mbias, H, S, 1 / math.sqrt(D), kvinfo)
+    qkv_r = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qkv_r, mask, H, S)
+    assert rel(out, ref) < 1.5e-2, rel(out, ref)
+    dout = torch.randn_like(out)
+    dbias = torch.zeros(3 * H * D, device=cuda)
+    dqkv = OPS.attn_bwd(qkv, mbias, out, dout, lse, H, S, 1 / math.sqrt(D), kvinfo, dbias)
+    g_ref = torch.autograd.grad(ref, qkv_r, dout.float())[0]
+    for part in range(3):
+        sl = slice(part * H * D, (part + 1) * H * D)
+        assert rel(dqkv[:, sl], g_ref[:, sl]) < 3e-2, (part, rel(dqkv[:, sl], g_ref[:, sl]))
+    HD = H * D
+    assert rel(dbias[:HD], dqkv[:, :HD].float().sum(0)) < 1e-4
+    assert rel(dbias[2 * HD:], dout.float().sum(0)) < 1e-4
+
+
 def test_embedding(cuda):
     torch.manual_seed(2)
     B, S, E, V = 4, 128, 128, 1000
