@@ -732,15 +732,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16_t* __res
 }
 
 // ------------------------------------------------------------------------------------------ bwd dkdv
-template <bool RING>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __restrict__ qkv, long ld,
-                                                               const float* __restrict__ mbias,
-                                                               const int* __restrict__ kvinfo,
-                                                               const bf16_t* __restrict__ dout, long ldo,
-                                                               const float* __restrict__ lse,
-                                                               const float* __restrict__ delta,
-                                                               bf16_t* __restrict__ dqkv, int B, int H, int S,
-                                                               float sl2, float scale, int xcd) {
+// KS = 32-key sub-blocks per wave: with KS = 2 every Q / dO fragment read from LDS feeds two
+// MFMAs; the dK/dV accumulators (128 registers) need the whole 512-entry register file, so that
+// form runs one wave per SIMD (launch bound 256 x 1) and hides latency by ILP instead of waves.
+template <bool RING, int KS>
+__global__ __launch_bounds__(256, KS == 2 ? 1 : 2) void attn_bwd_dkdv_kernel(
+    const bf16_t* __restrict__ qkv, long ld, const float* __restrict__ mbias, const int* __restrict__ kvinfo,
+    const bf16_t* __restrict__ dout, long ldo, const float* __restrict__ lse, const float* __restrict__ delta,
+    bf16_t* __restrict__ dqkv, int B, int H, int S, float sl2, float scale, int xcd) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[RING ? NBUF * STAGE : 4 * TILE_BYTES + 2 * 2 * 64 * 4];
   const BlockId bid = block_id(xcd);
   const int b = bid.b, h = bid.h;
@@ -754,18 +753,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
   const float* del_g = delta + ((long)b * H + h) * S;
   float* rowv = reinterpret_cast<float*>(smem + 4 * TILE_BYTES);  // [2 buf][lse 64 | delta 64]
 
-  const int k = bid.x * 128 + w * 32 + r;
-  const int kc = min(k, S - 1);
+  int k[KS];
+#pragma unroll
+  for (int u = 0; u < KS; ++u) k[u] = bid.x * (128 * KS) + w * (32 * KS) + 32 * u + r;
   bool use_len;
   const int kv_end = kv_end_of(kvinfo, B, b, S, use_len);
-  if (use_len && bid.x * 128 >= kv_end) {  // every key of this block is padding: dK = dV = 0
-    if (k < S) {
-      bf16_t* dkp = dqkv + (rb + k) * ld + (long)H * HD + h * HD;
-      bf16_t* dvp = dqkv + (rb + k) * ld + 2L * H * HD + h * HD;
+  if (use_len && bid.x * (128 * KS) >= kv_end) {  // every key of this block is padding: dK = dV = 0
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {  // the same 64 columns the regular epilogue covers (32t + 8u' + 4hh)
-        store4(dkp + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
-        store4(dvp + 8 * u + 4 * hh, 0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < KS; ++u) {
+      if (k[u] < S) {
+        bf16_t* dkp = dqkv + (rb + k[u]) * ld + (long)H * HD + h * HD;
+        bf16_t* dvp = dqkv + (rb + k[u]) * ld + 2L * H * HD + h * HD;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {  // the same 64 columns the regular epilogue covers (32t + 8v' + 4hh)
+          store4(dkp + 8 * v + 4 * hh, 0.f, 0.f, 0.f, 0.f);
+          store4(dvp + 8 * v + 4 * hh, 0.f, 0.f, 0.f, 0.f);
+        }
       }
     }
     return;
@@ -780,27 +783,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
   if constexpr (RING) {
     for (int s0 = 0; s0 < NBUF - 1 && s0 < nt; ++s0) issue(s0);
   }
-  bf16x8 kf[4], vf[4];
+  bf16x8 kf[KS][4], vf[KS][4];
+  float mbk[KS];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    kf[ks] = gload8(Kg + (long)kc * ld + ks * 16 + 8 * hh);
-    vf[ks] = gload8(Vg + (long)kc * ld + ks * 16 + 8 * hh);
-  }
-  float mbk = use_len ? (k < kv_end ? 0.f : NEG_BIG) : (mbias ? mbias[rb + kc] : 0.f);
-  if constexpr (RING) {
-    settle(mbk);
+  for (int u = 0; u < KS; ++u) {
+    const int kc = min(k[u], S - 1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      settle(kf[ks]);
-      settle(vf[ks]);
+      kf[u][ks] = gload8(Kg + (long)kc * ld + ks * 16 + 8 * hh);
+      vf[u][ks] = gload8(Vg + (long)kc * ld + ks * 16 + 8 * hh);
+    }
+    mbk[u] = use_len ? (k[u] < kv_end ? 0.f : NEG_BIG) : (mbias ? mbias[rb + kc] : 0.f);
+    if constexpr (RING) {
+      settle(mbk[u]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        settle(kf[u][ks]);
+        settle(vf[u][ks]);
+      }
     }
   }
 
-  floatx16 dk[2], dv[2];
+  floatx16 dk[KS][2], dv[KS][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int u = 0; u < KS; ++u)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { dk[t][i] = 0.f; dv[t][i] = 0.f; }
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { dk[u][t][i] = 0.f; dv[u][t][i] = 0.f; }
 
   TileRegs qr, dr;
   float rv = 0.f;
@@ -839,29 +849,47 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
     const float* del_s = lse_s + 64;
 #pragma unroll
     for (int i2 = 0; i2 < 2; ++i2) {
-      floatx16 s, dp;
+      floatx16 sc[KS], dp[KS];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { s[i] = 0.f; dp[i] = 0.f; }
+      for (int u = 0; u < KS; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sc[u][i] = 0.f; dp[u][i] = 0.f; }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        s = mfma32(lds_row_frag(Qs, 32 * i2 + r, 2 * ks + hh), kf[ks], s);
-        dp = mfma32(lds_row_frag(Ds, 32 * i2 + r, 2 * ks + hh), vf[ks], dp);
+        const bf16x8 qfr = lds_row_frag(Qs, 32 * i2 + r, 2 * ks + hh);
+        const bf16x8 dfr = lds_row_frag(Ds, 32 * i2 + r, 2 * ks + hh);
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+          sc[u] = mfma32(qfr, kf[u][ks], sc[u]);
+          dp[u] = mfma32(dfr, vf[u][ks], dp[u]);
+        }
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qq = 32 * i2 + crow(i, hh);
-        const float p = __builtin_amdgcn_exp2f(s[i] * sl2 + mbk - lse_s[qq]);
-        s[i] = p;
-        dp[i] = p * (dp[i] - del_s[qq]);
-      }
+      for (int u = 0; u < KS; ++u)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qq = 32 * i2 + crow(i, hh);
+          const float p = __builtin_amdgcn_exp2f(sc[u][i] * sl2 + mbk[u] - lse_s[qq]);
+          sc[u][i] = p;
+          dp[u][i] = p * (dp[u][i] - del_s[qq]);
+        }
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack_acc(s, ss);
-        const bf16x8 db = pack_acc(dp, ss);
+        bf16x8 pb[KS], db[KS];
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+          pb[u] = pack_acc(sc[u], ss);
+          db[u] = pack_acc(dp[u], ss);
+        }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          dv[t] = mfma32(tr_operand(Ds, 32 * i2 + 16 * ss, hh, t, lane), pb, dv[t]);
-          dk[t] = mfma32(tr_operand(Qs, 32 * i2 + 16 * ss, hh, t, lane), db, dk[t]);
+          const bf16x8 dtr = tr_operand(Ds, 32 * i2 + 16 * ss, hh, t, lane);
+          const bf16x8 qtr = tr_operand(Qs, 32 * i2 + 16 * ss, hh, t, lane);
+#pragma unroll
+          for (int u = 0; u < KS; ++u) {
+            dv[u][t] = mfma32(dtr, pb[u], dv[u][t]);
+            dk[u][t] = mfma32(qtr, db[u], dk[u][t]);
+          }
         }
       }
     }
@@ -875,17 +903,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16_t* __r
       __syncthreads();
     }
   }
-  if (k < S) {
-    bf16_t* dkp = dqkv + (rb + k) * ld + (long)H * HD + h * HD;
-    bf16_t* dvp = dqkv + (rb + k) * ld + 2L * H * HD + h * HD;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+  for (int u = 0; u < KS; ++u) {
+    if (k[u] < S) {
+      bf16_t* dkp = dqkv + (rb + k[u]) * ld + (long)H * HD + h * HD;
+      bf16_t* dvp = dqkv + (rb + k[u]) * ld + 2L * H * HD + h * HD;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        store4(dkp + 32 * t + 8 * u + 4 * hh, dk[t][4 * u] * scale, dk[t][4 * u + 1] * scale,
-               dk[t][4 * u + 2] * scale, dk[t][4 * u + 3] * scale);
-        store4(dvp + 32 * t + 8 * u + 4 * hh, dv[t][4 * u], dv[t][4 * u + 1], dv[t][4 * u + 2], dv[t][4 * u + 3]);
-      }
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          store4(dkp + 32 * t + 8 * v + 4 * hh, dk[u][t][4 * v] * scale, dk[u][t][4 * v + 1] * scale,
+                 dk[u][t][4 * v + 2] * scale, dk[u][t][4 * v + 3] * scale);
+          store4(dvp + 32 * t + 8 * v + 4 * hh, dv[u][t][4 * v], dv[u][t][4 * v + 1], dv[u][t][4 * v + 2],
+                 dv[u][t][4 * v + 3]);
+        }
+    }
   }
 }
 
@@ -907,6 +939,13 @@ int attn_fwd_qs() {
 int attn_dq_qs() {
   const char* e = std::getenv("DEDLOC_ATTN_DQ_QS");
   return (e && e[0] == '1') ? 1 : 2;
+}
+
+// DEDLOC_ATTN_DKDV_KS = key sub-blocks per wave in the dK/dV kernel (1 or 2; default 1: the
+// one-wave-per-SIMD KS=2 form measured 8% slower, profiles/README.md)
+int attn_dkdv_ks() {
+  const char* e = std::getenv("DEDLOC_ATTN_DKDV_KS");
+  return (e && e[0] == '2') ? 2 : 1;
 }
 
 // DEDLOC_ATTN_XCD=0 restores the hardware block order (A/B measurement)
@@ -961,11 +1000,16 @@ int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
   else
     attn_bwd_dq_kernel<false, 1><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
                                                           dbias, B, H, S, sl2, scale, attn_xcd());
-  if (attn_ring(false))
-    attn_bwd_dkdv_kernel<true><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S, sl2,
-                                                     scale, attn_xcd());
+  const int ks = attn_dkdv_ks();
+  dim3 grid_kv((S + 128 * ks - 1) / (128 * ks), H, B);
+  if (ks == 2)
+    attn_bwd_dkdv_kernel<true, 2><<<grid_kv, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H,
+                                                           S, sl2, scale, attn_xcd());
+  else if (attn_ring(false))
+    attn_bwd_dkdv_kernel<true, 1><<<grid_kv, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H,
+                                                           S, sl2, scale, attn_xcd());
   else
-    attn_bwd_dkdv_kernel<false><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H, S,
-                                                      sl2, scale, attn_xcd());
+    attn_bwd_dkdv_kernel<false, 1><<<grid_kv, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H,
+                                                            S, sl2, scale, attn_xcd());
   return 0;
 }

@@ -184,6 +184,7 @@ VARIANTS = [  # (forward sub-blocks, dQ sub-blocks, staging) — every kernel fo
     {"DEDLOC_ATTN_QS": "1", "DEDLOC_ATTN_DQ_QS": "1", "DEDLOC_ATTN_RING": "1"},
     {"DEDLOC_ATTN_QS": "2", "DEDLOC_ATTN_DQ_QS": "2", "DEDLOC_ATTN_RING": "0"},
     {"DEDLOC_ATTN_QS": "2", "DEDLOC_ATTN_DQ_QS": "2"},  # default staging per kernel
+    {"DEDLOC_ATTN_DKDV_KS": "2"},  # two key sub-blocks per wave, one wave per SIMD (AGPR accumulators)
 ]
 
 
