@@ -9,6 +9,8 @@
 #include <c10/hip/HIPStream.h>
 
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "dl_kernels.h"
 #include "dl_lt.h"
@@ -571,6 +573,49 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
   gemm_acc_f32_split(a, b, c, trans_a, trans_b, 8);
 }
 
+// Weight gradient of a weight that several consecutive backward calls share (ALBERT's one layer,
+// applied 24 times): the token-split fp32 slabs of gemm_acc_f32 persist across the calls — the
+// first call writes them (beta = 0), later calls accumulate (beta = 1) — and are added into the
+// gradient once, by the last call.  That replaces 24 slab-sum passes per weight and micro-step
+// by one.  Without the split form (no hipBLASLt plan, one slice) every call accumulates directly.
+at::Tensor& shared_slabs(const at::Tensor& c, int64_t S) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, at::Tensor> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  at::Tensor& t = cache[c.data_ptr()];
+  if (!t.defined() || t.size(0) != S || t.size(1) != c.size(0) || t.size(2) != c.size(1) || t.device() != c.device())
+    t = at::empty({S, c.size(0), c.size(1)}, c.options());
+  return t;
+}
+
+void gemm_acc_f32_shared(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b,
+                         bool first, bool last) {
+  expect(c, at::kFloat, "c");
+  if (!force_mfma_gemm() && lt_ok(a, b) && trans_a && !trans_b && c.is_contiguous()) {
+    DlLtArgs l = lt_args(a, b, trans_a, trans_b);
+    const int S = wgrad_splits(l.M, l.N, l.K, 8);
+    if (S > 1) {
+      at::Tensor& slabs = shared_slabs(c, S);
+      const long kslice = l.K / S;
+      l.K = (int)kslice;
+      l.batch = S;
+      l.strideA = kslice * l.lda;
+      l.strideB = kslice * l.ldb;
+      l.strideD = (long)l.M * l.N;
+      l.D = slabs.data_ptr();
+      l.ldd = l.N;
+      l.d_f32 = 1;
+      l.beta = first ? 0.f : 1.f;
+      if (dl_lt_matmul(l, cur_stream(a)) == 0) {
+        if (last) check(dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), cur_stream(a)), "sum_slabs");
+        return;
+      }
+      TORCH_CHECK(first, "gemm_acc_f32_shared: hipBLASLt failed after earlier calls accumulated into the slabs");
+    }
+  }
+  gemm_acc_f32_split(a, b, c, trans_a, trans_b, 8);
+}
+
 // fused FFN-up: H = x W^T + b (pre-activation, kept for backward), G = gelu_new(H)
 std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias) {
   auto H = at::empty({x.size(0), w.size(0)}, x.options());
@@ -956,6 +1001,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("attn_bwd", &attn_bwd);
   m.impl("gemm", &gemm);
   m.impl("gemm_acc_f32", &gemm_acc_f32);
+  m.impl("gemm_acc_f32_shared", &gemm_acc_f32_shared);
   m.impl("gemm_gelu", &gemm_gelu);
   m.impl("gemm_dgelu", &gemm_dgelu);
 }

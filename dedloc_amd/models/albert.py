@@ -111,6 +111,10 @@ _RESIDUAL_IN_GEMM = os.environ.get("DEDLOC_RESIDUAL", "gemm") != "ln"
 # encoder call (the 24 layers share them): hipBLASLt's "NT" kernels (the forward's layout) beat the
 # "NN" ones by 10-15% on these shapes (profiles/README.md).  DEDLOC_DGRAD_WT=0: plain weights.
 _DGRAD_WT = os.environ.get("DEDLOC_DGRAD_WT", "1") != "0"
+# Weight gradients of the shared layer keep their token-split fp32 slabs across the layer
+# applications and add them into the flat gradient once, at the last backward call
+# (gemm_acc_f32_shared).  DEDLOC_SHARED_WGRAD=0: one slab sum per call.
+_SHARED_WGRAD = os.environ.get("DEDLOC_SHARED_WGRAD", "1") != "0"
 
 
 class _AlbertLayerFn(torch.autograd.Function):
@@ -155,24 +159,33 @@ class _AlbertLayerFn(torch.autograd.Function):
         dy = dy.contiguous()
         # LN backward also accumulates colsum(ds) = the bias grad of the Linear that fed it
         ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True, lv["gb2"])
-        O.gemm_acc_f32(ds2, g, lv["gw2"], True, False)
+        _wgrad(O, ds2, g, lv, "gw2")
         wt = "w2t" in lv  # transposed weight copies present (see _DGRAD_WT)
         # dgrad * gelu'(f) + ffn bias grad, one kernel
         df = O.gemm_dgelu(ds2, lv["w2t"], f, lv["gb1"], True) if wt else O.gemm_dgelu(ds2, lv["w2"], f, lv["gb1"])
-        O.gemm_acc_f32(df, h1, lv["gw1"], True, False)
+        _wgrad(O, df, h1, lv, "gw1")
         dh1 = _dgrad(O, df, lv, "w1", ds2)  # residual branch folded in
         del df
         ds1 = O.layernorm_bwd(dh1, s1, lv["ln1g"], m1, r1, lv["gln1g"], lv["gln1b"], True, lv["gbo"])
-        O.gemm_acc_f32(ds1, att, lv["gwo"], True, False)
+        _wgrad(O, ds1, att, lv, "gwo")
         datt = _dgrad(O, ds1, lv, "wo", None)
         H = ctx.H
         # the QKV bias gradient rides in the attention backward (query: colsum dQ, value: colsum
         # datt, key: exactly zero — softmax is shift invariant), no separate column-sum pass
         dqkv = O.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
                           ctx.mask[1], lv["gbqkv"])
-        O.gemm_acc_f32(dqkv, h, lv["gwqkv"], True, False)
+        _wgrad(O, dqkv, h, lv, "gwqkv")
         dh = _dgrad(O, dqkv, lv, "wqkv", ds1)
         return dh, None, None, None, None, None
+
+
+def _wgrad(O, dy, x, lv, name):
+    """lv[name] += dY^T X; with the layer's position among the applications of its weights
+    (``wg_first`` / ``wg_last``, set by encode) the slab sum is deferred to the last backward call."""
+    if "wg_first" in lv:
+        O.gemm_acc_f32_shared(dy, x, lv[name], True, False, lv["wg_first"], lv["wg_last"])
+    else:
+        O.gemm_acc_f32(dy, x, lv[name], True, False)
 
 
 def _dgrad(O, dy, lv, name, residual):
@@ -394,10 +407,17 @@ class AlbertPreTrainedModel(nn.Module):
         if _DGRAD_WT and torch.is_grad_enabled():
             views = [[_with_transposed_weights(lv) for lv in row] for row in views]
         per_group = c.num_hidden_layers // c.num_hidden_groups
+        group_of = [int(layer / per_group) for layer in range(c.num_hidden_layers)]
         for layer in range(c.num_hidden_layers):
-            g = int(layer / per_group)
+            g = group_of[layer]
+            uses = [x for x in range(c.num_hidden_layers) if group_of[x] == g]
             for i in range(c.inner_group_num):
-                h = self._albert_layer(h, views[g][i], mask, Sp)
+                lv = views[g][i]
+                if _SHARED_WGRAD and torch.is_grad_enabled():
+                    # backward runs the layers in reverse: the last application is the first to
+                    # write the weight's gradient slabs, the first application sums them in
+                    lv = dict(lv, wg_first=layer == uses[-1], wg_last=layer == uses[0])
+                h = self._albert_layer(h, lv, mask, Sp)
         return h, Sp
 
     def num_parameters(self) -> int:

@@ -42,6 +42,7 @@ _SCHEMAS = [
     "Tensor? kvinfo=None, Tensor(a!)? dbias=None) -> Tensor",
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
+    "gemm_acc_f32_shared(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b, bool first, bool last) -> ()",
     "gemm_gelu(Tensor x, Tensor w, Tensor bias) -> (Tensor, Tensor)",
     "sinkhorn(Tensor scores, int bs, float eps, int iters) -> Tensor",
     "swav_ce(Tensor scores, Tensor q, Tensor(a!) dscores, Tensor(b!) loss, float temperature, float scale) -> ()",
@@ -414,6 +415,11 @@ def _gemm_acc_cpu(a, b, c, trans_a, trans_b):
     A = a.float().t() if trans_a else a.float()
     Bm = b.float().t() if trans_b else b.float()
     c.add_(A @ Bm)
+
+
+@_impl("gemm_acc_f32_shared")
+def _gemm_acc_shared_cpu(a, b, c, trans_a, trans_b, first, last):
+    _gemm_acc_cpu(a, b, c, trans_a, trans_b)  # same sum; the slab deferral is a GPU-side schedule
 
 
 @_impl("sinkhorn")

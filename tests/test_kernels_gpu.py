@@ -549,6 +549,34 @@ def test_albert_layer_dgrad_transposed_weights(cuda):
     assert rel(grads[True], grads[False]) < 2e-2
 
 
+@pytest.mark.parametrize("groups", [1, 2])
+def test_albert_shared_weight_gradient_slabs(cuda, groups):
+    """Deferred slab sums of the shared layer's weight gradients (gemm_acc_f32_shared) match one
+    slab sum per layer call, over two backward passes (the first call of each pass resets the
+    slabs) and with two layer groups (each group's weights have their own first / last call)."""
+    from dedloc_amd.models import albert as A
+
+    cfg = A.AlbertConfig.tiny(hidden_size=256, intermediate_size=1024, num_attention_heads=4, num_hidden_layers=4,
+                              num_hidden_groups=groups, max_position_embeddings=512)
+    torch.manual_seed(19)
+    model = A.AlbertForPreTraining(cfg)
+    model.materialize(cuda)
+    ids = torch.randint(5, cfg.vocab_size, (8, 512), device=cuda)
+    grads = {}
+    try:
+        for shared in (False, True):
+            A._SHARED_WGRAD = shared
+            model.flat.grad.zero_()
+            for _ in range(2):
+                h, _ = model.encode(ids)
+                h.float().pow(2).mean().backward()
+            grads[shared] = model.flat.grad.clone()
+    finally:
+        A._SHARED_WGRAD = True
+    assert torch.isfinite(grads[True]).all()
+    assert rel(grads[True], grads[False]) < 1e-3
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 192), (777, 1024, 320), (2048, 256, 4096)])
 def test_gemm8_pipeline_depths(cuda, force_mfma, M, N, K):
     """gemm8.hip: K-tile counts 1, 3, 5 and 64 exercise the prologue, the odd-tile buffer parity and
