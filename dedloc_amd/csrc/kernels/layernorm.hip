@@ -7,6 +7,7 @@
 //
 // fwd:  s = x (+ r);  y = (s - mean) * rstd * gamma + beta;  saves mean/rstd (fp32) and s (bf16)
 // bwd:  ds = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)),  dgamma/dbeta column partials
+#include <algorithm>
 #include <cstdlib>
 
 #include "dl_common.h"
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 // Each block handles a contiguous chunk of rows (one wave per row, grid-strided inside the
 // block) and writes one fp32 partial row of dgamma/dbeta; dl_colsum_f32 reduces the partials.
 template <int D, int R>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+__global__ __launch_bounds__(512) void ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ ds,
                                                      float* __restrict__ dgamma_part, float* __restrict__ dbeta_part,
@@ -157,30 +158,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(ds + base + col_of<D>(lane, i), gy[u] + i * C::VW);
     }
   }
-  // reduce the per-wave column partials through LDS: 3 x nw x D floats
+  // reduce the per-wave column partials through LDS, one quantity at a time through one nw x D
+  // buffer (so an 8-wave block needs 32 KiB, not 96), then one fp32 atomic per column per block
+  // straight into the (accumulating) gradient buffers; dsum = column sum of ds = the bias gradient
+  // of the Linear that produced the LN input
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #pragma unroll
-  for (int i = 0; i < C::NV; ++i)
+  for (int which = 0; which < 3; ++which) {
+    float* dst = which == 0 ? dgamma_part : which == 1 ? dbeta_part : dsum;
+    if (dst == nullptr) break;  // block-uniform
+    const float* v = which == 0 ? dg : which == 1 ? db : dx;
+    if (which) __syncthreads();  // the previous round's column reads are done
 #pragma unroll
-    for (int j = 0; j < C::VW; ++j) {
-      const int c = col_of<D>(lane, i) + j;
-      lds[wid * D + c] = dg[i * C::VW + j];
-      lds[(nw + wid) * D + c] = db[i * C::VW + j];
-      lds[(2 * nw + wid) * D + c] = dx[i * C::VW + j];
+    for (int i = 0; i < C::NV; ++i)
+#pragma unroll
+      for (int j = 0; j < C::VW; ++j) lds[wid * D + col_of<D>(lane, i) + j] = v[i * C::VW + j];
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += blockDim.x) {
+      float sum = 0.f;
+      for (int w = 0; w < nw; ++w) sum += lds[w * D + c];
+      atomicAdd(&dst[c], sum);
     }
-  __syncthreads();
-  // one fp32 atomic per column per block straight into the (accumulating) gradient buffers;
-  // dsum = column sum of ds = the bias gradient of the Linear that produced the LN input
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float sg = 0.f, sb = 0.f, sx = 0.f;
-    for (int w = 0; w < nw; ++w) {
-      sg += lds[w * D + c];
-      sb += lds[(nw + w) * D + c];
-      sx += lds[(2 * nw + w) * D + c];
-    }
-    atomicAdd(&dgamma_part[c], sg);
-    atomicAdd(&dbeta_part[c], sb);
-    if (dsum) atomicAdd(&dsum[c], sx);
   }
 }
 
@@ -200,9 +198,14 @@ void launch_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const floa
 template <int D>
 void launch_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
                 bf16_t* ds, float* dg_part, float* db_part, float* dsum, int rows, int nparts, hipStream_t st) {
-  const int wpb = 4;
+  // waves per block (DEDLOC_LN_WPB, measurement override): 8 measured equal to 4 — the two-row
+  // form's 202 VGPRs cap the kernel at 2 waves per SIMD either way
+  static const int wpb = [] {
+    const char* e = std::getenv("DEDLOC_LN_WPB");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+  }();
   const int rpb = (rows + nparts - 1) / nparts;
-  size_t lds = (size_t)3 * wpb * D * sizeof(float);
+  size_t lds = (size_t)wpb * D * sizeof(float);
   // DEDLOC_LN_ROWS=1|2|4: rows in flight per wave (A/B measurement); default 2
   static const int R = [] {
     const char* e = std::getenv("DEDLOC_LN_ROWS");
