@@ -140,11 +140,12 @@ __device__ __forceinline__ void wait_vm_all() {
 template <typename T>
 __device__ __forceinline__ void settle(T& v) { asm volatile("" : "+v"(v)); }
 
-// this wave's two 1-KiB pieces (p = w, w + 4) of a 64-row tile starting at global row row0
+// this wave's 1-KiB pieces (p = w, w + NW, ...) of a 64-row tile starting at global row row0
+template <int NW = 4>
 __device__ __forceinline__ void dma_tile(const bf16_t* g, long ld, int row0, uint8_t* tile, int w, int lane) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int p = w + 4 * j;
+  for (int j = 0; j < 8 / NW; ++j) {
+    const int p = w + NW * j;
     const int row = 8 * p + (lane >> 3);
     const int c = (lane & 7) ^ swzf((row >> 1) & 7);
     dma16(g + (long)(row0 + row) * ld + c * 8, lds_u32(tile + p * 1024));
@@ -157,17 +158,18 @@ __device__ __forceinline__ void dma_f32x64(const float* g, uint8_t* dst, int lan
 }
 
 // Wait until this wave's pieces of the oldest in-flight stage have landed, leaving `ahead` later
-// stages (0..NBUF-2) in flight; npw = vector-memory ops this wave issues per stage (4 or 5).
-__device__ __forceinline__ void wait_stages(int ahead, bool five) {
-  if (five) {
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+// stages (0..NBUF-2) in flight; N = vector-memory ops this wave issues per stage.
+template <int N>
+__device__ __forceinline__ void wait_cnt(int ahead) {
+  if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory");
+  else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// PIECES = K + V tile pieces per wave per stage; the optional mask-bias piece adds one
+template <int PIECES = 4>
+__device__ __forceinline__ void wait_stages(int ahead, bool bias) {
+  if (bias) wait_cnt<PIECES + 1>(ahead);
+  else wait_cnt<PIECES>(ahead);
 }
 
 // store 4 consecutive bf16 (8 bytes)
@@ -253,11 +255,12 @@ struct FwdCtx {
   uint8_t* smem;
   float* mbs;
   int w, lane;
-  // RING: issue stage s (key tile s) into ring slot s % NBUF
+  // RING: issue stage s (key tile s) into ring slot s % NBUF (NW waves share the tile pieces)
+  template <int NW = 4>
   __device__ __forceinline__ void issue(int s) const {
     uint8_t* slot = smem + (s % NBUF) * STAGE;
-    dma_tile(Kg, ld, s * 64, slot, w, lane);
-    dma_tile(Vg, ld, s * 64, slot + TILE_BYTES, w, lane);
+    dma_tile<NW>(Kg, ld, s * 64, slot, w, lane);
+    dma_tile<NW>(Vg, ld, s * 64, slot + TILE_BYTES, w, lane);
     if (mb_g) dma_f32x64(mb_g + s * 64, slot + 2 * TILE_BYTES, lane);
   }
 };
@@ -269,7 +272,7 @@ __device__ __forceinline__ float key_bias(const FwdCtx& c, int key) {
 // QS = 32-row query sub-blocks per wave (1 or 2).  With QS = 2 every K fragment (row reads) and V
 // fragment (tr-reads) read from LDS feeds two MFMAs, and each wave carries two independent softmax
 // chains the scheduler can interleave (the loop is latency-bound: PMC, profiles/README.md).
-template <bool LEAN, bool RING, int QS>
+template <bool LEAN, bool RING, int QS, int NW>
 __device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int nt, const bf16x8 (&qf)[QS][4],
                                           floatx16 (&o)[QS][2], float (&m)[QS], float (&l)[QS], int r, int hh,
                                           int lane) {
@@ -282,9 +285,9 @@ __device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int
     if constexpr (RING) {
       // stage kt landed (this wave) -> barrier: every wave's pieces landed and every wave is done
       // with slot (kt - 1) % NBUF, which the stage issued next overwrites
-      wait_stages(min(nt - 1 - kt, NBUF - 2), c.mb_g != nullptr);
+      wait_stages<16 / NW>(min(nt - 1 - kt, NBUF - 2), c.mb_g != nullptr);
       __syncthreads();
-      if (kt + NBUF - 1 < nt) c.issue(kt + NBUF - 1);
+      if (kt + NBUF - 1 < nt) c.template issue<NW>(kt + NBUF - 1);
       Ks = c.smem + (kt % NBUF) * STAGE;
       mb = reinterpret_cast<const float*>(Ks + 2 * TILE_BYTES);
     } else {
@@ -395,9 +398,11 @@ __device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int
   }
 }
 
-// Block = 4 waves x QS x 32 query rows of one (batch, head).
-template <bool RING, int QS>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
+// Block = NW waves x QS x 32 query rows of one (batch, head).  NW = 8 (ring only): one 512-query
+// block per head at S = 512, so K / V are staged once per head, and each SIMD's two waves belong
+// to one block (DEDLOC_ATTN_NW=8).
+template <bool RING, int QS, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                           const float* __restrict__ mbias,
                                                           const int* __restrict__ kvinfo, bf16_t* __restrict__ out,
                                                           long ldo, float* __restrict__ lse, int B, int H, int S,
@@ -422,15 +427,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   c.w = w;
   c.lane = lane;
 
+  static_assert(NW == 4 || (NW == 8 && RING), "8-wave blocks stage through the ring");
   const int nt = (c.kv_end + 63) / 64;
   if constexpr (RING) {
-    for (int s0 = 0; s0 < NBUF - 1 && s0 < nt; ++s0) c.issue(s0);
+    for (int s0 = 0; s0 < NBUF - 1 && s0 < nt; ++s0) c.template issue<NW>(s0);
   }
   int q[QS];
   bf16x8 qf[QS][4];
 #pragma unroll
   for (int u = 0; u < QS; ++u) {
-    q[u] = bid.x * (128 * QS) + w * (32 * QS) + 32 * u + r;
+    q[u] = bid.x * (32 * QS * NW) + w * (32 * QS) + 32 * u + r;
     const int qc = min(q[u], S - 1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[u][ks] = gload8(Qg + (long)qc * ld + ks * 16 + 8 * hh);
@@ -467,8 +473,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
   // lean tiles first (every tile when there is no mask), then the masked remainder: the boundary
   // tile of a length mask, or all tiles of a generic additive mask
   const int nlean = c.mb_g ? 0 : c.kv_end / 64;
-  fwd_tiles<true, RING, QS>(c, 0, nlean, nt, qf, o, m, l, r, hh, lane);
-  fwd_tiles<false, RING, QS>(c, nlean, nt, nt, qf, o, m, l, r, hh, lane);
+  fwd_tiles<true, RING, QS, NW>(c, 0, nlean, nt, qf, o, m, l, r, hh, lane);
+  fwd_tiles<false, RING, QS, NW>(c, nlean, nt, nt, qf, o, m, l, r, hh, lane);
 
 #pragma unroll
   for (int u = 0; u < QS; ++u) {
@@ -935,6 +941,12 @@ int attn_fwd_qs() {
   return (e && e[0] == '1') ? 1 : 2;
 }
 
+// DEDLOC_ATTN_NW = waves per forward block (4 or 8; default 4 — 8 measured 5% slower)
+int attn_fwd_nw() {
+  const char* e = std::getenv("DEDLOC_ATTN_NW");
+  return (e && e[0] == '8') ? 8 : 4;
+}
+
 // DEDLOC_ATTN_DQ_QS = query sub-blocks per wave in the dQ backward kernel (1 or 2; default 2)
 int attn_dq_qs() {
   const char* e = std::getenv("DEDLOC_ATTN_DQ_QS");
@@ -964,6 +976,11 @@ int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
   const int qs = attn_fwd_qs();
+  if (attn_fwd_nw() == 8 && qs == 2) {
+    dim3 grid8((S + 511) / 512, H, B);
+    attn_fwd_kernel<true, 2, 8><<<grid8, 512, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
+    return 0;
+  }
   dim3 grid((S + 128 * qs - 1) / (128 * qs), H, B);
   if (attn_ring(qs == 2)) {
     if (qs == 2)

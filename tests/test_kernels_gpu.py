@@ -185,6 +185,7 @@ VARIANTS = [  # (forward sub-blocks, dQ sub-blocks, staging) — every kernel fo
     {"DEDLOC_ATTN_QS": "2", "DEDLOC_ATTN_DQ_QS": "2", "DEDLOC_ATTN_RING": "0"},
     {"DEDLOC_ATTN_QS": "2", "DEDLOC_ATTN_DQ_QS": "2"},  # default staging per kernel
     {"DEDLOC_ATTN_DKDV_KS": "2"},  # two key sub-blocks per wave, one wave per SIMD (AGPR accumulators)
+    {"DEDLOC_ATTN_NW": "8"},  # 8-wave forward blocks (512 queries per block)
 ]
 
 
