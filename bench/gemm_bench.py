@@ -73,6 +73,9 @@ def main():
         if name == "ffn2":
             f = (torch.randn(T, K, device=dev)).bfloat16()
             kinds.append(("dgrad_dgelu", lambda: O.gemm_dgelu(dy, w, f, db)))
+            if os.environ.get("DGRAD_T"):
+                w2t = w.t().contiguous()
+                kinds.append(("dgrad_dgelu_wT", lambda: O.gemm_dgelu(dy, w2t, f, db, True)))
         for kind, fn in kinds:
             if check:
                 outs = {}

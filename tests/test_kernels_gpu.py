@@ -551,6 +551,33 @@ def test_albert_layer_dgrad_transposed_weights(cuda):
 
 
 @pytest.mark.parametrize("groups", [1, 2])
+def test_albert_weight_gradients_on_side_stream(cuda, groups):
+    """Weight-gradient GEMMs issued on a side stream (DEDLOC_WGRAD_STREAM) give the same gradients."""
+    from dedloc_amd.models import albert as A
+
+    cfg = A.AlbertConfig.tiny(hidden_size=256, intermediate_size=1024, num_attention_heads=4, num_hidden_layers=4,
+                              num_hidden_groups=groups, max_position_embeddings=512)
+    torch.manual_seed(20)
+    model = A.AlbertForPreTraining(cfg)
+    model.materialize(cuda)
+    ids = torch.randint(5, cfg.vocab_size, (8, 512), device=cuda)
+    grads = {}
+    try:
+        for side in (False, True):
+            A._WGRAD_STREAM = side
+            model.flat.grad.zero_()
+            for _ in range(2):
+                h, _ = model.encode(ids)
+                h.float().pow(2).mean().backward()
+            grads[side] = model.flat.grad.clone()
+    finally:
+        A._WGRAD_STREAM = False
+    # (not bitwise: the bias / LayerNorm column sums use fp32 atomics in any order)
+    assert torch.isfinite(grads[True]).all()
+    assert rel(grads[True], grads[False]) < 1e-4, rel(grads[True], grads[False])
+
+
+@pytest.mark.parametrize("groups", [1, 2])
 def test_albert_shared_weight_gradient_slabs(cuda, groups):
     """Deferred slab sums of the shared layer's weight gradients (gemm_acc_f32_shared) match one
     slab sum per layer call, over two backward passes (the first call of each pass resets the
