@@ -191,7 +191,8 @@ VARIANTS = [  # (forward sub-blocks, dQ sub-blocks, staging) — every kernel fo
 
 @pytest.mark.parametrize("variant", range(len(VARIANTS)))
 @pytest.mark.parametrize("S,lens,generic", [(192, (192, 100, 64), False), (512, (512, 300, 17), False),
-                                             (256, (256, 130, 200), True)])
+                                             (256, (256, 130, 200), True), (64, (64, 33, 1), False),
+                                             (1024, (1024, 700, 513), False)])
 def test_attention_kernel_variants(cuda, monkeypatch, variant, S, lens, generic):
     """Register-staged vs LDS-DMA ring staging and one vs two query sub-blocks per wave, forward and
     backward (incl. the fused QKV bias gradient), on length masks and on the generic additive bias;
