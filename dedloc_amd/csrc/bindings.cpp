@@ -746,7 +746,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& x, const
                                                       const at::Tensor& gamma, const at::Tensor& beta,
                                                       const c10::optional<at::Tensor>& running_mean,
                                                       const c10::optional<at::Tensor>& running_var, double eps,
-                                                      double momentum, bool relu, int64_t groups) {
+                                                      double momentum, bool relu, int64_t groups,
+                                                      const c10::optional<at::Tensor>& sums) {
   expect_nhwc(x, "x");
   if (res.has_value()) expect_nhwc(*res, "res");
   expect(gamma, at::kFloat, "gamma");
@@ -758,9 +759,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& x, const
   auto stats = at::empty({4 * G * C}, gamma.options());  // sums[G,2C] | mean[G,C] | rstd[G,C]
   float* rm = running_mean.has_value() ? f32(*running_mean) : nullptr;
   float* rv = running_var.has_value() ? f32(*running_var) : nullptr;
-  check(dl_bn_fwd(cbf(x), res.has_value() ? cbf(*res) : nullptr, bf(y), f32(gamma), f32(beta), f32(stats),
+  float* sp = f32(stats);
+  if (sums.has_value()) {  // caller's pre-zeroed [G, 2C] slice: no memset per call
+    expect(*sums, at::kFloat, "sums");
+    TORCH_CHECK(sums->numel() == 2 * G * C, "sums must hold 2 * groups * C floats");
+    sp = f32(*sums);
+  }
+  check(dl_bn_fwd(cbf(x), res.has_value() ? cbf(*res) : nullptr, bf(y), f32(gamma), f32(beta), sp,
                   f32(stats) + 2 * G * C, f32(stats) + 3 * G * C, rm, rv, R, (int)C, (int)G, (float)eps,
-                  (float)momentum, relu, cur_stream(x)),
+                  (float)momentum, relu, cur_stream(x), sums.has_value() ? 1 : 0),
         "bn_fwd (channels must be 64..2048, a power-of-two multiple of 8)");
   return {y, stats.narrow(0, 2 * G * C, G * C).view({G, C}), stats.narrow(0, 3 * G * C, G * C).view({G, C})};
 }
@@ -768,7 +775,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& x, const
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& y,
                                                                   const at::Tensor& x, const at::Tensor& mean,
                                                                   const at::Tensor& rstd, const at::Tensor& gamma,
-                                                                  bool relu, bool want_dres) {
+                                                                  bool relu, bool want_dres,
+                                                                  const c10::optional<at::Tensor>& sums,
+                                                                  const c10::optional<at::Tensor>& dgamma_acc,
+                                                                  const c10::optional<at::Tensor>& dbeta_acc) {
   const int64_t G = mean.dim() == 2 ? mean.size(0) : 1;
   expect_nhwc(x, "x");
   expect_nhwc(y, "y");
@@ -779,10 +789,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
   auto dx = at::empty_like(x);
   auto dres = want_dres ? at::empty_like(x) : at::Tensor();
   auto ws = at::empty({2 * G * C + 2 * C}, gamma.options());  // sums[G,2C] | dgamma[C] | dbeta[C]
-  check(dl_bn_bwd(cbf(g), cbf(y), cbf(x), f32(mean), f32(rstd), f32(gamma), f32(ws), bf(dx),
-                  want_dres ? bf(dres) : nullptr, f32(ws) + 2 * G * C, f32(ws) + 2 * G * C + C, R, (int)C, (int)G,
-                  relu, cur_stream(x)),
+  float* sp = f32(ws);
+  if (sums.has_value()) {  // caller's pre-zeroed [G, 2C] slice: no memset per call
+    expect(*sums, at::kFloat, "sums");
+    TORCH_CHECK(sums->numel() == 2 * G * C, "sums must hold 2 * groups * C floats");
+    sp = f32(*sums);
+  }
+  // dgamma_acc / dbeta_acc: accumulate straight into the parameters' gradient buffers (then the
+  // returned dgamma / dbeta are empty) instead of returning them for autograd to add
+  const bool acc = dgamma_acc.has_value() && dbeta_acc.has_value();
+  if (acc) {
+    expect(*dgamma_acc, at::kFloat, "dgamma_acc");
+    expect(*dbeta_acc, at::kFloat, "dbeta_acc");
+    TORCH_CHECK(dgamma_acc->numel() == C && dbeta_acc->numel() == C, "parameter gradient size mismatch");
+  }
+  float* dgp = acc ? f32(*dgamma_acc) : f32(ws) + 2 * G * C;
+  float* dbp = acc ? f32(*dbeta_acc) : f32(ws) + 2 * G * C + C;
+  check(dl_bn_bwd(cbf(g), cbf(y), cbf(x), f32(mean), f32(rstd), f32(gamma), sp, bf(dx),
+                  want_dres ? bf(dres) : nullptr, dgp, dbp, R, (int)C, (int)G, relu, cur_stream(x),
+                  sums.has_value() ? 1 : 0, acc ? 1 : 0),
         "bn_bwd");
+  if (acc) return {dx, want_dres ? dres : at::empty({0}, x.options()), at::empty({0}, gamma.options()),
+                   at::empty({0}, gamma.options())};
   return {dx, want_dres ? dres : at::empty({0}, x.options()), ws.narrow(0, 2 * G * C, C),
           ws.narrow(0, 2 * G * C + C, C)};
 }

@@ -26,21 +26,35 @@ from torch.utils.checkpoint import checkpoint
 
 
 class _BNAct(torch.autograd.Function):
-    """Training-mode BN (+ residual) (+ ReLU) on channels-last bf16 via the fused HIP kernels."""
+    """Training-mode BN (+ residual) (+ ReLU) on channels-last bf16 via the fused HIP kernels.
+
+    ``ws``: this call's slices of the trunk pass's pre-zeroed statistics workspace (forward and
+    backward sums; one memset per pass instead of two hipMemsetAsync launches per BatchNorm).
+    With ``module.inplace_grad`` and fp32 gradient buffers bound to gamma / beta (the flat
+    gradient), the backward adds dgamma / dbeta into them directly, like the conv weight gradients,
+    so autograd launches no per-pass accumulation adds."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running_mean, running_var, relu, eps, momentum, groups):
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, relu, eps, momentum, groups, ws, module):
         y, mean, rstd = torch.ops.dedloc.bn_fwd(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu,
-                                                groups)
+                                                groups, None if ws is None else ws[0])
         ctx.save_for_backward(x, y, mean, rstd, gamma)
-        ctx.relu, ctx.has_res = relu, res is not None
+        ctx.relu, ctx.has_res, ctx.ws, ctx.module = relu, res is not None, ws, module
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, y, mean, rstd, gamma = ctx.saved_tensors
-        dx, dres, dgamma, dbeta = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, gamma, ctx.relu, ctx.has_res)
-        return dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None
+        m = ctx.module
+        gw, gb = (m.weight.grad, m.bias.grad) if m is not None else (None, None)
+        acc = (m is not None and m.inplace_grad and gw is not None and gb is not None
+               and gw.dtype == torch.float32 and gb.dtype == torch.float32)
+        dx, dres, dgamma, dbeta = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, gamma, ctx.relu, ctx.has_res,
+                                                          None if ctx.ws is None else ctx.ws[1],
+                                                          gw if acc else None, gb if acc else None)
+        if acc:
+            dgamma = dbeta = None
+        return (dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None)
 
 
 class _ConvNHWC(torch.autograd.Function):
@@ -50,7 +64,15 @@ class _ConvNHWC(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride, pad, module):
-        wb = weight.detach().to(torch.bfloat16)  # keeps the channels-last (KRSC) strides
+        # bf16 copy of the weight (keeps the channels-last KRSC strides), shared by the trunk passes
+        # of one SwAVModel.forward (one cast per iteration instead of one per resolution group); the
+        # model clears the cache at the start and end of every forward, so an optimizer update
+        # between iterations can never be missed
+        wb = getattr(module, "_wb_cache", None)
+        if wb is None:
+            wb = weight.detach().to(torch.bfloat16)
+            if module._wb_share:
+                module._wb_cache = wb
         ctx.save_for_backward(x, wb)
         ctx.stride, ctx.pad, ctx.module = stride, pad, module
         return torch.ops.dedloc.conv2d_fwd(x, wb, stride, pad)
@@ -92,6 +114,8 @@ class ConvNHWC(nn.Conv2d):
     shapes (~20 s once): 1982.1 samples/s vs 1953.9 for hip + MIOpen stem and 1905.5 for all-hip."""
 
     native = os.environ.get("DEDLOC_CONV", "hip") == "hip"
+    _wb_cache = None    # bf16 weight shared across the trunk passes of one model forward
+    _wb_share = False   # set by SwAVModel.forward for the duration of that forward
     # False: return the weight gradient through autograd instead of adding it into the bound .grad
     # (HIP-graph capture via make_graphed_callables needs every parameter to receive an autograd grad)
     inplace_wgrad = True
@@ -114,10 +138,16 @@ class BNAct(nn.BatchNorm2d):
     the stock module followed by the add / ReLU.
     """
 
+    # False: return dgamma / dbeta through autograd (HIP-graph capture needs an autograd grad for
+    # every parameter); True: accumulate into the bound fp32 .grad buffers in the kernel
+    inplace_grad = True
+
     def __init__(self, num_features, relu: bool = False, fused: bool = True):
         super().__init__(num_features)
         self.relu, self.fused = relu, fused
         self.stat_groups = 1  # >1: the batch holds that many crops, each normalised with its own stats
+        self.pass_ws = None   # set by ResNet50Trunk.forward: (fwd sums, bwd sums) slices, pre-zeroed
+        self.count_deferred = False  # num_batches_tracked is advanced by the trunk, one launch per pass
 
     def forward(self, x, res=None):
         G = self.stat_groups if self.training else 1
@@ -125,9 +155,11 @@ class BNAct(nn.BatchNorm2d):
                 and x.is_contiguous(memory_format=torch.channels_last)
                 and (res is None or (res.dtype == torch.bfloat16
                                      and res.is_contiguous(memory_format=torch.channels_last)))):
-            self.num_batches_tracked.add_(G)
+            if not self.count_deferred:
+                self.num_batches_tracked.add_(G)
+            ws, self.pass_ws = self.pass_ws, None
             return _BNAct.apply(x, self.weight, self.bias, res, self.running_mean, self.running_var, self.relu,
-                                self.eps, self.momentum, G)
+                                self.eps, self.momentum, G, ws, self)
         if G > 1:  # reference semantics without the fused kernel: one BN call per crop chunk
             y = torch.cat([super(BNAct, self).forward(c) for c in x.chunk(G)])
         else:
@@ -158,6 +190,8 @@ class Bottleneck(nn.Module):
 
 
 class ResNet50Trunk(nn.Module):
+    pass_workspace = True  # False: per-call BN statistics memsets and counter adds (A/B, tests)
+
     def __init__(self, layers=(3, 4, 6, 3), zero_init_residual=False, checkpoint_stages: bool = False):
         super().__init__()
         self.inplanes = 64
@@ -190,7 +224,34 @@ class ResNet50Trunk(nn.Module):
         layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
+    def _prepare_bn_pass(self, x):
+        """One zeroed workspace for every BatchNorm's forward and backward statistics sums of this
+        pass, and one multi-tensor add for their num_batches_tracked counters (instead of two
+        memsets and one add launch per BatchNorm; each is a ~5 us kernel at b=64)."""
+        if (not self.pass_workspace or not self.training or self.checkpoint_stages or not x.is_cuda
+                or x.dtype != torch.bfloat16 or not x.is_contiguous(memory_format=torch.channels_last)):
+            for m in self._bn_modules():
+                m.count_deferred, m.pass_ws = False, None
+            return
+        bns = self._bn_modules()
+        G = bns[0].stat_groups
+        sizes = [2 * G * m.num_features for m in bns]
+        ws = torch.zeros(2 * sum(sizes), dtype=torch.float32, device=x.device)
+        off = 0
+        for m, n in zip(bns, sizes):
+            m.pass_ws = (ws[off:off + n], ws[off + n:off + 2 * n])
+            m.count_deferred = True
+            off += 2 * n
+        torch._foreach_add_([m.num_batches_tracked for m in bns], G)
+
+    def _bn_modules(self):
+        bns = getattr(self, "_bns", None)
+        if bns is None:
+            bns = self._bns = [m for m in self.modules() if isinstance(m, BNAct)]
+        return bns
+
     def forward(self, x):
+        self._prepare_bn_pass(x)
         x = self.maxpool(self.bn1(self.conv1(x)))
         for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
             if self.checkpoint_stages and self.training and x.requires_grad:
@@ -259,6 +320,16 @@ class SwAVModel(nn.Module):
         one trunk pass per crop computes — every other trunk op is per-sample.  Without it, BN
         statistics span the whole resolution group (original SwAV's idx_crops grouping).
         """
+        convs = [m for m in self.trunk.modules() if isinstance(m, ConvNHWC)]
+        for m in convs:
+            m._wb_cache, m._wb_share = None, True
+        try:
+            return self._forward(crops)
+        finally:
+            for m in convs:
+                m._wb_cache, m._wb_share = None, False
+
+    def _forward(self, crops):
         feats, i = [], 0
         while i < len(crops):
             j = i

@@ -49,8 +49,9 @@ _SCHEMAS = [
     "row_normalize_(Tensor(a!) w) -> ()",
     "multicrop(Tensor pool, Tensor params, int size, int rad, float[] mean, float[] std) -> Tensor",
     "bn_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-    "float eps, float momentum, bool relu, int groups=1) -> (Tensor, Tensor, Tensor)",
-    "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres) "
+    "float eps, float momentum, bool relu, int groups=1, Tensor(c!)? sums=None) -> (Tensor, Tensor, Tensor)",
+    "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres, "
+    "Tensor(a!)? sums=None, Tensor(b!)? dgamma_acc=None, Tensor(c!)? dbeta_acc=None) "
     "-> (Tensor, Tensor, Tensor, Tensor)",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
     "conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor",
@@ -461,7 +462,7 @@ def _multicrop_cpu(pool, params, size, rad, mean, std):
 
 
 @_impl("bn_fwd")
-def _bn_fwd_cpu(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, groups=1):
+def _bn_fwd_cpu(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, groups=1, sums=None):
     G = groups
     xf = x.float().reshape(G, x.shape[0] // G, *x.shape[1:])
     R = xf[0].numel() // xf.shape[2]
@@ -500,7 +501,7 @@ def _conv2d_wgrad_cpu(dy, x, dw, stride, pad):
 
 
 @_impl("bn_bwd")
-def _bn_bwd_cpu(dy, y, x, mean, rstd, gamma, relu, want_dres):
+def _bn_bwd_cpu(dy, y, x, mean, rstd, gamma, relu, want_dres, sums=None, dgamma_acc=None, dbeta_acc=None):
     mean2 = mean.reshape(-1, x.shape[1])
     rstd2 = rstd.reshape(-1, x.shape[1])
     G = mean2.shape[0]
@@ -516,4 +517,9 @@ def _bn_bwd_cpu(dy, y, x, mean, rstd, gamma, relu, want_dres):
                                                     - xh * (sgx / R)[:, None, :, None, None])
     cl = torch.channels_last
     dres = g.to(x.dtype).contiguous(memory_format=cl) if want_dres else torch.empty(0, dtype=x.dtype)
-    return dx.reshape(x.shape).to(x.dtype).contiguous(memory_format=cl), dres, sgx.sum(0), sb.sum(0)
+    dxo = dx.reshape(x.shape).to(x.dtype).contiguous(memory_format=cl)
+    if dgamma_acc is not None and dbeta_acc is not None:
+        dgamma_acc.add_(sgx.sum(0))
+        dbeta_acc.add_(sb.sum(0))
+        return dxo, dres, torch.empty(0), torch.empty(0)
+    return dxo, dres, sgx.sum(0), sb.sum(0)

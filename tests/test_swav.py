@@ -480,3 +480,48 @@ def test_swav_nan_loss_dumps_state_and_stops(tmp_path):
     finally:
         peer.shutdown()
         dht.shutdown()
+
+
+@pytest.mark.gpu
+def test_trunk_bn_pass_workspace_and_inplace_grads(cuda):
+    """Per-pass zeroed BN statistics workspace, batched num_batches_tracked, in-place dgamma/dbeta
+    accumulation and the forward-scoped bf16 conv weight cache give the same gradients, running
+    statistics and counters as the per-call path (two trunk passes with 2 and 6 stat groups)."""
+    from dedloc_amd.models.resnet_swav import BNAct, ResNet50Trunk
+    from dedloc_amd.utils.flat import FlatParams
+
+    torch.manual_seed(0)
+    out = {}
+    for fast in (False, "again", True):
+        torch.manual_seed(0)
+        trunk = ResNet50Trunk().to(cuda).to(memory_format=torch.channels_last)
+        flat = FlatParams(trunk.named_parameters(), device=cuda, with_bf16=False, autograd=True)
+        ResNet50Trunk.pass_workspace = fast is True
+        BNAct.inplace_grad = fast is True
+        try:
+            g = torch.Generator(device="cpu").manual_seed(1)
+            for G, res in ((2, 64), (6, 32)):
+                for m in trunk.modules():
+                    if isinstance(m, BNAct):
+                        m.stat_groups = G
+                x = torch.randn(2 * G, 3, res, res, generator=g).to(cuda).bfloat16().contiguous(
+                    memory_format=torch.channels_last)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    y = trunk(x)
+                y.float().pow(2).mean().backward()
+        finally:
+            ResNet50Trunk.pass_workspace = True
+            BNAct.inplace_grad = True
+        out[fast] = (flat.grad.clone(), torch.cat([b.float().flatten() for n, b in trunk.named_buffers()]))
+    g0, b0 = out[False]
+    ga, ba = out["again"]  # the per-call path re-run: run-to-run spread (fp32 atomics in the BN
+    g1, b1 = out[True]     # statistics, amplified through 50 bf16 layers into the deep running stats)
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+
+    assert torch.isfinite(g1).all()
+    assert rel(g1, g0) < 1e-3
+    assert rel(b1, b0) < max(3 * rel(ba, b0), 1e-4), (rel(b1, b0), rel(ba, b0))
+    n_tracked = [b for n, b in ResNet50Trunk().named_buffers() if n.endswith("num_batches_tracked")]
+    assert len(n_tracked) == 53 and b1[-1].item() == 8.0  # 2 + 6 statistics groups counted
