@@ -64,6 +64,15 @@ def parse():
     return ap.parse_args()
 
 
+def _protocol_breakdown(gathered, keys):
+    out = {}
+    for i, k in enumerate(keys[:-1]):
+        vals = [float(g[3 + i]) / max(1.0, float(g[3 + len(keys) - 1])) for g in gathered]
+        out[k.replace("_s", "_ms") if k.endswith("_s") else k] = round(
+            sum(vals) / len(vals) * (1e3 if k.endswith("_s") else 1.0), 3)
+    return out
+
+
 def main():
     args = parse()
     logging.basicConfig(level=logging.INFO if args.verbose else logging.WARNING,
@@ -121,7 +130,8 @@ def main():
     if world > 1:
         dist.barrier()
     sync()
-    ema_start = co.performance_ema.samples_per_second
+    keys = ("fetch_s", "averaging_s", "optimizer_s", "local_steps", "global_steps")
+    st0 = {k: co.stats[k] for k in keys}
     t0 = time.perf_counter()
     samples = run_until(base + args.warmup + args.steps)
     sync()
@@ -130,7 +140,7 @@ def main():
     sync()
     dt = time.perf_counter() - t0
     ema = co.performance_ema.samples_per_second
-    stats = torch.tensor([samples, dt, ema], dtype=torch.float64, device=dev)
+    stats = torch.tensor([samples, dt, ema] + [co.stats[k] - st0[k] for k in keys], dtype=torch.float64, device=dev)
     if world > 1:
         gathered = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(gathered, stats)
@@ -153,6 +163,9 @@ def main():
                           "compression": args.compression, "optimizer": "LAMB", "impl": args.impl},
                "ema_samples_per_s_sum": round(ema_sum, 2), "averaging_rounds": co.stats["averaging_rounds"],
                "averaging_failed": co.stats["averaging_failed"],
+               # timed-region breakdown, mean over peers: host seconds per global step in the state
+               # fetch / matchmaking + all-reduce / optimizer launch, local micro-steps per global step
+               "protocol": _protocol_breakdown(gathered, keys),
                "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"}}
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -105,7 +105,11 @@ class CollaborativeOptimizer:
         self.performance_ema = PerformanceEMA(alpha=performance_ema_alpha)
         self.last_step_time = None
         self.last_group: Optional[Dict] = None
-        self.stats = {"global_steps": 0, "averaging_rounds": 0, "averaging_failed": 0, "state_loads": 0}
+        self.stats = {"global_steps": 0, "averaging_rounds": 0, "averaging_failed": 0, "state_loads": 0,
+                      # where a global step's time goes (host clock, seconds, summed over steps): the
+                      # state fetch, matchmaking + all-reduce, the optimizer, and the local micro-steps
+                      # that went into each global batch
+                      "fetch_s": 0.0, "averaging_s": 0.0, "optimizer_s": 0.0, "local_steps": 0}
 
         self.averager = DecentralizedAverager(
             [self.flat.fp32, self.flat.grad], dht, prefix, peer_id=peer_id,
@@ -232,7 +236,9 @@ class CollaborativeOptimizer:
 
         logger.log(self.status_loglevel, f"beginning global optimizer step #{self.collaboration_state.optimizer_step}")
         self._finish_param_round()
+        t_fetch = time.perf_counter()
         self.collaboration_state = self.fetch_collaboration_state()
+        self.stats["fetch_s"] += time.perf_counter() - t_fetch
         self.collaboration_state_updated.set()
         if not self.is_synchronized:
             self.load_state_from_peers()
@@ -243,6 +249,7 @@ class CollaborativeOptimizer:
             # grads = accumulator / local_steps   (hivemind apply_accumulated_grads_)
             torch.ops.dedloc.axpby(self.flat.grad, self.accumulator, 0.0, 1.0 / max(1, self.local_steps_accumulated))
             group = None
+            t_avg = time.perf_counter()
             if cs.num_peers > 1:
                 mean_samples = self.target_batch_size / cs.num_peers
                 weight = self.local_samples_accumulated / mean_samples
@@ -257,9 +264,13 @@ class CollaborativeOptimizer:
                                                      "or the round failed; applying local gradients")
             else:
                 logger.log(self.status_loglevel, "Skipped averaging: collaboration consists of this peer alone")
+            t_opt = time.perf_counter()
             self.opt.step()
             if self.delay_param_averaging and group is not None:
                 self._start_param_round(weight, cs.num_peers + self._num_aux())
+            self.stats["averaging_s"] += t_opt - t_avg
+            self.stats["optimizer_s"] += time.perf_counter() - t_opt  # launch time (kernels run async)
+            self.stats["local_steps"] += self.local_steps_accumulated
             self._reset_accumulators()
             self.collaboration_state.register_step(self.local_step + 1)
             self.local_step += 1

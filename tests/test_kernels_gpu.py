@@ -573,9 +573,12 @@ def test_albert_weight_gradients_on_side_stream(cuda, groups):
             grads[side] = model.flat.grad.clone()
     finally:
         A._WGRAD_STREAM = False
-    # (not bitwise: the bias / LayerNorm column sums use fp32 atomics in any order)
+    # Not bitwise: the bias / LayerNorm column sums use fp32 atomics in any order, and the
+    # overlapped backward rounds the FFN-down data gradient to bf16 before GELU' (gemm + gelu_bwd)
+    # where the default path applies GELU' to the fp32 accumulators (gemm_dgelu): measured
+    # 0.8e-4 - 1.2e-4 relative across boxes, so the bound sits at a few bf16 half-ulps / sqrt(n).
     assert torch.isfinite(grads[True]).all()
-    assert rel(grads[True], grads[False]) < 1e-4, rel(grads[True], grads[False])
+    assert rel(grads[True], grads[False]) < 4e-4, rel(grads[True], grads[False])
 
 
 @pytest.mark.parametrize("groups", [1, 2])
