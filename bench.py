@@ -44,10 +44,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=3, help="timed collaborative steps")
     ap.add_argument("--warmup", type=int, default=1, help="untimed collaborative steps")
     ap.add_argument("--micro_batch", type=int, default=None,
-                    help="per-peer micro-batch (default: min(256, target / peers), at least 64 — measured on "
-                         "MI355X 64: 905, 128: 935, 256: 940 samples/s per micro-step; with the ETA slack the "
-                         "8-peer protocol efficiency is ~92-94%% for 2, 4 or 8 micro-steps per global step "
-                         "(profiles/README.md), so the largest micro-batch wins)")
+                    help="per-peer micro-batch (default: min(512, target / peers), at least 64 — measured on "
+                         "MI355X 64: 905, 128: 935, 256: 940 samples/s per micro-step, 512 +0.8%% over 256 on one "
+                         "box (about 170 GB of activations, fits the 288 GB HBM); with the ETA slack the 8-peer "
+                         "protocol efficiency does not drop with fewer micro-steps per global step (1 micro-step: "
+                         "89.5%% vs 2: 87.8%% in the CPU emulation, profiles/README.md), so the largest "
+                         "micro-batch wins)")
     ap.add_argument("--grad_accum", type=int, default=1)
     ap.add_argument("--seq_len", type=int, default=512)
     ap.add_argument("--target_batch_size", type=int, default=4096)
@@ -87,7 +89,7 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if args.micro_batch is None:
-        args.micro_batch = 2 if args.cpu_test else min(256, max(64, args.target_batch_size // world))
+        args.micro_batch = 2 if args.cpu_test else min(512, max(64, args.target_batch_size // world))
     from dedloc_amd.cli.arguments import AlbertTrainingArguments, CollaborationArguments, DatasetArguments
     from dedloc_amd.dht import DHT
     from dedloc_amd.training.albert_peer import AlbertPeer
