@@ -13,6 +13,7 @@ The total work per step is fixed as N grows, so scaling is "strong".
 
     python bench.py                         # 1 GPU
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+    python bench.py --model swav            # BASELINE config 3 (collaborative SwAV ResNet-50), same contract
 """
 from __future__ import annotations
 
@@ -41,6 +42,9 @@ EAGER_BASELINE_SPS_PER_GPU = 263.48
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--model", default="albert", choices=["albert", "swav"],
+                    help="albert = the headline (BASELINE.json metric); swav = BASELINE config 3, collaborative "
+                         "SwAV ResNet-50 (b=64 per peer, 2x224+6x96 crops, LARC-SGD, target 32768, groups of 4)")
     ap.add_argument("--steps", type=int, default=3, help="timed collaborative steps")
     ap.add_argument("--warmup", type=int, default=1, help="untimed collaborative steps")
     ap.add_argument("--micro_batch", type=int, default=None,
@@ -52,13 +56,15 @@ def parse():
                          "micro-batch wins)")
     ap.add_argument("--grad_accum", type=int, default=1)
     ap.add_argument("--seq_len", type=int, default=512)
-    ap.add_argument("--target_batch_size", type=int, default=4096)
+    ap.add_argument("--target_batch_size", type=int, default=None,
+                    help="samples per collaborative step (default: 4096 ALBERT, 32768 SwAV — the reference values)")
     ap.add_argument("--compression", default="FLOAT16")
     ap.add_argument("--impl", default="dedloc", choices=["dedloc", "eager"],
                     help="eager = HF AlbertForPreTraining + per-tensor torch LAMB (the measured baseline)")
     ap.add_argument("--cpu_test", default=None, metavar="CONFIG_DIR",
-                    help="plumbing test only: run on CPU/gloo with the tiny model config in CONFIG_DIR "
-                         "(exercises the multi-rank orchestration of this script; not a measurement)")
+                    help="plumbing test only: run on CPU/gloo with the tiny ALBERT config in CONFIG_DIR (with "
+                         "--model swav the value is ignored: full ResNet-50, use a tiny --micro_batch) — exercises "
+                         "the multi-rank orchestration of this script; not a measurement")
     ap.add_argument("--throttle", type=float, default=0.0,
                     help="emulation only: idle seconds added after every micro-step (with --cpu_test, stands in "
                          "for GPU compute time when studying the collaboration protocol's overheads)")
@@ -75,6 +81,71 @@ def _protocol_breakdown(gathered, keys):
     return out
 
 
+def _albert_peer(args, rank, world, dev, root_ep):
+    """The headline: one ALBERT-large run_trainer peer (AlbertPeer) per GPU."""
+    if args.target_batch_size is None:
+        args.target_batch_size = 4096
+    if args.micro_batch is None:
+        args.micro_batch = 2 if args.cpu_test else min(512, max(64, args.target_batch_size // world))
+    from dedloc_amd.cli.arguments import AlbertTrainingArguments, CollaborationArguments, DatasetArguments
+    from dedloc_amd.training.albert_peer import AlbertPeer
+
+    targs = AlbertTrainingArguments(per_device_train_batch_size=args.micro_batch,
+                                    gradient_accumulation_steps=args.grad_accum, seq_length=args.seq_len,
+                                    save_steps=0, output_dir=f"/tmp/dedloc_bench_{os.getpid()}", seed=1234,
+                                    throttle=args.throttle)
+    dargs = DatasetArguments(config_path=args.cpu_test or "albert-large-v2")
+    cargs = CollaborationArguments(experiment_prefix="bench", initial_peers=[root_ep], dht_listen_on="127.0.0.1:*",
+                                   target_batch_size=args.target_batch_size, compression=args.compression,
+                                   listen_on="127.0.0.1:*", averaging_expiration=5.0, averaging_timeout=60.0,
+                                   min_refresh_period=0.2, default_refresh_period=0.5)
+    if args.impl == "eager":
+        dargs.mask_mode = "hf"
+    peer = AlbertPeer(targs, dargs, cargs, dev, rank=rank, dht=None, impl=args.impl)
+
+    def describe(value, world):
+        return {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "higher_is_better": True,
+                "scaling": "strong",
+                "vs_baseline": (round(value / (EAGER_BASELINE_SPS_PER_GPU * world), 3)
+                                if EAGER_BASELINE_SPS_PER_GPU else None),
+                "dtype": "bf16", "data": "synthetic (WikiText-103 SOP shapes, seq 512, 15% MLM; random-init weights)",
+                "config": {"model": "albert-large-v2", "global_batch": args.target_batch_size,
+                           "seq_len": args.seq_len, "parallelism": f"collaborative-dp{world}",
+                           "micro_batch": args.micro_batch, "grad_accum": args.grad_accum,
+                           "compression": args.compression, "optimizer": "LAMB", "impl": args.impl}}
+    return peer, args.micro_batch * args.grad_accum, describe
+
+
+def _swav_peer(args, rank, dev, root_ep):
+    """BASELINE config 3: one collaborative SwAV ResNet-50 peer (SwavPeer, the reference's
+    sgd_collaborative + vissl train step) per GPU, with the reference's recipe values (local batch 64,
+    target 32768 samples per collaborative step, LARC-SGD, FLOAT16 wire, matchmaking groups of 4)."""
+    if args.target_batch_size is None:
+        args.target_batch_size = 32768
+    b = args.micro_batch or 64
+    from dedloc_amd.training.swav_peer import SwavPeer
+    from dedloc_amd.utils.config import load_config
+
+    ov = [f"config.DATA.TRAIN.BATCHSIZE_PER_REPLICA={b}", f"config.OPTIMIZER.batch_size_for_tracking={b}",
+          f"config.OPTIMIZER.target_batch_size={args.target_batch_size}",
+          f"config.OPTIMIZER.compression={args.compression}",
+          f'config.OPTIMIZER.dht_initial_peers=["{root_ep}"]', f"config.CHECKPOINT.DIR=/tmp/dedloc_swav_bench_{os.getpid()}",
+          "config.CHECKPOINT.AUTO_RESUME=false", "config.CHECKPOINT.CHECKPOINT_ITER_FREQUENCY=0"]
+    cfg = load_config("swav_1node_resnet_submit", ov)
+    peer = SwavPeer(cfg, dev, rank=rank)
+
+    def describe(value, world):
+        return {"metric": "samples/sec (whole node) SwAV ResNet-50 at 1/2/4/8 peers", "value": round(value, 2),
+                "unit": "samples/s", "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "dtype": "bf16", "data": "synthetic (ImageNet-224-sized image pool, 2x224 + 6x96 multi-crop on the "
+                                         "GPU; random-init weights)",
+                "config": {"model": "swav-resnet50", "global_batch": args.target_batch_size, "batch_per_peer": b,
+                           "crops": "2x224+6x96", "parallelism": f"collaborative-dp{world}",
+                           "compression": args.compression, "optimizer": "LARC-SGD",
+                           "target_group_size": int(cfg.OPTIMIZER.target_group_size)}}
+    return peer, b, describe
+
+
 def main():
     args = parse()
     logging.basicConfig(level=logging.INFO if args.verbose else logging.WARNING,
@@ -88,31 +159,18 @@ def main():
             torch.cuda.synchronize()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    if args.micro_batch is None:
-        args.micro_batch = 2 if args.cpu_test else min(512, max(64, args.target_batch_size // world))
-    from dedloc_amd.cli.arguments import AlbertTrainingArguments, CollaborationArguments, DatasetArguments
     from dedloc_amd.dht import DHT
-    from dedloc_amd.training.albert_peer import AlbertPeer
 
     # control plane: rank 0 hosts the DHT root, everyone else bootstraps from it
     root = DHT(listen_on="127.0.0.1:*") if rank == 0 else None
     ep = [root.endpoint if root is not None else None]
     if world > 1:
         dist.broadcast_object_list(ep, src=0)
-    targs = AlbertTrainingArguments(per_device_train_batch_size=args.micro_batch,
-                                    gradient_accumulation_steps=args.grad_accum, seq_length=args.seq_len,
-                                    save_steps=0, output_dir=f"/tmp/dedloc_bench_{os.getpid()}", seed=1234,
-                                    throttle=args.throttle)
-    dargs = DatasetArguments(config_path=args.cpu_test or "albert-large-v2")
-    cargs = CollaborationArguments(experiment_prefix="bench", initial_peers=[ep[0]], dht_listen_on="127.0.0.1:*",
-                                   target_batch_size=args.target_batch_size, compression=args.compression,
-                                   listen_on="127.0.0.1:*", averaging_expiration=5.0, averaging_timeout=60.0,
-                                   min_refresh_period=0.2, default_refresh_period=0.5)
-    if args.impl == "eager":
-        dargs.mask_mode = "hf"
-    peer = AlbertPeer(targs, dargs, cargs, dev, rank=rank, dht=None, impl=args.impl)
+    if args.model == "swav":
+        peer, bs, describe = _swav_peer(args, rank, dev, ep[0])
+    else:
+        peer, bs, describe = _albert_peer(args, rank, world, dev, ep[0])
     co = peer.collab_opt
-    bs = args.micro_batch * args.grad_accum
 
     def run_until(step):
         n = 0
@@ -153,22 +211,15 @@ def main():
     ema_sum = sum(float(g[2]) for g in gathered)
     if rank == 0:
         value = total_samples / max_dt
-        out = {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(max_dt / args.steps * 1e3, 2),
-               "higher_is_better": True, "scaling": "strong",
-               "vs_baseline": (round(value / (EAGER_BASELINE_SPS_PER_GPU * world), 3)
-                               if EAGER_BASELINE_SPS_PER_GPU else None),
-               "dtype": "bf16", "data": "synthetic (WikiText-103 SOP shapes, seq 512, 15% MLM; random-init weights)",
-               "config": {"model": "albert-large-v2", "global_batch": args.target_batch_size,
-                          "seq_len": args.seq_len, "parallelism": f"collaborative-dp{world}",
-                          "micro_batch": args.micro_batch, "grad_accum": args.grad_accum,
-                          "compression": args.compression, "optimizer": "LAMB", "impl": args.impl},
+        out = dict(describe(value, world), n_gpus=world, steps=args.steps, warmup=args.warmup,
+                   ms_per_step=round(max_dt / args.steps * 1e3, 2))
+        out.update({
                "ema_samples_per_s_sum": round(ema_sum, 2), "averaging_rounds": co.stats["averaging_rounds"],
                "averaging_failed": co.stats["averaging_failed"],
                # timed-region breakdown, mean over peers: host seconds per global step in the state
                # fetch / matchmaking + all-reduce / optimizer launch, local micro-steps per global step
                "protocol": _protocol_breakdown(gathered, keys),
-               "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"}}
+               "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"}})
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -50,3 +50,23 @@ def test_bench_multi_rank_cpu_plumbing(tmp_path, nproc):
     # a fresh collaboration starts at once (no circular state downloads between step-0 peers) and
     # no step waits out a matchmaking window
     assert out["ms_per_step"] < 4000 and wall < 120, (out["ms_per_step"], wall)
+
+
+@pytest.mark.multiproc
+@pytest.mark.timeout(600)
+def test_bench_swav_mode_two_ranks_cpu():
+    """bench.py --model swav (BASELINE config 3): two collaborative SwAV ResNet-50 peers on CPU/gloo run
+    global steps with averaging and rank 0 prints one JSON line with the SwAV metric."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--model", "swav", "--gpus", "2", "--steps", "1",
+           "--warmup", "1", "--cpu_test", "swav", "--micro_batch", "2", "--target_batch_size", "8"]
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=560, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert KEYS <= set(out)
+    assert out["metric"].startswith("samples/sec (whole node) SwAV ResNet-50") and out["n_gpus"] == 2
+    assert out["config"]["model"] == "swav-resnet50" and out["config"]["optimizer"] == "LARC-SGD"
+    assert out["averaging_rounds"] >= 2 and out["averaging_failed"] == 0 and out["last_group"]["size"] == 2
