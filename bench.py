@@ -35,8 +35,10 @@ METRIC = "samples/sec (whole node) ALBERT-large MLM pretrain at 1/2/4/8 peers"
 # Measured PyTorch-eager reference on MI355X: the reference's compute stack (HF AlbertForPreTraining,
 # bf16 autocast, SDPA attention, per-tensor torch LAMB, clip_grad_norm_) driven by this repo's
 # collaborative engine — `python bench.py --impl eager` (training/eager_baseline.py), samples/s per
-# GPU at N=1, micro-batch 64 (BASELINE.md "Measured MI355X results").  vs_baseline = value / (this x N).
-EAGER_BASELINE_SPS_PER_GPU = 263.48
+# GPU at N=1 in its best micro-batch: 64 -> 263.48, 128 -> 272.02, 256 runs out of the 288 GB (HF
+# materialises the full [B*S, 30000] MLM logits; BASELINE.md "Measured MI355X results",
+# profiles/bench_eager_mb128.log).  vs_baseline = value / (this x N).
+EAGER_BASELINE_SPS_PER_GPU = 272.02
 
 
 def parse():
