@@ -47,6 +47,9 @@ def test_bench_multi_rank_cpu_plumbing(tmp_path, nproc):
     # every global step (warm-up + timed) averaged over the world communicator with all peers
     assert out["averaging_rounds"] >= 3 and out["averaging_failed"] == 0
     assert out["last_group"]["size"] == nproc
+    # timed-region protocol breakdown: every global step took at least one local micro-step
+    prot = out["protocol"]
+    assert prot["local_steps"] >= 1 and min(prot["fetch_ms"], prot["averaging_ms"], prot["optimizer_ms"]) >= 0
     # a fresh collaboration starts at once (no circular state downloads between step-0 peers) and
     # no step waits out a matchmaking window
     assert out["ms_per_step"] < 4000 and wall < 120, (out["ms_per_step"], wall)
