@@ -7,8 +7,10 @@ A auxiliary peers, all on one node, with the AWS fleet's heterogeneity injected 
         --experiment_prefix albert -- --per_device_train_batch_size 32 --target_batch_size 4096
 
 Everything after ``--`` is passed to every trainer (and aux peer).  Trainers and aux peers share one
-torch.distributed world (the data plane: RCCL over xGMI), trainer i on GPU i, aux peers on GPU
-``i % n_gpus`` (the reference used CPU aux instances; here they are extra reducer processes).
+torch.distributed world (the data plane: RCCL over xGMI), trainer i on GPU i, aux peer j on GPU
+``n_trainers + j`` (the reference used CPU aux instances; here they are reducer-only processes on
+spare GPUs: an RCCL communicator cannot hold two ranks on one device, so trainers + aux peers must
+not exceed the node's GPUs).
 The coordinator is not part of the world (it only reads metrics and downloads state over TCP).
 This process never touches the GPU itself; children are plain subprocesses.
 """
@@ -52,7 +54,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--n_trainers", type=int, default=8)
     ap.add_argument("--n_aux", type=int, default=0)
-    ap.add_argument("--n_gpus", type=int, default=None, help="GPUs on this node (default: n_trainers)")
+    ap.add_argument("--n_gpus", type=int, default=None,
+                    help="GPUs on this node (default: n_trainers + n_aux, one per peer)")
     ap.add_argument("--experiment_prefix", default="albert")
     ap.add_argument("--fleet", choices=["uniform", "aws"], default="uniform")
     ap.add_argument("--client_every", type=int, default=0, help="every k-th trainer runs in client mode")
@@ -95,13 +98,16 @@ def main(argv=None):
 
     # 2. trainer + aux world
     world = args.n_trainers + args.n_aux
-    n_gpus = args.n_gpus or args.n_trainers
+    n_gpus = args.n_gpus or world
+    if world > n_gpus:
+        raise SystemExit(f"{args.n_trainers} trainers + {args.n_aux} aux peers need {world} GPUs (one RCCL rank per "
+                         f"device), the node has {n_gpus}")
     port = _free_port()
     common = ["--experiment_prefix", args.experiment_prefix, *(["--initial_peers", root] if root else [])]
     common += fleet_flags(args.fleet, args.n_trainers, args.client_every) + extra
     for r in range(world):
         aux = r >= args.n_trainers
-        env = dict(env0, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r % n_gpus), MASTER_ADDR="127.0.0.1",
+        env = dict(env0, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port))
         mod = "dedloc_amd.cli.run_aux" if aux else "dedloc_amd.cli.run_trainer"
         cmd = [py, "-m", mod, *common, *(["--sahajbert"] if args.sahajbert and not aux else [])]

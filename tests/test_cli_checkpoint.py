@@ -120,3 +120,31 @@ def test_run_trainer_single_cpu_peer(tmp_path, sahajbert):
         assert max(rec["step"] for rec in recs) >= 2
     finally:
         root.shutdown()
+
+
+@pytest.mark.multiproc
+@pytest.mark.timeout(420)
+def test_launch_collaboration_coordinator_trainers_aux_cpu(tmp_path):
+    """The single-node launcher (AWS_runner stand-in, D9): coordinator + 2 trainers + 1 auxiliary peer
+    in one world on CPU/gloo; the trainers finish their global steps and the coordinator's metrics
+    file reports both trainers alive (the aux peer publishes no training metrics)."""
+    logs = tmp_path / "logs"
+    cmd = [sys.executable, "-m", "dedloc_amd.cli.launch_collaboration", "--n_trainers", "2", "--n_aux", "1",
+           "--experiment_prefix", "launch", "--log_dir", str(logs), "--duration", "360", "--",
+           "--device", "cpu", "--config_path", _tiny_dir(tmp_path), "--per_device_train_batch_size", "2",
+           "--seq_length", "64", "--target_batch_size", "8", "--stop_after_global_steps", "3", "--save_steps", "0",
+           "--output_dir", str(tmp_path / "out"), "--min_refresh_period", "0.05", "--default_refresh_period", "0.1",
+           "--dht_listen_on", "127.0.0.1:*", "--listen_on", "127.0.0.1:*", "--averaging_expiration", "3",
+           "--compression", "NONE"]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400, env=env)
+    tails = {p.name: p.read_text()[-1500:] for p in logs.glob("*.log")}
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:], tails)
+    assert "coordinator DHT root at" in r.stdout
+    for t in ("trainer0.log", "trainer1.log"):
+        assert "Traceback" not in tails[t], tails[t]
+    recs = [json.loads(x) for x in (logs / "coordinator_metrics.jsonl").read_text().splitlines()] \
+        if (logs / "coordinator_metrics.jsonl").exists() else []
+    assert recs and max(rec["step"] for rec in recs) >= 1 and max(rec["alive peers"] for rec in recs) == 2, tails
