@@ -10,6 +10,14 @@
 //     gathered into a group that closes when it reaches `target` members, when `expected` live
 //     peers have joined, or when the window of the first joiner expires (failing if it is then
 //     smaller than `min`).  Every member receives the same ordered member list + group id.
+//   * Small groups (Moshpit-style, `target` < `expected`, e.g. SwAV's target_group_size 4 with 8
+//     peers): the round gathers every expected peer, then splits them into G = ceil(n / target)
+//     groups by rank in peer-id order, alternating between two partitions — contiguous blocks on
+//     even rounds of the key, stride-G classes on odd rounds.  Each stride class holds a member
+//     of every block (G <= target), so two consecutive rounds of equal-weight peers reproduce the
+//     exact global average, and only 2G member sets ever occur (their data-plane communicators
+//     are created once).  Closing at the first `target` arrivals instead would let an always-
+//     faster subset average only among itself, and the collaboration would split in two.
 //
 // Transport: TCP, one thread per connection, length-prefixed frames:
 //   request  = u32 len | u8 op | payload      response = u32 len | payload
@@ -20,6 +28,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -65,8 +74,51 @@ struct Group {
   std::vector<Member> members;
   double deadline = 0;
   uint32_t target = 0, min_size = 2, expected = 0;
+  uint64_t round = 0;                 // completed rounds of this group key before this one
   bool closed = false, failed = false;
+  // filled at close: member index -> sub-group, and per sub-group its member indices, id, failed
+  std::vector<int> part_of;
+  std::vector<std::vector<int>> parts;
+  std::vector<uint64_t> part_ids;
+  std::vector<bool> part_failed;
 };
+
+// Close a gathered round: one group of everybody, or the Moshpit split described at the top.
+void close_group(Group& gr, uint64_t& next_id) {
+  gr.closed = true;
+  const int n = (int)gr.members.size();
+  gr.part_of.assign(n, 0);
+  gr.parts.clear();
+  gr.part_ids.clear();
+  gr.part_failed.clear();
+  const int target = (int)std::max<uint32_t>(1, gr.target);
+  if (n <= target) {
+    std::vector<int> all(n);
+    for (int i = 0; i < n; ++i) all[i] = i;
+    gr.parts.push_back(all);
+    gr.part_ids.push_back(gr.id);
+    gr.part_failed.push_back(n < (int)gr.min_size);
+    gr.failed = gr.part_failed[0];
+    return;
+  }
+  std::vector<int> order(n);
+  for (int i = 0; i < n; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(),
+            [&](int a, int b) { return gr.members[a].peer_id < gr.members[b].peer_id; });
+  const int G = (n + target - 1) / target;
+  const int block = (n + G - 1) / G;
+  gr.parts.assign(G, {});
+  for (int p = 0; p < n; ++p) {
+    const int part = (gr.round & 1) ? p % G : p / block;
+    gr.parts[part].push_back(order[p]);
+    gr.part_of[order[p]] = part;
+  }
+  for (int q = 0; q < G; ++q) {
+    gr.part_ids.push_back(q == 0 ? gr.id : ++next_id);
+    gr.part_failed.push_back((int)gr.parts[q].size() < (int)gr.min_size);
+  }
+  gr.failed = false;
+}
 
 // ------------------------------------------------------------------ wire helpers
 struct Reader {
@@ -190,8 +242,8 @@ class Server {
       for (auto it = groups_.begin(); it != groups_.end();) {
         Group& gr = *it->second;
         if (!gr.closed && t >= gr.deadline) {
-          gr.closed = true;
-          gr.failed = gr.members.size() < gr.min_size;
+          close_group(gr, next_group_);
+          ++rounds_[it->first];
           changed = true;
         }
         if (gr.closed) it = groups_.erase(it);  // members hold shared_ptrs
@@ -319,7 +371,16 @@ class Server {
     if (it != groups_.end() && !it->second->closed) {
       gr = it->second;
       for (auto& m : gr->members)
-        if (m.peer_id == peer) { gr.reset(); break; }  // duplicate join: start a fresh group
+        if (m.peer_id == peer) {  // duplicate join (the peer gave up on this round): the round fails
+          close_group(*gr, next_group_);
+          for (size_t q = 0; q < gr->part_failed.size(); ++q) gr->part_failed[q] = true;
+          gr->failed = true;
+          ++rounds_[gkey];
+          groups_.erase(it);
+          cv_.notify_all();
+          gr.reset();
+          break;
+        }
     }
     if (!gr) {
       gr = std::make_shared<Group>();
@@ -328,24 +389,37 @@ class Server {
       gr->target = std::max<uint32_t>(1, target);
       gr->min_size = std::max<uint32_t>(1, min_size);
       gr->expected = expected;
+      gr->round = rounds_[gkey];
       groups_[gkey] = gr;
     }
     gr->members.push_back(Member{peer, info});
+    const int me = (int)gr->members.size() - 1;
     if (expected > gr->expected) gr->expected = expected;
     const size_t n = gr->members.size();
-    if (n >= gr->target || (gr->expected > 0 && n >= gr->expected)) {
-      gr->closed = true;
-      gr->failed = n < gr->min_size;
+    // with more expected peers than the target group size the round gathers everybody first
+    // (then splits); otherwise it closes at the target size or when the expected peers are in
+    const bool split_round = gr->expected > gr->target;
+    if ((!split_round && n >= gr->target) || (gr->expected > 0 && n >= gr->expected)) {
+      close_group(*gr, next_group_);
+      ++rounds_[gkey];
       groups_.erase(gkey);
       cv_.notify_all();
     }
     cv_.wait(g, [&] { return gr->closed || !running_; });
-    w.pod<uint8_t>(gr->failed || !running_ ? 1 : 0);
-    w.pod<uint64_t>(gr->id);
-    w.pod<uint32_t>((uint32_t)gr->members.size());
-    for (auto& m : gr->members) {
-      w.bytes(m.peer_id);
-      w.bytes(m.info);
+    const bool closed_ok = running_ && gr->closed && me < (int)gr->part_of.size();
+    const int part = closed_ok ? gr->part_of[me] : 0;
+    const bool failed = !closed_ok || gr->part_failed[part];
+    w.pod<uint8_t>(failed ? 1 : 0);
+    w.pod<uint64_t>(closed_ok ? gr->part_ids[part] : gr->id);
+    if (!closed_ok) {
+      w.pod<uint32_t>(0);
+      return;
+    }
+    const std::vector<int>& mine = gr->parts[part];
+    w.pod<uint32_t>((uint32_t)mine.size());
+    for (int i : mine) {
+      w.bytes(gr->members[i].peer_id);
+      w.bytes(gr->members[i].info);
     }
   }
 
@@ -375,6 +449,7 @@ class Server {
   std::condition_variable cv_, done_cv_;
   std::map<std::string, Record> store_;
   std::map<std::string, std::shared_ptr<Group>> groups_;
+  std::map<std::string, uint64_t> rounds_;  // closed rounds per group key (partition parity)
   std::vector<int> clients_;
   int active_ = 0;
   uint64_t next_group_ = 0, stores_ = 0, gets_ = 0, sweep_ = 0;

@@ -97,6 +97,71 @@ def test_dht_matchmaking_forms_one_group(dht):
     assert sorted(m[1]["rank"] for m in out[0][2]) == [0, 1, 2]
 
 
+def test_dht_matchmaking_small_groups_alternate_partitions(dht):
+    """target_group_size < peers (SwAV: groups of 4 out of 8): every round gathers all expected peers
+    and splits them; even rounds take contiguous blocks of the peer-id order, odd rounds stride
+    classes, so two rounds of equal-weight averaging mix the whole collaboration (Moshpit), and an
+    always-early subset can no longer average only among itself."""
+    import threading
+
+    def one_round():
+        out = {}
+
+        def join(i):
+            time.sleep(0.01 * (7 - i))  # arrival order is the reverse of the peer-id order
+            out[i] = dht.join_group(b"moshpit", f"p{i}".encode(), {"rank": i}, target_size=4, min_size=2,
+                                    expected_size=8, window=5.0, timeout=10.0)
+
+        ts = [threading.Thread(target=join, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert all(out[i][0] for i in range(8))
+        groups = {}
+        for i in range(8):
+            ranks = tuple(sorted(m[1]["rank"] for m in out[i][2]))
+            assert i in ranks and len(ranks) == 4
+            groups.setdefault(out[i][1], set()).add(ranks)
+        assert len(groups) == 2 and all(len(v) == 1 for v in groups.values())  # one member list per group id
+        return sorted(next(iter(v)) for v in groups.values())
+
+    r0, r1, r2 = one_round(), one_round(), one_round()
+    assert r0 == [(0, 1, 2, 3), (4, 5, 6, 7)]
+    assert r1 == [(0, 2, 4, 6), (1, 3, 5, 7)]
+    assert r2 == r0
+    # two rounds of plain averaging in these groups give every peer the global mean
+    x = np.arange(8, dtype=np.float64)
+    for part in (r0, r1):
+        for grp in part:
+            x[list(grp)] = x[list(grp)].mean()
+    assert np.allclose(x, 3.5)
+
+
+def test_dht_matchmaking_duplicate_join_fails_the_open_round(dht):
+    """A peer that re-joins a round it already waits in (it gave up on it client-side) fails that round
+    for everybody in it instead of leaving them blocked, and starts a fresh one."""
+    import threading
+
+    out = {}
+
+    def join(tag, peer, timeout):
+        try:
+            out[tag] = dht.join_group(b"dup", peer, {}, target_size=4, min_size=2, expected_size=3, window=30.0,
+                                      timeout=timeout)
+        except OSError as e:  # the re-joined peer waits alone in the fresh round until its own timeout
+            out[tag] = e
+
+    t1 = threading.Thread(target=join, args=("a", b"p0", 20.0))
+    t1.start()
+    time.sleep(0.3)
+    t2 = threading.Thread(target=join, args=("b", b"p0", 2.0))  # the same peer again: round 1 fails
+    t2.start()
+    t1.join(timeout=15)
+    assert not t1.is_alive() and out["a"][0] is False
+    t2.join(timeout=15)
+
+
 # ----------------------------------------------------------------------------- crypto + validators
 def test_rsa_sign_verify_roundtrip():
     k = RSAPrivateKey(bits=1024)
