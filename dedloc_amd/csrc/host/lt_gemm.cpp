@@ -11,19 +11,33 @@
 //
 // Epilogues: BIAS (fp32 bias read in the epilogue — no per-call bias cast kernel) and beta=1
 // accumulation with a separate C (residual-branch sums, fp32 weight-gradient accumulation).
-// GELU_AUX_BIAS / DGELU_BGRAD are wired but NOT used: on ROCm 7.2 / gfx950 the former has no
-// solution and the latter returned wrong results for our layout (scripts/lt_debug.py, measured).
+// GELU_AUX_BIAS / DGELU_BGRAD are wired but NOT used: on ROCm 7.2 / gfx950 neither has a solution
+// (bench/hip/lt_epilogue_probe.cpp, profiles/hipblaslt_gelu_epilogue_probe.log).
+//
+// Plan choice, at the first call of a (layout, shape, epilogue) key:
+//   1. the tuning database (DEDLOC_LT_DB, default the in-package lt_tuning_gfx950.txt written by
+//      python on import): key -> hipBLASLt solution index, verified with matmulIsAlgoSupported;
+//   2. otherwise autotune: time the heuristic's top-64 candidates; for large bf16-output problems
+//      (forward / data-gradient GEMMs) also EVERY supported solution of the problem type
+//      (hipblaslt_ext::getAllAlgos).  The heuristic list misses the direct-to-LDS "CMS" 256x256
+//      kernels: forward QKV at T = 262144 runs 1021 us (1.61 PF/s) vs 1207 us for the best of the
+//      top-64 (bench/hip/lt_allalgos_probe.cpp, profiles/allalgos_fwd_qkv.log); the weight-gradient
+//      GEMMs gain nothing from it and skip it.  Newly tuned keys are appended to DEDLOC_LT_DB_OUT.
 #include <algorithm>
 #include <utility>
 #include <vector>
 #include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
 
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <map>
+#include <sstream>
+#include <string>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -62,6 +76,38 @@ struct DevState {
 
 std::mutex g_mu;
 std::map<Key, Plan> g_plans;
+
+// ---- tuning database: one "key index" line per plan (key = every Key field but the device)
+std::string key_str(const Key& k) {
+  std::ostringstream o;
+  o << k.ta << ',' << k.tb << ',' << k.M << ',' << k.N << ',' << k.K << ',' << k.lda << ',' << k.ldb << ',' << k.ldd
+    << ',' << k.ldaux << ',' << k.d_f32 << ',' << k.in_f32 << ',' << k.beta_nz << ',' << k.epi << ',' << k.bias_f32
+    << ',' << k.batch << ',' << k.sA << ',' << k.sB << ',' << k.sD;
+  return o.str();
+}
+
+std::map<std::string, int>& tuning_db() {
+  static std::map<std::string, int> db;
+  static bool loaded = false;
+  if (!loaded) {
+    loaded = true;
+    if (const char* path = std::getenv("DEDLOC_LT_DB")) {
+      std::ifstream f(path);
+      std::string key;
+      int idx;
+      while (f >> key >> idx) db[key] = idx;
+    }
+  }
+  return db;
+}
+
+void record_tuning(const std::string& key, int idx) {
+  tuning_db()[key] = idx;
+  if (const char* out = std::getenv("DEDLOC_LT_DB_OUT")) {
+    std::ofstream f(out, std::ios::app);
+    f << key << ' ' << idx << '\n';
+  }
+}
 std::map<int, DevState> g_dev;
 
 constexpr size_t kWorkspace = 128ull << 20;
@@ -102,7 +148,7 @@ bool set_ptrs(hipblasLtMatmulDesc_t desc, const DlLtArgs& a) {
   return true;
 }
 
-bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
+bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st, const std::string& kstr) {
   const hipDataType in_t = a.in_f32 ? HIP_R_32F : HIP_R_16BF;
   const hipDataType d_t = a.d_f32 ? HIP_R_32F : HIP_R_16BF;
   if (hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return false;
@@ -141,6 +187,28 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
   }
   if (!set_ptrs(p.desc, a)) return false;
 
+  const float alpha_one = 1.f;
+  const bool dbg = std::getenv("DEDLOC_LT_DEBUG") != nullptr;
+  {  // 1. tuning database
+    auto it = tuning_db().find(kstr);
+    if (it != tuning_db().end()) {
+      std::vector<int> idx{it->second};
+      std::vector<hipblasLtMatmulHeuristicResult_t> r;
+      size_t need = 0;
+      if (hipblaslt_ext::getAlgosFromIndex(s->handle, idx, r) == HIPBLAS_STATUS_SUCCESS && !r.empty() &&
+          hipblaslt_ext::matmulIsAlgoSupported(s->handle, p.desc, &alpha_one, p.la, p.lb, &a.beta, p.ld, p.ld,
+                                               r[0].algo, need) == HIPBLAS_STATUS_SUCCESS &&
+          need <= s->ws_size) {
+        p.algo = r[0].algo;
+        p.ws = need;
+        p.ok = true;
+        if (dbg) std::fprintf(stderr, "[lt] plan %s: tuning database solution %d\n", kstr.c_str(), it->second);
+        return true;
+      }
+      if (dbg) std::fprintf(stderr, "[lt] plan %s: database solution %d not usable, retuning\n", kstr.c_str(), it->second);
+    }
+  }
+
   hipblasLtMatmulPreference_t pref;
   hipblasLtMatmulPreferenceCreate(&pref);
   uint64_t wsz = s->ws_size;
@@ -159,9 +227,23 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
                  a.transA, a.transB, a.M, a.N, a.K, a.epilogue, a.d_f32, a.beta, (int)hs, n);
   if (hs != HIPBLAS_STATUS_SUCCESS || n <= 0) return false;
 
+  // 2. autotune over candidate algos: the heuristic list, plus every supported solution of the
+  // problem type for large bf16-output problems
+  std::vector<hipblasLtMatmulAlgo_t> cand;
+  std::vector<size_t> cand_ws;
+  for (int i = 0; i < n; ++i)
+    if (res[i].state == HIPBLAS_STATUS_SUCCESS && res[i].workspaceSize <= s->ws_size) {
+      cand.push_back(res[i].algo);
+      cand_ws.push_back(res[i].workspaceSize);
+    }
+  if (cand.empty()) return false;
+  const double flops = 2.0 * a.M * a.N * a.K * std::max(1, a.batch);
+  const char* ex_env = std::getenv("DEDLOC_LT_EXHAUSTIVE");
+  const bool exhaustive = !(ex_env && ex_env[0] == '0') && !a.d_f32 && !a.in_f32 && flops >= 2e11 &&
+                          a.epilogue != DL_LT_GELU_AUX_BIAS && a.epilogue != DL_LT_DGELU_BGRAD;
   int best = 0;
-  if (n > 1) {
-    // autotune: time every candidate into a scratch output (inputs are read-only; beta=0)
+  if (cand.size() > 1 || exhaustive) {
+    // time every candidate into a scratch output (inputs are read-only)
     const size_t d_bytes = (size_t)(a.batch > 1 ? a.strideD * a.batch : a.ldd * a.M) * (a.d_f32 ? 4 : 2);
     const size_t aux_bytes = (a.aux ? (size_t)a.ldaux * a.M * 2 : 0);
     const size_t bias_bytes = (size_t)a.N * 4;
@@ -182,45 +264,77 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st) {
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
       hipEventCreate(&e1);
-      const float one = 1.f, zero = 0.f;
-      auto run = [&](int i) {
-        return hipblasLtMatmul(s->handle, p.desc, &one, a.B, p.la, a.A, p.lb, &zero, t.D, p.ld, t.D, p.ld,
-                               &res[i].algo, s->workspace, s->ws_size, st);
+      const float one = 1.f;
+      auto run = [&](hipblasLtMatmulAlgo_t& algo) {
+        return hipblasLtMatmul(s->handle, p.desc, &one, a.B, p.la, a.A, p.lb, &a.beta, t.D, p.ld, t.D, p.ld, &algo,
+                               s->workspace, s->ws_size, st);
       };
-      auto time_ms = [&](int i, int reps) {
+      auto time_ms = [&](hipblasLtMatmulAlgo_t& algo, int reps) {
         hipEventRecord(e0, st);
-        for (int r = 0; r < reps; ++r) run(i);
+        for (int r = 0; r < reps; ++r) run(algo);
         hipEventRecord(e1, st);
         hipEventSynchronize(e1);
         float ms = 0.f;
         hipEventElapsedTime(&ms, e0, e1);
         return ms / reps;
       };
-      // round 1: every candidate, 3 runs; round 2: the 4 fastest again with 10 runs each, so a
-      // single noisy round-1 timing (clock ramp, a neighbour's traffic) cannot pick the plan
+      // round 1: every heuristic candidate, 3 runs
       std::vector<std::pair<float, int>> timed;
-      for (int i = 0; i < n; ++i) {
-        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize > s->ws_size) continue;
-        if (run(i) != HIPBLAS_STATUS_SUCCESS) continue;
-        timed.emplace_back(time_ms(i, 3), i);
+      for (size_t i = 0; i < cand.size(); ++i) {
+        if (run(cand[i]) != HIPBLAS_STATUS_SUCCESS) continue;
+        timed.emplace_back(time_ms(cand[i], 3), (int)i);
       }
       std::sort(timed.begin(), timed.end());
+      std::vector<std::pair<float, int>> finalists(timed.begin(), timed.begin() + std::min<size_t>(4, timed.size()));
+      if (exhaustive) {  // every supported solution once (after an untimed first launch)
+        std::vector<hipblasLtMatmulHeuristicResult_t> all;
+        const hipDataType io = HIP_R_16BF;
+        const hipDataType dt = a.d_f32 ? HIP_R_32F : HIP_R_16BF;
+        const hipblasOperation_t opA = a.transB ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+        const hipblasOperation_t opB = a.transA ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+        std::vector<std::pair<float, int>> ex;
+        const size_t first = cand.size();
+        if (hipblaslt_ext::getAllAlgos(s->handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, opA, opB, io, io, dt, dt,
+                                       HIPBLAS_COMPUTE_32F, all) == HIPBLAS_STATUS_SUCCESS) {
+          for (auto& r : all) {
+            size_t w = 0;
+            if (hipblaslt_ext::matmulIsAlgoSupported(s->handle, p.desc, &one, p.la, p.lb, &a.beta, p.ld, p.ld, r.algo,
+                                                     w) != HIPBLAS_STATUS_SUCCESS ||
+                w > s->ws_size)
+              continue;
+            if (run(r.algo) != HIPBLAS_STATUS_SUCCESS) continue;
+            cand.push_back(r.algo);
+            cand_ws.push_back(w);
+            ex.emplace_back(time_ms(r.algo, 1), (int)(cand.size() - 1));
+          }
+        }
+        std::sort(ex.begin(), ex.end());
+        for (size_t k = 0; k < ex.size() && k < 4; ++k) finalists.push_back(ex[k]);
+        std::fprintf(stderr, "[lt] exhaustive tune M=%d N=%d K=%d batch=%d: %zu heuristic + %zu supported solutions\n",
+                     a.M, a.N, a.K, a.batch, first, cand.size() - first);
+      }
+      // round 2: the finalists again with 10 runs each, so a single noisy round-1 timing (clock
+      // ramp, a neighbour's traffic) cannot pick the plan
       float best_ms = 1e30f;
-      for (size_t k = 0; k < timed.size() && k < 4; ++k) {
-        const float ms = time_ms(timed[k].second, 10);
+      for (auto& f : finalists) {
+        const float ms = time_ms(cand[f.second], 10);
         if (ms < best_ms) {
           best_ms = ms;
-          best = timed[k].second;
+          best = f.second;
         }
       }
+      if (exhaustive || dbg)
+        std::fprintf(stderr, "[lt] plan M=%d N=%d K=%d: %.1f us (%s)\n", a.M, a.N, a.K, best_ms * 1e3,
+                     best >= n ? "exhaustive" : "heuristic");
       hipEventDestroy(e0);
       hipEventDestroy(e1);
       set_ptrs(p.desc, a);
     }
   }
-  p.algo = res[best].algo;
-  p.ws = res[best].workspaceSize;
+  p.algo = cand[best];
+  p.ws = cand_ws[best];
   p.ok = true;
+  if (exhaustive) record_tuning(kstr, hipblaslt_ext::getIndexFromAlgo(p.algo));
   return true;
 }
 
@@ -237,7 +351,7 @@ int dl_lt_matmul(const DlLtArgs& a, hipStream_t st) {
   auto it = g_plans.find(k);
   if (it == g_plans.end()) {
     Plan p;
-    if (!build_plan(p, a, s, st)) p.ok = false;
+    if (!build_plan(p, a, s, st, key_str(k))) p.ok = false;
     it = g_plans.emplace(k, p).first;
   }
   Plan& p = it->second;
