@@ -3,8 +3,10 @@
 // dedloc's plan cache (csrc/host/lt_gemm.cpp) autotunes over the top-64 candidates of
 // hipblasLtMatmulAlgoGetHeuristic.  This probe times EVERY solution hipblaslt_ext::getAllAlgos
 // knows for the same problem type (supported ones only) to see whether a faster kernel exists
-// outside the heuristic's list — the weight-gradient GEMMs ("TN": both operands reduction-outer)
-// run at ~1.1 PF/s vs ~1.36 PF/s for the forward / data-gradient ones (profiles/README.md).
+// outside the heuristic's list.  Result (profiles/allalgos2_*.log, random operands): the forward
+// GEMMs have direct-to-LDS 256x256 solutions 11-13% faster back to back than the top-64's best;
+// the weight-gradient GEMMs none.  Inside the model step the gain shrinks to +0.4%
+// (profiles/lt_exhaustive_tune_b512.log), which is why lt_gemm.cpp keeps the search opt-in.
 //
 // Row-major contract as in lt_gemm.cpp: D[M,N] = op(A)[M,K] . op(B)[K,N], handed to hipBLASLt as the
 // column-major D^T = op(B)^T op(A)^T.
@@ -12,7 +14,7 @@
 //   fwd  : A = X [M=T, K], B = W [N, K] (transB), D bf16 [M, N]
 //
 //   hipcc --offload-arch=gfx950 -O2 bench/hip/lt_allalgos_probe.cpp -lhipblaslt -o bench/hip/probe_lt_allalgos
-//   ./probe_lt_allalgos wgrad M N T S | fwd M N K
+//   ./probe_lt_allalgos wgrad M N T S | fwd M N K | fwdb M N K  (fwdb: with the fp32 bias epilogue)
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>
@@ -24,6 +26,21 @@
 #include <string>
 #include <vector>
 
+// pseudo-random bf16 in [-1, 1) (constant operands let the chip clock higher and flatter the
+// timings by 10-30%: the first version of this probe filled 0x3c3c and overstated every kernel)
+__global__ void fill_random(uint16_t* p, long n, uint32_t seed) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    const float f = (float)(h & 0xffff) / 32768.f - 1.f;
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    p[i] = (uint16_t)(u >> 16);
+  }
+}
+
 #define CK(x)                                                                       \
   do {                                                                              \
     auto _s = (x);                                                                  \
@@ -32,11 +49,12 @@
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    std::printf("usage: %s wgrad M N T S | fwd M N K\n", argv[0]);
+    std::printf("usage: %s wgrad M N T S | fwd M N K | fwdb M N K\n", argv[0]);
     return 1;
   }
   const std::string mode = argv[1];
   const bool wg = mode == "wgrad";
+  const bool with_bias = mode == "fwdb";  // forward with the fp32-bias epilogue (what the model uses)
   const long M = std::atol(argv[2]), N = std::atol(argv[3]), KT = std::atol(argv[4]);
   const int S = wg && argc > 5 ? std::atoi(argv[5]) : 1;
   const long K = wg ? KT / S : KT;  // per-batch reduction length
@@ -51,8 +69,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&B, b_elems * 2));
   CK(hipMalloc(&D, d_bytes));
   CK(hipMalloc(&ws, wsz));
-  CK(hipMemset(A, 0x3c, a_elems * 2));  // ~1.0 in bf16 halves: finite, nonzero data
-  CK(hipMemset(B, 0x3c, b_elems * 2));
+  fill_random<<<4096, 256>>>((uint16_t*)A, a_elems, 1u);
+  fill_random<<<4096, 256>>>((uint16_t*)B, b_elems, 2u);
+  void* bias = nullptr;
+  CK(hipMalloc(&bias, N * 4));
+  CK(hipMemset(bias, 0, N * 4));
   hipblasLtHandle_t h;
   CK(hipblasLtCreate(&h));
   hipblasLtMatmulDesc_t desc;
@@ -61,6 +82,13 @@ int main(int argc, char** argv) {
   const hipblasOperation_t opB = transA ? HIPBLAS_OP_T : HIPBLAS_OP_N;  // hip "B" = our A
   CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
   CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
+  if (with_bias) {
+    const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
+    const int32_t bt = HIP_R_32F;
+    CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
+    CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+    CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
+  }
   const hipDataType dt = wg ? HIP_R_32F : HIP_R_16BF;
   hipblasLtMatrixLayout_t la, lb, ld;
   const uint64_t a_rows = transB ? K : N, a_cols = transB ? N : K;

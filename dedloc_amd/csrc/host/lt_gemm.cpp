@@ -17,12 +17,16 @@
 // Plan choice, at the first call of a (layout, shape, epilogue) key:
 //   1. the tuning database (DEDLOC_LT_DB, default the in-package lt_tuning_gfx950.txt written by
 //      python on import): key -> hipBLASLt solution index, verified with matmulIsAlgoSupported;
-//   2. otherwise autotune: time the heuristic's top-64 candidates; for large bf16-output problems
-//      (forward / data-gradient GEMMs) also EVERY supported solution of the problem type
-//      (hipblaslt_ext::getAllAlgos).  The heuristic list misses the direct-to-LDS "CMS" 256x256
-//      kernels: forward QKV at T = 262144 runs 1021 us (1.61 PF/s) vs 1207 us for the best of the
-//      top-64 (bench/hip/lt_allalgos_probe.cpp, profiles/allalgos_fwd_qkv.log); the weight-gradient
-//      GEMMs gain nothing from it and skip it.  Newly tuned keys are appended to DEDLOC_LT_DB_OUT.
+//   2. otherwise autotune: time the heuristic's top-64 candidates; with DEDLOC_LT_EXHAUSTIVE=1, for
+//      large bf16-output problems (forward / data-gradient GEMMs) also EVERY supported solution of
+//      the problem type (hipblaslt_ext::getAllAlgos, ~230 runnable per plan, about 5 s each).  In
+//      isolation the heuristic list misses direct-to-LDS 256x256 kernels that run the forward
+//      GEMMs 11-13% faster back to back on random operands (bench/hip/lt_allalgos_probe.cpp,
+//      profiles/allalgos2_*.log), but inside the model step the heuristic's stream-K picks hold up:
+//      micro-step 936.5 (exhaustive) vs 932.6 (heuristic) samples/s on one box
+//      (profiles/lt_exhaustive_tune_b512.log), so the search is opt-in; its results for the
+//      micro-batch-512 shapes ship as lt_tuning_gfx950.txt (935.3 from the database on the same box,
+//      and no tuning at start-up).  Newly tuned keys are appended to DEDLOC_LT_DB_OUT.
 #include <algorithm>
 #include <utility>
 #include <vector>
@@ -239,7 +243,7 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st, const s
   if (cand.empty()) return false;
   const double flops = 2.0 * a.M * a.N * a.K * std::max(1, a.batch);
   const char* ex_env = std::getenv("DEDLOC_LT_EXHAUSTIVE");
-  const bool exhaustive = !(ex_env && ex_env[0] == '0') && !a.d_f32 && !a.in_f32 && flops >= 2e11 &&
+  const bool exhaustive = (ex_env && ex_env[0] == '1') && !a.d_f32 && !a.in_f32 && flops >= 2e11 &&
                           a.epilogue != DL_LT_GELU_AUX_BIAS && a.epilogue != DL_LT_DGELU_BGRAD;
   int best = 0;
   if (cand.size() > 1 || exhaustive) {

@@ -43,7 +43,8 @@ def test_exhaustive_autotune_database_roundtrip(cuda, tmp_path):
     import torch
 
     db = tmp_path / "lt_db.txt"
-    rel1, err1 = _run({"DEDLOC_LT_DB": str(tmp_path / "none.txt"), "DEDLOC_LT_DB_OUT": str(db)}, str(tmp_path / "y1.pt"))
+    rel1, err1 = _run({"DEDLOC_LT_DB": str(tmp_path / "none.txt"), "DEDLOC_LT_DB_OUT": str(db),
+                       "DEDLOC_LT_EXHAUSTIVE": "1"}, str(tmp_path / "y1.pt"))
     assert rel1 < 1e-2
     assert "[lt] exhaustive tune" in err1
     lines = db.read_text().split("\n")
