@@ -778,7 +778,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
                                                                   bool relu, bool want_dres,
                                                                   const c10::optional<at::Tensor>& sums,
                                                                   const c10::optional<at::Tensor>& dgamma_acc,
-                                                                  const c10::optional<at::Tensor>& dbeta_acc) {
+                                                                  const c10::optional<at::Tensor>& dbeta_acc,
+                                                                  const c10::optional<at::Tensor>& beta) {
   const int64_t G = mean.dim() == 2 ? mean.size(0) : 1;
   expect_nhwc(x, "x");
   expect_nhwc(y, "y");
@@ -805,9 +806,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
   }
   float* dgp = acc ? f32(*dgamma_acc) : f32(ws) + 2 * G * C;
   float* dbp = acc ? f32(*dbeta_acc) : f32(ws) + 2 * G * C + C;
+  // beta (BatchNorm+ReLU without a residual branch only): the ReLU mask comes from x, y is not read
+  const bool xmask = beta.has_value() && relu && !want_dres;
+  if (xmask) {
+    expect(*beta, at::kFloat, "beta");
+    TORCH_CHECK(beta->numel() == C, "beta size mismatch");
+  }
   check(dl_bn_bwd(cbf(g), cbf(y), cbf(x), f32(mean), f32(rstd), f32(gamma), sp, bf(dx),
                   want_dres ? bf(dres) : nullptr, dgp, dbp, R, (int)C, (int)G, relu, cur_stream(x),
-                  sums.has_value() ? 1 : 0, acc ? 1 : 0),
+                  sums.has_value() ? 1 : 0, acc ? 1 : 0, xmask ? f32(*beta) : nullptr),
         "bn_bwd");
   if (acc) return {dx, want_dres ? dres : at::empty({0}, x.options()), at::empty({0}, gamma.options()),
                    at::empty({0}, gamma.options())};

@@ -84,7 +84,7 @@ int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
               float momentum, int relu, hipStream_t st, int sums_zeroed = 0);
 int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
               const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
-              int G, int relu, hipStream_t st, int sums_zeroed = 0, int accumulate = 0);
+              int G, int relu, hipStream_t st, int sums_zeroed = 0, int accumulate = 0, const float* beta = nullptr);
 
 // conv.hip — implicit-GEMM NHWC convolutions.  The gathered operand is an NHWC image
 // [Nimg, H, W, C]; GEMM rows m = (n, i, j) over [Nimg, I, J]; tap t = (tr < TR, ts < TS) reads

@@ -159,12 +159,18 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------------------------- backward stats
+// ReLU mask without reading y: for a BatchNorm+ReLU with no residual branch, y > 0 exactly when the
+// pre-activation fmaf(x, gamma*rstd, beta - mean*gamma*rstd) > 0 — the forward's own expression over
+// the saved mean / rstd — so with `beta` given the backward passes read dy and x only (2 of 3
+// streams; with a residual the mask depends on it and y is read).
 __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __restrict__ dy,
                                                                 const bf16_t* __restrict__ y,
                                                                 const bf16_t* __restrict__ x,
                                                                 const float* __restrict__ mean,
                                                                 const float* __restrict__ rstd, float* __restrict__ sums,
-                                                                long R, int C, long rpb, int relu) {
+                                                                long R, int C, long rpb, int relu,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta) {
   __shared__ float red[kThreads * 16];
   const int CV = C >> 3, rpi = kThreads / CV;
   const int cv = threadIdx.x % CV, rsub = threadIdx.x / CV;
@@ -176,11 +182,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
   rstd += (long)blockIdx.y * C;
   sums += (long)blockIdx.y * 2 * C;
   const long r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
-  float mu[8], rs[8];
+  float mu[8], rs[8], sc[8], sh[8];
+  const bool xmask = relu && beta != nullptr;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mu[j] = mean[cv * 8 + j];
     rs[j] = rstd[cv * 8 + j];
+    if (xmask) {
+      sc[j] = gamma[cv * 8 + j] * rs[j];
+      sh[j] = beta[cv * 8 + j] - mu[j] * sc[j];
+    }
   }
   float sg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sgx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   long r = r0 + rsub;
@@ -191,13 +202,14 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
       const long off = (r + u * rpi) * C + cv * 8;
       ld8(dy + off, g[u]);
       ld8(x + off, xv[u]);
-      if (relu) ld8(y + off, yv[u]);
+      if (relu && !xmask) ld8(y + off, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float gg = (!relu || yv[u][j] > 0.f) ? g[u][j] : 0.f;
+        const bool live = !relu || (xmask ? fmaf(xv[u][j], sc[j], sh[j]) > 0.f : yv[u][j] > 0.f);
+        const float gg = live ? g[u][j] : 0.f;
         sg[j] += gg;
         sgx[j] = fmaf(gg, (xv[u][j] - mu[j]) * rs[j], sgx[j]);
       }
@@ -207,7 +219,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
     float g[8], xv[8];
     ld8(dy + off, g);
     ld8(x + off, xv);
-    if (relu) {
+    if (xmask) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+    } else if (relu) {
       float yv[8];
       ld8(y + off, yv);
 #pragma unroll
@@ -243,8 +258,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
                                                              const float* __restrict__ sums, bf16_t* __restrict__ dx,
                                                              bf16_t* __restrict__ dres, float* __restrict__ dgamma,
                                                              float* __restrict__ dbeta, long R, int C, int relu,
-                                                             int accumulate) {
-  __shared__ float k1[2048], mg[2048], mgx[2048], mu_s[2048], rs_s[2048];
+                                                             int accumulate, const float* __restrict__ beta) {
+  __shared__ float k1[2048], mg[2048], mgx[2048], mu_s[2048], rs_s[2048], sh_s[2048];
+  const bool xmask = relu && beta != nullptr;  // ReLU mask from x (see bn_bwd_stats_kernel)
   const int grp = blockIdx.y, G = gridDim.y;
   const float invR = 1.f / (float)R;
   for (int c = threadIdx.x; c < C; c += kThreads) {
@@ -252,6 +268,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
     rs_s[c] = rstd[(long)grp * C + c];
     mu_s[c] = mean[(long)grp * C + c];
     k1[c] = gamma[c] * rs_s[c];
+    if (xmask) sh_s[c] = beta[c] - mu_s[c] * k1[c];
     mg[c] = sg[c] * invR;
     mgx[c] = sg[C + c] * invR;
     if (blockIdx.x == 0 && grp == 0) {  // parameter grads: sum over the statistics groups
@@ -286,13 +303,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
     for (int u = 0; u < 2; ++u) {
       ld8(dy + (i + u * stride) * 8, g[u]);
       ld8(x + (i + u * stride) * 8, xv[u]);
-      if (relu) ld8(y + (i + u * stride) * 8, yv[u]);
+      if (relu && !xmask) ld8(y + (i + u * stride) * 8, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const long iv = i + u * stride;
       const int c0 = ((int)iv & (CV - 1)) * 8;
-      if (relu) {
+      if (xmask) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[u][j] = fmaf(xv[u][j], k1[c0 + j], sh_s[c0 + j]) > 0.f ? g[u][j] : 0.f;
+      } else if (relu) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[u][j] = yv[u][j] > 0.f ? g[u][j] : 0.f;
       }
@@ -312,7 +332,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
     float g[8], xv[8];
     ld8(dy + i * 8, g);
     ld8(x + i * 8, xv);
-    if (relu) {
+    if (xmask) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], k1[c0 + j], sh_s[c0 + j]) > 0.f ? g[j] : 0.f;
+    } else if (relu) {
       float yv[8];
       ld8(y + i * 8, yv);
 #pragma unroll
@@ -374,16 +397,18 @@ int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
 }
 
 // accumulate: dgamma / dbeta += (the parameters' gradient buffers) instead of =
+// beta: non-null -> the ReLU mask is recomputed from x (BatchNorm+ReLU without a residual branch;
+// y is then not read at all)
 int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
               const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
-              int G, int relu, hipStream_t st, int sums_zeroed, int accumulate) {
+              int G, int relu, hipStream_t st, int sums_zeroed, int accumulate, const float* beta) {
   if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
   if (!sums_zeroed) DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
   long rpb;
   const int nb = stats_blocks(R, C, rpb);
-  bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu);
+  bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu, gamma, beta);
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
   bn_bwd_dx_kernel<<<dim3(na, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
-                                                     relu, accumulate);
+                                                     relu, accumulate, beta);
   return 0;
 }

@@ -25,6 +25,11 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 
+# BN+ReLU (no residual) backward reads only dy and x: the ReLU mask is recomputed from x
+# (DEDLOC_BN_XMASK=0: read y instead — A/B measurement switch)
+_BN_XMASK = os.environ.get("DEDLOC_BN_XMASK", "1") != "0"
+
+
 class _BNAct(torch.autograd.Function):
     """Training-mode BN (+ residual) (+ ReLU) on channels-last bf16 via the fused HIP kernels.
 
@@ -38,20 +43,22 @@ class _BNAct(torch.autograd.Function):
     def forward(ctx, x, gamma, beta, res, running_mean, running_var, relu, eps, momentum, groups, ws, module):
         y, mean, rstd = torch.ops.dedloc.bn_fwd(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu,
                                                 groups, None if ws is None else ws[0])
-        ctx.save_for_backward(x, y, mean, rstd, gamma)
+        ctx.save_for_backward(x, y, mean, rstd, gamma, beta)
         ctx.relu, ctx.has_res, ctx.ws, ctx.module = relu, res is not None, ws, module
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, rstd, gamma = ctx.saved_tensors
+        x, y, mean, rstd, gamma, beta = ctx.saved_tensors
         m = ctx.module
         gw, gb = (m.weight.grad, m.bias.grad) if m is not None else (None, None)
         acc = (m is not None and m.inplace_grad and gw is not None and gb is not None
                and gw.dtype == torch.float32 and gb.dtype == torch.float32)
         dx, dres, dgamma, dbeta = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, gamma, ctx.relu, ctx.has_res,
                                                           None if ctx.ws is None else ctx.ws[1],
-                                                          gw if acc else None, gb if acc else None)
+                                                          gw if acc else None, gb if acc else None,
+                                                          # BN+ReLU without a residual: ReLU mask from x, y unread
+                                                          beta if (_BN_XMASK and ctx.relu and not ctx.has_res) else None)
         if acc:
             dgamma = dbeta = None
         return (dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None)

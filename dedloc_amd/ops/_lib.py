@@ -51,7 +51,7 @@ _SCHEMAS = [
     "bn_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
     "float eps, float momentum, bool relu, int groups=1, Tensor(c!)? sums=None) -> (Tensor, Tensor, Tensor)",
     "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres, "
-    "Tensor(a!)? sums=None, Tensor(b!)? dgamma_acc=None, Tensor(c!)? dbeta_acc=None) "
+    "Tensor(a!)? sums=None, Tensor(b!)? dgamma_acc=None, Tensor(c!)? dbeta_acc=None, Tensor? beta=None) "
     "-> (Tensor, Tensor, Tensor, Tensor)",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
     "conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor",
@@ -507,7 +507,8 @@ def _conv2d_wgrad_cpu(dy, x, dw, stride, pad):
 
 
 @_impl("bn_bwd")
-def _bn_bwd_cpu(dy, y, x, mean, rstd, gamma, relu, want_dres, sums=None, dgamma_acc=None, dbeta_acc=None):
+def _bn_bwd_cpu(dy, y, x, mean, rstd, gamma, relu, want_dres, sums=None, dgamma_acc=None, dbeta_acc=None,
+                beta=None):  # beta: the GPU kernels' ReLU mask from x; the reference reads y
     mean2 = mean.reshape(-1, x.shape[1])
     rstd2 = rstd.reshape(-1, x.shape[1])
     G = mean2.shape[0]

@@ -362,6 +362,26 @@ def test_fused_bn_act_vs_torch(cuda, N, C, H, relu, res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,C,H,G", [(8, 64, 28, 1), (16, 256, 7, 1), (12, 128, 12, 3), (4, 2048, 3, 2)])
+def test_bn_bwd_relu_mask_from_x_equals_mask_from_y(cuda, N, C, H, G):
+    """BatchNorm+ReLU without a residual: the backward's ReLU mask recomputed from x (beta given, y
+    never read) gives the same gradients as the mask read from y, statistics groups included."""
+    torch.manual_seed(13)
+    cl = torch.channels_last
+    x = (torch.randn(N, C, H, H, device=cuda) * 2 + 0.3).bfloat16().contiguous(memory_format=cl)
+    g, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, mean, rstd = torch.ops.dedloc.bn_fwd(x, None, g, b, rm, rv, 1e-5, 0.1, True, G)
+    dy = torch.randn_like(y)
+    ref = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, g, True, False)
+    garbage = torch.full_like(y, float("nan"))  # proves y is not read on the x-mask path
+    out = torch.ops.dedloc.bn_bwd(dy, garbage, x, mean, rstd, g, True, False, beta=b)
+    for a, r in ((out[0], ref[0]), (out[2], ref[2]), (out[3], ref[3])):
+        assert torch.isfinite(a.float()).all()
+        assert ((a.float() - r.float()).norm() / (r.float().norm() + 1e-12)).item() < 1e-5
+
+
+@pytest.mark.gpu
 def test_bnact_module_fused_matches_stock(cuda):
     from dedloc_amd.models.resnet_swav import BNAct
 
