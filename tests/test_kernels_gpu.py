@@ -635,3 +635,35 @@ def test_gemm_other_backends(cuda, monkeypatch, policy):
     a = torch.randn(512, 256, device=cuda).bfloat16()
     w = torch.randn(512, 256, device=cuda).bfloat16()
     assert rel(OPS.gemm(a, w, None, None, False, True, 0), a.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.timeout(240)
+def test_albert_pretraining_converges_on_gpu(cuda):
+    """End to end through the HIP kernels: a small shared-layer ALBERT memorises one fixed MLM+SOP batch
+    under fused LAMB + global-norm clipping (the collaborative step's optimizer path); the loss must
+    fall well below its start, with finite gradients throughout."""
+    from dedloc_amd.data.synthetic_mlm import SyntheticSOPStream
+    from dedloc_amd.models import albert as A
+    from dedloc_amd.optim.lamb import FusedLamb
+
+    torch.manual_seed(0)
+    cfg = A.AlbertConfig.tiny(hidden_size=256, intermediate_size=1024, num_attention_heads=4, num_hidden_layers=4,
+                              max_position_embeddings=128, vocab_size=1000)
+    model = A.AlbertForPreTraining(cfg)
+    model.materialize(cuda)
+    model.train()
+    opt = FusedLamb(model.flat, lr=2e-2, weight_decay=0.01, clamp_value=1e4, no_decay=model.no_decay_names())
+    batch = SyntheticSOPStream(16, 128, cfg.vocab_size, seed=3, device=cuda).next_batch()
+    losses = []
+    for _ in range(150):  # CPU reference ops, same seeds: 7.65 -> 1.98
+        model.flat.grad.zero_()
+        out = model(batch["input_ids"], batch["attention_mask"], batch["token_type_ids"],
+                    sentence_order_label=batch["sentence_order_label"], mlm_positions=batch["mlm_positions"],
+                    mlm_labels=batch["mlm_labels"])
+        out["loss"].backward()
+        gn = model.flat.grad.norm()
+        model.flat.grad.mul_(torch.clamp(1.0 / (gn + 1e-6), max=1.0))  # max_grad_norm = 1.0
+        opt.step()
+        losses.append(float(out["loss"].detach()))
+    assert all(math.isfinite(v) for v in losses)
+    assert losses[-1] < 0.5 * losses[0], (losses[0], losses[-1])
