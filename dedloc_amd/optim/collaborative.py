@@ -57,6 +57,7 @@ class CollaborationState:
     num_clients: int
     eta_next_step: float
     next_fetch_time: float
+    own_samples: int = 0  # this peer's samples as counted in samples_accumulated
 
     @property
     def ready_for_step(self) -> bool:
@@ -65,6 +66,7 @@ class CollaborationState:
     def register_step(self, local_step: int):
         self.optimizer_step = max(local_step, self.optimizer_step)
         self.samples_accumulated = 0
+        self.own_samples = 0
         self.eta_next_step = float("inf")
 
 
@@ -231,7 +233,8 @@ class CollaborativeOptimizer:
 
         if self._param_round is not None and not self._param_round.is_alive():
             self._finish_param_round()
-        if not (self.collaboration_state.ready_for_step or self._ready_within_slack(batch_size)):
+        if not (self.collaboration_state.ready_for_step or self._ready_exact()
+                or self._ready_within_slack(batch_size)):
             return None
 
         logger.log(self.status_loglevel, f"beginning global optimizer step #{self.collaboration_state.optimizer_step}")
@@ -282,6 +285,16 @@ class CollaborativeOptimizer:
         self.last_step_time = get_dht_time()
         logger.log(self.status_loglevel, f"optimizer step #{self.local_step} done")
         return group
+
+    def _ready_exact(self) -> bool:
+        """The collaboration's sample count with OUR part brought up to date: the fetched state counts
+        our samples as of our last progress report, but we know our current count exactly.  A single
+        peer therefore steps exactly at the target (with only the stale count it ran one extra local
+        step per global step, +12.5% samples at 8 local steps), and with more peers the others' stale
+        counts only ever delay, never advance, the step."""
+        cs = self.collaboration_state
+        total = cs.samples_accumulated - cs.own_samples + self.local_samples_accumulated
+        return total >= self.target_batch_size
 
     def _ready_within_slack(self, batch_size: int) -> bool:
         """ETA slack (``eta_slack`` > 0, not in hivemind 0.9.x): start the global step now when the
@@ -459,24 +472,27 @@ class CollaborativeOptimizer:
         if not peers:
             local_eta = max(0, self.target_batch_size - self.local_samples_accumulated) / max(
                 self.performance_ema.samples_per_second, 1e-9)
-            return CollaborationState(self.local_step, self.local_samples_accumulated, self.target_batch_size,
+            local = self.local_samples_accumulated
+            return CollaborationState(self.local_step, local, self.target_batch_size,
                                       num_peers=0, num_clients=0, eta_next_step=now + local_eta,
-                                      next_fetch_time=now + self.default_refresh_period)
+                                      next_fetch_time=now + self.default_refresh_period, own_samples=local)
         num_peers = len(peers)
         num_clients = sum(p.client_mode for p in peers)
         global_step = max(0, self.local_step, *[p.step for p in peers if not p.client_mode] or [0])
         total_sps = sum(p.samples_per_second for p in peers)
-        samples_acc, est = 0, 0.0
+        samples_acc, est, own = 0, 0.0, 0
         for p in peers:
             if p.step == global_step:
                 samples_acc += p.samples_accumulated
                 est += p.samples_accumulated + max(0.0, now - p.time) * p.samples_per_second
+                if p.peer_id == self.peer_id:
+                    own = p.samples_accumulated
         eta = max(0.0, self.target_batch_size - est) / max(total_sps, 1e-9)
         expected_max_peers = max(num_peers + self.expected_drift_peers, num_peers * (1 + self.expected_drift_rate))
         refresh = eta * num_peers / expected_max_peers
         next_fetch = now + min(max(refresh, self.min_refresh_period), self.max_refresh_period)
         return CollaborationState(global_step, samples_acc, self.target_batch_size, num_peers, num_clients,
-                                  eta_next_step=now + eta, next_fetch_time=next_fetch)
+                                  eta_next_step=now + eta, next_fetch_time=next_fetch, own_samples=own)
 
     # ------------------------------------------------------------------ misc
     def state_dict(self) -> Dict[str, Any]:

@@ -1,5 +1,6 @@
 """FusedLamb semantics on CPU: torch_optimizer's adam mode and torch-format optimizer state dicts."""
 import math
+import pytest
 
 import torch
 
@@ -110,6 +111,35 @@ def test_eta_slack_readiness_rule():
         co.eta_slack = 0.5
         co.collaboration_state.num_peers = 1                   # alone: nobody to wait for
         assert not co._ready_within_slack(4)
+        co.shutdown()
+    finally:
+        dht.shutdown()
+
+
+@pytest.mark.parametrize("start", [False, True])
+def test_single_peer_steps_exactly_at_target(start):
+    """A lone peer knows its own sample count exactly: the global step happens at the local step that
+    reaches target_batch_size, not one local step later when a (stale) DHT progress record catches up
+    (which made every bench.py N=1 global step 9 micro-steps of 512 instead of 8)."""
+    import time
+
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.optim.collaborative import CollaborativeOptimizer
+
+    dht = DHT(listen_on="127.0.0.1:*")
+    try:
+        flat = FlatParams(_params(), with_bf16=False)
+        opt = FusedLamb(flat, lr=1e-3)
+        co = CollaborativeOptimizer(opt, dht=dht, prefix=f"exact{int(start)}", target_batch_size=8,
+                                    batch_size_per_step=2, start=start, allow_state_sharing=False,
+                                    min_refresh_period=0.05, default_refresh_period=0.1)
+        for call in range(1, 13):
+            flat.grad.normal_()
+            co.step()
+            assert co.local_step == call // 4, (call, co.local_step)
+            if start:
+                time.sleep(0.03)
+        assert co.stats["local_steps"] == 12 and co.stats["global_steps"] == 3
         co.shutdown()
     finally:
         dht.shutdown()
