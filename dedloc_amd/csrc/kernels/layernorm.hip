@@ -18,7 +18,9 @@ namespace {
 template <int D>
 struct RowCfg {
   static constexpr int EPL = D / 64;                  // elements per lane
-  static constexpr int VW = EPL >= 8 ? 8 : EPL;       // vector width (elements) per load
+  // vector width (elements) per load: the widest of 8 / 4 / 2 / 1 that divides EPL (D = 768 has 12
+  // elements per lane: three 4-wide vectors; 8-wide would leave a third of the row untouched)
+  static constexpr int VW = EPL % 8 == 0 ? 8 : EPL % 4 == 0 ? 4 : EPL % 2 == 0 ? 2 : 1;
   static constexpr int NV = EPL / VW;                 // vector loads per lane
 };
 

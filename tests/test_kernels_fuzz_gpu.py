@@ -1,0 +1,132 @@
+"""Shape fuzzing of the HIP kernels with hypothesis ("every HIP kernel against a
+PyTorch-eager oracle ... use hypothesis shape fuzzing").  Each property draws shapes inside the
+contract the op advertises (the binding rejects anything else) and compares against an fp32 PyTorch
+reference of the same op.  Derandomized, so a failure reproduces; few examples per property to keep
+the GPU tier short."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+hypothesis = pytest.importorskip("hypothesis")
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+FUZZ = settings(max_examples=12, deadline=None, derandomize=True,
+                suppress_health_check=[HealthCheck.function_scoped_fixture])
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.fixture(scope="module")
+def O():
+    import dedloc_amd.ops  # noqa: F401
+
+    return torch.ops.dedloc
+
+
+@FUZZ
+@given(rows=st.integers(1, 3000), D=st.sampled_from([64, 128, 256, 512, 768, 1024]), res=st.booleans(),
+       seed=st.integers(0, 2**16))
+def test_layernorm_fuzz(cuda, O, rows, D, res, seed):
+    torch.manual_seed(seed)
+    x = (torch.randn(rows, D, device=cuda) * 2).bfloat16()
+    r = torch.randn(rows, D, device=cuda).bfloat16() if res else None
+    g, b = torch.rand(D, device=cuda) + 0.5, torch.randn(D, device=cuda)
+    y, s, mean, rstd = O.layernorm_fwd(x, r, g, b, 1e-12)
+    s_ref = (x.float() + (r.float() if res else 0)).requires_grad_(True)
+    y_ref = F.layer_norm(s_ref, (D,), g, b, 1e-12)
+    assert rel(y, y_ref) < 1e-2
+    dy = torch.randn(rows, D, device=cuda).bfloat16()
+    dg, db, dsum = torch.zeros(D, device=cuda), torch.zeros(D, device=cuda), torch.zeros(D, device=cuda)
+    ds = O.layernorm_bwd(dy, s, g, mean, rstd, dg, db, True, dsum)
+    gref = torch.autograd.grad(y_ref, s_ref, dy.float())[0]
+    assert rel(ds, gref) < 2e-2
+    assert rel(db, dy.float().sum(0)) < 1e-3
+    assert rel(dsum, ds.float().sum(0)) < 1e-3
+
+
+def _attn_ref(qkv, mask, H, S):
+    T, ld = qkv.shape
+    D = ld // (3 * H)
+    B = T // S
+    x = qkv.float().reshape(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+    bias = torch.where(mask.bool(), 0.0, float("-inf"))[:, None, None, :]
+    o = F.scaled_dot_product_attention(x[0], x[1], x[2], attn_mask=bias)
+    return o.permute(0, 2, 1, 3).reshape(B * S, H * D)
+
+
+@FUZZ
+@given(B=st.integers(1, 3), H=st.integers(1, 4), S=st.sampled_from([64, 128, 192, 256, 384, 512]),
+       data=st.data())
+def test_attention_fuzz(cuda, O, B, H, S, data):
+    torch.manual_seed(data.draw(st.integers(0, 2**16)))
+    D = 64
+    lens = data.draw(st.lists(st.integers(1, S), min_size=B, max_size=B))
+    qkv = (torch.randn(B * S, 3 * H * D, device=cuda) * 1.5).bfloat16()
+    mask = (torch.arange(S, device=cuda)[None, :] < torch.tensor(lens, device=cuda)[:, None]).long()
+    mbias = torch.where(mask.bool(), 0.0, -1e30).float()
+    kvinfo = torch.cat([mask.sum(1).int(), torch.ones(1, dtype=torch.int32, device=cuda)]).contiguous()
+    use_len = data.draw(st.booleans())
+    out, lse = O.attn_fwd(qkv, mbias, H, S, 1 / math.sqrt(D), kvinfo if use_len else None)
+    qkv_r = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qkv_r, mask, H, S)
+    assert rel(out, ref) < 1.5e-2
+    dout = torch.randn_like(out)
+    dqkv = O.attn_bwd(qkv, mbias, out, dout, lse, H, S, 1 / math.sqrt(D), kvinfo if use_len else None)
+    g_ref = torch.autograd.grad(ref, qkv_r, dout.float())[0]
+    # absolute floor: with a single live key softmax is exactly 1, so dQ and dK are 0 up to
+    # rounding noise (~1e-7) on both sides and only dV carries signal
+    floor = 1e-4 * g_ref.norm().item()
+    for part in range(3):
+        sl = slice(part * H * D, (part + 1) * H * D)
+        err = (dqkv[:, sl].float() - g_ref[:, sl]).norm().item()
+        assert err <= 3e-2 * g_ref[:, sl].norm().item() + floor, (part, err)
+
+
+@FUZZ
+@given(rows=st.integers(1, 600), V=st.integers(2, 40000), seed=st.integers(0, 2**16))
+def test_xent_fuzz(cuda, O, rows, V, seed):
+    torch.manual_seed(seed)
+    x = (torch.randn(rows, V, device=cuda) * 3).bfloat16()
+    lab = torch.randint(0, V, (rows,), device=cuda)
+    lab[::5] = -100
+    if (lab != -100).sum() == 0:
+        lab[0] = 0
+    loss, dl = O.xent_fwd_bwd(x, lab, False, -100)
+    xr = x.float().requires_grad_(True)
+    lr = F.cross_entropy(xr, lab, ignore_index=-100)
+    assert abs(loss.item() - lr.item()) < 1e-3 * max(1, abs(lr.item()))
+    assert rel(dl, torch.autograd.grad(lr, xr)[0]) < 1e-2
+
+
+@FUZZ
+@given(n=st.integers(1, 50000), k=st.integers(1, 20), offset=st.integers(0, 7),
+       wire=st.sampled_from([torch.float16, torch.bfloat16, torch.float32]), seed=st.integers(0, 2**16))
+def test_averaging_kernels_fuzz(cuda, O, n, k, offset, wire, seed):
+    """Butterfly parts have arbitrary LP-chosen sizes and start at arbitrary element offsets of the
+    wire buffer: pack / reduce_delta / unpack must be exact for any length and alignment."""
+    torch.manual_seed(seed)
+    masters = [torch.randn(n, device=cuda) + 2.0 for _ in range(k)]
+    ws = torch.rand(k, device=cuda) + 0.25
+    parts = torch.empty(k * n + offset, dtype=wire, device=cuda)[offset:].view(k, n)    # misaligned start
+    deltas = torch.empty(k * n + offset, dtype=wire, device=cuda)[offset:].view(k, n)
+    for i in range(k):
+        O.pack(masters[i], parts[i], 1.0)
+    if wire != torch.float16:  # bf16 / fp32: round-to-nearest-even, exactly torch's cast
+        assert torch.equal(parts.float(), torch.stack(masters).to(wire).float())
+    O.reduce_delta(parts, ws, deltas)
+    pf = parts.float()
+    ref = ((pf * ws[:, None]).sum(0) / ws.sum())[None, :] - pf
+    tol = 1e-6 if wire == torch.float32 else (2e-3 if wire == torch.float16 else 1e-2)
+    assert (deltas.float() - ref).abs().max().item() <= tol * (ref.abs().max().item() + 1.0)
+    dst = torch.zeros(n + offset, device=cuda)[offset:]
+    m0 = masters[0].clone()
+    dst.copy_(m0)
+    O.unpack(deltas[0], dst, None, True)
+    torch.testing.assert_close(dst, m0 + deltas[0].float())
