@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 hypothesis = pytest.importorskip("hypothesis")
-from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import HealthCheck, assume, given, settings  # noqa: E402
 from hypothesis import strategies as st  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -130,3 +130,76 @@ def test_averaging_kernels_fuzz(cuda, O, n, k, offset, wire, seed):
     dst.copy_(m0)
     O.unpack(deltas[0], dst, None, True)
     torch.testing.assert_close(dst, m0 + deltas[0].float())
+
+
+@FUZZ
+@given(M=st.integers(1, 700), N=st.integers(1, 96).map(lambda v: 8 * v), K=st.integers(1, 96).map(lambda v: 8 * v),
+       bias=st.booleans(), res=st.booleans(), seed=st.integers(0, 2**16))
+def test_gemm_library_path_fuzz(cuda, O, M, N, K, bias, res, seed):
+    """Forward (NT, bias / residual epilogues), data-gradient (NN) and fp32 weight-gradient (TN,
+    token-split) GEMMs on the library path for arbitrary M and multiple-of-8 N, K."""
+    torch.manual_seed(seed)
+    x = torch.randn(M, K, device=cuda).bfloat16()
+    w = torch.randn(N, K, device=cuda).bfloat16()
+    b = torch.randn(N, device=cuda) if bias else None
+    r = torch.randn(M, N, device=cuda).bfloat16() if res else None
+    ref = x.float() @ w.float().t() + (b if bias else 0) + (r.float() if res else 0)
+    assert rel(O.gemm(x, w, b, r, False, True, 0), ref) < 1e-2
+    dy = torch.randn(M, N, device=cuda).bfloat16()
+    assert rel(O.gemm(dy, w, None, None, False, False, 0), dy.float() @ w.float()) < 1e-2
+    c = torch.randn(N, K, device=cuda)
+    ref_c = c + dy.float().t() @ x.float()
+    O.gemm_acc_f32(dy, x, c, True, False)
+    assert rel(c, ref_c) < 1e-4
+
+
+@FUZZ
+@given(n=st.integers(1, 8), C=st.sampled_from([64, 128, 256, 512, 1024, 2048]), H=st.integers(1, 20),
+       relu=st.booleans(), res=st.booleans(), groups=st.sampled_from([1, 2]), seed=st.integers(0, 2**16))
+def test_batchnorm_fuzz(cuda, O, n, C, H, relu, res, groups, seed):
+    assume(n * H * H > 1)  # training-mode BN needs more than one value per channel and group
+    torch.manual_seed(seed)
+    N = n * groups
+    cl = torch.channels_last
+    x = (torch.randn(N, C, H, H, device=cuda) * 2 + 0.3).bfloat16().contiguous(memory_format=cl)
+    r = torch.randn(N, C, H, H, device=cuda).bfloat16().contiguous(memory_format=cl) if res else None
+    g, b = torch.rand(C, device=cuda) + 0.5, torch.randn(C, device=cuda)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, mean, rstd = O.bn_fwd(x, r, g, b, rm, rv, 1e-5, 0.1, relu, groups)
+    xr = x.float().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    ys = [F.batch_norm(c, None, None, g, b, training=True, eps=1e-5) for c in xr.chunk(groups)]
+    yr = torch.cat(ys) + (rr if res else 0)
+    if relu:
+        yr = yr.clamp_min(0)
+    assert rel(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    dx, dres, dgamma, dbeta = O.bn_bwd(dy, y, x, mean, rstd, g, relu, res, beta=b)
+    gx = torch.autograd.grad(yr, [xr] + ([rr] if res else []), dy.float())
+    # absolute floor: with very few values per channel dx is mostly cancellation
+    assert (dx.float() - gx[0]).norm().item() <= 2e-2 * gx[0].norm().item() + 1e-3 * dy.float().norm().item()
+    if res:
+        assert rel(dres, gx[1]) < 1e-2
+
+
+@FUZZ
+@given(bs=st.integers(1, 128), extra=st.integers(0, 300), K=st.integers(2, 4000), seed=st.integers(0, 2**16))
+def test_sinkhorn_and_swav_ce_fuzz(cuda, O, bs, extra, K, seed):
+    torch.manual_seed(seed)
+    n = bs + extra
+    e = F.normalize(torch.randn(n, 128, device=cuda), dim=1)
+    p = F.normalize(torch.randn(K, 128, device=cuda), dim=1)
+    s = (e @ p.t()).contiguous()
+    q = O.sinkhorn(s, bs, 0.03, 3)
+    ref = O.sinkhorn(s.cpu(), bs, 0.03, 3)  # the op's fp32 PyTorch CPU implementation
+    assert q.shape == (bs, K)
+    assert torch.allclose(q.cpu(), ref, atol=1e-6, rtol=2e-3)
+    scores = (torch.randn(bs, K, device=cuda) * 0.5)
+    ds = torch.zeros(bs, K, device=cuda)
+    loss = torch.zeros(1, device=cuda)
+    O.swav_ce(scores, q, ds, loss, 0.1, 1.0 / bs)
+    sr = scores.cpu().requires_grad_(True)
+    lref = -(q.cpu() * torch.log_softmax(sr / 0.1, -1)).sum(1).mean()
+    (gref,) = torch.autograd.grad(lref, sr)
+    assert abs(loss.item() - lref.item()) < 1e-4 * max(1.0, abs(lref.item()))
+    assert torch.allclose(ds.cpu(), gref, atol=1e-6, rtol=1e-3)
