@@ -63,6 +63,7 @@ def main(argv=None):
     ap.add_argument("--log_dir", default="collab_logs")
     ap.add_argument("--sahajbert", action="store_true")
     ap.add_argument("--no_coordinator", action="store_true")
+    ap.add_argument("--coordinator_refresh", type=float, default=5.0, help="coordinator metrics poll period (s)")
     args = ap.parse_args(argv)
     log_dir = Path(args.log_dir)
     log_dir.mkdir(parents=True, exist_ok=True)
@@ -82,7 +83,7 @@ def main(argv=None):
         root = None
     else:
         spawn([py, "-m", "dedloc_amd.cli.run_first_peer", "--experiment_prefix", args.experiment_prefix,
-               "--dht_listen_on", "0.0.0.0:*", "--refresh_period", "5",
+               "--dht_listen_on", "0.0.0.0:*", "--refresh_period", str(args.coordinator_refresh),
                "--metrics_file", str(log_dir / "coordinator_metrics.jsonl"),
                *(["--max_runtime", str(args.duration)] if args.duration else [])], "coordinator.log", env0)
         root = None

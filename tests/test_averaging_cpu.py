@@ -120,7 +120,7 @@ def _stall_worker(rank, world, port, dht_ep, q):
         dht = DHT(initial_peers=[dht_ep], listen=False)
         x = torch.full((3000,), float(rank + 1))
         averager = DecentralizedAverager([x], dht, "stall", peer_id=f"peer{rank}".encode(), target_group_size=world,
-                                         averaging_expiration=2.0, averaging_timeout=timeout, compression="NONE",
+                                         averaging_expiration=10.0, averaging_timeout=timeout, compression="NONE",
                                          allow_state_sharing=False, rank=rank)
         results = []
         for rnd in range(2):

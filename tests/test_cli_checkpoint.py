@@ -130,9 +130,10 @@ def test_launch_collaboration_coordinator_trainers_aux_cpu(tmp_path):
     file reports both trainers alive (the aux peer publishes no training metrics)."""
     logs = tmp_path / "logs"
     cmd = [sys.executable, "-m", "dedloc_amd.cli.launch_collaboration", "--n_trainers", "2", "--n_aux", "1",
-           "--experiment_prefix", "launch", "--log_dir", str(logs), "--duration", "360", "--",
+           "--experiment_prefix", "launch", "--log_dir", str(logs), "--duration", "360",
+           "--coordinator_refresh", "0.3", "--",
            "--device", "cpu", "--config_path", _tiny_dir(tmp_path), "--per_device_train_batch_size", "2",
-           "--seq_length", "64", "--target_batch_size", "8", "--stop_after_global_steps", "3", "--save_steps", "0",
+           "--seq_length", "64", "--target_batch_size", "8", "--stop_after_global_steps", "6", "--save_steps", "0",
            "--output_dir", str(tmp_path / "out"), "--min_refresh_period", "0.05", "--default_refresh_period", "0.1",
            "--dht_listen_on", "127.0.0.1:*", "--listen_on", "127.0.0.1:*", "--averaging_expiration", "3",
            "--compression", "NONE"]
