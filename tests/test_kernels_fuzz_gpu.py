@@ -203,3 +203,34 @@ def test_sinkhorn_and_swav_ce_fuzz(cuda, O, bs, extra, K, seed):
     (gref,) = torch.autograd.grad(lref, sr)
     assert abs(loss.item() - lref.item()) < 1e-4 * max(1.0, abs(lref.item()))
     assert torch.allclose(ds.cpu(), gref, atol=1e-6, rtol=1e-3)
+
+
+@FUZZ
+@given(N=st.integers(1, 3), Cin=st.sampled_from([64, 128, 192, 256]), Cout=st.sampled_from([64, 128, 192, 256]),
+       H=st.integers(3, 20), geo=st.sampled_from([(1, 1, 0), (1, 2, 0), (3, 1, 1), (3, 2, 1)]),
+       route=st.sampled_from(["hip", "default"]), seed=st.integers(0, 2**16))
+def test_conv_fuzz(cuda, O, monkeypatch, N, Cin, Cout, H, geo, route, seed):
+    """NHWC convolution forward / data gradient / fp32 weight gradient (conv.hip implicit GEMM, or
+    the default per-shape routing through hipBLASLt for pointwise convs) at arbitrary spatial sizes."""
+    k, stride, pad = geo
+    if route == "hip":
+        monkeypatch.setenv("DEDLOC_CONV_GEMM", "hip")
+    else:
+        monkeypatch.delenv("DEDLOC_CONV_GEMM", raising=False)
+    cl = torch.channels_last
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(N, Cin, H, H, generator=g).bfloat16().to(cuda).contiguous(memory_format=cl)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).bfloat16().to(cuda)
+    w = w.contiguous(memory_format=cl)
+    P = (H + 2 * pad - k) // stride + 1
+    dy = torch.randn(N, Cout, P, P, generator=g).bfloat16().to(cuda).contiguous(memory_format=cl)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=stride, padding=pad)
+    dxr, dwr = torch.autograd.grad(yr, [xr, wr], dy.float())
+    y = O.conv2d_fwd(x, w, stride, pad)
+    assert y.shape == yr.shape and rel(y, yr) < 1e-2
+    dx = O.conv2d_dgrad(dy, w, stride, pad, H, H)
+    assert dx.shape == dxr.shape and rel(dx, dxr) < 1e-2
+    dw = torch.zeros(Cout, Cin, k, k, device=cuda).contiguous(memory_format=cl)
+    O.conv2d_wgrad(dy, x, dw, stride, pad)
+    assert rel(dw, dwr) < 1e-3
