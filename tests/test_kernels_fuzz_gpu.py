@@ -234,3 +234,80 @@ def test_conv_fuzz(cuda, O, monkeypatch, N, Cin, Cout, H, geo, route, seed):
     dw = torch.zeros(Cout, Cin, k, k, device=cuda).contiguous(memory_format=cl)
     O.conv2d_wgrad(dy, x, dw, stride, pad)
     assert rel(dw, dwr) < 1e-3
+
+
+@FUZZ
+@given(rows=st.integers(1, 2000), N=st.integers(1, 512).map(lambda v: 8 * v), seed=st.integers(0, 2**16))
+def test_gelu_fuzz(cuda, O, rows, N, seed):
+    """GELU forward and GELU backward fused with the bias-gradient column sums."""
+    torch.manual_seed(seed)
+    h = (torch.randn(rows, N, device=cuda) * 2).bfloat16()
+    hr = h.float().requires_grad_(True)
+    yr = F.gelu(hr, approximate="tanh")
+    assert rel(O.gelu_fwd(h), yr) < 1e-2
+    dy = torch.randn(rows, N, device=cuda).bfloat16()
+    db = torch.zeros(N, device=cuda)
+    dh = O.gelu_bwd(dy, h, db)
+    (gref,) = torch.autograd.grad(yr, hr, dy.float())
+    assert rel(dh, gref) < 1e-2
+    assert rel(db, dh.float().sum(0)) < 1e-3
+
+
+@FUZZ
+@given(sizes=st.lists(st.integers(1, 5000), min_size=1, max_size=8), seed=st.integers(0, 2**16))
+def test_lamb_fuzz(cuda, O, sizes, seed):
+    """Fused 2-phase multi-tensor LAMB over an arbitrary tensor list (chunked per 1000 elements) vs the
+    torch_optimizer.Lamb formula (debias, per-tensor trust ratio, clamp, no-decay tensors)."""
+    torch.manual_seed(seed)
+    wd = [0.01 if i % 2 == 0 else 0.0 for i in range(len(sizes))]
+    n = sum(sizes)
+    ct, cs, cl, offs = [], [], [], []
+    off = 0
+    for i, sz in enumerate(sizes):
+        offs.append(off)
+        for s0 in range(0, sz, 1000):
+            ct.append(i)
+            cs.append(off + s0)
+            cl.append(min(1000, sz - s0))
+        off += sz
+    ct = torch.tensor(ct, dtype=torch.int32, device=cuda)
+    cs = torch.tensor(cs, dtype=torch.int64, device=cuda)
+    cl = torch.tensor(cl, dtype=torch.int32, device=cuda)
+    twd = torch.tensor(wd, dtype=torch.float32, device=cuda)
+    p = torch.randn(n, device=cuda)
+    m, v = torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    norms = torch.zeros(2 * len(sizes), device=cuda)
+    lr, b1, b2, eps = 1.76e-3, 0.9, 0.999, 1e-6
+    for step in range(1, 3):
+        g = torch.randn(n, device=cuda)
+        bc = math.sqrt(1 - b2 ** step) / (1 - b1 ** step)
+        O.lamb_step(p, g, m, v, ct, cs, cl, twd, norms, b1, b2, eps, lr * bc, 10.0, 1.0)
+        for i, (o, sz) in enumerate(zip(offs, sizes)):
+            sl = slice(o, o + sz)
+            mr[sl] = b1 * mr[sl] + (1 - b1) * g[sl]
+            vr[sl] = b2 * vr[sl] + (1 - b2) * g[sl] ** 2
+            wn = pr[sl].norm().clamp(0, 10.0)
+            u = mr[sl] / (vr[sl].sqrt() + eps) + wd[i] * pr[sl]
+            un = u.norm()
+            trust = 1.0 if (wn == 0 or un == 0) else (wn / un).item()
+            pr[sl] -= lr * bc * trust * u
+    assert rel(p, pr) < 1e-5 and rel(m, mr) < 1e-5 and rel(v, vr) < 1e-4
+
+
+@FUZZ
+@given(n=st.integers(1, 300000), max_norm=st.floats(0.1, 10.0), seed=st.integers(0, 2**16))
+def test_clip_axpby_fuzz(cuda, O, n, max_norm, seed):
+    torch.manual_seed(seed)
+    g = torch.randn(n, device=cuda) * 3
+    ref = g.clone()
+    part = torch.zeros(256, device=cuda)
+    out = torch.zeros(2, device=cuda)
+    O.grad_norm_clip(g, max_norm, part, out)
+    nrm = ref.norm().item()
+    assert abs(out[0].item() - nrm) <= 1e-4 * nrm + 1e-6 and out[1].item() == 1.0
+    assert rel(g, ref * min(1.0, max_norm / (nrm + 1e-6))) < 1e-5
+    y = torch.randn(n, device=cuda)
+    y0 = y.clone()
+    O.axpby(y, g, 0.25, -1.5)
+    assert rel(y, 0.25 * y0 - 1.5 * g) < 1e-6
