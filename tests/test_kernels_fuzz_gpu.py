@@ -311,3 +311,37 @@ def test_clip_axpby_fuzz(cuda, O, n, max_norm, seed):
     y0 = y.clone()
     O.axpby(y, g, 0.25, -1.5)
     assert rel(y, 0.25 * y0 - 1.5 * g) < 1e-6
+
+
+@settings(max_examples=6, deadline=None, derandomize=True, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(hidden=st.sampled_from([128, 256, 768]), layers=st.integers(1, 3), shared=st.booleans(),
+       B=st.integers(1, 3), S=st.integers(8, 160), seed=st.integers(0, 2**16), data=st.data())
+def test_albert_config_fuzz_gpu_matches_cpu(cuda, O, hidden, layers, shared, B, S, seed, data):
+    """Whole ALBERT pre-training step through the HIP kernels vs the same model on the CPU reference ops,
+    over hidden sizes (768 = albert-base), layer / group counts, batch, unpadded lengths and padding."""
+    from dedloc_amd.models import albert as A
+
+    torch.manual_seed(seed)
+    cfg = A.AlbertConfig.tiny(hidden_size=hidden, intermediate_size=4 * hidden, num_attention_heads=hidden // 64,
+                              num_hidden_layers=layers, num_hidden_groups=1 if shared else layers,
+                              max_position_embeddings=256)
+    m_cpu = A.AlbertForPreTraining(cfg)
+    m_gpu = A.AlbertForPreTraining(cfg)
+    m_gpu.load_hf_state_dict(m_cpu.hf_state_dict())
+    m_cpu.materialize("cpu")
+    m_gpu.materialize(cuda)
+    m_cpu.eval()
+    m_gpu.eval()
+    lens = data.draw(st.lists(st.integers(2, S), min_size=B, max_size=B))
+    ids = torch.randint(5, cfg.vocab_size, (B, S))
+    am = (torch.arange(S)[None, :] < torch.tensor(lens)[:, None]).long()
+    labels = torch.full((B, S), -100)
+    for b, n in enumerate(lens):
+        labels[b, 1:n:3] = ids[b, 1:n:3]
+    sop = torch.randint(0, 2, (B,))
+    oc = m_cpu(ids, am, None, labels=labels, sentence_order_label=sop)
+    og = m_gpu(ids.to(cuda), am.to(cuda), None, labels=labels.to(cuda), sentence_order_label=sop.to(cuda))
+    assert abs(og["loss"].item() - oc["loss"].item()) < 3e-2 * max(1.0, abs(oc["loss"].item()))
+    oc["loss"].backward()
+    og["loss"].backward()
+    assert rel(m_gpu.flat.grad.cpu(), m_cpu.flat.grad) < 6e-2
