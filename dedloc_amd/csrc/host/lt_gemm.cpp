@@ -243,7 +243,11 @@ bool build_plan(Plan& p, const DlLtArgs& a, DevState* s, hipStream_t st, const s
   if (cand.empty()) return false;
   const double flops = 2.0 * a.M * a.N * a.K * std::max(1, a.batch);
   const char* ex_env = std::getenv("DEDLOC_LT_EXHAUSTIVE");
-  const bool exhaustive = (ex_env && ex_env[0] == '1') && !a.d_f32 && !a.in_f32 && flops >= 2e11 &&
+  static const double min_flops = [] {  // DEDLOC_LT_EXHAUSTIVE_MIN_GFLOP: problem-size floor (default 200)
+    const char* e = std::getenv("DEDLOC_LT_EXHAUSTIVE_MIN_GFLOP");
+    return (e ? std::atof(e) : 200.0) * 1e9;
+  }();
+  const bool exhaustive = (ex_env && ex_env[0] == '1') && !a.d_f32 && !a.in_f32 && flops >= min_flops &&
                           a.epilogue != DL_LT_GELU_AUX_BIAS && a.epilogue != DL_LT_DGELU_BGRAD;
   int best = 0;
   if (cand.size() > 1 || exhaustive) {
