@@ -65,6 +65,26 @@ class AlbertConfig:
         return cls(**base)
 
     @classmethod
+    def albert_base_v2(cls, **kw) -> "AlbertConfig":
+        """albert-base-v2 (HF model card sizes): 12 x 768, 12 heads of 64."""
+        base = dict(vocab_size=30000, embedding_size=128, hidden_size=768, num_hidden_layers=12,
+                    num_hidden_groups=1, num_attention_heads=12, intermediate_size=3072, inner_group_num=1)
+        base.update(kw)
+        return cls(**base)
+
+    @classmethod
+    def albert_xxlarge_v2(cls, **kw) -> "AlbertConfig":
+        """albert-xxlarge-v2 (= transformers.AlbertConfig's defaults): 12 x 4096, 64 heads of 64.
+        (albert-xlarge's heads are 128 wide, which the attention kernels do not take.)"""
+        base = dict(vocab_size=30000, embedding_size=128, hidden_size=4096, num_hidden_layers=12,
+                    num_hidden_groups=1, num_attention_heads=64, intermediate_size=16384, inner_group_num=1)
+        base.update(kw)
+        return cls(**base)
+
+    BUILTIN = {"albert-large-v2": "albert_large_v2", "albert-base-v2": "albert_base_v2",
+               "albert-xxlarge-v2": "albert_xxlarge_v2"}
+
+    @classmethod
     def tiny(cls, **kw) -> "AlbertConfig":
         base = dict(vocab_size=512, embedding_size=64, hidden_size=128, num_hidden_layers=3, num_hidden_groups=1,
                     num_attention_heads=2, intermediate_size=256, max_position_embeddings=128)
@@ -84,12 +104,13 @@ class AlbertConfig:
 
     @classmethod
     def from_pretrained(cls, path: str) -> "AlbertConfig":
-        """Accepts a directory containing config.json, a json file, or the name 'albert-large-v2'
-        (or the reference's S3 URL of that config — there is no network, so it maps to the
-        built-in copy)."""
-        if path in ("albert-large-v2",) or (isinstance(path, str) and path.endswith("albert-large-v2-config.json")
-                                            and not os.path.exists(path)):
-            return cls.albert_large_v2()
+        """Accepts a directory containing config.json, a json file, or the name 'albert-large-v2' /
+        'albert-base-v2' / 'albert-xxlarge-v2' (or the reference-style S3 URL of such a config —
+        there is no network, so it maps to the built-in copy)."""
+        for name, ctor in cls.BUILTIN.items():
+            if path == name or (isinstance(path, str) and path.endswith(f"{name}-config.json")
+                                and not os.path.exists(path)):
+                return getattr(cls, ctor)()
         if os.path.isdir(path):
             path = os.path.join(path, "config.json")
         with open(path) as f:

@@ -95,3 +95,23 @@ def test_finetune_heads_gpu(cuda):
     res = finetune.run(args)
     assert res["history"][-1]["eval_loss"] < res["history"][0]["eval_loss"] + 0.5
     assert res["test_accuracy"] > 0.5
+
+
+def test_builtin_albert_configs_match_transformers():
+    """Built-in configs for the other public ALBERT v2 sizes: xxlarge equals transformers' AlbertConfig
+    defaults; base has the model card's ~11.7M parameters; the reference-style URL maps to the copy."""
+    import transformers
+
+    from dedloc_amd.models.albert import AlbertConfig, AlbertForPreTraining
+
+    ours = AlbertConfig.from_pretrained("albert-xxlarge-v2")
+    hf = transformers.AlbertConfig()
+    for k in ("vocab_size", "embedding_size", "hidden_size", "num_hidden_layers", "num_attention_heads",
+              "intermediate_size", "num_hidden_groups", "inner_group_num"):
+        assert getattr(ours, k) == getattr(hf, k), k
+    base = AlbertConfig.from_pretrained("https://s3.amazonaws.com/models.huggingface.co/bert/albert-base-v2-config.json")
+    assert (base.hidden_size, base.num_attention_heads, base.intermediate_size) == (768, 12, 3072)
+    m = AlbertForPreTraining(base)
+    m.materialize("cpu")
+    n = m.flat.fp32.numel()  # the tied decoder counted once, like HF
+    assert 11.0e6 < n < 12.5e6, n
