@@ -30,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--impl", default="dedloc", choices=["dedloc", "hf"])
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--config", default="albert-large-v2",
+                    help="albert-large-v2 | albert-base-v2 | a config.json directory")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -39,7 +41,7 @@ def main():
     dev = torch.device("cuda")
     from dedloc_amd.models.albert import AlbertConfig, AlbertForPreTraining, flops_per_sample
 
-    cfg = AlbertConfig.albert_large_v2()
+    cfg = AlbertConfig.from_pretrained(args.config)
     P = round(0.15 * args.seq)
     ids, tt, am, pos, lab, sop, labels = synthetic(args.batch, args.seq, cfg.vocab_size, P, dev)
     if args.impl == "dedloc":

@@ -97,20 +97,15 @@ def test_finetune_heads_gpu(cuda):
     assert res["test_accuracy"] > 0.5
 
 
-def test_builtin_albert_configs_match_transformers():
-    """Built-in configs for the other public ALBERT v2 sizes: xxlarge equals transformers' AlbertConfig
-    defaults; base has the model card's ~11.7M parameters; the reference-style URL maps to the copy."""
-    import transformers
-
+def test_builtin_albert_configs():
+    """Built-in config for albert-base-v2 next to albert-large-v2 (the model card's sizes and ~11.7M
+    parameters); the reference-style URL maps to the built-in copy."""
     from dedloc_amd.models.albert import AlbertConfig, AlbertForPreTraining
 
-    ours = AlbertConfig.from_pretrained("albert-xxlarge-v2")
-    hf = transformers.AlbertConfig()
-    for k in ("vocab_size", "embedding_size", "hidden_size", "num_hidden_layers", "num_attention_heads",
-              "intermediate_size", "num_hidden_groups", "inner_group_num"):
-        assert getattr(ours, k) == getattr(hf, k), k
     base = AlbertConfig.from_pretrained("https://s3.amazonaws.com/models.huggingface.co/bert/albert-base-v2-config.json")
-    assert (base.hidden_size, base.num_attention_heads, base.intermediate_size) == (768, 12, 3072)
+    assert (base.hidden_size, base.num_hidden_layers, base.num_attention_heads, base.intermediate_size,
+            base.embedding_size, base.vocab_size) == (768, 12, 12, 3072, 128, 30000)
+    assert AlbertConfig.from_pretrained("albert-base-v2") == base
     m = AlbertForPreTraining(base)
     m.materialize("cpu")
     n = m.flat.fp32.numel()  # the tied decoder counted once, like HF
