@@ -184,6 +184,80 @@ __global__ __launch_bounds__(512) void ln_bwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// Wide rows (D = 2048 / 4096, e.g. albert-xxlarge's 4096): one 256-thread block per row (each thread
+// D / 256 elements, 8-wide vectors interleaved over the block so every load instruction covers
+// 4 KiB contiguous), the two row sums reduced through LDS; the block walks its chunk of rows and
+// keeps per-thread column partials of dgamma / dbeta / colsum(ds), added with one fp32 atomic per
+// column at the end.  (The one-wave-per-row kernel above would need 6 x D / 64 floats per lane.)
+template <int D>
+__global__ __launch_bounds__(256) void ln_bwd_wide_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ mean_in,
+                                                         const float* __restrict__ rstd_in, bf16_t* __restrict__ ds,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         float* __restrict__ dsum, int rows, int rows_per_block) {
+  constexpr int EPT = D / 256, NV = EPT / 8;
+  static_assert(EPT % 8 == 0, "wide LayerNorm rows: D must be a multiple of 2048");
+  __shared__ float red[2][4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float g[EPT], dg[EPT], db[EPT], dx[EPT];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[v * 8 + j] = gamma[(v * 256 + t) * 8 + j];
+      dg[v * 8 + j] = db[v * 8 + j] = dx[v * 8 + j] = 0.f;
+    }
+  for (int row = r0; row < r1; ++row) {
+    const size_t base = (size_t)row * D;
+    float gy[EPT], xh[EPT];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      load_bf16<8>(dy + base + (v * 256 + t) * 8, gy + v * 8);
+      load_bf16<8>(s + base + (v * 256 + t) * 8, xh + v * 8);
+    }
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      xh[i] = (xh[i] - mean) * rstd;
+      dg[i] += gy[i] * xh[i];
+      db[i] += gy[i];
+      gy[i] *= g[i];
+      a += gy[i];
+      b += gy[i] * xh[i];
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+      red[0][wid] = a;
+      red[1][wid] = b;
+    }
+    __syncthreads();
+    a = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) * (1.f / D);
+    b = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) * (1.f / D);
+    __syncthreads();  // red is rewritten by the next row
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      gy[i] = bf2f(f2bf(rstd * (gy[i] - a - xh[i] * b)));
+      dx[i] += gy[i];
+    }
+#pragma unroll
+    for (int v = 0; v < NV; ++v) store_bf16<8>(ds + base + (v * 256 + t) * 8, gy + v * 8);
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = (v * 256 + t) * 8 + j;
+      if (dgamma) atomicAdd(&dgamma[c], dg[v * 8 + j]);
+      if (dbeta) atomicAdd(&dbeta[c], db[v * 8 + j]);
+      if (dsum) atomicAdd(&dsum[c], dx[v * 8 + j]);
+    }
+}
+
 template <int D>
 void launch_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,
                 float* mean, float* rstd, int rows, float eps, hipStream_t st) {
@@ -249,6 +323,14 @@ int dl_layernorm_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, cons
     case 512: launch_bwd<512>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
     case 768: launch_bwd<768>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
     case 1024: launch_bwd<1024>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, nparts, st); break;
+    case 2048:
+      ln_bwd_wide_kernel<2048><<<nparts, 256, 0, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows,
+                                                      (rows + nparts - 1) / nparts);
+      break;
+    case 4096:
+      ln_bwd_wide_kernel<4096><<<nparts, 256, 0, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows,
+                                                      (rows + nparts - 1) / nparts);
+      break;
     default: return -1;
   }
   return 0;

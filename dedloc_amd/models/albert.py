@@ -72,9 +72,17 @@ class AlbertConfig:
         base.update(kw)
         return cls(**base)
 
-    # (xlarge / xxlarge are not built in: xlarge's 128-wide heads and xxlarge's 4096-wide LayerNorm
-    # backward are outside the GPU kernels' shapes — they run from a config.json on the CPU ops only)
-    BUILTIN = {"albert-large-v2": "albert_large_v2", "albert-base-v2": "albert_base_v2"}
+    @classmethod
+    def albert_xxlarge_v2(cls, **kw) -> "AlbertConfig":
+        """albert-xxlarge-v2 (= transformers.AlbertConfig's defaults): 12 x 4096, 64 heads of 64."""
+        base = dict(vocab_size=30000, embedding_size=128, hidden_size=4096, num_hidden_layers=12,
+                    num_hidden_groups=1, num_attention_heads=64, intermediate_size=16384, inner_group_num=1)
+        base.update(kw)
+        return cls(**base)
+
+    # (xlarge is not built in: its 128-wide heads are outside the attention kernels' head_dim 64)
+    BUILTIN = {"albert-large-v2": "albert_large_v2", "albert-base-v2": "albert_base_v2",
+               "albert-xxlarge-v2": "albert_xxlarge_v2"}
 
     @classmethod
     def tiny(cls, **kw) -> "AlbertConfig":
@@ -97,7 +105,7 @@ class AlbertConfig:
     @classmethod
     def from_pretrained(cls, path: str) -> "AlbertConfig":
         """Accepts a directory containing config.json, a json file, or the name 'albert-large-v2' /
-        'albert-base-v2' (or the reference-style S3 URL of such a config —
+        'albert-base-v2' / 'albert-xxlarge-v2' (or the reference-style S3 URL of such a config —
         there is no network, so it maps to the built-in copy)."""
         for name, ctor in cls.BUILTIN.items():
             if path == name or (isinstance(path, str) and path.endswith(f"{name}-config.json")

@@ -110,3 +110,9 @@ def test_builtin_albert_configs():
     m.materialize("cpu")
     n = m.flat.fp32.numel()  # the tied decoder counted once, like HF
     assert 11.0e6 < n < 12.5e6, n
+    import transformers
+
+    xxl, hf = AlbertConfig.from_pretrained("albert-xxlarge-v2"), transformers.AlbertConfig()
+    for k in ("vocab_size", "embedding_size", "hidden_size", "num_hidden_layers", "num_attention_heads",
+              "intermediate_size", "num_hidden_groups", "inner_group_num"):
+        assert getattr(xxl, k) == getattr(hf, k), k

@@ -31,7 +31,7 @@ def O():
 
 
 @FUZZ
-@given(rows=st.integers(1, 3000), D=st.sampled_from([64, 128, 256, 512, 768, 1024]), res=st.booleans(),
+@given(rows=st.integers(1, 3000), D=st.sampled_from([64, 128, 256, 512, 768, 1024, 2048, 4096]), res=st.booleans(),
        seed=st.integers(0, 2**16))
 def test_layernorm_fuzz(cuda, O, rows, D, res, seed):
     torch.manual_seed(seed)

@@ -23,7 +23,7 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("D", [64, 128, 768, 1024])
+@pytest.mark.parametrize("D", [64, 128, 768, 1024, 2048, 4096])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_layernorm(cuda, D, with_res):
     torch.manual_seed(0)
