@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--impl", default="dedloc", choices=["dedloc", "hf"])
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--config", default="albert-large-v2",
-                    help="albert-large-v2 | albert-base-v2 | albert-xxlarge-v2 | a config.json directory")
+                    help="albert-large-v2 | albert-base-v2 | albert-xlarge-v2 | albert-xxlarge-v2 | a config.json directory")
     ap.add_argument("--seq", type=int, default=512)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)

@@ -80,9 +80,18 @@ class AlbertConfig:
         base.update(kw)
         return cls(**base)
 
-    # (xlarge is not built in: its 128-wide heads are outside the attention kernels' head_dim 64)
+    @classmethod
+    def albert_xlarge_v2(cls, **kw) -> "AlbertConfig":
+        """albert-xlarge-v2 (HF model card sizes): 24 x 2048, 16 heads of 128 — outside the fused
+        attention kernels' head_dim 64, so its attention runs the composed path
+        (ops.attn_composed_fwd / _bwd: batched bf16 GEMMs, fp32 scores)."""
+        base = dict(vocab_size=30000, embedding_size=128, hidden_size=2048, num_hidden_layers=24,
+                    num_hidden_groups=1, num_attention_heads=16, intermediate_size=8192, inner_group_num=1)
+        base.update(kw)
+        return cls(**base)
+
     BUILTIN = {"albert-large-v2": "albert_large_v2", "albert-base-v2": "albert_base_v2",
-               "albert-xxlarge-v2": "albert_xxlarge_v2"}
+               "albert-xlarge-v2": "albert_xlarge_v2", "albert-xxlarge-v2": "albert_xxlarge_v2"}
 
     @classmethod
     def tiny(cls, **kw) -> "AlbertConfig":
@@ -168,7 +177,7 @@ class _AlbertLayerFn(torch.autograd.Function):
         O = ops.OPS
         mbias, kvinfo = mask
         qkv = O.gemm(h, lv["wqkv"], lv["bqkv32"], None, False, True, 0)
-        att, lse = O.attn_fwd(qkv, mbias, H, S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)), kvinfo)
+        att, lse = ops.attn_fwd(qkv, mbias, H, S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)), kvinfo)
         if _RESIDUAL_IN_GEMM:
             # residual sums ride in the GEMM epilogues (C = h, beta = 1): the LayerNorms then read one
             # tensor and write one (s is the GEMM output itself) — 2 of 4 LN HBM passes removed
@@ -210,7 +219,7 @@ class _AlbertLayerFn(torch.autograd.Function):
         datt = _dgrad(O, ds1, lv, "wo", None)
         # the QKV bias gradient rides in the attention backward (query: colsum dQ, value: colsum
         # datt, key: exactly zero — softmax is shift invariant), no separate column-sum pass
-        dqkv = O.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
+        dqkv = ops.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
                           ctx.mask[1], lv["gbqkv"])
         _wgrad(O, dqkv, h, lv, "gwqkv")
         dh = _dgrad(O, dqkv, lv, "wqkv", ds1)
@@ -240,7 +249,7 @@ class _AlbertLayerFn(torch.autograd.Function):
         _join_wgrads(lv)
         datt = _dgrad(O, ds1, lv, "wo", None)
         H = ctx.H
-        dqkv = O.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
+        dqkv = ops.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
                           ctx.mask[1], lv["gbqkv"])
         dh = _dgrad(O, dqkv, lv, "wqkv", ds1)
         _wgrad(O, ds1, att, lv, "gwo")

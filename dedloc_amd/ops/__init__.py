@@ -107,10 +107,92 @@ def add_layernorm(x, res, gamma, beta, ggamma=None, gbeta=None, eps=1e-12):
     return _AddLayerNorm.apply(x, res, gamma, beta, ggamma, gbeta, eps)
 
 
+_LOG2E = math.log2(math.e)
+_BMM_OUT_F32 = True  # torch.bmm(..., out_dtype=float32) available (bf16 in, fp32 out)
+
+
+def _bmm_f32(a, b):
+    """[N, M, K] x [N, K, P] bf16 -> fp32 without rounding the product through bf16."""
+    global _BMM_OUT_F32
+    if a.is_cuda and _BMM_OUT_F32:
+        try:
+            return torch.bmm(a, b, out_dtype=torch.float32)
+        except (RuntimeError, TypeError):
+            _BMM_OUT_F32 = False
+    return torch.bmm(a.float(), b.float())
+
+
+def _attn_split(qkv, H, S):
+    T, ld = qkv.shape
+    D = ld // (3 * H)
+    B = T // S
+    x = qkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)  # 3, B, H, S, D
+    return (x[0].reshape(B * H, S, D), x[1].reshape(B * H, S, D), x[2].reshape(B * H, S, D)), B, D
+
+
+def _attn_scores(q, k, mbias, B, H, S, scale):
+    s = _bmm_f32(q, k.transpose(1, 2)).mul_(scale * _LOG2E)  # log2 units, like the fused kernels
+    if mbias is not None:
+        s.view(B, H, S, S).add_(mbias.view(B, 1, 1, S))
+    return s
+
+
+def attn_composed_fwd(qkv, mbias, H, S, scale):
+    """Attention for head sizes outside the fused kernels' 64 (albert-xlarge: 128) as batched
+    bf16 GEMMs with fp32 scores and softmax — same inputs / outputs as ``attn_fwd`` (out
+    [B*S, H*D] bf16, lse [B, H, S] fp32 in log2 units), but the [B*H, S, S] scores go through HBM."""
+    (q, k, v), B, D = _attn_split(qkv, H, S)
+    s = _attn_scores(q, k, mbias, B, H, S, scale)
+    m = s.amax(-1, keepdim=True)
+    p = torch.exp2(s.sub_(m))
+    den = p.sum(-1, keepdim=True)
+    lse = (m + torch.log2(den)).view(B, H, S)
+    o = torch.bmm(p.div_(den).bfloat16(), v)
+    return o.view(B, H, S, D).transpose(1, 2).reshape(B * S, H * D), lse
+
+
+def attn_composed_bwd(qkv, mbias, out, dout, lse, H, S, scale, dbias=None):
+    """Backward of ``attn_composed_fwd`` (probabilities recomputed from lse); dQKV in the packed
+    layout, and — like the fused backward — the QKV bias gradient accumulated into ``dbias``."""
+    (q, k, v), B, D = _attn_split(qkv, H, S)
+    p = torch.exp2(_attn_scores(q, k, mbias, B, H, S, scale).sub_(lse.view(B * H, S, 1)))
+    do = dout.view(B, S, H, D).transpose(1, 2).reshape(B * H, S, D)
+    o = out.view(B, S, H, D).transpose(1, 2).reshape(B * H, S, D)
+    dv = torch.bmm(p.bfloat16().transpose(1, 2), do)
+    dp = _bmm_f32(do, v.transpose(1, 2))
+    delta = (do.float() * o.float()).sum(-1, keepdim=True)
+    ds = p.mul_(dp.sub_(delta)).mul_(scale).bfloat16()
+    dq = torch.bmm(ds, k)
+    dk = torch.bmm(ds.transpose(1, 2), q)
+    g = torch.stack([dq, dk, dv], 0).view(3, B, H, S, D).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * H * D)
+    if dbias is not None:  # query: colsum dQ; key: 0 (softmax shift invariance); value: colsum dout
+        HD = H * D
+        dbias[:HD] += g[:, :HD].float().sum(0)
+        dbias[2 * HD:] += dout.float().sum(0)
+    return g
+
+
+def _fused_attention(qkv, H):
+    return not qkv.is_cuda or qkv.shape[-1] // (3 * H) == 64
+
+
+def attn_fwd(qkv, mbias, H, S, scale, kvinfo=None):
+    """The fused flash kernels for head_dim 64 (CPU: the fp32 reference), else the composed path."""
+    if _fused_attention(qkv, H):
+        return OPS.attn_fwd(qkv, mbias, H, S, scale, kvinfo)
+    return attn_composed_fwd(qkv, mbias, H, S, scale)
+
+
+def attn_bwd(qkv, mbias, out, dout, lse, H, S, scale, kvinfo=None, dbias=None):
+    if _fused_attention(qkv, H):
+        return OPS.attn_bwd(qkv, mbias, out, dout, lse, H, S, scale, kvinfo, dbias)
+    return attn_composed_bwd(qkv, mbias, out, dout, lse, H, S, scale, dbias)
+
+
 class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, mbias, H, S, scale):
-        out, lse = OPS.attn_fwd(qkv, mbias, H, S, scale)
+        out, lse = attn_fwd(qkv, mbias, H, S, scale)
         ctx.save_for_backward(qkv, out, lse)
         ctx.mbias, ctx.H, ctx.S, ctx.scale = mbias, H, S, scale
         return out
@@ -118,7 +200,7 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse = ctx.saved_tensors
-        dqkv = OPS.attn_bwd(qkv, ctx.mbias, out, dout.contiguous(), lse, ctx.H, ctx.S, ctx.scale)
+        dqkv = attn_bwd(qkv, ctx.mbias, out, dout.contiguous(), lse, ctx.H, ctx.S, ctx.scale)
         return dqkv, None, None, None, None
 
 

@@ -110,6 +110,13 @@ def test_builtin_albert_configs():
     m.materialize("cpu")
     n = m.flat.fp32.numel()  # the tied decoder counted once, like HF
     assert 11.0e6 < n < 12.5e6, n
+    xl = AlbertConfig.from_pretrained("albert-xlarge-v2")
+    assert (xl.hidden_size, xl.num_hidden_layers, xl.num_attention_heads, xl.intermediate_size,
+            xl.embedding_size) == (2048, 24, 16, 8192, 128)
+    m = AlbertForPreTraining(xl)
+    m.materialize("cpu")
+    assert 57e6 < m.flat.fp32.numel() < 61e6  # the model card's ~59M
+    del m
     import transformers
 
     xxl, hf = AlbertConfig.from_pretrained("albert-xxlarge-v2"), transformers.AlbertConfig()
