@@ -339,6 +339,49 @@ at::Tensor attn_bwd(const at::Tensor& qkv, const c10::optional<at::Tensor>& mbia
   return dqkv;
 }
 
+// composed attention (head sizes other than 64): row softmax over GEMM-produced fp32 scores
+std::tuple<at::Tensor, at::Tensor> attn_softmax_fwd(const at::Tensor& s, const c10::optional<at::Tensor>& mbias,
+                                                    int64_t H, double c) {
+  expect(s, at::kFloat, "s");
+  const int64_t S = s.size(-1), rows = s.numel() / S;
+  TORCH_CHECK(rows % (H * S) == 0, "attn_softmax_fwd: scores must be [B*H*S, S]");
+  const float* mb = nullptr;
+  if (mbias.has_value()) {
+    expect(*mbias, at::kFloat, "mbias");
+    TORCH_CHECK(mbias->numel() == rows / H, "attn_softmax_fwd: mbias must be [B, S]");
+    mb = f32(*mbias);
+  }
+  auto p = at::empty(s.sizes(), s.options().dtype(at::kBFloat16));
+  auto lse = at::empty({rows}, s.options());
+  check(dl_attn_softmax_fwd(f32(s), mb, bf(p), f32(lse), rows, (int)H, (int)S, (float)c, cur_stream(s)),
+        "attn_softmax_fwd");
+  return {p, lse};
+}
+
+std::tuple<at::Tensor, at::Tensor> attn_softmax_bwd(const at::Tensor& s, const at::Tensor& dp,
+                                                    const c10::optional<at::Tensor>& mbias, const at::Tensor& lse,
+                                                    const at::Tensor& delta, int64_t H, double c, double scale) {
+  expect(s, at::kFloat, "s");
+  expect(dp, at::kFloat, "dp");
+  expect(lse, at::kFloat, "lse");
+  expect(delta, at::kFloat, "delta");
+  const int64_t S = s.size(-1), rows = s.numel() / S;
+  TORCH_CHECK(dp.numel() == s.numel() && lse.numel() == rows && delta.numel() == rows && rows % (H * S) == 0,
+              "attn_softmax_bwd: shape mismatch");
+  const float* mb = nullptr;
+  if (mbias.has_value()) {
+    expect(*mbias, at::kFloat, "mbias");
+    TORCH_CHECK(mbias->numel() == rows / H, "attn_softmax_bwd: mbias must be [B, S]");
+    mb = f32(*mbias);
+  }
+  auto p = at::empty(s.sizes(), s.options().dtype(at::kBFloat16));
+  auto ds = at::empty_like(p);
+  check(dl_attn_softmax_bwd(f32(s), f32(dp), mb, f32(lse), f32(delta), bf(p), bf(ds), rows, (int)H, (int)S, (float)c,
+                            (float)scale, cur_stream(s)),
+        "attn_softmax_bwd");
+  return {p, ds};
+}
+
 // ------------------------------------------------------------------ GEMM (library path)
 // Plain and fused-epilogue GEMMs go straight to hipBLASLt (csrc/host/lt_gemm.cpp: fp32 bias read
 // in the epilogue, GELU_AUX_BIAS for the FFN-up forward, DGELU_BGRAD for the FFN dgrad, per-shape
@@ -1034,6 +1077,8 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("xent_fwd_bwd", &xent_fwd_bwd);
   m.impl("attn_fwd", &attn_fwd);
   m.impl("attn_bwd", &attn_bwd);
+  m.impl("attn_softmax_fwd", &attn_softmax_fwd);
+  m.impl("attn_softmax_bwd", &attn_softmax_bwd);
   m.impl("gemm", &gemm);
   m.impl("gemm_acc_f32", &gemm_acc_f32);
   m.impl("gemm_acc_f32_shared", &gemm_acc_f32_shared);

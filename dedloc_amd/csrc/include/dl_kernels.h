@@ -105,6 +105,13 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
 int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int P, int Q, int SCp,
               int Kp, bf16_t* col, hipStream_t st);
 
+// attn_softmax.hip (composed attention for head sizes other than 64): scores s [rows = B*H*S, S]
+// fp32, mbias [B, S] log2 units (optional), c = scale * log2(e); lse / delta [rows]
+int dl_attn_softmax_fwd(const float* s, const float* mbias, bf16_t* p, float* lse, long rows, int H, int S, float c,
+                        hipStream_t st);
+int dl_attn_softmax_bwd(const float* s, const float* dp, const float* mbias, const float* lse, const float* delta,
+                        bf16_t* p, bf16_t* ds, long rows, int H, int S, float c, float scale, hipStream_t st);
+
 // attention.hip
 int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, bf16_t* out, long ldo, float* lse,
                 int B, int H, int S, int D, float scale, hipStream_t st);

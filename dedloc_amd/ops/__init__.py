@@ -130,38 +130,33 @@ def _attn_split(qkv, H, S):
     return (x[0].reshape(B * H, S, D), x[1].reshape(B * H, S, D), x[2].reshape(B * H, S, D)), B, D
 
 
-def _attn_scores(q, k, mbias, B, H, S, scale):
-    s = _bmm_f32(q, k.transpose(1, 2)).mul_(scale * _LOG2E)  # log2 units, like the fused kernels
-    if mbias is not None:
-        s.view(B, H, S, S).add_(mbias.view(B, 1, 1, S))
-    return s
-
-
 def attn_composed_fwd(qkv, mbias, H, S, scale):
-    """Attention for head sizes outside the fused kernels' 64 (albert-xlarge: 128) as batched
-    bf16 GEMMs with fp32 scores and softmax — same inputs / outputs as ``attn_fwd`` (out
-    [B*S, H*D] bf16, lse [B, H, S] fp32 in log2 units), but the [B*H, S, S] scores go through HBM."""
+    """Attention for head sizes outside the fused kernels' 64 (albert-xlarge: 128): batched bf16
+    GEMMs with fp32 scores around the ``attn_softmax_fwd`` kernel (scale, key bias, log2-unit
+    softmax in one pass) — same inputs / outputs as ``attn_fwd`` (out [B*S, H*D] bf16, lse
+    [B, H, S] fp32 in log2 units), but the [B*H, S, S] scores go through HBM."""
     (q, k, v), B, D = _attn_split(qkv, H, S)
-    s = _attn_scores(q, k, mbias, B, H, S, scale)
-    m = s.amax(-1, keepdim=True)
-    p = torch.exp2(s.sub_(m))
-    den = p.sum(-1, keepdim=True)
-    lse = (m + torch.log2(den)).view(B, H, S)
-    o = torch.bmm(p.div_(den).bfloat16(), v)
-    return o.view(B, H, S, D).transpose(1, 2).reshape(B * S, H * D), lse
+    s = _bmm_f32(q, k.transpose(1, 2))
+    p, lse = OPS.attn_softmax_fwd(s, mbias, H, scale * _LOG2E)
+    del s
+    o = torch.bmm(p, v)
+    return o.view(B, H, S, D).transpose(1, 2).reshape(B * S, H * D), lse.view(B, H, S)
 
 
 def attn_composed_bwd(qkv, mbias, out, dout, lse, H, S, scale, dbias=None):
-    """Backward of ``attn_composed_fwd`` (probabilities recomputed from lse); dQKV in the packed
-    layout, and — like the fused backward — the QKV bias gradient accumulated into ``dbias``."""
+    """Backward of ``attn_composed_fwd`` (probabilities recomputed from lse by the
+    ``attn_softmax_bwd`` kernel, which also forms dS); dQKV in the packed layout, and — like the
+    fused backward — the QKV bias gradient accumulated into ``dbias``."""
     (q, k, v), B, D = _attn_split(qkv, H, S)
-    p = torch.exp2(_attn_scores(q, k, mbias, B, H, S, scale).sub_(lse.view(B * H, S, 1)))
     do = dout.view(B, S, H, D).transpose(1, 2).reshape(B * H, S, D)
     o = out.view(B, S, H, D).transpose(1, 2).reshape(B * H, S, D)
-    dv = torch.bmm(p.bfloat16().transpose(1, 2), do)
+    s = _bmm_f32(q, k.transpose(1, 2))
     dp = _bmm_f32(do, v.transpose(1, 2))
-    delta = (do.float() * o.float()).sum(-1, keepdim=True)
-    ds = p.mul_(dp.sub_(delta)).mul_(scale).bfloat16()
+    delta = (do.float() * o.float()).sum(-1)
+    p, ds = OPS.attn_softmax_bwd(s, dp, mbias, lse.reshape(-1).contiguous(), delta.reshape(-1), H,
+                                 scale * _LOG2E, scale)
+    del s, dp
+    dv = torch.bmm(p.transpose(1, 2), do)
     dq = torch.bmm(ds, k)
     dk = torch.bmm(ds.transpose(1, 2), q)
     g = torch.stack([dq, dk, dv], 0).view(3, B, H, S, D).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * H * D)

@@ -40,6 +40,9 @@ _SCHEMAS = [
     "attn_fwd(Tensor qkv, Tensor? mbias, int H, int S, float scale, Tensor? kvinfo=None) -> (Tensor, Tensor)",
     "attn_bwd(Tensor qkv, Tensor? mbias, Tensor out, Tensor dout, Tensor lse, int H, int S, float scale, "
     "Tensor? kvinfo=None, Tensor(a!)? dbias=None) -> Tensor",
+    "attn_softmax_fwd(Tensor s, Tensor? mbias, int H, float c) -> (Tensor, Tensor)",
+    "attn_softmax_bwd(Tensor s, Tensor dp, Tensor? mbias, Tensor lse, Tensor delta, int H, float c, float scale) "
+    "-> (Tensor, Tensor)",
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
     "gemm_acc_f32_shared(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b, bool first, bool last) -> ()",
@@ -389,6 +392,27 @@ def _attn_bwd_cpu(qkv, mbias, out, dout, lse, H, S, scale, kvinfo=None, dbias=No
         dbias[:HD] += g[:, :HD].float().sum(0)
         dbias[2 * HD:] += dout.float().reshape(-1, HD).sum(0)
     return g
+
+
+def _softmax_logits(s, mbias, H, c):
+    S = s.shape[-1]
+    x = s.float().reshape(-1, H, S, S) * c
+    if mbias is not None:
+        x = x + mbias.reshape(-1, 1, 1, S)
+    return x.reshape(s.shape)
+
+
+@_impl("attn_softmax_fwd")
+def _attn_softmax_fwd_cpu(s, mbias, H, c):
+    x = _softmax_logits(s, mbias, H, c)
+    lse = torch.logsumexp(x / math.log2(math.e), -1) * math.log2(math.e)
+    return _bf(torch.exp2(x - lse[..., None])), lse.reshape(-1).contiguous()
+
+
+@_impl("attn_softmax_bwd")
+def _attn_softmax_bwd_cpu(s, dp, mbias, lse, delta, H, c, scale):
+    p = torch.exp2(_softmax_logits(s, mbias, H, c) - lse.reshape(s.shape[:-1])[..., None])
+    return _bf(p), _bf(p * (dp.float() - delta.reshape(s.shape[:-1])[..., None]) * scale)
 
 
 @_impl("gemm")
