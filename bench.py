@@ -148,13 +148,29 @@ def _swav_peer(args, rank, dev, root_ep):
     return peer, b, describe
 
 
+def _harness_world(cpu: bool):
+    """The BENCH HARNESS's own process group (gloo, host-side): barriers around the timed region,
+    the DHT root's address, and the max-over-ranks reduction.  The collaboration itself never sees
+    it — peers find each other through the DHT and build their RCCL communicators there
+    (dedloc_amd/parallel/comm.py)."""
+    from dedloc_amd.parallel import local_device
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dev = local_device(torch.device("cpu") if cpu else None)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        import datetime
+
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=1800))
+    return rank, world, dev
+
+
 def main():
     args = parse()
     logging.basicConfig(level=logging.INFO if args.verbose else logging.WARNING,
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
-    from dedloc_amd.parallel import init_world
-
-    rank, world, dev = init_world(device=torch.device("cpu") if args.cpu_test else None)
+    rank, world, dev = _harness_world(cpu=bool(args.cpu_test))
 
     def sync():
         if dev.type == "cuda":
@@ -202,7 +218,7 @@ def main():
     sync()
     dt = time.perf_counter() - t0
     ema = co.performance_ema.samples_per_second
-    stats = torch.tensor([samples, dt, ema] + [co.stats[k] - st0[k] for k in keys], dtype=torch.float64, device=dev)
+    stats = torch.tensor([samples, dt, ema] + [co.stats[k] - st0[k] for k in keys], dtype=torch.float64)
     if world > 1:
         gathered = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(gathered, stats)

@@ -69,16 +69,19 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
             jobs_list.append(["hipcc", *hip_flags, *inc, "-c", src, "-o", obj])
 
     tinc, tlib, abi = _torch_paths()
-    bind_src = os.path.join(CSRC, "bindings.cpp")
-    bind_obj = os.path.join(BUILD, "bindings.o")
-    objs.append(bind_obj)
-    if _newer(bind_obj, [bind_src] + headers):
-        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__",
-               "-DUSE_ROCM", "-I", f"{ROCM}/include", *inc]
-        for p in tinc:
-            cmd += ["-I", p]
-        cmd += ["-I", sysconfig.get_paths()["include"], "-c", bind_src, "-o", bind_obj]
-        jobs_list.append(cmd)
+    # translation units that include torch: the operator bindings and the RCCL data plane (csrc/comm)
+    torch_srcs = [os.path.join(CSRC, "bindings.cpp")] + sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
+    for src in torch_srcs:
+        name = os.path.basename(src).replace(".cpp", ".o")
+        obj = os.path.join(BUILD, name if src.endswith("bindings.cpp") else "comm_" + name)
+        objs.append(obj)
+        if _newer(obj, [src] + headers):
+            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__",
+                   "-DUSE_ROCM", "-I", f"{ROCM}/include", *inc]
+            for p in tinc:
+                cmd += ["-I", p]
+            cmd += ["-I", sysconfig.get_paths()["include"], "-c", src, "-o", obj]
+            jobs_list.append(cmd)
 
     # host-side C++ that talks to ROCm libraries (hipBLASLt) but not to torch
     for src in sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))):
@@ -103,7 +106,8 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         cmd = ["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", SO_PATH]
         for p in tlib:
             cmd += ["-L", p, f"-Wl,-rpath,{p}"]
-        cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-L", f"{ROCM}/lib",
+        # -lrccl resolves in torch's lib dir first: the same librccl.so.1 torch loads (one RCCL per process)
+        cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl", "-L", f"{ROCM}/lib",
                 f"-Wl,-rpath,{ROCM}/lib", "-lhipblaslt"]
         _run(cmd, verbose)
     if rt_objs and _newer(DHT_SO_PATH, rt_objs):

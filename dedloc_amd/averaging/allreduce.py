@@ -1,14 +1,14 @@
 """Butterfly all-reduce over a group communicator (RCCL on GPUs, gloo on CPU).
 
-A matchmade group (any subset of the world) averages a list of flat fp32 tensors:
+A matchmade group (any set of live peers) averages a list of flat fp32 tensors:
 
   1. pack   : wire = compress(x)                             (one HIP pack kernel per tensor)
-  2. scatter: member j receives part j of everyone's wire    (grouped isend/irecv, all pairs at once —
+  2. scatter: member j receives part j of everyone's wire    (one grouped send/recv, all pairs at once —
               on an 8-GPU xGMI mesh every GPU drives its 7 links concurrently instead of the one
               link per hop of a ring)
   3. reduce : avg_j = sum_k w_k wire_k[j] / sum_k w_k in fp32, and for every sender k the delta
               d_k[j] = compress(avg_j - decompress(wire_k[j]))     (one HIP reduce_delta kernel)
-  4. return : member j sends d_k[j] back to sender k          (grouped isend/irecv)
+  4. return : member j sends d_k[j] back to sender k          (one grouped send/recv)
   5. unpack : x += decompress(d)                              (fp32, on the live tensor)
 
 Returning averaged-part *deltas* (hivemind 0.9.x's ``averaged_part - tensor_part`` rule) instead of
@@ -21,32 +21,32 @@ exactly zero.
 Part sizes come from the load-balancing LP; client-mode members own no part (they only send and
 receive), auxiliary members contribute no tensor (weight 0) but reduce a part.
 
-Timeouts: completion is polled on the host against a deadline (an RCCL ``Work.wait`` only orders
-streams, it never times out); on expiry the round raises ``AllreduceException`` and the caller must
-abort the communicator (``parallel.GroupCommunicators.invalidate``) so the operations still posted
-on it cannot be matched by a later round.
+Timeouts: completion is polled on the host against a deadline; on expiry the communicator is
+aborted (``ncclCommAbort`` for RCCL) so the operations still posted on it can never be matched by a
+later round, and the round raises ``AllreduceException``; the caller drops the communicator from its
+cache (``parallel.GroupCommunicators.invalidate``).
 """
 from __future__ import annotations
 
-import datetime
 import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
 import torch
-import torch.distributed as dist
+
+from ..parallel.comm import CommError
 
 WIRE_DTYPES = {"NONE": torch.float32, "FLOAT32": torch.float32, "FLOAT16": torch.float16,
                "BFLOAT16": torch.bfloat16}
 
 
-class AllreduceException(RuntimeError):
+class AllreduceException(CommError):
     pass
 
 
 @dataclass
 class GroupSpec:
-    ranks: List[int]            # world rank of each member, in group order
+    ranks: List[int]            # communicator rank of each member, in group order
     part_sizes: List[int]       # elements of the averaged vector owned by each member
     weights: List[float]        # averaging weight of each member (0 for auxiliary peers)
     contributes: List[bool]     # False for auxiliary peers (they send no tensor)
@@ -57,37 +57,19 @@ class GroupSpec:
         return len(self.ranks)
 
 
-def _run_p2p(p2p, deadline: Optional[float], pg=None):
-    """Post one batch of grouped P2P operations and wait for all of them, at most until ``deadline``
-    (``time.monotonic()`` seconds)."""
-    if not p2p:
+def _p2p(comm, sends, send_peers, recvs, recv_peers, deadline, tag):
+    if not sends and not recvs:
         return
-    works = dist.batch_isend_irecv(p2p)
-    if dist.get_backend(pg) == "gloo":
-        # gloo send/recv works only complete inside wait(), which honours a timeout
-        for w in works:
-            left = None if deadline is None else max(1e-3, deadline - time.monotonic())
-            try:
-                ok = w.wait(timeout=datetime.timedelta(seconds=left)) if left is not None else w.wait()
-            except RuntimeError as e:
-                raise AllreduceException(f"all-reduce failed: {e}") from e
-            if ok is False:
-                raise AllreduceException("all-reduce timed out")
-        return
-    pending = list(works)
-    while pending:
-        pending = [w for w in pending if not w.is_completed()]
-        if not pending:
-            break
-        if deadline is not None and time.monotonic() > deadline:
-            raise AllreduceException("all-reduce timed out")
-        time.sleep(2e-4)
-    for w in works:  # surfaces a backend error; orders the current stream after the transfer
-        w.wait()
+    if comm is None:
+        raise AllreduceException("a group of more than one member needs a communicator")
+    try:
+        comm.p2p(sends, send_peers, recvs, recv_peers, deadline, tag=tag)
+    except CommError as e:
+        raise AllreduceException(str(e)) from e
 
 
 def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compression: str = "FLOAT16",
-                        pg=None, timeout: Optional[float] = 30.0, sources: Optional[Sequence[torch.Tensor]] = None):
+                        comm=None, timeout: Optional[float] = 30.0, sources: Optional[Sequence[torch.Tensor]] = None):
     """Average ``tensors`` in place across the group described by ``spec``.
 
     ``sources``: pack these instead of ``tensors`` (same shapes) and add the averaging deltas to
@@ -122,20 +104,22 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
     nc = len(contrib_idx)
     recv = torch.empty((max(1, nc), max(P, 1)), dtype=wire, device=dev)
 
-    # 2. reduce-scatter: part j of every contributor's wire goes to member j
-    p2p = []
+    # 2. reduce-scatter: part j of every contributor's wire goes to member j (one grouped launch)
+    sends, send_peers, recvs, recv_peers = [], [], [], []
     for slot, j in enumerate(contrib_idx):
         if j == me:
             if P:
                 recv[slot, :P].copy_(send[my_lo:my_hi])
             continue
         if P:
-            p2p.append(dist.P2POp(dist.irecv, recv[slot, :P], spec.ranks[j], group=pg))
+            recvs.append(recv[slot, :P])
+            recv_peers.append(spec.ranks[j])
     if i_contribute:
         for j in range(spec.size):
             if j != me and spec.part_sizes[j] > 0:
-                p2p.append(dist.P2POp(dist.isend, send[starts[j]:starts[j + 1]], spec.ranks[j], group=pg))
-    _run_p2p(p2p, deadline, pg)
+                sends.append(send[starts[j]:starts[j + 1]])
+                send_peers.append(spec.ranks[j])
+    _p2p(comm, sends, send_peers, recvs, recv_peers, deadline, tag=1)
 
     # 3. weighted fp32 average of my part and one delta row per contributor
     deltas = None
@@ -147,19 +131,21 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
 
     # 4. every contributor receives its deltas for every part
     dbuf = torch.empty(V if i_contribute else 0, dtype=wire, device=dev)
-    p2p = []
+    sends, send_peers, recvs, recv_peers = [], [], [], []
     for slot, j in enumerate(contrib_idx):
         if j == me:
             if P:
                 dbuf[my_lo:my_hi].copy_(deltas[slot])
             continue
         if P:
-            p2p.append(dist.P2POp(dist.isend, deltas[slot], spec.ranks[j], group=pg))
+            sends.append(deltas[slot])
+            send_peers.append(spec.ranks[j])
     if i_contribute:
         for j in range(spec.size):
             if j != me and spec.part_sizes[j] > 0:
-                p2p.append(dist.P2POp(dist.irecv, dbuf[starts[j]:starts[j + 1]], spec.ranks[j], group=pg))
-    _run_p2p(p2p, deadline, pg)
+                recvs.append(dbuf[starts[j]:starts[j + 1]])
+                recv_peers.append(spec.ranks[j])
+    _p2p(comm, sends, send_peers, recvs, recv_peers, deadline, tag=2)
 
     # 5. unpack: x += delta (auxiliary peers hold no averaged tensor)
     if i_contribute:

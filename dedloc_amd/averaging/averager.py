@@ -5,14 +5,16 @@ In-process design (no helper processes, no host staging of the averaged tensors)
     ``target_group_size``, when every live peer of the collaboration has joined, or when the
     ``averaging_expiration`` window of its first member ends;
   * the data plane is the butterfly all-reduce (``allreduce.butterfly_allreduce``) with LP-balanced
-    parts and FLOAT16/BFLOAT16 wire compression, on a group communicator keyed by (member set,
-    data-plane epoch) (``parallel.GroupCommunicators``).  Every member announces its epoch in its
-    matchmaking info and the group runs on epoch max(announced), so all members pick the same
-    communicator; a failed round aborts that communicator and the member moves to epoch + 1, which
-    forces a fresh communicator the next time it averages with any of those peers;
-  * state sharing: every peer with ``allow_state_sharing`` runs a small TCP state server
-    (``listen_on``) and advertises it under ``{prefix}_state_sharing``; ``load_state_from_peers``
-    downloads (metadata, tensors) from the freshest donor.
+    parts and FLOAT16/BFLOAT16 wire compression, on a communicator the group's members build
+    through the DHT (``parallel.GroupCommunicators``: RCCL between GPU peers, gloo when a CPU peer
+    is a member).  Nothing depends on a launch-time world, so any process that can reach the DHT
+    — a late volunteer, a respawned spot instance — averages in the next round it joins.  A failed
+    round aborts its communicator; members reuse a communicator only while all of them still hold
+    it;
+  * state sharing: every peer with ``allow_state_sharing`` runs a state server (``listen_on``) and
+    advertises it under ``{prefix}_state_sharing``; ``load_state_from_peers`` downloads (metadata,
+    tensors) from the freshest donor — GPU to GPU over a one-off RCCL communicator, or streamed over
+    TCP for CPU peers (``StateServer``).
 """
 from __future__ import annotations
 
@@ -24,12 +26,11 @@ import time
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import msgpack
-import numpy as np
 import torch
-import torch.distributed as dist
 
 from ..dht import DHT, get_dht_time, parse_endpoint
-from .allreduce import AllreduceException, GroupSpec, WIRE_DTYPES, butterfly_allreduce
+from ..parallel.comm import CommError, GroupCommunicators, pairwise_rccl, rccl_available, RcclGroupComm
+from .allreduce import GroupSpec, WIRE_DTYPES, butterfly_allreduce
 from .load_balancing import load_balance_peers
 
 logger = logging.getLogger(__name__)
@@ -37,31 +38,54 @@ logger = logging.getLogger(__name__)
 _DT = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16, "int64": torch.int64}
 
 
+_CHUNK = 32 << 20  # bytes per host-staging chunk of a GPU tensor sent over TCP
+
+
 def _recv_exact(sock, n):
     buf = bytearray(n)
-    view = memoryview(buf)
-    got = 0
+    _recv_into(sock, memoryview(buf))
+    return bytes(buf)
+
+
+def _recv_into(sock, view: memoryview):
+    got, n = 0, len(view)
     while got < n:
         k = sock.recv_into(view[got:], n - got)
         if k == 0:
             raise ConnectionError("peer closed")
         got += k
-    return bytes(buf)
+
+
+def _byte_view(t: torch.Tensor) -> memoryview:
+    """Zero-copy bytes of a contiguous CPU tensor."""
+    return memoryview(t.reshape(-1).view(torch.uint8).numpy())
 
 
 class StateServer:
-    """Serves ``get_state() -> (metadata, [tensors])`` to joining peers over TCP."""
+    """Serves ``get_state() -> (metadata, [tensors])`` to joining peers.
 
-    def __init__(self, get_state: Callable[[], Tuple[Dict, List[torch.Tensor]]], listen_on: str = "0.0.0.0:0"):
+    Request: ``b"STATE" + mode`` with mode ``R`` (followed by a 128-byte RCCL unique id made by the
+    requester) or ``T``.  A GPU donor answers an ``R`` request by sending the snapshot device-to-
+    device over a 2-rank RCCL communicator on its own HIP stream (no host staging at all); otherwise
+    the tensors are streamed over TCP — GPU tensors through two pinned host chunks (the D2H copy of
+    chunk i+1 overlaps the socket send of chunk i), CPU tensors straight from their storage (no
+    ``tobytes`` copies).  The trainer only ever blocks for the snapshot itself: ``get_state`` clones
+    the state on the device under the optimizer's step lock and the transfer runs outside it."""
+
+    def __init__(self, get_state: Callable[[], Tuple[Dict, List[torch.Tensor]]], listen_on: str = "0.0.0.0:0",
+                 device: Optional[torch.device] = None, transfer_timeout: float = 120.0):
         host, port = parse_endpoint(listen_on.replace("*", "0"))
         bind = "0.0.0.0" if listen_on.startswith(("0.0.0.0", "[::]", "*")) else host
         self.get_state = get_state
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.transfer_timeout = transfer_timeout
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self.sock.bind((bind, port))
         self.sock.listen(16)
         self.port = self.sock.getsockname()[1]
         self.endpoint = f"{'127.0.0.1' if bind == '0.0.0.0' else bind}:{self.port}"
+        self.served = {"R": 0, "T": 0}
         self._stop = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="state-server")
         self.thread.start()
@@ -72,25 +96,81 @@ class StateServer:
                 conn, _ = self.sock.accept()
             except OSError:
                 break
-            threading.Thread(target=self._serve, args=(conn,), daemon=True).start()
+            threading.Thread(target=self._serve, args=(conn,), daemon=True, name="state-transfer").start()
 
     def _serve(self, conn):
         try:
             with conn:
-                req = _recv_exact(conn, 5)
-                if req != b"STATE":
+                conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                req = _recv_exact(conn, 6)
+                if req[:5] != b"STATE":
                     return
+                uid = _recv_exact(conn, 128) if req[5:6] == b"R" else None
+                if self.device.type == "cuda":
+                    torch.cuda.set_device(self.device)
                 meta, tensors = self.get_state()
+                rccl = uid is not None and rccl_available(self.device) and all(t.is_cuda for t in tensors)
                 descs = [(str(t.dtype).replace("torch.", ""), list(t.shape)) for t in tensors]
-                header = msgpack.packb({"metadata": meta, "tensors": descs}, use_bin_type=True)
+                header = msgpack.packb({"metadata": meta, "tensors": descs, "mode": "R" if rccl else "T"},
+                                       use_bin_type=True)
                 conn.sendall(struct.pack("<Q", len(header)) + header)
-                for t in tensors:
-                    arr = t.detach().contiguous().cpu()
-                    conn.sendall(struct.pack("<Q", arr.numel() * arr.element_size()))
-                    conn.sendall(arr.view(torch.uint8).numpy().tobytes() if arr.dtype == torch.bfloat16
-                                 else arr.numpy().tobytes())
+                if rccl:
+                    self._send_rccl(uid, tensors)
+                    self.served["R"] += 1
+                else:
+                    self._send_tcp(conn, tensors)
+                    self.served["T"] += 1
         except Exception as e:  # noqa: BLE001
-            logger.debug(f"state transfer failed: {e}")
+            logger.warning(f"state transfer failed: {e}")
+
+    def _send_rccl(self, uid: bytes, tensors: List[torch.Tensor]):
+        ready = torch.cuda.Event()
+        ready.record()  # the snapshot copies were queued on this thread's current stream
+        stream = torch.cuda.Stream(self.device)
+        deadline = time.monotonic() + self.transfer_timeout
+        with torch.cuda.stream(stream):
+            stream.wait_event(ready)
+            comm = pairwise_rccl(uid, 0, self.device, deadline)
+            try:
+                comm.p2p([t.reshape(-1) for t in tensors], [1] * len(tensors), [], [], deadline)
+            finally:
+                comm.abort()
+
+    def _send_tcp(self, conn, tensors: List[torch.Tensor]):
+        staging, stream = None, None
+        for t in tensors:
+            nbytes = t.numel() * t.element_size()
+            conn.sendall(struct.pack("<Q", nbytes))
+            if not t.is_cuda:
+                if nbytes:
+                    conn.sendall(_byte_view(t.detach().contiguous()))
+                continue
+            if staging is None:
+                staging = [torch.empty(_CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+                stream = torch.cuda.Stream(t.device)
+                ready = torch.cuda.Event()
+                ready.record()
+                stream.wait_event(ready)
+            flat = t.detach().reshape(-1).view(torch.uint8)
+            events, offs = [], list(range(0, nbytes, _CHUNK))
+            with torch.cuda.stream(stream):
+                for i, off in enumerate(offs[:2]):
+                    n = min(_CHUNK, nbytes - off)
+                    staging[i % 2][:n].copy_(flat[off:off + n], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    events.append(ev)
+                for i, off in enumerate(offs):
+                    n = min(_CHUNK, nbytes - off)
+                    events[i].synchronize()
+                    conn.sendall(_byte_view(staging[i % 2])[:n])
+                    j = i + 2
+                    if j < len(offs):  # refill this buffer with chunk i+2 while chunk i+1 is sent
+                        m = min(_CHUNK, nbytes - offs[j])
+                        staging[j % 2][:m].copy_(flat[offs[j]:offs[j] + m], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(stream)
+                        events.append(ev)
 
     def shutdown(self):
         self._stop.set()
@@ -100,19 +180,37 @@ class StateServer:
             pass
 
 
-def download_state(endpoint: str, timeout: float = 60.0):
+def download_state(endpoint: str, timeout: float = 60.0, device: Optional[torch.device] = None,
+                   allow_rccl: bool = True):
+    """(metadata, tensors) from a state server.  A GPU requester asks for the RCCL transfer (the
+    tensors arrive on ``device``); otherwise the tensors arrive over TCP into host memory.  The
+    metadata carries the transfer mode under ``_mode`` ("R" or "T")."""
     host, port = parse_endpoint(endpoint)
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    uid = RcclGroupComm.new_unique_id() if allow_rccl and rccl_available(device) else None
+    deadline = time.monotonic() + timeout
     with socket.create_connection((host, port), timeout=timeout) as s:
-        s.sendall(b"STATE")
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        s.sendall(b"STATER" + uid if uid is not None else b"STATET")
         (hl,) = struct.unpack("<Q", _recv_exact(s, 8))
         header = msgpack.unpackb(_recv_exact(s, hl), raw=False)
-        tensors = []
-        for dtype, shape in header["tensors"]:
+        descs = [(_DT[dt], shape) for dt, shape in header["tensors"]]
+        if header.get("mode") == "R":
+            out = [torch.empty(shape, dtype=dt, device=device) for dt, shape in descs]
+            comm = pairwise_rccl(uid, 1, device, deadline)
+            try:
+                comm.p2p([], [], [t.reshape(-1) for t in out], [0] * len(out), deadline)
+            finally:
+                comm.abort()
+            return dict(header["metadata"], _mode="R"), out
+        out = []
+        for dt, shape in descs:
             (nb,) = struct.unpack("<Q", _recv_exact(s, 8))
-            raw = bytearray(_recv_exact(s, nb))
-            t = torch.frombuffer(raw, dtype=_DT[dtype]).reshape(shape) if nb else torch.empty(shape, dtype=_DT[dtype])
-            tensors.append(t)
-        return header["metadata"], tensors
+            t = torch.empty(shape, dtype=dt)
+            if nb:
+                _recv_into(s, _byte_view(t))
+            out.append(t)
+        return dict(header["metadata"], _mode="T"), out
 
 
 class DecentralizedAverager:
@@ -120,10 +218,10 @@ class DecentralizedAverager:
                  target_group_size: int = 256, min_group_size: int = 2, averaging_expiration: float = 5.0,
                  averaging_timeout: float = 30.0, compression: str = "FLOAT16", throughput: Optional[float] = None,
                  client_mode: bool = False, auxiliary: bool = False, allow_state_sharing: bool = True,
-                 listen_on: str = "0.0.0.0:*", metadata_expiration: float = 30.0, pg=None, rank: Optional[int] = None,
-                 emulate_transfer_delay: bool = False, **_unused):
+                 listen_on: str = "0.0.0.0:*", metadata_expiration: float = 30.0, device: Optional[torch.device] = None,
+                 max_cached_comms: int = 8, emulate_transfer_delay: bool = False, **_unused):
         self.averaged_tensors = list(averaged_tensors)
-        self.dht, self.prefix, self.peer_id = dht, prefix, peer_id
+        self.dht, self.prefix, self.peer_id = dht, prefix, bytes(peer_id)
         self.target_group_size, self.min_group_size = target_group_size, min_group_size
         self.averaging_expiration, self.averaging_timeout = averaging_expiration, averaging_timeout
         if compression not in WIRE_DTYPES:
@@ -133,19 +231,20 @@ class DecentralizedAverager:
         self.client_mode, self.auxiliary = client_mode, auxiliary
         self.allow_state_sharing = allow_state_sharing and not auxiliary
         self.metadata_expiration = metadata_expiration
-        self.pg = pg
-        self.epoch = 0
-        self.comms = None
-        if pg is None:
-            from ..parallel import GroupCommunicators
-
-            self.comms = GroupCommunicators(timeout_s=max(60.0, 2 * averaging_timeout))
-        self.rank = rank if rank is not None else (dist.get_rank() if dist.is_available() and dist.is_initialized() else 0)
+        if device is None:
+            device = self.averaged_tensors[0].device if self.averaged_tensors else torch.device("cpu")
+        self.device = torch.device(device)
+        host = parse_endpoint(listen_on.replace("*", "0").replace("[::]", "0.0.0.0"))[0]
+        self.host = "127.0.0.1" if host in ("0.0.0.0", "") else host
+        self.comms = GroupCommunicators(dht, prefix, self.peer_id, self.device,
+                                        timeout_s=max(30.0, 2 * averaging_timeout), max_cached=max_cached_comms,
+                                        host=self.host)
         self.lock_averaged_tensors = threading.RLock()
         self.last_group: Optional[Dict] = None
-        self.state_server = StateServer(self._serve_state, listen_on.replace("[::]", "0.0.0.0")) \
+        self.state_server = StateServer(self._serve_state, listen_on.replace("[::]", "0.0.0.0"), device=self.device) \
             if self.allow_state_sharing else None
         self.local_step_for_state = 0
+        self.last_download: Optional[Dict] = None
         self.emulate_transfer_delay = emulate_transfer_delay
 
     # ------------------------------------------------------------------ averaging
@@ -158,13 +257,10 @@ class DecentralizedAverager:
         snapshots instead of the live tensors, ``key_suffix`` selects an independent matchmaking key
         (so a delayed parameter round never mixes with a gradient round)."""
         tensors = list(tensors) if tensors is not None else self.averaged_tensors
-        if not (dist.is_available() and dist.is_initialized()):
-            logger.warning("averaging requires the collaboration's world communicator; skipping")
-            return None
         weight = 0.0 if self.auxiliary else float(weight)
         bw = 0.0 if self.client_mode else (self.throughput if self.throughput is not None else 1.0)
-        info = {"rank": self.rank, "bandwidth": bw, "weight": weight, "aux": self.auxiliary, "gather": gather or {},
-                "epoch": self.epoch}
+        info = {"bandwidth": bw, "weight": weight, "aux": self.auxiliary, "gather": gather or {}}
+        info.update(self.comms.announce())
         window = self.averaging_expiration
         t_join = time.perf_counter()
         try:
@@ -179,29 +275,29 @@ class DecentralizedAverager:
             logger.info(f"averaging round failed: group of {len(members)} < {self.min_group_size}")
             return None
         infos = [m[1] for m in members]
-        my_index = [m[0] for m in members].index(self.peer_id)
+        pids = [bytes(m[0]) for m in members]
+        my_index = pids.index(self.peer_id)
         V = sum(t.numel() for t in tensors)
         parts = load_balance_peers(V, [i["bandwidth"] for i in infos], min_size=0)
-        spec = GroupSpec(ranks=[i["rank"] for i in infos], part_sizes=list(parts),
-                         weights=[i["weight"] for i in infos], contributes=[not i["aux"] for i in infos],
-                         my_index=my_index)
-        if sum(w for w, c in zip(spec.weights, spec.contributes) if c) <= 0:
+        if sum(i["weight"] for i in infos if not i["aux"]) <= 0:
             return None
-        epoch = max(int(i.get("epoch", 0)) for i in infos)
-        self.epoch = max(self.epoch, epoch)
         t0 = time.perf_counter()
+        deadline = time.monotonic() + (timeout or self.averaging_timeout)
+        comm = None
         try:
-            pg = self.pg if self.pg is not None else self.comms.get(spec.ranks, epoch)
+            comm, rank_of = self.comms.get(members, gid, deadline)
+            spec = GroupSpec(ranks=[rank_of[p] for p in pids], part_sizes=list(parts),
+                             weights=[i["weight"] for i in infos], contributes=[not i["aux"] for i in infos],
+                             my_index=my_index)
             with self.lock_averaged_tensors:
-                butterfly_allreduce(tensors, spec, self.compression, pg=pg,
-                                    timeout=timeout or self.averaging_timeout, sources=sources)
-        except (AllreduceException, RuntimeError) as e:
-            # the communicator may still hold posted operations: abort it and move to a new epoch
-            # so no later round can be matched against them
-            logger.warning(f"all-reduce failed ({e}); skipping this round (data-plane epoch {epoch} -> {epoch + 1})")
-            if self.comms is not None:
-                self.comms.invalidate(spec.ranks, epoch)
-            self.epoch = max(self.epoch, epoch + 1)
+                butterfly_allreduce(tensors, spec, self.compression, comm=comm,
+                                    timeout=max(1e-3, deadline - time.monotonic()), sources=sources)
+        except (CommError, RuntimeError) as e:
+            # the communicator may still hold posted operations: it is aborted and forgotten, so the
+            # next round between these peers runs on a fresh one
+            logger.warning(f"all-reduce failed ({e}); skipping this round")
+            if comm is not None:
+                self.comms.invalidate(comm)
             return None
         if self.emulate_transfer_delay and bw > 0:  # emulate the volunteer's link (AWS_runner wondershaper caps)
             from ..emulation.heterogeneity import emulated_transfer_seconds
@@ -212,7 +308,8 @@ class DecentralizedAverager:
             if want > spent:
                 time.sleep(want - spent)
         self.last_group = {"group_id": gid, "size": len(members), "gathered": [i["gather"] for i in infos],
-                           "matchmaking_s": t_match, "allreduce_s": time.perf_counter() - t0, "parts": list(parts)}
+                           "matchmaking_s": t_match, "allreduce_s": time.perf_counter() - t0, "parts": list(parts),
+                           "backend": comm.backend if comm is not None else None}
         return self.last_group
 
     # ------------------------------------------------------------------ state sharing
@@ -245,16 +342,20 @@ class DecentralizedAverager:
                 continue
             donors.append((v.value.get("step", 0), v.value["endpoint"]))
         for step, ep in sorted(donors, reverse=True):
-            try:
-                meta, tensors = download_state(ep, timeout=timeout)
-                logger.info(f"downloaded state (step {meta.get('step')}) from {ep}")
-                return meta, tensors
-            except Exception as e:  # noqa: BLE001
-                logger.warning(f"failed to download state from {ep}: {e}")
+            for rccl in ((True, False) if rccl_available(self.device) else (False,)):
+                try:
+                    t0 = time.perf_counter()
+                    meta, tensors = download_state(ep, timeout=timeout, device=self.device, allow_rccl=rccl)
+                    self.last_download = {"endpoint": ep, "mode": meta.pop("_mode", "T"),
+                                          "bytes": sum(t.numel() * t.element_size() for t in tensors),
+                                          "seconds": time.perf_counter() - t0}
+                    logger.info(f"downloaded state (step {meta.get('step')}) from {ep}: {self.last_download}")
+                    return meta, tensors
+                except Exception as e:  # noqa: BLE001
+                    logger.warning(f"failed to download state from {ep} ({'RCCL' if rccl else 'TCP'}): {e}")
         return None
 
     def shutdown(self):
         if self.state_server is not None:
             self.state_server.shutdown()
-        if self.comms is not None:
-            self.comms.close()
+        self.comms.close()

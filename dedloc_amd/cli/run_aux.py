@@ -24,10 +24,13 @@ def main(argv=None):
         raise ValueError("Please specify at least one network endpoint in initial peers.")
     import torch
 
-    from ..parallel import init_world
+    import os
+
+    from ..parallel import local_device
     from ..training.albert_peer import AlbertPeer
 
-    rank, world, device = init_world(device=None if training_args.device is None else torch.device(training_args.device))
+    rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local_device(None if training_args.device is None else torch.device(training_args.device))
     setup_logging(rank)
     peer = AlbertPeer(training_args, dataset_args, collaboration_args, device, rank=rank, auxiliary=True)
     try:

@@ -40,9 +40,12 @@ def main(argv=None):
         return
     import torch
 
-    from ..parallel import init_world
+    import os
 
-    rank, world, device = init_world(device=None if args.device is None else torch.device(args.device))
+    from ..parallel import local_device
+
+    rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local_device(None if args.device is None else torch.device(args.device))
     logging.basicConfig(format="%(asctime)s - %(levelname)s - %(name)s -   %(message)s",
                         level=logging.INFO if rank == 0 else logging.WARNING)
     from ..training.swav_peer import SwavPeer

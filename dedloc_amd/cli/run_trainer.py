@@ -33,9 +33,13 @@ def main(argv=None, sahajbert: bool = False):
         sahajbert = True
     parser = HfArgumentParser((AlbertTrainingArguments, DatasetArguments, CollaborationArguments))
     training_args, dataset_args, collaboration_args = parser.parse_args_into_dataclasses(argv)
-    from ..parallel import init_world
+    import os
 
-    rank, world, device = init_world(device=None if training_args.device is None else __import__("torch").device(training_args.device))
+    from ..parallel import local_device
+
+    # the launcher's per-process GPU index doubles as this peer's slot in the heterogeneity profiles
+    rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local_device(None if training_args.device is None else __import__("torch").device(training_args.device))
     setup_logging(rank)
     logger.info(f"Found {len(collaboration_args.initial_peers)} initial peers: {collaboration_args.initial_peers}")
     if not sahajbert and len(collaboration_args.initial_peers) == 0:

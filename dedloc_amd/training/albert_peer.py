@@ -65,7 +65,7 @@ def build_optimizer(model: AlbertForPreTraining, training_args):
 class AlbertPeer:
     """Everything one GPU peer owns: model, optimizer, DHT node, collaborative optimizer, data."""
 
-    def __init__(self, training_args, dataset_args, collab_args, device, pg=None, rank: int = 0,
+    def __init__(self, training_args, dataset_args, collab_args, device, rank: int = 0,
                  dht: Optional[DHT] = None, auxiliary: bool = False, publish_only_synchronized: bool = False,
                  impl: str = "dedloc"):
         self.args, self.dargs, self.cargs = training_args, dataset_args, collab_args
@@ -132,7 +132,7 @@ class AlbertPeer:
             listen_on=ca.listen_on, min_refresh_period=ca.min_refresh_period, max_refresh_period=ca.max_refresh_period,
             default_refresh_period=ca.default_refresh_period, expected_drift_peers=ca.expected_drift_peers,
             expected_drift_rate=ca.expected_drift_rate, performance_ema_alpha=ca.performance_ema_alpha,
-            target_group_size=ca.target_group_size, metadata_expiration=ca.metadata_expiration, pg=pg, rank=rank,
+            target_group_size=ca.target_group_size, metadata_expiration=ca.metadata_expiration, device=self.device,
             delay_param_averaging=getattr(ca, "delay_param_averaging", False),
             emulate_transfer_delay=getattr(ca, "emulate_transfer_delay", False), eta_slack=getattr(ca, "eta_slack", 0.0))
         self.statistics_expiration = ca.statistics_expiration

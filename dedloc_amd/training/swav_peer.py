@@ -58,7 +58,7 @@ def _port_endpoint(port) -> str:
 
 
 class SwavPeer:
-    def __init__(self, cfg, device, dht: Optional[DHT] = None, pg=None, rank: int = 0):
+    def __init__(self, cfg, device, dht: Optional[DHT] = None, rank: int = 0):
         self.cfg = cfg
         self.device = torch.device(device)
         torch.manual_seed(int(cfg.get("SEED_VALUE", 0)))
@@ -106,7 +106,7 @@ class SwavPeer:
             listen_on=_port_endpoint(ocfg.averager_listen_on_port),
             averaging_expiration=float(ocfg.get("averaging_expiration", 5.0)),
             metadata_expiration=float(ocfg.get("metadata_expiration", 30)),
-            averaging_timeout=float(ocfg.get("averaging_timeout", 30)), pg=pg, rank=rank)
+            averaging_timeout=float(ocfg.get("averaging_timeout", 30)), device=self.device)
         q = lcfg.queue
         self.loss_fn = SwAVLoss(num_crops=sum(dcfg.MULTICROP.num_crops), crops_for_assign=lcfg.crops_for_assign,
                                 temperature=float(lcfg.temperature), epsilon=float(lcfg.epsilon),

@@ -1,16 +1,21 @@
-"""Data-plane numerics and failure handling of the decentralized averager (gloo world on CPU).
+"""Data-plane numerics and failure handling of the decentralized averager (gloo on CPU).
 
 * FLOAT16 wire compression must not round the fp32 master tensors: the all-reduce returns
   averaged-part deltas, so parameter updates far below half an fp16 ulp survive many rounds
   (replacing the tensor by the decoded average kept ~1.5% of the movement).
 * A member that stalls past ``averaging_timeout`` fails the round for its group; the communicator
-  that still holds the posted operations is aborted and the next round (new data-plane epoch)
+  that still holds the posted operations is aborted and the next round (a fresh communicator)
   must produce the exact weighted average (stale operations on a shared communicator
   were matched by the next round).
+* Communicator reuse needs every member to still hold the communicator: a peer whose cache is
+  smaller than the others' evicts early, and the group must then build a fresh one instead of
+  half the members waiting on a communicator the other half dropped.
+
+No process here is part of any launch-time world: every group communicator is bootstrapped
+through the DHT by its members (dedloc_amd/parallel/comm.py).
 """
 import multiprocessing as mp
 import os
-import socket
 import time
 
 import pytest
@@ -21,66 +26,65 @@ import dedloc_amd.ops  # noqa: F401
 pytestmark = pytest.mark.multiproc
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _init(rank, world, port):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+def _init():
     torch.set_num_threads(1)
     import dedloc_amd.ops  # noqa: F401  (registers the dedloc:: operators)
-    from dedloc_amd.parallel import init_world
-
-    init_world(backend="gloo", device=torch.device("cpu"))
 
 
 # ----------------------------------------------------------------------------- fp16 small updates
-def _small_update_worker(rank, world, port, rounds, q):
+def _small_update_worker(rank, world, dht_ep, rounds, q):
     try:
-        _init(rank, world, port)
+        _init()
         from dedloc_amd.averaging.allreduce import GroupSpec, butterfly_allreduce
+        from dedloc_amd.dht import DHT
         from dedloc_amd.parallel import GroupCommunicators
 
-        comms = GroupCommunicators(timeout_s=60)
+        dht = DHT(initial_peers=[dht_ep], listen=False)
+        comms = GroupCommunicators(dht, "fp16", f"peer{rank}".encode(), torch.device("cpu"), timeout_s=60)
         g = torch.Generator().manual_seed(0)
         p = torch.randn(4096, generator=g) + 3.0  # same start on every peer
         p0 = p.clone()
         step = 2e-4 * p0.abs()                    # relative update 2e-4 (< half an fp16 ulp ~4.9e-4)
         own = (1.0 + 0.5 * rank) * step           # peers take different updates; expected mean of them
         grad = torch.randn(4096, generator=torch.Generator().manual_seed(rank + 1))
-        pg = comms.get(list(range(world)), 0)
-        spec = GroupSpec(ranks=list(range(world)), part_sizes=[2048, 2048], weights=[1.0, 3.0],
+        # what matchmaking would return to every member: the same member list and group id
+        members = [(f"peer{r}".encode(), {"backend": "gloo", "comms": []}) for r in range(world)]
+        comm, rank_of = comms.get(members, b"round-0")
+        spec = GroupSpec(ranks=[rank_of[m] for m, _ in members], part_sizes=[2048, 2048], weights=[1.0, 3.0],
                          contributes=[True, True], my_index=rank)
         g_avg = grad.clone()
-        butterfly_allreduce([g_avg], spec, "FLOAT16", pg=pg, timeout=30)
+        butterfly_allreduce([g_avg], spec, "FLOAT16", comm=comm, timeout=30)
         for _ in range(rounds):
             p += own
-            butterfly_allreduce([p], spec, "FLOAT16", pg=pg, timeout=30)
-        q.put({"rank": rank, "p": p, "p0": p0, "g_avg": g_avg, "grad": grad, "step": step})
+            butterfly_allreduce([p], spec, "FLOAT16", comm=comm, timeout=30)
+        # numpy: pickled by value (a torch tensor would be shared through an fd of this exiting process)
+        q.put({"rank": rank, "p": p.numpy(), "p0": p0.numpy(), "g_avg": g_avg.numpy(), "grad": grad.numpy(),
+               "step": step.numpy()})
         comms.close()
+        dht.shutdown()
     except Exception as e:  # noqa: BLE001
         q.put({"rank": rank, "error": repr(e)})
 
 
 @pytest.mark.timeout(240)
 def test_fp16_averaging_keeps_sub_ulp_parameter_updates():
+    from dedloc_amd.dht import DHT
+
     world, rounds = 2, 100
-    port = _free_port()
+    root = DHT(listen_on="127.0.0.1:*")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_small_update_worker, args=(r, world, port, rounds, q)) for r in range(world)]
+    procs = [ctx.Process(target=_small_update_worker, args=(r, world, root.endpoint, rounds, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda r: r["rank"])
     for p in procs:
         p.join(timeout=30)
+    root.shutdown()
     for r in res:
         assert "error" not in r, r
+        for k in ("p", "p0", "g_avg", "grad", "step"):
+            r[k] = torch.from_numpy(r[k])
     weights = torch.tensor([1.0, 3.0])
     # gradient round: weighted mean, fp16-accurate
     exp_g = (weights[0] * res[0]["grad"] + weights[1] * res[1]["grad"]) / weights.sum()
@@ -99,9 +103,9 @@ def test_fp16_averaging_keeps_sub_ulp_parameter_updates():
 
 
 # ----------------------------------------------------------------------------- stalled member
-def _stall_worker(rank, world, port, dht_ep, q):
+def _stall_worker(rank, world, barrier, dht_ep, q):
     try:
-        _init(rank, world, port)
+        _init()
         import dedloc_amd.averaging.averager as avg_mod
         from dedloc_amd.averaging.averager import DecentralizedAverager
         from dedloc_amd.dht import DHT
@@ -121,16 +125,14 @@ def _stall_worker(rank, world, port, dht_ep, q):
         x = torch.full((3000,), float(rank + 1))
         averager = DecentralizedAverager([x], dht, "stall", peer_id=f"peer{rank}".encode(), target_group_size=world,
                                          averaging_expiration=10.0, averaging_timeout=timeout, compression="NONE",
-                                         allow_state_sharing=False, rank=rank)
+                                         allow_state_sharing=False)
         results = []
         for rnd in range(2):
             x.fill_(float(rank + 1) * (rnd + 1))
-            # all peers enter each round together (the stalled one fails last); the world group
-            # is untouched by the failed round
-            torch.distributed.barrier()
+            # all peers enter each round together (the stalled one fails last)
+            barrier.wait(timeout=60)
             out = averager.step(weight=float(rank + 1), expected_group_size=world, key_suffix=f"_r{rnd}")
-            results.append({"ok": out is not None, "x": x.clone(), "epoch": averager.epoch,
-                            "size": None if out is None else out["size"]})
+            results.append({"ok": out is not None, "x": x.clone().numpy(), "size": None if out is None else out["size"]})
         q.put({"rank": rank, "results": results, "created": averager.comms.created,
                "aborted": averager.comms.aborted})
         averager.shutdown()
@@ -147,10 +149,10 @@ def test_stalled_member_aborts_round_and_next_round_is_exact():
 
     world = 3
     root = DHT(listen_on="127.0.0.1:*")
-    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_stall_worker, args=(r, world, port, root.endpoint, q)) for r in range(world)]
+    barrier = ctx.Barrier(world)
+    procs = [ctx.Process(target=_stall_worker, args=(r, world, barrier, root.endpoint, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda r: r["rank"])
@@ -159,10 +161,9 @@ def test_stalled_member_aborts_round_and_next_round_is_exact():
     root.shutdown()
     for r in res:
         assert "error" not in r, r["error"]
-    # round 0: the stall makes the round fail on every member, each aborts the epoch-0 communicator
+    # round 0: the stall makes the round fail on every member, each aborts its communicator
     for r in res:
         assert not r["results"][0]["ok"], r
-        assert r["results"][0]["epoch"] == 1
         assert r["aborted"] >= 1
     # round 1 runs on a fresh communicator and is the exact weighted mean of this round's tensors
     w = [1.0, 2.0, 3.0]
@@ -170,9 +171,10 @@ def test_stalled_member_aborts_round_and_next_round_is_exact():
     exp = sum(wi * vi for wi, vi in zip(w, vals)) / sum(w)
     for r in res:
         r1 = r["results"][1]
+        r1["x"] = torch.from_numpy(r1["x"])
         assert r1["ok"] and r1["size"] == world, r
         assert torch.allclose(r1["x"], torch.full_like(r1["x"], exp), rtol=0, atol=1e-5), (r["rank"], r1["x"][:4], exp)
-        assert r["created"] == 2  # epoch 0 and epoch 1
+        assert r["created"] == 2  # the aborted one and a fresh one
 
 
 def test_reduce_delta_cpu_contract():
@@ -187,3 +189,60 @@ def test_reduce_delta_cpu_contract():
     same = x[:1].expand(5, 101).contiguous()
     torch.ops.dedloc.reduce_delta(same, w, d)
     assert d.abs().max().item() == 0.0
+
+
+@pytest.mark.timeout(120)
+def test_comm_reuse_requires_every_member_to_hold_it():
+    """Peer "a" caches ONE communicator, "b" and "c" eight.  Rounds {a,b} -> {a,b,c} -> {a,b}: "a"
+    evicted the {a,b} communicator during round 2, "b" still holds it, so round 3 must agree on a
+    fresh one (and round 4 reuses that).  Threads stand in for processes (gloo ranks)."""
+    import threading
+
+    from dedloc_amd.averaging.allreduce import GroupSpec, butterfly_allreduce
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.parallel import GroupCommunicators
+
+    root = DHT(listen_on="127.0.0.1:*")
+    pids = [b"a", b"b", b"c"]
+    dhts = [DHT(initial_peers=[root.endpoint], listen=False) for _ in pids]
+    comms = {p: GroupCommunicators(d, "reuse", p, torch.device("cpu"), timeout_s=20, max_cached=1 if p == b"a" else 8)
+             for p, d in zip(pids, dhts)}
+    out, errors = {}, []
+
+    def member(p, members, infos, gid, val):
+        try:
+            comm, rank_of = comms[p].get([(m, infos[m]) for m in members], gid)
+            n = len(members)
+            sizes = [999 // n] * (n - 1) + [999 - 999 // n * (n - 1)]
+            x = torch.full((999,), val)
+            spec = GroupSpec(ranks=[rank_of[m] for m in members], part_sizes=sizes, weights=[1.0] * n,
+                             contributes=[True] * n, my_index=members.index(p))
+            butterfly_allreduce([x], spec, "NONE", comm=comm, timeout=20)
+            out[(gid, p)] = (x.mean().item(), comm)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    rounds = [[b"a", b"b"], [b"a", b"b", b"c"], [b"b", b"a"], [b"a", b"b"]]
+    for rnd, members in enumerate(rounds):
+        infos = {m: comms[m].announce() for m in members}
+        gid = f"group{rnd}".encode()
+        ts = [threading.Thread(target=member, args=(m, members, infos, gid, float(i + 1))) for i, m in enumerate(members)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not errors, errors
+        exp = (len(members) + 1) / 2
+        for m in members:
+            assert abs(out[(gid, m)][0] - exp) < 1e-6, (rnd, m, out[(gid, m)][0])
+    # round 3 ("b","a") could not reuse round 1's communicator: "a" had evicted it
+    assert out[(b"group2", b"b")][1] is not out[(b"group0", b"b")][1]
+    # round 4 reuses round 3's (both still hold it)
+    assert out[(b"group3", b"a")][1] is out[(b"group2", b"a")][1]
+    assert out[(b"group3", b"b")][1] is out[(b"group2", b"b")][1]
+    assert comms[b"a"].created == 3 and comms[b"b"].created == 3 and comms[b"a"].aborted == 2
+    for c in comms.values():
+        c.close()
+    for d in dhts:
+        d.shutdown()
+    root.shutdown()

@@ -1,9 +1,18 @@
-"""RCCL group-communicator plumbing on one GPU (a world of one rank, in a child process): member-only
-group creation without ncclCommSplit, batched P2P with host-polled completion (the path the
-butterfly uses), and abort of a group communicator — the NCCL-specific code the CPU/gloo
-multi-process tests cannot reach."""
+"""The native RCCL data plane (csrc/comm/rccl_comm.cpp, parallel/comm.py) on one GPU, in a child
+process with no torch.distributed world at all:
+
+* a communicator bootstrapped through the DHT by ``GroupCommunicators`` (the leader publishes the
+  unique id), non-blocking init polled to readiness, grouped send/recv (to itself: a one-rank
+  group) with host-polled completion, reuse of the cached communicator, abort;
+* a bootstrap whose second member never arrives is abandoned at the deadline (the host never
+  hangs in ncclCommInitRank) and the communicator is aborted;
+* a peer state download GPU-to-GPU: the RCCL path is requested first; two ranks on ONE device
+  are refused by RCCL, so on a one-GPU box the download must fall back to the TCP stream and still
+  deliver the exact tensors (on a multi-GPU node the RCCL path carries it).
+
+Multi-rank RCCL traffic between GPUs needs a multi-GPU node (the driver's scaling bench); the
+CPU/gloo multi-process tests cover the protocol with any number of ranks."""
 import os
-import socket
 import subprocess
 import sys
 import textwrap
@@ -14,48 +23,65 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = textwrap.dedent("""
-    import os, time, torch, torch.distributed as dist
+    import os, time, torch
+    import torch.distributed as dist
     import dedloc_amd.ops
-    from dedloc_amd.parallel import init_world, GroupCommunicators, abort_group
-    from dedloc_amd.averaging.allreduce import _run_p2p
-    rank, world, dev = init_world(force=True)
-    assert dist.get_backend() == "nccl" and dev.type == "cuda"
-    assert dist.distributed_c10d._get_default_group().bound_device_id is None
-    comms = GroupCommunicators(timeout_s=60)
-    pg = comms.get([0], 0)
-    assert dist.get_backend(pg) == "nccl"
-    src = torch.arange(1024, device=dev, dtype=torch.float16)
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.parallel import CommError, GroupCommunicators, RcclGroupComm, local_device, rccl_available
+    dev = local_device()
+    assert not dist.is_initialized()
+    assert rccl_available(dev), "the native RCCL data plane must be built into _C.so"
+    root = DHT(listen_on="127.0.0.1:*")
+    comms = GroupCommunicators(root, "rccl-test", b"solo", dev, timeout_s=60)
+    members = [(b"solo", comms.announce())]
+    assert members[0][1]["backend"] == "rccl"
+    comm, rank_of = comms.get(members, b"round-1")
+    assert comm.backend == "rccl" and rank_of == {b"solo": 0} and comms.created == 1
+    src = torch.arange(1 << 20, device=dev, dtype=torch.float16)
     dst = torch.zeros_like(src)
-    _run_p2p([dist.P2POp(dist.isend, src, 0, group=pg), dist.P2POp(dist.irecv, dst, 0, group=pg)],
-             time.monotonic() + 30, pg)
+    comm.p2p([src], [0], [dst], [0], time.monotonic() + 30)
     torch.cuda.synchronize()
     assert torch.equal(src, dst)
-    assert comms.get([0], 0) is pg and comms.created == 1
-    comms.invalidate([0], 0)
-    assert comms.aborted == 1
-    pg2 = comms.get([0], 1)
-    dst.zero_()
-    _run_p2p([dist.P2POp(dist.isend, src, 0, group=pg2), dist.P2POp(dist.irecv, dst, 0, group=pg2)],
-             time.monotonic() + 30, pg2)
-    torch.cuda.synchronize()
-    assert torch.equal(src, dst) and comms.created == 2
-    comms.close()
-    dist.destroy_process_group()
-    print("RCCL_GROUP_OK", flush=True)
+    # the next round announces the token and reuses the communicator
+    members = [(b"solo", comms.announce())]
+    comm2, _ = comms.get(members, b"round-2")
+    assert comm2 is comm and comms.created == 1
+    comms.invalidate(comm)
+    assert comms.aborted == 1 and not comm.alive
+    # a member that never shows up: the bootstrap is abandoned at the deadline
+    uid = RcclGroupComm.new_unique_id()
+    t0 = time.monotonic()
+    try:
+        RcclGroupComm.create(uid, 2, 0, dev, time.monotonic() + 5.0)
+        raise SystemExit("a 2-rank communicator came up with one rank")
+    except CommError as e:
+        waited = time.monotonic() - t0
+        assert waited < 30, waited
+        print("abandoned bootstrap after", round(waited, 2), "s:", e, flush=True)
+    assert torch.ops.dedloc_comm.comm_count() == 0
+    # state download on one GPU (RCCL refused for two ranks on one device -> TCP fallback)
+    from dedloc_amd.averaging.averager import DecentralizedAverager
+    x = torch.randn(3_000_000, device=dev)
+    m = torch.randn(3_000_000, device=dev)
+    donor = DecentralizedAverager([x, m], root, "rccl-test", peer_id=b"donor", device=dev,
+                                  listen_on="127.0.0.1:*")
+    donor.publish_state_sharing(5)
+    rx = DecentralizedAverager([torch.zeros_like(x), torch.zeros_like(m)], root, "rccl-test", peer_id=b"rx",
+                               device=dev, listen_on="127.0.0.1:*", allow_state_sharing=False)
+    meta, tensors = rx.load_state_from_peers(timeout=30)
+    assert meta["step"] == 5
+    assert torch.equal(tensors[0].to(dev), x) and torch.equal(tensors[1].to(dev), m)
+    print("download", rx.last_download, flush=True)
+    donor.shutdown(); rx.shutdown(); comms.close(); root.shutdown()
+    print("RCCL_NATIVE_OK", flush=True)
 """)
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-@pytest.mark.timeout(180)
-def test_rccl_group_communicator_lifecycle(cuda):
-    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-               MASTER_PORT=str(_port()), PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-c", CHILD], cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
-    assert r.returncode == 0 and "RCCL_GROUP_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+@pytest.mark.timeout(240)
+def test_native_rccl_group_comm_lifecycle(cuda):
+    env = dict(os.environ, PYTHONPATH=ROOT, LOCAL_RANK="0")
+    for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", CHILD], cwd=ROOT, env=env, capture_output=True, text=True, timeout=220)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0 and "RCCL_NATIVE_OK" in r.stdout, (r.stdout[-3000:], r.stderr[-5000:])
