@@ -1,39 +1,41 @@
 #!/usr/bin/env python
 """Single-node collaboration launcher — the MI355X stand-in for ``albert/AWS_runner.ipynb`` (SURVEY.md
 §2.1 D9): one coordinator (DHT root + metrics aggregation, ``run_first_peer``), N GPU trainer peers and
-A auxiliary peers, all on one node, with the AWS fleet's heterogeneity injected per rank.
+A auxiliary peers, with the AWS fleet's heterogeneity injected per peer slot and its spot churn
+(preemption + the respawn loop of ``AWS_runner.ipynb:342-370``) reproduced at process level.
 
-    python -m dedloc_amd.cli.launch_collaboration --n_trainers 8 --fleet aws --duration 600 \\
+    python -m dedloc_amd.cli.launch_collaboration --n_trainers 8 --n_aux 4 --fleet aws --duration 600 \\
+        --kill_schedule 120:3,300:5 --respawn --respawn_delay 30 \\
         --experiment_prefix albert -- --per_device_train_batch_size 32 --target_batch_size 4096
 
-Everything after ``--`` is passed to every trainer (and aux peer).  Trainers and aux peers share one
-torch.distributed world (the data plane: RCCL over xGMI), trainer i on GPU i, aux peer j on GPU
-``n_trainers + j`` (the reference used CPU aux instances; here they are reducer-only processes on
-spare GPUs: an RCCL communicator cannot hold two ranks on one device, so trainers + aux peers must
-not exceed the node's GPUs).
-The coordinator is not part of the world (it only reads metrics and downloads state over TCP).
+Everything after ``--`` is passed to every trainer (and aux peer).  There is no launch-time world:
+every peer is an independent process that bootstraps from the coordinator's DHT and averages over
+communicators its matchmade groups build themselves (``parallel/comm.py``), so a killed trainer can
+be replaced by a brand-new process (new peer id) that downloads the state and joins the next round.
+
+* trainer i runs on GPU i (``LOCAL_RANK=i``, also its heterogeneity slot), or on the CPU with
+  ``--cpu`` (plumbing / tests);
+* auxiliary peers run on the CPU by default, like the reference's ``r5.large`` aux instances
+  (``AWS_runner.ipynb:30, 186-217``): they need no spare GPU; a round that contains one runs over
+  gloo.  ``--aux_device gpu`` puts them on GPUs ``n_trainers..`` instead;
+* ``--kill_schedule T:i[,T:i...]`` SIGKILLs trainer i T seconds after launch (a spot preemption: no
+  clean-up, no tombstone); with ``--respawn`` every trainer that dies is restarted as a fresh process
+  in its slot after ``--respawn_delay`` seconds.  Events go to ``launcher_events.jsonl``.
+
 This process never touches the GPU itself; children are plain subprocesses.
 """
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import signal
-import socket
 import subprocess
 import sys
 import time
 from pathlib import Path
 
 from ..emulation.heterogeneity import aws_fleet_profiles
-
-
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 def fleet_flags(fleet: str, n: int, client_every: int = 0):
@@ -45,6 +47,33 @@ def fleet_flags(fleet: str, n: int, client_every: int = 0):
             "--peer_client_mode", ",".join(str(int(p.client_mode)) for p in profs)]
 
 
+def parse_kill_schedule(spec):
+    out = []
+    for item in (spec or "").split(","):
+        if item.strip():
+            t, slot = item.split(":")
+            out.append((float(t), int(slot)))
+    return sorted(out)
+
+
+class _Proc:
+    def __init__(self, name, cmd, env, log_dir: Path, generation: int):
+        self.name, self.cmd, self.env, self.generation = name, cmd, env, generation
+        self.log_path = log_dir / (f"{name}.log" if generation == 0 else f"{name}.gen{generation}.log")
+        self.f = open(self.log_path, "w")
+        self.p = subprocess.Popen(cmd, stdout=self.f, stderr=subprocess.STDOUT, env=env, start_new_session=True)
+
+    def alive(self):
+        return self.p.poll() is None
+
+    def kill(self, sig=signal.SIGKILL):
+        if self.alive():
+            try:
+                os.killpg(self.p.pid, sig)
+            except ProcessLookupError:
+                pass
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     extra = []
@@ -54,12 +83,17 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--n_trainers", type=int, default=8)
     ap.add_argument("--n_aux", type=int, default=0)
-    ap.add_argument("--n_gpus", type=int, default=None,
-                    help="GPUs on this node (default: n_trainers + n_aux, one per peer)")
+    ap.add_argument("--n_gpus", type=int, default=None, help="GPUs on this node (default: one per GPU peer)")
+    ap.add_argument("--cpu", action="store_true", help="run the trainers on the CPU (plumbing / tests)")
+    ap.add_argument("--aux_device", choices=["cpu", "gpu"], default="cpu")
     ap.add_argument("--experiment_prefix", default="albert")
+    ap.add_argument("--model_config_path", default=None, help="model config for the coordinator's replica")
     ap.add_argument("--fleet", choices=["uniform", "aws"], default="uniform")
     ap.add_argument("--client_every", type=int, default=0, help="every k-th trainer runs in client mode")
     ap.add_argument("--duration", type=float, default=None, help="stop everything after this many seconds")
+    ap.add_argument("--kill_schedule", default=None, help="T:slot[,T:slot...] — SIGKILL trainer `slot` at T s")
+    ap.add_argument("--respawn", action="store_true", help="restart dead trainers as fresh processes")
+    ap.add_argument("--respawn_delay", type=float, default=30.0)
     ap.add_argument("--log_dir", default="collab_logs")
     ap.add_argument("--sahajbert", action="store_true")
     ap.add_argument("--no_coordinator", action="store_true")
@@ -70,74 +104,112 @@ def main(argv=None):
     py = sys.executable
     env0 = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
                 PYTHONUNBUFFERED="1")
-    procs = []
+    for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE", "GROUP_RANK"):
+        env0.pop(k, None)
+    events = open(log_dir / "launcher_events.jsonl", "a")
+    t_start = time.time()
 
-    def spawn(cmd, log, env):
-        f = open(log_dir / log, "w")
-        p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, env=env, start_new_session=True)
-        procs.append((p, f, log))
-        return p
+    def event(kind, **kw):
+        events.write(json.dumps(dict(kind=kind, t=round(time.time() - t_start, 3), **kw)) + "\n")
+        events.flush()
+        print(f"[launcher +{time.time() - t_start:7.1f}s] {kind} {kw}", flush=True)
+
+    others = []
 
     # 1. coordinator (DHT root)
-    if args.no_coordinator:
-        root = None
-    else:
-        spawn([py, "-m", "dedloc_amd.cli.run_first_peer", "--experiment_prefix", args.experiment_prefix,
+    root = None
+    if not args.no_coordinator:
+        cmd = [py, "-m", "dedloc_amd.cli.run_first_peer", "--experiment_prefix", args.experiment_prefix,
                "--dht_listen_on", "0.0.0.0:*", "--refresh_period", str(args.coordinator_refresh),
                "--metrics_file", str(log_dir / "coordinator_metrics.jsonl"),
-               *(["--max_runtime", str(args.duration)] if args.duration else [])], "coordinator.log", env0)
-        root = None
+               *(["--model_config_path", args.model_config_path] if args.model_config_path else []),
+               *(["--max_runtime", str(args.duration)] if args.duration else [])]
+        coord = _Proc("coordinator", cmd, env0, log_dir, 0)
+        others.append(coord)
         t0 = time.time()
         while root is None and time.time() - t0 < 300:
             time.sleep(0.5)
-            for line in (log_dir / "coordinator.log").read_text().splitlines():
+            for line in coord.log_path.read_text().splitlines():
                 if line.startswith("Running DHT root at"):
                     root = line.split()[-1]
+            if not coord.alive():
+                break
         if root is None:
-            raise RuntimeError("coordinator did not start; see coordinator.log")
-        print(f"coordinator DHT root at {root}", flush=True)
+            raise RuntimeError(f"coordinator did not start; see {coord.log_path}")
+        event("coordinator", dht_root=root)
 
-    # 2. trainer + aux world
-    world = args.n_trainers + args.n_aux
-    n_gpus = args.n_gpus or world
-    if world > n_gpus:
-        raise SystemExit(f"{args.n_trainers} trainers + {args.n_aux} aux peers need {world} GPUs (one RCCL rank per "
-                         f"device), the node has {n_gpus}")
-    port = _free_port()
+    # 2. peers
+    n_gpu_peers = (0 if args.cpu else args.n_trainers) + (args.n_aux if args.aux_device == "gpu" else 0)
+    n_gpus = args.n_gpus if args.n_gpus is not None else n_gpu_peers
+    if n_gpu_peers > n_gpus:
+        raise SystemExit(f"{n_gpu_peers} GPU peers need {n_gpu_peers} GPUs (one RCCL rank per device), the node has "
+                         f"{n_gpus}; run auxiliary peers on the CPU (--aux_device cpu)")
     common = ["--experiment_prefix", args.experiment_prefix, *(["--initial_peers", root] if root else [])]
     common += fleet_flags(args.fleet, args.n_trainers, args.client_every) + extra
-    for r in range(world):
-        aux = r >= args.n_trainers
-        env = dict(env0, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
-        mod = "dedloc_amd.cli.run_aux" if aux else "dedloc_amd.cli.run_trainer"
-        cmd = [py, "-m", mod, *common, *(["--sahajbert"] if args.sahajbert and not aux else [])]
-        spawn(cmd, f"{'aux' if aux else 'trainer'}{r}.log", env)
+
+    def trainer_cmd(slot):
+        dev = ["--device", "cpu"] if args.cpu else []
+        return [py, "-m", "dedloc_amd.cli.run_trainer", *common, *dev, *(["--sahajbert"] if args.sahajbert else [])]
+
+    trainers = {}
+    for r in range(args.n_trainers):
+        trainers[r] = _Proc(f"trainer{r}", trainer_cmd(r), dict(env0, LOCAL_RANK=str(r)), log_dir, 0)
+        event("start", slot=r, pid=trainers[r].p.pid, generation=0)
+    for j in range(args.n_aux):
+        on_gpu = args.aux_device == "gpu"
+        env = dict(env0, LOCAL_RANK=str(args.n_trainers + j if on_gpu else 0))
+        cmd = [py, "-m", "dedloc_amd.cli.run_aux", *common, *([] if on_gpu else ["--device", "cpu"])]
+        others.append(_Proc(f"aux{j}", cmd, env, log_dir, 0))
+        event("start_aux", index=j, device="gpu" if on_gpu else "cpu")
     print(f"launched {args.n_trainers} trainers + {args.n_aux} aux peers; logs in {log_dir}", flush=True)
 
-    # 3. supervise: stop at duration, or when every trainer has exited
-    t0 = time.time()
+    # 3. supervise: scripted preemptions, respawn loop, stop at duration / when all trainers finished
+    kills = parse_kill_schedule(args.kill_schedule)
+    respawn_at = {}
     rc = 0
     try:
         while True:
-            time.sleep(1.0)
-            trainers = [p for p, _, log in procs if log.startswith("trainer")]
-            if all(p.poll() is not None for p in trainers):
-                rc = max((p.returncode or 0) for p in trainers)
+            time.sleep(0.2)
+            now = time.time() - t_start
+            while kills and kills[0][0] <= now:
+                _, slot = kills.pop(0)
+                proc = trainers.get(slot)
+                if proc is not None and proc.alive():
+                    proc.kill(signal.SIGKILL)
+                    event("kill", slot=slot, pid=proc.p.pid, generation=proc.generation)
+            for slot, proc in trainers.items():
+                if proc.alive() or slot in respawn_at:
+                    continue
+                code = proc.p.returncode
+                finished = code == 0
+                if args.respawn and not finished:
+                    respawn_at[slot] = now + args.respawn_delay
+                    event("died", slot=slot, returncode=code, respawn_in=args.respawn_delay)
+            for slot, t in list(respawn_at.items()):
+                if t <= now:
+                    del respawn_at[slot]
+                    gen = trainers[slot].generation + 1
+                    trainers[slot].f.close()
+                    trainers[slot] = _Proc(f"trainer{slot}", trainer_cmd(slot), dict(env0, LOCAL_RANK=str(slot)),
+                                           log_dir, gen)
+                    event("respawn", slot=slot, pid=trainers[slot].p.pid, generation=gen)
+            if not respawn_at and not kills and all(not p.alive() for p in trainers.values()):
+                rc = max((p.p.returncode or 0) for p in trainers.values())
                 break
-            if args.duration is not None and time.time() - t0 > args.duration:
+            if args.duration is not None and now > args.duration:
                 break
     finally:
-        for p, f, _ in procs:
-            if p.poll() is None:
-                os.killpg(p.pid, signal.SIGTERM)
+        for proc in list(trainers.values()) + others:
+            proc.kill(signal.SIGTERM)
         deadline = time.time() + 30
-        for p, f, _ in procs:
+        for proc in list(trainers.values()) + others:
             try:
-                p.wait(timeout=max(0.1, deadline - time.time()))
+                proc.p.wait(timeout=max(0.1, deadline - time.time()))
             except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
-            f.close()
+                proc.kill(signal.SIGKILL)
+            proc.f.close()
+        event("stop")
+        events.close()
     return rc
 
 

@@ -11,9 +11,12 @@ Grammar (``--churn_schedule``): comma-separated events ``[MODE@]AT[s]:DURATION``
                ``restart``: like a preempted spot instance that is respawned — the peer also DROPS
                its parameters, optimizer state and step counter and must download them on return.
 
-Example: ``leave@5:20,restart@120s:30``.  Process-level kill/respawn (``AWS_runner.ipynb:342-370``)
-is provided by the launcher (``cli/launch_collaboration.py``) for peers that do not share a
-communicator; inside one RCCL world a dead rank cannot rejoin, so ``restart`` is the in-world form.
+Example: ``leave@5:20,restart@120s:30``.  These are IN-PROCESS events.  Real process-level churn
+— a SIGKILLed trainer (spot preemption, no clean-up) replaced by a brand-new process with a new
+peer id, the reference's respawn loop (``AWS_runner.ipynb:342-370``) — is the launcher's
+``--kill_schedule`` / ``--respawn`` (``cli/launch_collaboration.py``; tested in
+``tests/test_launcher_churn.py``).  Both work because no peer belongs to a launch-time world: every
+averaging group builds its communicators through the DHT (``parallel/comm.py``).
 """
 from __future__ import annotations
 

@@ -190,6 +190,9 @@ class CollaborativeOptimizer:
             self.update_scheduler()
             self.stats["state_loads"] += 1
             self.averager.publish_state_sharing(self.local_step)
+        dl = self.averager.last_download or {}
+        logger.warning(f"downloaded state from peers: step {self.local_step}, {dl.get('bytes', 0) / 2**20:.0f} MiB in "
+                       f"{dl.get('seconds', 0.0):.2f}s over {'RCCL' if dl.get('mode') == 'R' else 'TCP'}")
         return True
 
     def _reset_accumulators(self):
