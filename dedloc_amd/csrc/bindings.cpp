@@ -621,14 +621,49 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
 // first call writes them (beta = 0), later calls accumulate (beta = 1) — and are added into the
 // gradient once, by the last call.  That replaces 24 slab-sum passes per weight and micro-step
 // by one.  Without the split form (no hipBLASLt plan, one slice) every call accumulates directly.
-at::Tensor& shared_slabs(const at::Tensor& c, int64_t S) {
-  static std::mutex mu;
-  static std::unordered_map<const void*, at::Tensor> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  at::Tensor& t = cache[c.data_ptr()];
-  if (!t.defined() || t.size(0) != S || t.size(1) != c.size(0) || t.size(2) != c.size(1) || t.device() != c.device())
-    t = at::empty({S, c.size(0), c.size(1)}, c.options());
-  return t;
+// The slab workspace of one gradient tensor lives from the first to the last call of a micro-step,
+// so it is keyed by the gradient (pointer, device, shape, split count).  The cache is bounded: when a
+// new key would exceed kMaxSlabSets entries (gradient buffers re-allocated, several models in one
+// process), the least recently used workspace is freed; `dedloc_ws::clear_workspaces()` frees all.
+struct SlabKey {
+  const void* ptr;
+  int64_t dev, S, M, N;
+  bool operator==(const SlabKey& o) const {
+    return ptr == o.ptr && dev == o.dev && S == o.S && M == o.M && N == o.N;
+  }
+};
+struct SlabKeyHash {
+  size_t operator()(const SlabKey& k) const {
+    return std::hash<const void*>()(k.ptr) ^ (size_t)(k.S * 1000003 + k.M * 10007 + k.N * 31 + k.dev);
+  }
+};
+constexpr size_t kMaxSlabSets = 16;
+std::mutex g_slab_mu;
+std::unordered_map<SlabKey, std::pair<at::Tensor, uint64_t>, SlabKeyHash> g_slabs;
+uint64_t g_slab_clock = 0;
+
+at::Tensor shared_slabs(const at::Tensor& c, int64_t S) {
+  std::lock_guard<std::mutex> lock(g_slab_mu);
+  const SlabKey key{c.data_ptr(), (int64_t)c.get_device(), S, c.size(0), c.size(1)};
+  auto it = g_slabs.find(key);
+  if (it == g_slabs.end()) {
+    while (g_slabs.size() >= kMaxSlabSets) {
+      auto lru = g_slabs.begin();
+      for (auto j = g_slabs.begin(); j != g_slabs.end(); ++j)
+        if (j->second.second < lru->second.second) lru = j;
+      g_slabs.erase(lru);
+    }
+    it = g_slabs.emplace(key, std::make_pair(at::empty({S, c.size(0), c.size(1)}, c.options()), 0)).first;
+  }
+  it->second.second = ++g_slab_clock;
+  return it->second.first;
+}
+
+int64_t clear_workspaces() {
+  std::lock_guard<std::mutex> lock(g_slab_mu);
+  const int64_t n = (int64_t)g_slabs.size();
+  g_slabs.clear();
+  return n;
 }
 
 void gemm_acc_f32_shared(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b,
@@ -638,7 +673,7 @@ void gemm_acc_f32_shared(const at::Tensor& a, const at::Tensor& b, at::Tensor c,
     DlLtArgs l = lt_args(a, b, trans_a, trans_b);
     const int S = wgrad_splits(l.M, l.N, l.K, 8);
     if (S > 1) {
-      at::Tensor& slabs = shared_slabs(c, S);
+      at::Tensor slabs = shared_slabs(c, S);
       const long kslice = l.K / S;
       l.K = (int)kslice;
       l.batch = S;
@@ -1088,3 +1123,5 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
 
 // a tiny C entry point so that the loader can verify the library really is the gfx950 build
 extern "C" int dedloc_amd_native_abi_version() { return 1; }
+
+TORCH_LIBRARY(dedloc_ws, m) { m.def("clear_workspaces() -> int", &clear_workspaces); }

@@ -108,17 +108,30 @@ def add_layernorm(x, res, gamma, beta, ggamma=None, gbeta=None, eps=1e-12):
 
 
 _LOG2E = math.log2(math.e)
-_BMM_OUT_F32 = True  # torch.bmm(..., out_dtype=float32) available (bf16 in, fp32 out)
+_BMM_OUT_F32 = None  # torch.bmm(..., out_dtype=float32) supported for bf16 on this build? (probed once)
+
+
+def _bmm_out_f32_supported(device) -> bool:
+    """One tiny probe: only an unsupported-signature/dtype error disables the bf16-in / fp32-out
+    path; errors of real calls (an OutOfMemoryError on the [B*H, S, S] scores) propagate."""
+    global _BMM_OUT_F32
+    if _BMM_OUT_F32 is None:
+        x = torch.zeros(1, 2, 2, dtype=torch.bfloat16, device=device)
+        try:
+            _BMM_OUT_F32 = torch.bmm(x, x, out_dtype=torch.float32).dtype == torch.float32
+        except (TypeError, NotImplementedError):
+            _BMM_OUT_F32 = False
+        except RuntimeError as e:
+            if isinstance(e, torch.OutOfMemoryError):
+                raise
+            _BMM_OUT_F32 = False
+    return _BMM_OUT_F32
 
 
 def _bmm_f32(a, b):
     """[N, M, K] x [N, K, P] bf16 -> fp32 without rounding the product through bf16."""
-    global _BMM_OUT_F32
-    if a.is_cuda and _BMM_OUT_F32:
-        try:
-            return torch.bmm(a, b, out_dtype=torch.float32)
-        except (RuntimeError, TypeError):
-            _BMM_OUT_F32 = False
+    if a.is_cuda and _bmm_out_f32_supported(a.device):
+        return torch.bmm(a, b, out_dtype=torch.float32)
     return torch.bmm(a.float(), b.float())
 
 

@@ -296,6 +296,10 @@ class CollaborativeOptimizer:
         step per global step, +12.5% samples at 8 local steps), and with more peers the others' stale
         counts only ever delay, never advance, the step."""
         cs = self.collaboration_state
+        if cs.optimizer_step > self.local_step:
+            # we are behind: our samples belong to an older step and must not count toward this
+            # one (the resynchronisation rule handles a peer that is behind)
+            return False
         total = cs.samples_accumulated - cs.own_samples + self.local_samples_accumulated
         return total >= self.target_batch_size
 

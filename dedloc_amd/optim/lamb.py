@@ -29,6 +29,10 @@ class _FlatOptimizer:
         self.tables = flat.chunk_table(chunk, weight_decay_of)
         self.norms = torch.zeros(2 * len(flat.names), dtype=torch.float32, device=flat.device)
         self.step_count = 0
+        self.no_decay = set()
+
+    def _is_no_decay(self, name: str) -> bool:
+        return name in self.no_decay
 
     @property
     def lr(self) -> float:
@@ -49,6 +53,7 @@ class FusedLamb(_FlatOptimizer):
         wd = {n: (0.0 if n in no_decay else weight_decay) for n in flat.names}
         super().__init__(flat, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
                                     clamp_value=clamp_value, debias=debias, adam=adam), wd)
+        self.no_decay = no_decay
         self.exp_avg = torch.zeros_like(flat.fp32)
         self.exp_avg_sq = torch.zeros_like(flat.fp32)
 
@@ -73,9 +78,12 @@ class FusedLamb(_FlatOptimizer):
 
     def _groups(self) -> List[List[int]]:
         """Flat indices of the reference's parameter groups, in its order: decayed first, then the
-        no-decay group (albert/run_trainer.py:74-84); inside a group, model (flat) order."""
-        return [[i for i, n in enumerate(self.flat.names) if self.weight_decay_of[n] == wd_val]
-                for wd_val in sorted(set(self.weight_decay_of.values()), reverse=True)]
+        no-decay group (albert/run_trainer.py:74-84); inside a group, model (flat) order.  Membership
+        follows the no-decay NAME rule, not the weight-decay value, so the two groups exist even at
+        weight_decay = 0 (a reference optimizer.pt always has two)."""
+        nd = [self._is_no_decay(n) for n in self.flat.names]
+        groups = [[i for i, f in enumerate(nd) if not f], [i for i, f in enumerate(nd) if f]]
+        return [g for g in groups if g]
 
     def state_dict(self) -> Dict:
         m, v = self._per_param(self.exp_avg), self._per_param(self.exp_avg_sq)
@@ -129,6 +137,7 @@ class FusedLarcSGD(_FlatOptimizer):
         wd = {n: (0.0 if n in no_decay else weight_decay) for n in flat.names}
         super().__init__(flat, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov,
                                     trust_coefficient=trust_coefficient, clip=clip, eps=eps), wd)
+        self.no_decay = no_decay
         self.momentum_buffer = torch.zeros_like(flat.fp32)
 
     @torch.no_grad()

@@ -143,3 +143,24 @@ def test_single_peer_steps_exactly_at_target(start):
         co.shutdown()
     finally:
         dht.shutdown()
+
+
+def test_lamb_weight_decay_zero_keeps_two_groups():
+    """at weight_decay = 0 the groups must still be [decayed, no_decay] (by name), so a
+    reference / HF optimizer.pt (always two groups) loads and our state_dict has the same layout."""
+    named_t = _params()
+    decay = [p for n, p in named_t if n not in NO_DECAY]
+    no_decay = [p for n, p in named_t if n in NO_DECAY]
+    topt = torch.optim.Adam([{"params": decay, "weight_decay": 0.0}, {"params": no_decay, "weight_decay": 0.0}],
+                            lr=3e-3)
+    for _, p in named_t:
+        p.grad = torch.randn_like(p)
+    topt.step()
+    flat = FlatParams(_params(), with_bf16=False)
+    opt = FusedLamb(flat, lr=1e-3, weight_decay=0.0, no_decay=NO_DECAY)
+    sd = opt.state_dict()
+    assert [len(g["params"]) for g in sd["param_groups"]] == [3, 2]
+    opt.load_state_dict(topt.state_dict())  # must not raise a group-size mismatch
+    by_name = {n: topt.state[p] for n, p in named_t}
+    for n in flat.names:
+        torch.testing.assert_close(flat.view(opt.exp_avg, n), by_name[n]["exp_avg"])
