@@ -122,7 +122,8 @@ def is_sop_dataset(path: Optional[str]) -> bool:
 
 class DiskSOPStream:
     """Infinite, per-peer shuffled device batches from a ``build_dataset`` directory, padded to the
-    batch's longest row and MLM-masked like ``DataCollatorForLanguageModeling`` (labels [B, S] form)."""
+    batch's longest row and MLM-masked like ``DataCollatorForLanguageModeling`` (labels [B, S] form,
+    plus the equivalent fixed-shape ``mlm_positions`` / ``mlm_labels`` the model consumes sync-free)."""
 
     def __init__(self, path: str, batch_size: int, seed: int = 0, device="cpu", mlm_probability: float = 0.15):
         import datasets
@@ -177,8 +178,29 @@ def collate_mlm(rows: Dict[str, List], meta: Dict[str, int], gen: torch.Generato
     ids = torch.where(to_rand, torch.randint(meta["vocab_size"], (B, L), generator=gen), ids)
     batch = {"input_ids": ids, "token_type_ids": tt, "attention_mask": am, "labels": labels,
              "sentence_order_label": torch.tensor(rows["sentence_order_label"], dtype=torch.long)}
+    batch.update(mlm_targets(picked, labels))
     dev = torch.device(device) if device is not None else torch.device("cpu")
     return {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
+
+
+def mlm_targets(picked: torch.Tensor, labels: torch.Tensor, multiple: int = 8) -> Dict[str, torch.Tensor]:
+    """HF ``labels`` [B, L] -> fixed-shape ``mlm_positions`` / ``mlm_labels`` [B, P] (-100 pads), computed
+    on the HOST while collating, so the model's MLM head gathers its rows on the device without a
+    ``nonzero`` (a host synchronisation per micro-step).  P = the batch's largest masked count rounded
+    up to ``multiple`` (few distinct shapes)."""
+    counts = picked.sum(1)
+    P = max(1, int(counts.max()) if counts.numel() else 1)
+    P = (P + multiple - 1) // multiple * multiple
+    B, L = picked.shape
+    # stable sort puts each row's picked positions first, in order
+    order = torch.sort((~picked).to(torch.int8), dim=1, stable=True).indices
+    if P > L:
+        order = torch.cat([order, torch.zeros(B, P - L, dtype=order.dtype)], 1)
+    order = order[:, :P]
+    valid = torch.arange(P)[None, :] < counts[:, None]
+    pos = torch.where(valid, order, torch.zeros_like(order))
+    lab = torch.where(valid, labels.gather(1, pos), torch.full_like(pos, -100))
+    return {"mlm_positions": pos, "mlm_labels": lab}
 
 
 class StreamingSOPStream:

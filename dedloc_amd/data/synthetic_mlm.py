@@ -12,7 +12,10 @@ by default (``length_mode="wikitext"`` adds the short document-tail instances).
 Two masking forms:
   * ``fixed`` — exactly round(0.15 * n_real) positions per sequence, returned as fixed-shape
     ``mlm_positions``/``mlm_labels`` (BERT's max_predictions_per_seq form; graph-capturable);
-  * ``hf`` — Bernoulli(0.15) per token, returned as HF ``labels`` [B, S] with -100 elsewhere.
+  * ``hf`` — Bernoulli(0.15) per token, returned as HF ``labels`` [B, S] with -100 elsewhere AND as
+    ``mlm_positions``/``mlm_labels`` [B, P_hf] so the model needs no ``nonzero`` (host sync).  P_hf is
+    the mean + 6 sigma of the per-row count (128 at S = 512); a row drawing more (p < 1e-9) keeps
+    its first P_hf picks and leaves the rest unmasked, so labels and positions always agree.
 """
 from __future__ import annotations
 
@@ -35,6 +38,8 @@ class SyntheticSOPStream:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seed) % (2 ** 63))
         self.P = max(1, round(self.p * (seq_len - 3)))
+        sd = (seq_len * self.p * (1 - self.p)) ** 0.5
+        self.P_hf = min(seq_len, int(-(-(self.p * seq_len + 6 * sd) // 8) * 8))
 
     def __iter__(self) -> Iterator[Dict[str, torch.Tensor]]:
         return self
@@ -97,11 +102,18 @@ class SyntheticSOPStream:
     def _mask_hf(self, ids, special):
         prob = torch.full(ids.shape, self.p, device=self.device).masked_fill(special.bool(), 0.0)
         masked = torch.bernoulli(prob, generator=self.gen).bool()
+        P = self.P_hf
+        order = torch.sort((~masked).to(torch.int8), dim=1, stable=True).indices[:, :P]  # picks first
+        valid = torch.arange(P, device=self.device)[None, :] < masked.sum(1, keepdim=True)
+        masked = torch.zeros_like(masked).scatter_(1, order, valid) & masked  # cap at P picks per row
+        pos = torch.where(valid, order, torch.zeros_like(order))
+        mlm_labels = torch.where(valid, torch.gather(ids, 1, pos), torch.full_like(pos, -100))
         labels = torch.where(masked, ids, torch.full_like(ids, -100))
         r = torch.rand(ids.shape, generator=self.gen, device=self.device)
         rnd = self._rand(*ids.shape, high=self.V - FIRST_REGULAR_ID) + FIRST_REGULAR_ID
         new = torch.where(r < 0.8, torch.full_like(ids, MASK_ID), torch.where(r < 0.9, rnd, ids))
-        return {"input_ids": torch.where(masked, new, ids), "labels": labels}
+        return {"input_ids": torch.where(masked, new, ids), "labels": labels, "mlm_positions": pos,
+                "mlm_labels": mlm_labels}
 
 
 def peer_seed(local_public_key: bytes, base_seed: int = 0) -> int:
