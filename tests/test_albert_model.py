@@ -123,7 +123,7 @@ def _train_curve(impl, cfg_dir, device, steps, init_sd):
 
     targs = AlbertTrainingArguments(per_device_train_batch_size=16, gradient_accumulation_steps=1, seq_length=128,
                                     warmup_steps=10, max_steps=10 ** 6, learning_rate=1.76e-3, save_steps=0,
-                                    output_dir=f"/tmp/dedloc_curve_{os.getpid()}_{impl}", seed=7, perf_timers=False)
+                                    output_dir=f"/tmp/dedloc_curve_{os.getpid()}_{impl}", seed=7)
     dargs = DatasetArguments(config_path=cfg_dir, mask_mode="hf")
     root = DHT(listen_on="127.0.0.1:*")
     cargs = CollaborationArguments(experiment_prefix=f"curve_{impl}", initial_peers=[root.endpoint],
