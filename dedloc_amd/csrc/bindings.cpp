@@ -900,6 +900,68 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
           ws.narrow(0, 2 * G * C + C, C)};
 }
 
+// ------------------------------------------------------------------ pools and head normalisation (pool.hip)
+std::tuple<at::Tensor, at::Tensor> maxpool_fwd(const at::Tensor& x) {
+  expect_nhwc(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t P = (H - 1) / 2 + 1, Q = (W - 1) / 2 + 1;
+  auto y = at::empty({N, C, P, Q}, x.options(), at::MemoryFormat::ChannelsLast);
+  auto arg = at::empty({N, C, P, Q}, x.options().dtype(at::kByte), at::MemoryFormat::ChannelsLast);
+  check(dl_maxpool_fwd(cbf(x), bf(y), arg.data_ptr<uint8_t>(), (int)N, (int)H, (int)W, (int)C, (int)P, (int)Q,
+                       cur_stream(x)),
+        "maxpool_fwd");
+  return {y, arg};
+}
+
+at::Tensor maxpool_bwd(const at::Tensor& dy_in, const at::Tensor& arg, int64_t H, int64_t W) {
+  const at::Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  expect_nhwc(dy, "dy");
+  TORCH_CHECK(arg.sizes() == dy.sizes() && arg.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_bwd: arg");
+  const int64_t N = dy.size(0), C = dy.size(1), P = dy.size(2), Q = dy.size(3);
+  auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  check(dl_maxpool_bwd(cbf(dy), arg.data_ptr<uint8_t>(), bf(dx), (int)N, (int)H, (int)W, (int)C, (int)P, (int)Q,
+                       cur_stream(dy)),
+        "maxpool_bwd");
+  return dx;
+}
+
+at::Tensor avgpool_fwd(const at::Tensor& x) {
+  expect_nhwc(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  auto y = at::empty({N, C}, x.options());
+  check(dl_avgpool_fwd(cbf(x), bf(y), (int)N, (int)HW, (int)C, cur_stream(x)), "avgpool_fwd");
+  return y;
+}
+
+at::Tensor avgpool_bwd(const at::Tensor& dy_in, int64_t H, int64_t W) {
+  const at::Tensor dy = dy_in.contiguous();
+  expect(dy, at::kBFloat16, "dy");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  check(dl_avgpool_bwd(cbf(dy), bf(dx), (int)N, (int)(H * W), (int)C, cur_stream(dy)), "avgpool_bwd");
+  return dx;
+}
+
+std::tuple<at::Tensor, at::Tensor> l2norm_fwd(const at::Tensor& x_in, double eps) {
+  const at::Tensor x = x_in.contiguous();
+  expect(x, at::kBFloat16, "x");
+  const int64_t rows = x.size(0), D = x.size(1);
+  auto y = at::empty_like(x);
+  auto rinv = at::empty({rows}, x.options().dtype(at::kFloat));
+  check(dl_l2norm_fwd(cbf(x), bf(y), f32(rinv), (int)rows, (int)D, (float)eps, cur_stream(x)), "l2norm_fwd");
+  return {y, rinv};
+}
+
+at::Tensor l2norm_bwd(const at::Tensor& dy_in, const at::Tensor& y, const at::Tensor& rinv) {
+  const at::Tensor dy = dy_in.contiguous().to(at::kBFloat16);
+  expect(y, at::kBFloat16, "y");
+  expect(rinv, at::kFloat, "rinv");
+  auto dx = at::empty_like(y);
+  check(dl_l2norm_bwd(cbf(dy), cbf(y), f32(rinv), bf(dx), (int)y.size(0), (int)y.size(1), cur_stream(y)),
+        "l2norm_bwd");
+  return dx;
+}
+
 // ------------------------------------------------------------------ implicit-GEMM convolution (NHWC, conv.hip)
 // Weights arrive as [Cout, Cin, R, S] tensors whose memory is KRSC (channels_last), which is how the
 // flat parameter buffer stores every conv weight; permute(0,2,3,1) is then a free view.
@@ -1090,6 +1152,12 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("sinkhorn", &sinkhorn);
   m.impl("swav_ce", &swav_ce);
   m.impl("row_normalize_", &row_normalize_);
+  m.impl("maxpool_fwd", &maxpool_fwd);
+  m.impl("maxpool_bwd", &maxpool_bwd);
+  m.impl("avgpool_fwd", &avgpool_fwd);
+  m.impl("avgpool_bwd", &avgpool_bwd);
+  m.impl("l2norm_fwd", &l2norm_fwd);
+  m.impl("l2norm_bwd", &l2norm_bwd);
   m.impl("multicrop", &multicrop);
   m.impl("layernorm_fwd", &layernorm_fwd);
   m.impl("layernorm_bwd", &layernorm_bwd);

@@ -120,3 +120,12 @@ int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
 int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinfo, const bf16_t* out,
                 const bf16_t* dout, long ldo, const float* lse, float* delta, bf16_t* dqkv, float* dbias, int B, int H,
                 int S, int D, float scale, hipStream_t st);
+
+// pool.hip (SwAV trunk pools and head normalisation; channels-last bf16, C % 8 == 0)
+int dl_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, hipStream_t st);
+int dl_maxpool_bwd(const bf16_t* dy, const uint8_t* arg, bf16_t* dx, int N, int H, int W, int C, int P, int Q,
+                   hipStream_t st);
+int dl_avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);
+int dl_avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
+int dl_l2norm_fwd(const bf16_t* x, bf16_t* y, float* rinv, int rows, int D, float eps, hipStream_t st);
+int dl_l2norm_bwd(const bf16_t* dy, const bf16_t* y, const float* rinv, bf16_t* dx, int rows, int D, hipStream_t st);

@@ -30,11 +30,15 @@ FIRST_REGULAR_ID = 5
 class SyntheticSOPStream:
     def __init__(self, batch_size: int, seq_len: int = 512, vocab_size: int = 30000, seed: int = 0,
                  device="cpu", mask_mode: str = "fixed", mlm_probability: float = 0.15,
-                 length_mode: str = "full", min_len: int = 64):
+                 length_mode: str = "full", min_len: int = 64, pattern_period: int = 0):
         self.B, self.S, self.V = batch_size, seq_len, vocab_size
         self.device = torch.device(device)
         self.mask_mode, self.p = mask_mode, mlm_probability
         self.length_mode, self.min_len = length_mode, min_len
+        # > 0: LEARNABLE token rows (convergence tests): token i of a row is
+        # FIRST_REGULAR_ID + (phase + i) % pattern_period with a random phase per row, so a masked
+        # token is predictable from its neighbours; 0: independent uniform tokens (throughput runs)
+        self.pattern_period = int(pattern_period)
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seed) % (2 ** 63))
         self.P = max(1, round(self.p * (seq_len - 3)))
@@ -59,8 +63,12 @@ class SyntheticSOPStream:
             lo = min(self.min_len, max(8, S // 2))  # short sequences: never below 8 tokens
             short = torch.rand(B, generator=self.gen, device=dev) < 0.1
             lengths = torch.where(short, self._rand(B, high=max(1, S - lo)) + lo, torch.full((B,), S, device=dev))
-        ids = self._rand(B, S, high=self.V - FIRST_REGULAR_ID) + FIRST_REGULAR_ID
         ar = torch.arange(S, device=dev)[None, :]
+        if self.pattern_period > 0:
+            phase = self._rand(B, 1, high=self.pattern_period)
+            ids = (phase + ar) % min(self.pattern_period, self.V - FIRST_REGULAR_ID) + FIRST_REGULAR_ID
+        else:
+            ids = self._rand(B, S, high=self.V - FIRST_REGULAR_ID) + FIRST_REGULAR_ID
         # segment A ends at a random split (>= 1 token each side)
         split = (torch.rand(B, generator=self.gen, device=dev) * (lengths - 4).float()).long() + 2
         attn = (ar < lengths[:, None]).long()

@@ -176,6 +176,53 @@ class BNAct(nn.BatchNorm2d):
         return F.relu(y) if self.relu else y
 
 
+def _native_nhwc(x) -> bool:
+    return x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y, arg = torch.ops.dedloc.maxpool_fwd(x)
+        ctx.save_for_backward(arg)
+        ctx.hw = (x.shape[2], x.shape[3])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        return torch.ops.dedloc.maxpool_bwd(dy, arg, *ctx.hw)
+
+
+class MaxPool3x3s2(nn.MaxPool2d):
+    """The stem's MaxPool2d(3, stride 2, padding 1); on channels-last bf16 GPU activations the
+    pool.hip kernels (the backward routes each gradient to its window's recorded maximum)."""
+
+    def __init__(self):
+        super().__init__(3, stride=2, padding=1)
+
+    def forward(self, x):
+        return _MaxPool.apply(x) if _native_nhwc(x) else super().forward(x)
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return torch.ops.dedloc.avgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return torch.ops.dedloc.avgpool_bwd(dy.to(torch.bfloat16), *ctx.hw)
+
+
+def global_avgpool(x):
+    """AdaptiveAvgPool2d(1) + flatten -> [N, C] (pool.hip on channels-last bf16 GPU activations)."""
+    if _native_nhwc(x):
+        return _AvgPool.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
 class Bottleneck(nn.Module):
     expansion = 4
 
@@ -204,7 +251,7 @@ class ResNet50Trunk(nn.Module):
         self.inplanes = 64
         self.conv1 = ConvNHWC(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = BNAct(64, relu=True)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool3x3s2()
         self.layer1 = self._make_layer(64, layers[0])
         self.layer2 = self._make_layer(128, layers[1], stride=2)
         self.layer3 = self._make_layer(256, layers[2], stride=2)
@@ -265,7 +312,7 @@ class ResNet50Trunk(nn.Module):
                 x = checkpoint(stage, x, use_reentrant=False)
             else:
                 x = stage(x)
-        return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return global_avgpool(x)
 
 
 class SwAVPrototypesHead(nn.Module):

