@@ -24,24 +24,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=6, help="untimed iterations (MIOpen find + graph capture)")
+    ap.add_argument("--warmup", type=int, default=4, help="untimed iterations (first-call allocations, graph capture)")
     ap.add_argument("--grouped", action="store_true", help="one trunk pass per crop resolution")
     ap.add_argument("--queue", action="store_true", help="queue active (3840 rows in Sinkhorn)")
     ap.add_argument("--graph", action="store_true", help="capture trunk+head fwd/bwd as HIP graphs")
-    ap.add_argument("--no_find", action="store_true", help="MIOpen immediate mode (cudnn.benchmark=False)")
-    ap.add_argument("--conv", default=None, choices=["hip", "miopen", "auto"], help="conv backend (default: config)")
-    ap.add_argument("--stem", default=None, choices=["hip", "miopen", "null"], help="stem conv backend (default: config)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     ov = [f"config.DATA.TRAIN.BATCHSIZE_PER_REPLICA={args.batch}", f"config.OPTIMIZER.batch_size_for_tracking={args.batch}",
           "config.OPTIMIZER.target_batch_size=100000000", f"config.MODEL.SINGLE_PASS_EVERY_CROP={not args.grouped}",
-          f"config.LOSS.swav_loss.queue.start_iter={0 if args.queue else 10**9}", "config.CHECKPOINT.DIR=/tmp/swav_bench", f"config.MODEL.CUDA_GRAPH={args.graph}", f"config.MODEL.MIOPEN_FIND={not args.no_find}"] + ([f"config.MODEL.CONV_IMPL={args.conv}"] if args.conv else []) \
-        + ([f"config.MODEL.STEM_CONV_IMPL={args.stem}"] if args.stem else [])
+          f"config.LOSS.swav_loss.queue.start_iter={0 if args.queue else 10**9}", "config.CHECKPOINT.DIR=/tmp/swav_bench", f"config.MODEL.CUDA_GRAPH={args.graph}"]
     cfg = load_config("swav_1node_resnet_submit", ov)
     dht = DHT(start=True)
     peer = SwavPeer(cfg, dev, dht=dht)
     try:
-        for i in range(args.warmup):  # progress lines: MIOpen's first-call search can take minutes
+        for i in range(args.warmup):
             t0 = time.perf_counter()
             peer.train_step()
             torch.cuda.synchronize()
@@ -64,7 +60,6 @@ def main():
         print(json.dumps({"metric": "swav_rn50_local_samples_per_sec_per_gpu", "value": args.batch / dt,
                           "ms_per_iter": dt * 1e3, "data_ms": data_ms, "larc_sgd_step_ms": opt_ms,
                           "batch": args.batch, "crops": "2x224+6x96", "grouped": args.grouped, "queue": args.queue, "hip_graph": args.graph,
-                          "conv": peer.cfg.MODEL.get("CONV_IMPL"), "stem_conv": peer.cfg.MODEL.get("STEM_CONV_IMPL"), "miopen_find": not args.no_find,
                           "peak_mem_gb": torch.cuda.max_memory_allocated() / 2**30}))
     finally:
         peer.shutdown()

@@ -83,7 +83,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
             cmd += ["-I", sysconfig.get_paths()["include"], "-c", src, "-o", obj]
             jobs_list.append(cmd)
 
-    # host-side C++ that talks to ROCm libraries (hipBLASLt) but not to torch
+    # host-side C++ that does not include torch
     for src in sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))):
         obj = os.path.join(BUILD, "host_" + os.path.basename(src).replace(".cpp", ".o"))
         objs.append(obj)
@@ -108,7 +108,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
             cmd += ["-L", p, f"-Wl,-rpath,{p}"]
         # -lrccl resolves in torch's lib dir first: the same librccl.so.1 torch loads (one RCCL per process)
         cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl", "-L", f"{ROCM}/lib",
-                f"-Wl,-rpath,{ROCM}/lib", "-lhipblaslt"]
+                f"-Wl,-rpath,{ROCM}/lib"]
         _run(cmd, verbose)
     if rt_objs and _newer(DHT_SO_PATH, rt_objs):
         _run(["g++", "-shared", "-fPIC", *rt_objs, "-o", DHT_SO_PATH, "-lpthread"], verbose)

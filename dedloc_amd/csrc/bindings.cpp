@@ -13,7 +13,6 @@
 #include <unordered_map>
 
 #include "dl_kernels.h"
-#include "dl_lt.h"
 
 namespace {
 
@@ -382,38 +381,29 @@ std::tuple<at::Tensor, at::Tensor> attn_softmax_bwd(const at::Tensor& s, const a
   return {p, ds};
 }
 
-// ------------------------------------------------------------------ GEMM (library path)
-// Plain and fused-epilogue GEMMs go straight to hipBLASLt (csrc/host/lt_gemm.cpp: fp32 bias read
-// in the epilogue, GELU_AUX_BIAS for the FFN-up forward, DGELU_BGRAD for the FFN dgrad, per-shape
-// autotuned algorithm); ATen is only the fallback when hipBLASLt offers no solution.
-// (bf16 in, fp32 accumulate; the fp32-accumulating form writes straight into the fp32 gradient
-// buffer with beta=1 so the shared ALBERT layer's 24 weight-gradient contributions never round
-// through bf16.)
-// GEMM dispatch policy, chosen from measurements on MI355X (bench/gemm_bench.py, profiles/):
-//   * the dedloc MFMA kernel (gemm.hip) wins the weight-gradient GEMMs whose output has few
-//     256x256 tiles (split-K over the token dimension: 1024x1024 wgrad 168 us vs 198 us);
-//   * hipBLASLt currently wins the large forward/dgrad GEMMs (its deeper LDS-DMA pipeline reaches
-//     1.1-1.5 PF/s on these shapes vs ~0.6-0.95 for gemm.hip's register-staged loop).
-// DEDLOC_GEMM=mfma forces gemm.hip everywhere (correctness tests), =lib forces the library;
-// DEDLOC_LT=0 routes the library path through ATen instead of the direct hipBLASLt calls.
-int gemm_policy() {  // 0 auto, 1 mfma, 2 lib, 3 mfma with the register-staged gemm.hip only
+// ------------------------------------------------------------------ GEMM
+// Every GPU GEMM runs on this repository's MFMA kernels (bf16 in, fp32 accumulation):
+//   gemm8.hip      LDS-DMA 8-phase pipeline, 256x256 tiles — every ALBERT layer GEMM, fused
+//                  epilogues (bias, residual, bias + GELU, GELU' + bias gradient, fp32 split-K slabs)
+//   gemm.hip       register-staged 256x256 tiles — tiled shapes outside gemm8's contract
+//                  (N % 256 != 0: the SwAV 1x1 convs with 64 / 128 outputs, the stem)
+//   gemm_small.hip any shape and stride, 64x64 tiles — the rest (SwAV prototypes N = K = 3000,
+//                  small heads); a few GFLOP per step at most
+// There is no vendor-library or ATen path: a shape no kernel takes is an error, not a fallback.
+// The fp32-accumulating weight-gradient form writes straight into the fp32 gradient buffer, so the
+// shared ALBERT layer's 24 weight-gradient contributions never round through bf16.
+// DEDLOC_GEMM=mfma1 skips gemm8 (A/B measurements of the two tiled kernels).
+bool use_gemm8() {
   const char* e = std::getenv("DEDLOC_GEMM");
-  if (!e) return 0;
-  if (!std::strcmp(e, "mfma1")) return 3;
-  return e[0] == 'm' ? 1 : (e[0] == 'l' ? 2 : 0);
-}
-bool use_gemm8() { return gemm_policy() != 3; }
-bool use_mfma_gemm() { return gemm_policy() != 2; }
-bool force_mfma_gemm() { const int g = gemm_policy(); return g == 1 || g == 3; }
-bool use_lt() {
-  const char* e = std::getenv("DEDLOC_LT");
-  return !(e && e[0] == '0');
+  return !(e && !std::strcmp(e, "mfma1"));
 }
 
 struct Mat {  // (rows, k) operand view: K-inner means element (r, k) at p[r*ld + k]
   const at::Tensor& t;
   bool kouter;
   int64_t rows, k, ld;
+  long srow() const { return kouter ? 1 : (long)ld; }
+  long sk() const { return kouter ? (long)ld : 1; }
 };
 
 // op(a) is [M, K]; trans_a=False -> a is [M,K] K-inner; trans_a=True -> a is [K,M] (K-outer)
@@ -425,30 +415,11 @@ inline Mat b_view(const at::Tensor& b, bool trans_b) {
   return trans_b ? Mat{b, false, b.size(0), b.size(1), b.stride(0)} : Mat{b, true, b.size(1), b.size(0), b.stride(0)};
 }
 
-inline bool mfma_ok(const at::Tensor& a, const at::Tensor& b) {
-  return use_mfma_gemm() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 &&
-         a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1;
-}
-
-inline bool lt_ok(const at::Tensor& a, const at::Tensor& b) {
-  return use_lt() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 &&
-         b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1;
-}
-
-inline DlLtArgs lt_args(const at::Tensor& a, const at::Tensor& b, bool trans_a, bool trans_b) {
-  const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
-  TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
-  DlLtArgs l;
-  l.transA = trans_a;
-  l.transB = trans_b;
-  l.M = (int)A.rows;
-  l.N = (int)B.rows;
-  l.K = (int)A.k;
-  l.A = a.data_ptr();
-  l.lda = a.stride(0);
-  l.B = b.data_ptr();
-  l.ldb = b.stride(0);
-  return l;
+inline void expect_operands(const at::Tensor& a, const at::Tensor& b) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm operands must be GPU tensors");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "gemm operands must be bf16");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
+              "gemm operands must be 2-D with unit inner stride");
 }
 
 inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias) {
@@ -456,8 +427,7 @@ inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias) {
   return bias->scalar_type() == at::kFloat ? bias->contiguous() : bias->to(at::kFloat).contiguous();
 }
 
-// The hand-written kernels: gemm8.hip (LDS-DMA 8-phase pipeline) where its contract holds,
-// gemm.hip (register-staged) otherwise.  Returns 0 on success.
+// The tiled kernels: gemm8.hip where its contract holds, gemm.hip otherwise.  0 on success.
 int own_gemm(int akout, int bkout, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
              bf16_t* C, long ldc, float* Cf, long ldcf, const float* bias, const bf16_t* R, long ldr, bf16_t* H,
              long ldh, float* dbias, hipStream_t st) {
@@ -467,16 +437,51 @@ int own_gemm(int akout, int bkout, int epi, const bf16_t* A, long lda, const bf1
   return dl_gemm(akout, bkout, epi, A, lda, B, ldb, M, N, K, C, ldc, Cf, ldcf, bias, R, ldr, H, ldh, dbias, 1, st);
 }
 
+// C (bf16) = op(A) op(B) (+ bias) (+ R): tiled kernels, else gemm_small.
+void gemm_store(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, bf16_t* C, long ldc,
+                const float* bias, const bf16_t* R, long ldr, hipStream_t st) {
+  if (own_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, C, ldc, nullptr,
+               0, bias, R, ldr, nullptr, 0, nullptr, st) == 0)
+    return;
+  check(dl_gemm_small(0, cbf(a), A.srow(), A.sk(), cbf(b), B.srow(), B.sk(), (int)A.rows, (int)B.rows, (int)A.k, C,
+                      ldc, nullptr, 0, 0, bias, R, ldr, st),
+        "gemm");
+}
+
+at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                const c10::optional<at::Tensor>& residual, bool trans_a, bool trans_b, int64_t epilogue) {
+  expect_operands(a, b);
+  const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
+  TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
+  if (residual.has_value()) {
+    TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->is_contiguous() &&
+                    residual->size(0) == A.rows && residual->size(1) == B.rows,
+                "gemm residual must be a contiguous bf16 [M, N] tensor");
+  }
+  auto c = at::empty({A.rows, B.rows}, a.options());
+  const at::Tensor bias32 = f32_bias(bias);
+  const float* bp = bias32.defined() ? f32(bias32) : nullptr;
+  const bf16_t* rp = residual.has_value() ? cbf(*residual) : nullptr;
+  gemm_store(A, B, a, b, bf(c), B.rows, bp, rp, B.rows, cur_stream(a));
+  if (epilogue == 1) check(dl_gelu_fwd(cbf(c), bf(c), c.numel(), cur_stream(c)), "gemm gelu epilogue");
+  return c;
+}
+
 // fp32-accumulating weight gradient c += op(a) op(b) through gemm8: the token (reduction) dimension
 // is split into S slices written as fp32 slabs and summed into c (no atomics); -1 if unsupported.
-int own_wgrad(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, at::Tensor c, hipStream_t st) {
-  if (!use_gemm8() || !c.is_contiguous()) return -1;
+int wgrad_splits8(const Mat& A, const Mat& B) {
   const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
   int S = 1;
   if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) S = std::max(1, std::atoi(e));
   else
     while (S < 16 && tiles * S * 2 <= 512 && A.k % (S * 2 * 64) == 0 && A.k / (S * 2) >= 1024) S *= 2;
   while (S > 1 && A.k % (S * 64)) S /= 2;
+  return S;
+}
+
+int own_wgrad(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, at::Tensor c, hipStream_t st) {
+  if (!use_gemm8() || !c.is_contiguous()) return -1;
+  const int S = wgrad_splits8(A, B);
   if (S == 1)
     return dl_gemm8(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, nullptr, 0,
                     f32(c), c.stride(0), 0, 1, nullptr, nullptr, 0, nullptr, 0, nullptr, 1, st);
@@ -488,143 +493,33 @@ int own_wgrad(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor&
   return dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), st);
 }
 
-at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
-                const c10::optional<at::Tensor>& residual, bool trans_a, bool trans_b, int64_t epilogue) {
-  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "gemm operands must be GPU tensors");
-  if (force_mfma_gemm() && mfma_ok(a, b) && epilogue == 0 && (!residual.has_value() || residual->is_contiguous())) {
-    const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
-    TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
-    auto c = at::empty({A.rows, B.rows}, a.options());
-    const at::Tensor bias32 = f32_bias(bias);
-    const int rc = own_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
-                            bf(c), B.rows, nullptr, 0, bias32.defined() ? f32(bias32) : nullptr,
-                            residual.has_value() ? cbf(*residual) : nullptr, B.rows, nullptr, 0, nullptr,
-                            cur_stream(a));
-    if (rc == 0) return c;
-  }
-  if (lt_ok(a, b) && (!residual.has_value() || (residual->is_contiguous() && residual->scalar_type() == at::kBFloat16))) {
-    DlLtArgs l = lt_args(a, b, trans_a, trans_b);
-    auto c = at::empty({l.M, l.N}, a.options());
-    const at::Tensor bias32 = f32_bias(bias);
-    l.D = c.data_ptr();
-    l.ldd = l.N;
-    if (residual.has_value()) {  // C = residual: the residual-branch gradient sum rides in the GEMM
-      l.C = residual->data_ptr();
-      l.beta = 1.f;
-    }
-    if (bias32.defined()) {
-      l.epilogue = epilogue == 1 ? DL_LT_GELU_BIAS : DL_LT_BIAS;
-      l.bias = bias32.data_ptr();
-    }
-    if (dl_lt_matmul(l, cur_stream(a)) == 0) {
-      if (epilogue == 1 && !bias32.defined()) check(dl_gelu_fwd(cbf(c), bf(c), c.numel(), cur_stream(c)), "gemm gelu");
-      return c;
-    }
-  }
-  const at::Tensor A = trans_a ? a.t() : a;
-  const at::Tensor B = trans_b ? b.t() : b;
-  at::Tensor c;
-  if (residual.has_value()) {
-    // C = residual + A.B in one GEMM (beta = 1): fuses the residual-branch gradient sum
-    c = at::addmm(*residual, A, B);
-    if (bias.has_value()) c.add_(*bias);
-  } else {
-    c = bias.has_value() ? at::addmm(bias->to(a.scalar_type()), A, B) : at::mm(A, B);
-  }
-  if (!c.is_contiguous()) c = c.contiguous();
-  if (epilogue == 1) {
-    TORCH_CHECK(c.is_contiguous(), "gemm output must be contiguous");
-    check(dl_gelu_fwd(cbf(c), bf(c), c.numel(), cur_stream(c)), "gemm gelu epilogue");
-  }
-  return c;
-}
-
-// Weight gradients (dW[N_out, K_in] += dY^T X over T tokens) have few output tiles and a very long
-// reduction, which under-fills 256 CUs.  Split the token dimension into S slices run as ONE strided
-// batched hipBLASLt GEMM into fp32 partial slabs, then add the slabs into the fp32 gradient:
-// measured at T=32768 (bench/wgrad_bench.py) 1024x1024: 174 -> ~80 us, 4096x1024: 307 -> ~280 us,
-// 3072x1024: 244 -> ~200 us.  S = largest power of two <= min(8, 256 / #256x256-tiles).
-int wgrad_splits(int64_t M, int64_t N, int64_t K, int max_splits = 8) {
-  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) {  // measurement override (bench/wgrad_bench.py)
-    int s = std::max(1, std::atoi(e));
-    while (s > 1 && (K % (s * 64) || K / s < 256)) s /= 2;
-    return s;
-  }
-  int s = 1;
-  while (s < max_splits && tiles * s * 2 <= 256 && K % (s * 2 * 64) == 0 && K / (s * 2) >= 1024) s *= 2;
-  return s;
-}
-
-void gemm_acc_f32_split(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b,
-                        int max_splits) {
-  expect(c, at::kFloat, "c");
-  const Mat Av = a_view(a, trans_a), Bv = b_view(b, trans_b);
-  const int64_t ntiles = ((Av.rows + 255) / 256) * ((Bv.rows + 255) / 256);
-  if (force_mfma_gemm() && mfma_ok(a, b)) {
-    const Mat A = Av, B = Bv;
-    TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
-    if (own_wgrad(A, B, a, b, c, cur_stream(a)) == 0) return;
-    // split the reduction so that at least ~2 workgroups per CU exist (wgrad: few output tiles,
-    // very long token reduction); splits accumulate with fp32 atomics
-    const int64_t tiles = ntiles;
-    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(A.k / 1024, (512 + tiles - 1) / tiles));
-    const int rc = dl_gemm(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
-                           nullptr, 0, f32(c), c.stride(0), nullptr, nullptr, 0, nullptr, 0, nullptr, splits,
-                           cur_stream(a));
-    if (rc == 0) return;
-  }
-  if (lt_ok(a, b) && c.stride(1) == 1) {
-    DlLtArgs l = lt_args(a, b, trans_a, trans_b);
-    const int S = (trans_a && !trans_b && c.is_contiguous()) ? wgrad_splits(l.M, l.N, l.K, max_splits) : 1;
-    if (S > 1) {  // token-split batched GEMM into fp32 slabs + slab sum
-      auto slabs = at::empty({S, l.M, l.N}, c.options());
-      const long kslice = l.K / S;
-      l.K = (int)kslice;
-      l.batch = S;
-      l.strideA = kslice * l.lda;  // A = dY stored [T, M]: slice s starts at row s*kslice
-      l.strideB = kslice * l.ldb;  // B = X stored [T, N]
-      l.strideD = (long)l.M * l.N;
-      l.D = slabs.data_ptr();
-      l.ldd = l.N;
-      l.d_f32 = 1;
-      if (dl_lt_matmul(l, cur_stream(a)) == 0) {
-        check(dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), cur_stream(a)), "sum_slabs");
-        return;
-      }
-      l = lt_args(a, b, trans_a, trans_b);
-    }
-    l.D = c.data_ptr();
-    l.ldd = c.stride(0);
-    l.d_f32 = 1;
-    l.beta = 1.f;
-    if (dl_lt_matmul(l, cur_stream(a)) == 0) return;
-  }
-  if (mfma_ok(a, b) && ntiles <= 16) {
-    int splits = (int)std::max<int64_t>(1, std::min<int64_t>(Av.k / 1024, (512 + ntiles - 1) / ntiles));
-    const int rc = dl_gemm(Av.kouter, Bv.kouter, 3, cbf(a), Av.ld, cbf(b), Bv.ld, (int)Av.rows, (int)Bv.rows,
-                           (int)Av.k, nullptr, 0, f32(c), c.stride(0), nullptr, nullptr, 0, nullptr, 0, nullptr,
-                           splits, cur_stream(a));
-    if (rc == 0) return;
-  }
-  const at::Tensor A = trans_a ? a.t() : a;
-  const at::Tensor B = trans_b ? b.t() : b;
-  at::_ops::addmm_dtype_out::call(c, A, B, at::kFloat, 1, 1, c);
-}
-
 void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b) {
-  gemm_acc_f32_split(a, b, c, trans_a, trans_b, 8);
+  expect_operands(a, b);
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat && c.dim() == 2 && c.stride(1) == 1,
+              "gemm_acc_f32: c must be an fp32 [M, N] GPU tensor with unit inner stride");
+  const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
+  TORCH_CHECK(A.k == B.k, "gemm inner dimensions differ");
+  TORCH_CHECK(c.size(0) == A.rows && c.size(1) == B.rows, "gemm_acc_f32: c shape mismatch");
+  if (own_wgrad(A, B, a, b, c, cur_stream(a)) == 0) return;
+  // gemm.hip: split the long reduction over ~2 workgroups per CU, fp32 atomics into c
+  const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
+  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(A.k / 1024, (512 + tiles - 1) / tiles));
+  if (dl_gemm(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, nullptr, 0,
+              f32(c), c.stride(0), nullptr, nullptr, 0, nullptr, 0, nullptr, splits, cur_stream(a)) == 0)
+    return;
+  check(dl_gemm_small(1, cbf(a), A.srow(), A.sk(), cbf(b), B.srow(), B.sk(), (int)A.rows, (int)B.rows, (int)A.k,
+                      nullptr, 0, f32(c), c.stride(0), 1, nullptr, nullptr, 0, cur_stream(a)),
+        "gemm_acc_f32");
 }
 
 // Weight gradient of a weight that several consecutive backward calls share (ALBERT's one layer,
-// applied 24 times): the token-split fp32 slabs of gemm_acc_f32 persist across the calls — the
-// first call writes them (beta = 0), later calls accumulate (beta = 1) — and are added into the
-// gradient once, by the last call.  That replaces 24 slab-sum passes per weight and micro-step
-// by one.  Without the split form (no hipBLASLt plan, one slice) every call accumulates directly.
-// The slab workspace of one gradient tensor lives from the first to the last call of a micro-step,
-// so it is keyed by the gradient (pointer, device, shape, split count).  The cache is bounded: when a
+// applied 24 times): gemm8's token-split fp32 slabs persist across the calls — the first call
+// writes them, later calls accumulate into them (the kernel's EPI_F32 accumulate form) — and are
+// added into the gradient once, by the last call: one slab-sum pass per weight and micro-step
+// instead of 24.  The slab workspace of one gradient tensor lives from the first to the last call,
+// so it is keyed by the gradient (pointer, device, shape, split count); the cache is bounded: when a
 // new key would exceed kMaxSlabSets entries (gradient buffers re-allocated, several models in one
-// process), the least recently used workspace is freed; `dedloc_ws::clear_workspaces()` frees all.
+// process) the least recently used workspace is freed; `dedloc_ws::clear_workspaces()` frees all.
 struct SlabKey {
   const void* ptr;
   int64_t dev, S, M, N;
@@ -668,96 +563,59 @@ int64_t clear_workspaces() {
 
 void gemm_acc_f32_shared(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool trans_a, bool trans_b,
                          bool first, bool last) {
-  expect(c, at::kFloat, "c");
-  if (!force_mfma_gemm() && lt_ok(a, b) && trans_a && !trans_b && c.is_contiguous()) {
-    DlLtArgs l = lt_args(a, b, trans_a, trans_b);
-    const int S = wgrad_splits(l.M, l.N, l.K, 8);
-    if (S > 1) {
-      at::Tensor slabs = shared_slabs(c, S);
-      const long kslice = l.K / S;
-      l.K = (int)kslice;
-      l.batch = S;
-      l.strideA = kslice * l.lda;
-      l.strideB = kslice * l.ldb;
-      l.strideD = (long)l.M * l.N;
-      l.D = slabs.data_ptr();
-      l.ldd = l.N;
-      l.d_f32 = 1;
-      l.beta = first ? 0.f : 1.f;
-      if (dl_lt_matmul(l, cur_stream(a)) == 0) {
-        if (last) check(dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), cur_stream(a)), "sum_slabs");
-        return;
-      }
-      TORCH_CHECK(first, "gemm_acc_f32_shared: hipBLASLt failed after earlier calls accumulated into the slabs");
+  expect_operands(a, b);
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kFloat, "gemm_acc_f32_shared: c must be fp32");
+  const Mat A = a_view(a, trans_a), B = b_view(b, trans_b);
+  TORCH_CHECK(A.k == B.k && c.size(0) == A.rows && c.size(1) == B.rows, "gemm_acc_f32_shared: shape mismatch");
+  const int S = use_gemm8() && c.is_contiguous() ? wgrad_splits8(A, B) : 1;
+  if (S > 1) {
+    at::Tensor slabs = shared_slabs(c, S);
+    const int rc = dl_gemm8(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
+                            nullptr, 0, f32(slabs), B.rows, A.rows * B.rows, first ? 0 : 1, nullptr, nullptr, 0,
+                            nullptr, 0, nullptr, S, cur_stream(a));
+    if (rc == 0) {
+      if (last) check(dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), cur_stream(a)), "sum_slabs");
+      return;
     }
+    TORCH_CHECK(first, "gemm_acc_f32_shared: gemm8 refused a shape it accepted for an earlier call");
   }
-  gemm_acc_f32_split(a, b, c, trans_a, trans_b, 8);
+  gemm_acc_f32(a, b, c, trans_a, trans_b);
 }
 
 // fused FFN-up: H = x W^T + b (pre-activation, kept for backward), G = gelu_new(H)
 std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias) {
+  expect_operands(x, w);
   auto H = at::empty({x.size(0), w.size(0)}, x.options());
   auto G = at::empty_like(H);
-  if (force_mfma_gemm() && mfma_ok(x, w)) {
-    const at::Tensor bias32 = f32_bias(bias);
-    const int rc = own_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0),
-                            (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1),
-                            nullptr, cur_stream(x));
-    if (rc == 0) return {H, G};
-  }
-  // hipBLASLt on ROCm 7.2 has no gfx950 solution for GELU_AUX_BIAS (scripts/lt_debug.py), so the
-  // library path is a bias-epilogue GEMM (fp32 bias, no cast kernel) + the gelu kernel
   const at::Tensor bias32 = f32_bias(bias);
-  if (lt_ok(x, w)) {
-    DlLtArgs l = lt_args(x, w, false, true);
-    l.D = H.data_ptr();
-    l.ldd = H.size(1);
-    l.epilogue = DL_LT_BIAS;
-    l.bias = bias32.data_ptr();
-    if (dl_lt_matmul(l, cur_stream(x)) == 0) {
-      check(dl_gelu_fwd(cbf(H), bf(G), H.numel(), cur_stream(H)), "gelu_fwd");
-      return {H, G};
-    }
-  }
-  H = at::addmm(bias.to(x.scalar_type()), x, w.t()).contiguous();
+  if (own_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0), (int)x.size(1),
+               bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1), nullptr, cur_stream(x)) == 0)
+    return {H, G};
+  const Mat A = a_view(x, false), B = b_view(w, true);
+  gemm_store(A, B, x, w, bf(H), H.size(1), f32(bias32), nullptr, 0, cur_stream(x));
   check(dl_gelu_fwd(cbf(H), bf(G), H.numel(), cur_stream(H)), "gelu_fwd");
   return {H, G};
 }
 
 // fused FFN dgrad: C = (dy W) * gelu_new'(F), dbias += colsum(C).  trans_w: w holds W^T (the
-// forward-layout copy; hipBLASLt runs that "NT" form 13% faster than "NN" on the ALBERT shapes)
+// forward-layout copy, a K-inner operand for the tiled kernels)
 at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& F, at::Tensor dbias,
                       bool trans_w) {
+  expect_operands(dy, w);
   expect(F, at::kBFloat16, "F");
   expect(dbias, at::kFloat, "dbias");
   const int64_t nout = trans_w ? w.size(0) : w.size(1);
-  if (force_mfma_gemm() && mfma_ok(dy, w)) {
-    auto C = at::empty({dy.size(0), nout}, dy.options());
-    const int rc = own_gemm(0, trans_w ? 0 : 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0),
-                            (int)nout, (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1),
-                            nullptr, 0, f32(dbias), cur_stream(dy));
-    if (rc == 0) return C;
-  }
-  // (hipBLASLt's DGELU_BGRAD epilogue returns wrong results for this layout on ROCm 7.2 —
-  // scripts/lt_debug.py — so the dgrad is a plain GEMM followed by the fused gelu'/bias-grad kernel)
-  if (lt_ok(dy, w)) {
-    auto dg = at::empty({dy.size(0), nout}, dy.options());
-    DlLtArgs l = lt_args(dy, w, false, trans_w);
-    l.D = dg.data_ptr();
-    l.ldd = dg.size(1);
-    if (dl_lt_matmul(l, cur_stream(dy)) == 0) {
-      auto dh = at::empty_like(dg);
-      check(dl_gelu_bwd_colsum(cbf(dg), cbf(F), bf(dh), f32(dbias), (int)dg.size(0), (int)dg.size(1),
-                               cur_stream(dg)),
-            "gelu_bwd");
-      return dh;
-    }
-  }
-  auto dg = at::mm(dy, trans_w ? w.t() : w).contiguous();
-  auto dh = at::empty_like(dg);
-  check(dl_gelu_bwd_colsum(cbf(dg), cbf(F), bf(dh), f32(dbias), (int)dg.size(0), (int)dg.size(1), cur_stream(dg)),
+  auto C = at::empty({dy.size(0), nout}, dy.options());
+  if (own_gemm(0, trans_w ? 0 : 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0), (int)nout,
+               (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0, f32(dbias),
+               cur_stream(dy)) == 0)
+    return C;
+  auto dg = at::empty_like(C);
+  const Mat A = a_view(dy, false), B = b_view(w, trans_w);
+  gemm_store(A, B, dy, w, bf(dg), dg.size(1), nullptr, nullptr, 0, cur_stream(dy));
+  check(dl_gelu_bwd_colsum(cbf(dg), cbf(F), bf(C), f32(dbias), (int)dg.size(0), (int)dg.size(1), cur_stream(dg)),
         "gelu_bwd");
-  return dh;
+  return C;
 }
 
 // ------------------------------------------------------------------ SwAV
@@ -991,14 +849,15 @@ inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t
   return col;
 }
 
-// Convolutions that are plain GEMMs go to hipBLASLt: 1x1 stride-1 unpadded convs over NHWC tensors
-// (x[N*H*W, C] x W[K, C]^T, dgrad dY[N*H*W, K] x W, wgrad dY^T x X with the token-split fp32 slabs of
-// gemm_acc_f32) and the stem's column-matrix GEMM.  Measured on the SwAV b=64 shapes
-// (profiles/conv_bench_*.jsonl) the implicit-GEMM kernel runs these short-K / N=64 GEMMs at 40-50% of
-// the library's speed.  DEDLOC_CONV_GEMM=hip forces conv.hip everywhere (kernel tests).
-bool conv_lt() {
+// Convolutions that are plain GEMMs run on the tiled GEMM kernels (gemm8.hip / gemm.hip): 1x1
+// stride-1 unpadded convs over NHWC tensors (x[N*H*W, C] x W[K, C]^T; dgrad dY[N*H*W, K] x W
+// against the transposed weight [C, K], a K-inner operand) and the stem's column-matrix GEMM; their
+// weight gradients use gemm8's split-K slabs where both channel counts are multiples of 256 and the
+// implicit-GEMM conv.hip wgrad otherwise.  DEDLOC_CONV_GEMM=hip routes the 1x1 convs through
+// conv.hip too (kernel tests).
+bool conv_gemm() {
   const char* e = std::getenv("DEDLOC_CONV_GEMM");
-  return use_lt() && !(e && e[0] == 'h');
+  return !(e && e[0] == 'h');
 }
 inline bool is_pointwise(int64_t R, int64_t S, int64_t stride, int64_t pad) {
   return R == 1 && S == 1 && stride == 1 && pad == 0;
@@ -1006,13 +865,9 @@ inline bool is_pointwise(int64_t R, int64_t S, int64_t stride, int64_t pad) {
 inline at::Tensor rows2d(const at::Tensor& t) {  // channels-last [N, C, H, W] -> [N*H*W, C] view
   return t.permute({0, 2, 3, 1}).reshape({-1, t.size(1)});
 }
-// D[M, N] (bf16, row stride ldd) = A[M, K] . B[N, K]^T or A . B (trans_b false: B is [K, N])
-bool lt_plain(const at::Tensor& a, const at::Tensor& b, bool trans_b, void* d, int64_t ldd, hipStream_t st) {
-  if (!lt_ok(a, b)) return false;
-  DlLtArgs l = lt_args(a, b, false, trans_b);
-  l.D = d;
-  l.ldd = ldd;
-  return dl_lt_matmul(l, st) == 0;
+// D[M, N] (bf16, row stride ldd) = A[M, K] . B[N, K]^T
+void gemm_plain(const at::Tensor& a, const at::Tensor& b, bf16_t* d, int64_t ldd, hipStream_t st) {
+  gemm_store(a_view(a, false), b_view(b, true), a, b, d, ldd, nullptr, nullptr, 0, st);
 }
 
 inline DlConvGeom geom(const bf16_t* img, int64_t N, int64_t H, int64_t W, int64_t C, int64_t I, int64_t J,
@@ -1031,31 +886,23 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   const int64_t P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
   auto y = at::empty({N, K, P, Q}, x.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);
-  if (is_pointwise(R, S, stride, pad) && conv_lt() &&
-      lt_plain(rows2d(x), wk.view({K, C}), true, y.data_ptr(), K, cur_stream(x)))
+  if (is_pointwise(R, S, stride, pad) && conv_gemm()) {
+    gemm_plain(rows2d(x), wk.view({K, C}), bf(y), K, cur_stream(x));
     return y;
+  }
   if (C % 64 == 0) {
     check(dl_conv_fwd(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(wk), R * S * C,
                       (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x)),
           "conv2d_fwd");
     return y;
   }
-  // stem: im2col, then a GEMM (hipBLASLt) or a 1x1 conv (conv.hip) over the column matrix
-  const int64_t M = N * P * Q;
-  for (const bool lt : {true, false}) {
-    if (lt && !conv_lt()) continue;
-    const StemCols sc = stem_cols(R, S, C, lt);
-    const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
-    auto wp = at::zeros({K, sc.Kp}, w.options());
-    wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
-    if (lt) {
-      if (lt_plain(col, wp, true, y.data_ptr(), K, cur_stream(x))) return y;
-      continue;
-    }
-    check(dl_conv_fwd(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(wp), sc.Kp, (int)K, bf(y), 1,
-                      1, 1, 1, 0, 0, K, cur_stream(x)),
-          "conv2d_fwd(stem)");
-  }
+  // stem (3 input channels): im2col into a column matrix padded to a multiple of 64 columns, then
+  // one GEMM against the equally padded weight rows
+  const StemCols sc = stem_cols(R, S, C, false);
+  const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
+  auto wp = at::zeros({K, sc.Kp}, w.options());
+  wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
+  gemm_plain(col, wp, bf(y), K, cur_stream(x));
   return y;
 }
 
@@ -1074,9 +921,10 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
   TORCH_CHECK(K % 64 == 0, "conv2d_dgrad needs Cout % 64 == 0");
   auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);  // [K, R, S, C]
-  if (is_pointwise(R, S, stride, pad) && H == P && W == Q && conv_lt() &&
-      lt_plain(rows2d(dy), wk.view({K, C}), false, dx.data_ptr(), C, cur_stream(dy)))
+  if (is_pointwise(R, S, stride, pad) && H == P && W == Q && conv_gemm()) {
+    gemm_plain(rows2d(dy), wk.view({K, C}).t().contiguous(), bf(dx), C, cur_stream(dy));
     return dx;
+  }
   for (int64_t a = 0; a < stride; ++a) {
     const int64_t I = (H - a + stride - 1) / stride;
     const int64_t r0 = (a + pad) % stride, TR = r0 < R ? (R - 1 - r0) / stride + 1 : 0;
@@ -1115,28 +963,22 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
   const bool direct = dk.is_contiguous();
   at::Tensor acc = direct ? dk : at::zeros({K, R, S, C}, dw.options());
   int rc;
-  if (is_pointwise(R, S, stride, pad) && conv_lt()) {
-    gemm_acc_f32_split(rows2d(dy), rows2d(x), acc.view({K, C}), true, false, 32);
+  if (is_pointwise(R, S, stride, pad) && conv_gemm() && K % 256 == 0 && C % 256 == 0) {
+    gemm_acc_f32(rows2d(dy), rows2d(x), acc.view({K, C}), true, false);
   } else if (C % 8 == 0 && C >= 8 && C % 64 == 0) {
     rc = dl_conv_wgrad(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(dy), K, (int)K,
                        f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy));
     check(rc, "conv2d_wgrad");
   } else {
     // stem: wgrad over the padded column matrix into a [K, R, SCp] slab, then the real columns
-    const StemCols sc = stem_cols(R, S, C, conv_lt());
+    const StemCols sc = stem_cols(R, S, C, false);
     const int64_t M = N * P * Q;
     const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
-    if (conv_lt()) {
-      auto slab = at::zeros({K, sc.Kp}, dw.options());
-      gemm_acc_f32_split(rows2d(dy), col, slab, true, false, 32);
-      acc.view({K, R, S * C}).add_(slab.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C));
-    } else {
-      auto slab = at::zeros({K, R, sc.SCp}, dw.options());
-      rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K,
-                         f32(slab), R * sc.SCp, (int)(R * sc.SCp), cur_stream(dy));
-      check(rc, "conv2d_wgrad(stem)");
-      acc.view({K, R, S * C}).add_(slab.narrow(2, 0, S * C));
-    }
+    auto slab = at::zeros({K, R, sc.SCp}, dw.options());
+    rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K,
+                       f32(slab), R * sc.SCp, (int)(R * sc.SCp), cur_stream(dy));
+    check(rc, "conv2d_wgrad(stem)");
+    acc.view({K, R, S * C}).add_(slab.narrow(2, 0, S * C));
   }
   if (!direct) dk.add_(acc);
 }

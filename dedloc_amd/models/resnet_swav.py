@@ -107,20 +107,12 @@ class _ConvNHWC(torch.autograd.Function):
 
 
 class ConvNHWC(nn.Conv2d):
-    """``nn.Conv2d`` (same parameters / state-dict keys) whose GPU path on channels-last bf16
-    activations is the hand-written implicit-GEMM MFMA convolution (forward, dgrad, wgrad); other
-    inputs (CPU plumbing, fp32) take the stock module.
+    """``nn.Conv2d`` (same parameters / state-dict keys) that runs every GPU convolution on the
+    hand-written kernels (forward, dgrad, wgrad): the implicit-GEMM MFMA convolution (conv.hip) for
+    3x3 and strided convs, the tiled GEMM kernels (gemm8.hip / gemm.hip) for the 1x1 convs and the
+    stem's im2col matrix.  GPU inputs are brought to channels-last bf16 (autocast's compute dtype);
+    CPU inputs (the plumbing configuration) take the stock module.  There is no MIOpen path."""
 
-    Backend choice (``SwAVModel(conv_impl=...)``, config ``MODEL.CONV_IMPL``, env ``DEDLOC_CONV``),
-    measured on MI355X for the SwAV b=64 iteration (profiles/README.md): ``hip`` (default) 1518-1531
-    samples/s, first iteration ~15 s; MIOpen immediate mode 1405 samples/s, first iteration ~49 s;
-    MIOpen with exhaustive find (cudnn.benchmark) 1700 samples/s once its per-shape search is done, but
-    that search took from ~1 to >3 minutes per fresh process on the pool's boxes.  ``auto`` (the
-    config default) keeps MIOpen only where it clearly wins — the 3-channel stem (2.7x over
-    im2col + GEMM) and the 64-output-channel 3x3 convs (2x forward) — so the search covers four
-    shapes (~20 s once): 1982.1 samples/s vs 1953.9 for hip + MIOpen stem and 1905.5 for all-hip."""
-
-    native = os.environ.get("DEDLOC_CONV", "hip") == "hip"
     _wb_cache = None    # bf16 weight shared across the trunk passes of one model forward
     _wb_share = False   # set by SwAVModel.forward for the duration of that forward
     # False: return the weight gradient through autograd instead of adding it into the bound .grad
@@ -128,12 +120,15 @@ class ConvNHWC(nn.Conv2d):
     inplace_wgrad = True
 
     def forward(self, x):
-        if (self.native and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
-                and self.bias is None and self.groups == 1 and self.dilation == (1, 1)
+        if not x.is_cuda:
+            return super().forward(x)
+        if not (self.bias is None and self.groups == 1 and self.dilation == (1, 1)
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and self.padding_mode == "zeros"):
-            return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self)
-        return super().forward(x)
+            raise NotImplementedError("ConvNHWC: only the ResNet-50 conv forms (no bias, groups 1, square "
+                                      "stride/padding) have GPU kernels")
+        x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self)
 
 
 class BNAct(nn.BatchNorm2d):
@@ -315,50 +310,122 @@ class ResNet50Trunk(nn.Module):
         return global_avgpool(x)
 
 
+class _HeadLinearFn(torch.autograd.Function):
+    """y = x W^T (+ b) on the dedloc GEMM kernels (bf16 in/out, fp32 accumulation); the weight and
+    bias gradients accumulate in fp32 straight into the parameters' bound ``.grad`` (the flat
+    gradient buffer) when there is one, like the conv weight gradients."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, module):
+        wb = weight.detach().to(torch.bfloat16)
+        ctx.save_for_backward(x, wb)
+        ctx.module, ctx.has_bias = module, bias is not None
+        return torch.ops.dedloc.gemm(x, wb, None if bias is None else bias.detach(), None, False, True, 0)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        m = ctx.module
+        dx = torch.ops.dedloc.gemm(dy, wb, None, None, False, False, 0) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        g = m.weight.grad
+        if m.inplace_grad and g is not None and g.dtype == torch.float32 and g.is_contiguous():
+            torch.ops.dedloc.gemm_acc_f32(dy, x, g, True, False)
+        else:
+            dw = torch.zeros(m.weight.shape, dtype=torch.float32, device=dy.device)
+            torch.ops.dedloc.gemm_acc_f32(dy, x, dw, True, False)
+            dw = dw.to(m.weight.dtype)
+        if ctx.has_bias:
+            gb = m.bias.grad
+            if m.inplace_grad and gb is not None and gb.dtype == torch.float32:
+                torch.ops.dedloc.bias_grad(dy, gb, True)
+            else:
+                db = torch.zeros(m.bias.shape, dtype=torch.float32, device=dy.device)
+                torch.ops.dedloc.bias_grad(dy, db, True)
+                db = db.to(m.bias.dtype)
+        return dx, dw, db, None
+
+
+class HeadLinear(nn.Linear):
+    """``nn.Linear`` (same parameters / keys) on the dedloc GEMM kernels for GPU inputs."""
+
+    inplace_grad = True
+
+    def forward(self, x):
+        if x.is_cuda:
+            return _HeadLinearFn.apply(x.to(torch.bfloat16).contiguous(), self.weight, self.bias, self)
+        return super().forward(x)
+
+
+class HeadBN1dReLU(nn.BatchNorm1d):
+    """``BatchNorm1d`` + ReLU of the projection MLP (same keys as BatchNorm1d) through the fused BN
+    kernels of the trunk: the [N, C] batch is BN over N rows of a 1x1 channels-last image."""
+
+    inplace_grad = True
+    stat_groups = 1
+
+    def forward(self, x):
+        if self.training and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous():
+            N, C = x.shape
+            self.num_batches_tracked.add_(1)
+            y = _BNAct.apply(x.view(N, C, 1, 1), self.weight, self.bias, None, self.running_mean, self.running_var,
+                             True, self.eps, self.momentum, 1, None, self)
+            return y.view(N, C)
+        return F.relu(super().forward(x))
+
+
+class _L2Norm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eps):
+        y, rinv = torch.ops.dedloc.l2norm_fwd(x, eps)
+        ctx.save_for_backward(y, rinv)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, rinv = ctx.saved_tensors
+        return torch.ops.dedloc.l2norm_bwd(dy, y, rinv), None
+
+
+def l2_normalize(x, eps: float = 1e-12):
+    """F.normalize(x, p=2, dim=1) (pool.hip on GPU rows of up to 1024 values)."""
+    if x.is_cuda and x.dim() == 2 and x.shape[1] <= 1024:
+        return _L2Norm.apply(x.to(torch.bfloat16).contiguous(), eps)
+    return F.normalize(x, dim=1, p=2, eps=eps)
+
+
 class SwAVPrototypesHead(nn.Module):
-    """MLP [2048, 2048, 128] with BN+ReLU, L2 normalisation, prototypes 128 -> 3000 (no bias)."""
+    """MLP [2048, 2048, 128] with BN+ReLU, L2 normalisation, prototypes 128 -> 3000 (no bias)
+    (vissl swav_prototypes_head.py:61-112; module names and state-dict keys as there).  On the GPU
+    every op is a dedloc kernel: the GEMMs, BN1d+ReLU (batchnorm.hip) and the L2 normalisation."""
 
     def __init__(self, dims: Sequence[int] = (2048, 2048, 128), num_prototypes: int = 3000, use_bn: bool = True):
         super().__init__()
         layers: List[nn.Module] = []
         for i in range(len(dims) - 2):
-            layers += [nn.Linear(dims[i], dims[i + 1])]
+            layers += [HeadLinear(dims[i], dims[i + 1])]
+            layers += [HeadBN1dReLU(dims[i + 1]) if use_bn else nn.ReLU(inplace=True)]
             if use_bn:
-                layers += [nn.BatchNorm1d(dims[i + 1])]
-            layers += [nn.ReLU(inplace=True)]
-        layers += [nn.Linear(dims[-2], dims[-1])]
+                layers += [nn.Identity()]  # the ReLU is fused into the BN kernel (keeps vissl's indices)
+        layers += [HeadLinear(dims[-2], dims[-1])]
         self.projection_head = nn.Sequential(*layers)
-        self.prototypes0 = nn.Linear(dims[-1], num_prototypes, bias=False)
+        self.prototypes0 = HeadLinear(dims[-1], num_prototypes, bias=False)
 
     def forward(self, x):
-        emb = F.normalize(self.projection_head(x), dim=1, p=2)
+        emb = l2_normalize(self.projection_head(x))
         return emb, self.prototypes0(emb)
 
 
 class SwAVModel(nn.Module):
     def __init__(self, num_prototypes: int = 3000, single_pass_every_crop: bool = True,
-                 checkpoint_stages: bool = False, conv_impl: str | None = None, stem_conv_impl: str | None = None):
+                 checkpoint_stages: bool = False, conv_impl: str | None = None):
         super().__init__()
         self.trunk = ResNet50Trunk(checkpoint_stages=checkpoint_stages)
         self.heads = nn.ModuleList([SwAVPrototypesHead(num_prototypes=num_prototypes)])
         self.single_pass_every_crop = single_pass_every_crop
-        for impl in (conv_impl, stem_conv_impl):
-            if impl is not None and impl not in ("hip", "miopen", "auto"):
-                raise ValueError(f"conv backend must be 'hip', 'miopen' or 'auto', got {impl!r}")
-        if conv_impl is not None:
-            for m in self.trunk.modules():
-                if isinstance(m, ConvNHWC):
-                    m.native = conv_impl == "hip" or (conv_impl == "auto" and not self._miopen_wins(m))
-        if stem_conv_impl is not None:  # the 3-channel 7x7 stem alone (MODEL.STEM_CONV_IMPL)
-            self.trunk.conv1.native = stem_conv_impl == "hip"
-
-    @staticmethod
-    def _miopen_wins(m: "ConvNHWC") -> bool:
-        """Shape classes where MIOpen's kernels measured clearly faster than conv.hip on the SwAV b=64
-        shapes (profiles/conv_bench_v6_*.jsonl): the 3-channel stem (2.7x) and the 64-output-channel
-        3x3 convs (fwd 2x: a 128-wide output tile is half idle at N=64).  Only these shapes pay
-        MIOpen's one-time solver search."""
-        return m.in_channels == 3 or (m.kernel_size == (3, 3) and m.out_channels == 64)
+        if conv_impl not in (None, "hip", "auto"):  # "auto": round-2 configs (it chose MIOpen per shape)
+            raise ValueError(f"conv backend must be 'hip' (the hand-written kernels), got {conv_impl!r}")
 
     def set_bn_stat_groups(self, g: int):
         for m in self.trunk.modules():

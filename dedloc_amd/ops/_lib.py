@@ -89,11 +89,6 @@ def load_native(required: bool | None = None) -> bool:
         required = torch.cuda.is_available()
     pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(pkg, "_C.so")
-    # hipBLASLt tuning database (csrc/host/lt_gemm.cpp): solution indices found by the exhaustive
-    # autotune on MI355X for the ALBERT-large shapes, read at the first call of each GEMM plan
-    db = os.path.join(pkg, "lt_tuning_gfx950.txt")
-    if os.path.exists(db):
-        os.environ.setdefault("DEDLOC_LT_DB", db)
     try:
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} not built (run python -m dedloc_amd._build)")

@@ -68,11 +68,8 @@ class SwavPeer:
         self.model = SwAVModel(num_prototypes=int(mcfg.HEAD.num_clusters),
                                single_pass_every_crop=bool(mcfg.SINGLE_PASS_EVERY_CROP),
                                checkpoint_stages=bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING),
-                               conv_impl=mcfg.get("CONV_IMPL") or None,
-                               stem_conv_impl=mcfg.get("STEM_CONV_IMPL") or None)
+                               conv_impl=mcfg.get("CONV_IMPL") or None)
         self.model.to(self.device).train()
-        if self.device.type == "cuda":  # solver search for whatever runs on MIOpen (by default the stem only)
-            torch.backends.cudnn.benchmark = bool(mcfg.get("MIOPEN_FIND", True))
         hooks = cfg.get("HOOKS") or {}
         self.check_nan = bool(hooks.get("CHECK_NAN", True))
         self.log_frequency = max(1, int(cfg.get("LOG_FREQUENCY", 10)))

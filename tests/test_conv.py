@@ -159,7 +159,6 @@ def test_conv_module_grads_land_in_flat_buffer(cuda):
 
     torch.manual_seed(4)
     m = ConvNHWC(64, 128, 3, stride=2, padding=1, bias=False).to(cuda)
-    m.native = True  # the hand-written kernels (the SwAV default backend is MIOpen)
     w_ref = m.weight.detach().bfloat16().float().clone()
     flat = FlatParams(m.named_parameters(), device=cuda, with_bf16=False, autograd=True, channels_last=True)
     x = torch.randn(2, 64, 12, 12, device=cuda).bfloat16().contiguous(memory_format=CL).requires_grad_(True)
@@ -176,73 +175,75 @@ def test_conv_module_grads_land_in_flat_buffer(cuda):
     assert _rel(x.grad, 2 * xr.grad) < 1e-2
 
 
-@pytest.mark.gpu
-def test_resnet_trunk_hip_conv_matches_miopen(cuda):
-    """The SwAV trunk with the hand-written conv kernels (conv_impl="hip") vs the MIOpen path:
-    forward features and the flat-buffer weight gradients agree to bf16 accuracy."""
+def _fp32_twin(m, device):
+    """An fp32 copy of a module on ``device`` whose convs run through the stock (non-dedloc) path:
+    the plain PyTorch fp32 reference of the same ops."""
     import copy
 
+    from dedloc_amd.models.resnet_swav import BNAct, ConvNHWC
+
+    ref = copy.deepcopy(m).float().to(device)
+    for mod in ref.modules():
+        if isinstance(mod, ConvNHWC):
+            mod.forward = lambda x, _m=mod: F.conv2d(x, _m.weight, None, _m.stride, _m.padding)
+        if isinstance(mod, BNAct):
+            mod.fused = False
+    return ref
+
+
+@pytest.mark.gpu
+def test_resnet_trunk_hip_kernels_match_fp32(cuda):
+    """The SwAV trunk's stem + first stage on the hand-written kernels (convs, fused BN, max-pool)
+    vs the same module in fp32 PyTorch: forward features agree to bf16 accuracy."""
     from dedloc_amd.models.resnet_swav import SwAVModel
     from dedloc_amd.utils.flat import FlatParams
 
     torch.manual_seed(5)
     base = SwAVModel(num_prototypes=32)
     x = torch.randn(4, 3, 64, 64, device=cuda).bfloat16().contiguous(memory_format=CL)
-    outs = []
-    for impl in ("hip", "miopen"):
-        m = copy.deepcopy(base).to(cuda).train()
-        for mod in m.trunk.modules():
-            if hasattr(mod, "native"):
-                mod.native = impl == "hip"
-        flat = FlatParams(m.named_parameters(), device=cuda, with_bf16=False, autograd=True, channels_last=True)
-        t = m.trunk
-        # stem + the first stage only: two valid bf16 implementations drift apart through random-init
-        # conv/BN/ReLU stacks (ReLU sign flips compound: ~8 % after two stages), so deeper outputs
-        # would test the drift, not the kernels (each conv is checked against fp32 above)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            feat = t.layer1(t.maxpool(t.bn1(t.conv1(x))))
-        feat.float().pow(2).mean().backward()
-        outs.append((feat.detach().float(), flat.view(flat.grad, "trunk.layer1.0.conv2.weight").clone(),
-                     flat.view(flat.grad, "trunk.conv1.weight").clone()))
-    (f1, g1, s1), (f2, g2, s2) = outs
-    assert _rel(f1, f2) < 3e-2, _rel(f1, f2)
-    # gradients through a trunk with a loss on drifted features compound ReLU-mask / BN-centering
-    # differences (tens of %), so they are compared per Bottleneck with identical x and dY below
+    ref = _fp32_twin(base, cuda).train()
+    m = base.to(cuda).train()
+    FlatParams(m.named_parameters(), device=cuda, with_bf16=False, autograd=True, channels_last=True)
+    t, tr = m.trunk, ref.trunk
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        feat = t.layer1(t.maxpool(t.bn1(t.conv1(x))))
+    fr = tr.layer1(tr.maxpool(tr.bn1(tr.conv1(x.float()))))
+    # stem + first stage only: bf16 and fp32 drift apart through random-init conv/BN/ReLU stacks
+    # (ReLU sign flips compound), so deeper outputs would test the drift, not the kernels
+    assert _rel(feat.float(), fr) < 3e-2, _rel(feat.float(), fr)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cin,planes,stride,H", [(256, 64, 1, 16), (256, 128, 2, 16), (1024, 512, 2, 8)])
-def test_bottleneck_grads_hip_vs_miopen(cuda, cin, planes, stride, H):
+def test_bottleneck_grads_match_fp32(cuda, cin, planes, stride, H):
     """One Bottleneck (incl. the stride-2 downsample variant), identical x and dY: dX and every
-    parameter gradient (flat buffer, in-place fp32 wgrad) of the hip conv path match MIOpen's."""
+    parameter gradient (flat buffer, in-place fp32 wgrad) of the hand-written path match the fp32
+    PyTorch module's."""
     from dedloc_amd.models.resnet_swav import BNAct, Bottleneck, ConvNHWC
     from dedloc_amd.utils.flat import FlatParams
 
-    def make():
-        torch.manual_seed(0)
-        down = None
-        if stride != 1 or cin != planes * 4:
-            down = torch.nn.Sequential(ConvNHWC(cin, planes * 4, 1, stride=stride, bias=False), BNAct(planes * 4))
-        return Bottleneck(cin, planes, stride, down)
-
+    torch.manual_seed(0)
+    down = None
+    if stride != 1 or cin != planes * 4:
+        down = torch.nn.Sequential(ConvNHWC(cin, planes * 4, 1, stride=stride, bias=False), BNAct(planes * 4))
+    m = Bottleneck(cin, planes, stride, down)
+    ref = _fp32_twin(m, cuda).train()
+    m = m.to(cuda).train()
     torch.manual_seed(1)
     x = torch.randn(4, cin, H, H, device=cuda).bfloat16().contiguous(memory_format=CL)
     dy = torch.randn(4, planes * 4, H // stride, H // stride, device=cuda).bfloat16().contiguous(memory_format=CL)
-    res = {}
-    for impl in ("hip", "miopen"):
-        m = make().to(cuda).train()
-        for mod in m.modules():
-            if isinstance(mod, ConvNHWC):
-                mod.native = impl == "hip"
-        flat = FlatParams(m.named_parameters(), device=cuda, with_bf16=False, autograd=True, channels_last=True)
-        xx = x.clone().requires_grad_(True)
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = m(xx)
-        y.backward(dy)
-        res[impl] = (y.float(), xx.grad.float(), {n: flat.view(flat.grad, n).clone() for n, _ in m.named_parameters()})
-    # two bf16 implementations (each within 1e-2 of fp32 per op, tests above): the block's BN
-    # backward re-centres the gradient, so their relative difference grows to a few 1e-2 on dX
-    assert _rel(res["hip"][0], res["miopen"][0]) < 1e-2
-    assert _rel(res["hip"][1], res["miopen"][1]) < 4e-2
-    for n, g in res["hip"][2].items():
-        assert _rel(g, res["miopen"][2][n]) < 3e-2, (n, _rel(g, res["miopen"][2][n]))
+    flat = FlatParams(m.named_parameters(), device=cuda, with_bf16=False, autograd=True, channels_last=True)
+    xx = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(xx)
+    y.backward(dy)
+    xr = x.float().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(dy.float())
+    # bf16 vs fp32 (each op within 1e-2, kernel tests above): the block's BN backward re-centres the
+    # gradient, so the relative difference grows to a few 1e-2 on dX
+    assert _rel(y.float(), yr) < 1e-2
+    assert _rel(xx.grad.float(), xr.grad) < 4e-2
+    rp = dict(ref.named_parameters())
+    for n, _ in m.named_parameters():
+        assert _rel(flat.view(flat.grad, n), rp[n].grad) < 3e-2, (n, _rel(flat.view(flat.grad, n), rp[n].grad))

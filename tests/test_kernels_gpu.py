@@ -458,7 +458,7 @@ def test_albert_gpu_matches_cpu(cuda):
 
 @pytest.fixture
 def force_mfma(monkeypatch):
-    monkeypatch.setenv("DEDLOC_GEMM", "mfma")  # exercise gemm.hip even where the library is faster
+    monkeypatch.delenv("DEDLOC_GEMM", raising=False)  # the default dispatch: gemm8 -> gemm.hip -> gemm_small
     yield
 
 
@@ -511,10 +511,10 @@ def test_mfma_gemm_gelu_epilogues(cuda, force_mfma):
     assert rel(db, df.float().sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("policy", ["mfma", "lib"])
+@pytest.mark.parametrize("policy", ["gemm8", "mfma1"])
 def test_gemm_dgelu_transposed_weight(cuda, monkeypatch, policy):
     """gemm_dgelu(trans_w=True) against W^T's forward-layout copy equals the plain-weight form."""
-    monkeypatch.setenv("DEDLOC_GEMM", policy)
+    monkeypatch.setenv("DEDLOC_GEMM", "mfma1" if policy == "mfma1" else "")
     torch.manual_seed(17)
     M, H, I = 2048, 256, 1024
     w2 = (torch.randn(H, I, device=cuda) * 0.1).bfloat16()
@@ -627,14 +627,30 @@ def test_gemm8_pipeline_depths(cuda, force_mfma, M, N, K):
         assert rel(g, 0.5 + dy.float().t() @ a.float()) < 1e-5
 
 
-@pytest.mark.parametrize("policy", ["mfma1", "lib"])
-def test_gemm_other_backends(cuda, monkeypatch, policy):
-    """The register-staged gemm.hip and the hipBLASLt path stay correct (A/B baselines of gemm8)."""
-    monkeypatch.setenv("DEDLOC_GEMM", policy)
+def test_gemm_register_staged_backend(cuda, monkeypatch):
+    """The register-staged gemm.hip (DEDLOC_GEMM=mfma1: the A/B baseline of gemm8) stays correct."""
+    monkeypatch.setenv("DEDLOC_GEMM", "mfma1")
     torch.manual_seed(9)
     a = torch.randn(512, 256, device=cuda).bfloat16()
     w = torch.randn(512, 256, device=cuda).bfloat16()
     assert rel(OPS.gemm(a, w, None, None, False, True, 0), a.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 3000, 128), (1000, 128, 3000), (37, 70, 96), (3000, 128, 512)])
+def test_gemm_small_odd_shapes(cuda, M, N, K):
+    """Shapes outside the tiled kernels' contracts (the SwAV prototypes: N = 3000; their gradient
+    GEMMs: K = 3000) run on gemm_small.hip: forward with bias, dgrad (K-outer B) and the fp32
+    accumulating weight gradient, against fp32 references."""
+    torch.manual_seed(19)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    w = torch.randn(N, K, device=cuda).bfloat16()
+    b = torch.randn(N, device=cuda)
+    assert rel(OPS.gemm(a, w, b, None, False, True, 0), a.float() @ w.float().t() + b) < 1e-2
+    dy = torch.randn(M, N, device=cuda).bfloat16()
+    assert rel(OPS.gemm(dy, w, None, None, False, False, 0), dy.float() @ w.float()) < 1e-2
+    g = torch.full((N, K), 0.25, device=cuda)
+    OPS.gemm_acc_f32(dy, a, g, True, False)
+    assert rel(g, 0.25 + dy.float().t() @ a.float()) < 1e-3
 
 
 @pytest.mark.timeout(240)
