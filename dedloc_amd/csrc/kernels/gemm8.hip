@@ -36,6 +36,8 @@
 //   EPI_GELU   H = bf16(acc + bias); C = gelu_new(H)                          bf16 x2
 //   EPI_DGELU  C = bf16(acc) * gelu_new'(R[m,n]); dbias[n] += sum_m C         bf16 (+ fp32 atomics)
 //   EPI_F32    Cf[z][m,n] = acc  or  += acc (split z = blockIdx.y)            fp32
+#include <cstdlib>
+
 #include "dl_common.h"
 #include "dl_kernels.h"
 
@@ -106,8 +108,19 @@ __device__ __forceinline__ bf16x8 frag(const uint8_t* img, int r0, int ks, int l
   }
 }
 
-__device__ __forceinline__ void store8_bf16(bf16_t* dst, const float* v) {
-  *reinterpret_cast<uint4*>(dst) = pack8_bf16(v);
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Output tiles are written once and not re-read by this kernel: with `nt` the 16-byte stores are
+// non-temporal (streamed past the L2 instead of allocating in it), which keeps the operand tiles
+// of the other workgroups resident while 256 CUs flush their epilogues at once.
+__device__ __forceinline__ void store8_bf16(bf16_t* dst, const float* v, bool nt = false) {
+  const uint4 u = pack8_bf16(v);
+  if (nt) {
+    const u32x4 w = {u.x, u.y, u.z, u.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(dst));
+  } else {
+    *reinterpret_cast<uint4*>(dst) = u;
+  }
 }
 
 struct Args {
@@ -120,6 +133,7 @@ struct Args {
   const bf16_t* R; long ldr;     // residual (STORE) or pre-activation (DGELU)
   bf16_t* H; long ldh;           // pre-activation out (GELU)
   float* dbias;                  // column sums out (DGELU)
+  int nt;                        // non-temporal output stores (bf16 epilogues)
 };
 
 #define DL_MFMA_QUAD(QM, QN)                                                          \
@@ -325,15 +339,15 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] += rv[j];
           }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v);
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
         } else if constexpr (EPI == EPI_GELU) {
           float h[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
-          store8_bf16(p.H + (long)gm * p.ldh + gn, h);
+          store8_bf16(p.H + (long)gm * p.ldh + gn, h, p.nt);
 #pragma unroll
           for (int j = 0; j < 8; ++j) h[j] = gelu_tanh(h[j]);
-          store8_bf16(p.C + (long)gm * p.ldc + gn, h);
+          store8_bf16(p.C + (long)gm * p.ldc + gn, h, p.nt);
         } else if constexpr (EPI == EPI_DGELU) {
           float f[8];
           load_bf16<8>(p.R + (long)gm * p.ldr + gn, f);
@@ -342,7 +356,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
             v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad(f[j]));
             colsum[j] += v[j];
           }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v);
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
         } else {
           float* dst = p.Cf + (long)blockIdx.y * p.slab + (long)gm * p.ldcf + gn;
           if (p.accumulate) {
@@ -406,7 +420,11 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
     if (epi == EPI_DGELU && !R) return -1;
     if (splits != 1) return -1;
   }
-  Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias};
+  static const int nt = [] {
+    const char* e = std::getenv("DEDLOC_GEMM8_NT");
+    return e ? std::atoi(e) : 0;
+  }();
+  Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt};
 #define DL_GEMM8_CASE(AK, BK_, E) \
   if (a_kouter == AK && b_kouter == BK_ && epi == E) return launch8<AK, BK_, E>(a, splits, st);
   DL_GEMM8_CASE(0, 0, EPI_STORE)
