@@ -37,6 +37,7 @@
 //   EPI_DGELU  C = bf16(acc) * gelu_new'(R[m,n]); dbias[n] += sum_m C         bf16 (+ fp32 atomics)
 //   EPI_F32    Cf[z][m,n] = acc  or  += acc (split z = blockIdx.y)            fp32
 #include <cstdlib>
+#include <type_traits>
 
 #include "dl_common.h"
 #include "dl_kernels.h"
@@ -388,11 +389,316 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     }
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Persistent form with deferred output stores (bf16 epilogues).  A CU can issue only ~14 B/clk of
+// 16-byte stores, so a 256x256 bf16 tile (128 KiB) needs ~9K cycles to leave the CU; in the
+// one-tile-per-workgroup form those stores sit between two main loops (16% of the QKV GEMM).
+// Here one workgroup per CU walks its tiles, and tile i's output leaves during tile i+1:
+//   * the epilogue packs the tile into registers (acc is dead by then): 12 of its 16 x 16 B per
+//     lane are stored right after tile i+1's prologue loads are issued (queued behind them, so the
+//     prologue wait never waits for them);
+//   * the last 4 x 16 B per lane go to the 32 KiB of LDS the pipeline leaves free (128 + 32 = 160
+//     KiB) and leave one per phase of tile i+1's first K-tile, whose counted wait then allows
+//     vmcnt(6) instead of vmcnt(4) (two stores + two half-tiles issued after the awaited loads);
+//   * stores are raw buffer stores against a per-tile resource whose range ends at the last valid
+//     row: rows past M are dropped by the hardware range check, so every store instruction is
+//     issued (exact vmcnt accounting) and there is no divergent branch.
+// ---------------------------------------------------------------------------------------------
+constexpr int SPARE = 32768;
+
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, unsigned off, const uint4& v, bool nt) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  if (nt)
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 2);  // slc: streaming
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(bf16_t* base, long ld, int m0, int M) {
+  const long rows = min(BM, M - m0);
+  return __builtin_amdgcn_make_buffer_rsrc(base + (long)m0 * ld, 0, (int)(rows * ld * 2), 0x00020000);
+}
+
+template <bool AKO, bool BKO, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
+  static_assert(EPI != EPI_F32, "the persistent form covers the bf16 epilogues");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM + SPARE];
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int tiles_n = p.N / BN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int total = tiles_m * tiles_n;
+  const int nk = p.K / BK;
+  uint8_t* spare = smem + SMEM + w * 4096;  // this wave's deferred passes 4..7 (16 B per lane each)
+  const bool nt = p.nt != 0;
+
+  // the previous tile's output: qm = 0 half (imm) and the deferred qm = 1 half (dreg + spare)
+  int dm0 = -1;
+  __amdgpu_buffer_rsrc_t drs = tile_rsrc(p.C, p.ldc, 0, p.M);
+  uint4 imm[12];
+  // byte offset (in the deferred tile's resource) of pass j of row half qm for this lane
+  int lane = lane0;
+  auto out_off = [&](int dn0, int qm, int j) -> unsigned {
+    const int rch = lane & 7, rr = lane >> 3;
+    return (unsigned)((((long)(wm * 128 + qm * 64 + j * 8 + rr)) * p.ldc + dn0 + wn * 64 + rch * 8) * 2);
+  };
+  int dn0 = 0;
+
+  floatx4 acc[2][2][4][2];
+  bf16x8 af[4][2], bfr[2][2];
+  const int ra = wm * 64, cb = wn * 32;
+
+  for (int tix = blockIdx.x; tix < total; tix += gridDim.x) {
+    // the lane id through an opaque move, once per tile: every lane-dependent address below is
+    // then recomputed per tile instead of being hoisted out of the tile loop into ~40 registers
+    // that would stay live through the main loop (the persistent form's register limit)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
+    const int rch = lane & 7, rr = lane >> 3;
+    const int bid = xcd_remap(tix, total);
+    const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+#define DL_STAGEP(T, KSLOT)                                                                         \
+  do {                                                                                              \
+    uint8_t* slot_ = smem + ((T) & 1) * BUF + (KSLOT) * HALF;                                       \
+    const int k0_ = (T) * BK;                                                                       \
+    if ((KSLOT) == 0) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 0, slot_, w, lane);          \
+    else if ((KSLOT) == 1) stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 1, slot_, w, lane);      \
+    else if ((KSLOT) == 2) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 1, slot_, w, lane);     \
+    else stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 0, slot_, w, lane);                        \
+  } while (0)
+
+    // prologue: tile 0 and half of tile 1, then the previous tile's first row half behind them
+    DL_STAGEP(0, 0); DL_STAGEP(0, 1); DL_STAGEP(0, 2); DL_STAGEP(0, 3);
+    if (nk > 1) { DL_STAGEP(1, 0); DL_STAGEP(1, 1); }
+    const bool def = dm0 >= 0;
+    if (def) {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) bstore(drs, out_off(dn0, j >> 3, j & 7), imm[j], nt);
+      if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else {
+      if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    // accumulators zeroed only now: the previous tile's 48 output registers are free again
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int d = 0; d < 2; ++d) acc[a][b][c][d] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // one K-tile; CARRY: this K-tile issues the previous tile's 4 deferred stores (one per phase,
+    // from the spare LDS) — a compile-time flag, so the steady-state loop carries no store code
+    auto ktile = [&](int t, auto carry) {
+      constexpr bool CARRY = decltype(carry)::value;
+      const uint8_t* buf = smem + (t & 1) * BUF;
+      const uint8_t* iA0 = buf;
+      const uint8_t* iB1 = buf + HALF;
+      const uint8_t* iA1 = buf + 2 * HALF;
+      const uint8_t* iB0 = buf + 3 * HALF;
+      const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+      auto carry_store = [&](int ph) {
+        if constexpr (CARRY)
+          bstore(drs, out_off(dn0, 1, 4 + ph), *reinterpret_cast<const uint4*>(spare + ph * 1024 + lane * 16), nt);
+      };
+
+      // ---- phase 0
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA0, ra + mi * 16, ks, lane);
+      carry_store(0);
+      if (more1) DL_STAGEP(t + 1, 2);
+      __builtin_amdgcn_s_barrier();
+      DL_MFMA_QUAD(0, 0);
+      __builtin_amdgcn_s_barrier();
+
+      // ---- phase 1
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB1, cb + ni * 16, ks, lane);
+      carry_store(1);
+      if (more1) DL_STAGEP(t + 1, 3);
+      __builtin_amdgcn_s_barrier();
+      DL_MFMA_QUAD(0, 1);
+      __builtin_amdgcn_s_barrier();
+
+      // ---- phase 2
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA1, ra + mi * 16, ks, lane);
+      carry_store(2);
+      if (more2) DL_STAGEP(t + 2, 0);
+      __builtin_amdgcn_s_barrier();
+      DL_MFMA_QUAD(1, 1);
+      __builtin_amdgcn_s_barrier();
+
+      // ---- phase 3
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+      carry_store(3);
+      if (more2) {
+        DL_STAGEP(t + 2, 1);
+        // awaited: the half-tiles issued up to phase 1; after them: [store] 2 glds [store] 2 glds
+        if constexpr (CARRY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      DL_MFMA_QUAD(1, 0);
+      __builtin_amdgcn_s_barrier();
+    };
+    int t0 = 0;
+    if (def) {
+      ktile(0, std::true_type{});
+      t0 = 1;
+    }
+    for (int t = t0; t < nk; ++t) ktile(t, std::false_type{});
+#undef DL_STAGEP
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+    // every wave's deferred stores of the previous tile have left (the spare LDS is rewritten
+    // below) and every fragment read is done (the epilogue reuses the pipeline's LDS)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // ---------------------------------------------------------------- epilogue -> registers
+    uint8_t* ep = smem + w * 16384;
+    const int crow = 4 * (lane >> 4), ccol = lane & 15;
+    float bias_v[2][2];
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        bias_v[qn][ni] = 0.f;
+        if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
+          if (p.bias) bias_v[qn][ni] = p.bias[n0 + wn * 64 + qn * 32 + ni * 16 + ccol];
+      }
+    float colsum[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
+    const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.C, p.ldc, m0, p.M);
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm) {
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = mi * 16 + crow + i;
+              const int c = qn * 32 + ni * 16 + ccol;
+              const int q = (c >> 2) ^ (r & 1);
+              *reinterpret_cast<float*>(ep + r * 256 + q * 16 + (c & 3) * 4) = acc[qm][qn][mi][ni][i] + bias_v[qn][ni];
+            }
+#pragma unroll
+      for (int pass = 0; pass < 8; ++pass) {
+        const int r = pass * 8 + rr;
+        const float4 lo = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch) ^ (r & 1)) << 4));
+        const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int gm = m0 + wm * 128 + qm * 64 + r;
+        const int gmc = min(gm, p.M - 1);  // rows past M: computed, then dropped by the range check
+        const int gn = n0 + wn * 64 + rch * 8;
+        if constexpr (EPI == EPI_STORE) {
+          if (p.R) {
+            float rv[8];
+            load_bf16<8>(p.R + (long)gmc * p.ldr + gn, rv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += rv[j];
+          }
+        } else if constexpr (EPI == EPI_GELU) {
+          float h[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
+          bstore(tile_rsrc(p.H, p.ldh, m0, p.M),
+                 (unsigned)((((long)(wm * 128 + qm * 64 + r)) * p.ldh + gn) * 2), pack8_bf16(h), nt);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(h[j]);
+        } else {  // EPI_DGELU
+          float f[8];
+          load_bf16<8>(p.R + (long)gmc * p.ldr + gn, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad(f[j]));
+            if (gm < p.M) colsum[j] += v[j];
+          }
+        }
+        const uint4 packed = pack8_bf16(v);
+        if (qm == 0 || pass < 4) imm[qm * 8 + pass] = packed;
+        else *reinterpret_cast<uint4*>(spare + (pass - 4) * 1024 + lane * 16) = packed;
+      }
+    }
+    if constexpr (EPI == EPI_DGELU) {
+      if (p.dbias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float s = colsum[j];
+          s += __shfl_xor(s, 8, 64);
+          s += __shfl_xor(s, 16, 64);
+          s += __shfl_xor(s, 32, 64);
+          colsum[j] = s;
+        }
+        if (lane < 8) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + wn * 64 + lane * 8 + j], colsum[j]);
+        }
+      }
+    }
+    dm0 = m0;
+    dn0 = n0;
+    drs = crs;
+    // the next prologue's LDS-DMA overwrites the epilogue staging: all waves' reads done first
+    // (and the outstanding epilogue loads / GELU stores / atomics retired, for exact counting)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // the last tile: flush both row halves
+  if (dm0 >= 0) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) bstore(drs, out_off(dn0, j >> 3, j & 7), imm[j], nt);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bstore(drs, out_off(dn0, 1, 4 + j), *reinterpret_cast<const uint4*>(spare + j * 1024 + lane * 16), nt);
+  }
+}
+
 #undef DL_MFMA_QUAD
+
+int persistent_ctas() {  // read per call: tests and benchmarks A/B the two forms in one process
+  const char* e = std::getenv("DEDLOC_GEMM8_PERSIST");
+  return e ? std::atoi(e) : 0;
+}
 
 template <bool AKO, bool BKO, int EPI>
 int launch8(const Args& a, int splits, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
+  if constexpr (EPI != EPI_F32) {
+    // DEDLOC_GEMM8_PERSIST=n: the persistent deferred-store form on min(tiles, n) workgroups
+    // (n = 256: one per CU of an MI355X)
+    const int ctas = persistent_ctas();
+    if (ctas > 0 && splits == 1 && tiles > ctas && a.K / BK >= 2) {
+      gemm8p_kernel<AKO, BKO, EPI><<<dim3(ctas), NT, 0, st>>>(a);
+      return 0;
+    }
+  }
   gemm8_kernel<AKO, BKO, EPI><<<dim3(tiles, splits), NT, 0, st>>>(a);
   return 0;
 }
@@ -420,10 +726,8 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
     if (epi == EPI_DGELU && !R) return -1;
     if (splits != 1) return -1;
   }
-  static const int nt = [] {
-    const char* e = std::getenv("DEDLOC_GEMM8_NT");
-    return e ? std::atoi(e) : 0;
-  }();
+  const char* nte = std::getenv("DEDLOC_GEMM8_NT");
+  const int nt = nte ? std::atoi(nte) : 0;
   Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt};
 #define DL_GEMM8_CASE(AK, BK_, E) \
   if (a_kouter == AK && b_kouter == BK_ && epi == E) return launch8<AK, BK_, E>(a, splits, st);
@@ -431,6 +735,7 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
   DL_GEMM8_CASE(0, 0, EPI_GELU)
   DL_GEMM8_CASE(0, 1, EPI_STORE)
   DL_GEMM8_CASE(0, 1, EPI_DGELU)
+  DL_GEMM8_CASE(0, 0, EPI_DGELU)
   DL_GEMM8_CASE(1, 1, EPI_F32)
   DL_GEMM8_CASE(0, 0, EPI_F32)
 #undef DL_GEMM8_CASE

@@ -683,3 +683,40 @@ def test_albert_pretraining_converges_on_gpu(cuda):
         losses.append(float(out["loss"].detach()))
     assert all(math.isfinite(v) for v in losses)
     assert losses[-1] < 0.5 * losses[0], (losses[0], losses[-1])
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 1024), (3000, 3072, 256), (1000, 256, 128)])
+def test_gemm8_persistent_deferred_stores_bitwise(cuda, monkeypatch, M, N, K):
+    """The persistent gemm8 form (DEDLOC_GEMM8_PERSIST=n workgroups walking the tiles, each tile's
+    output stored during the next tile's prologue / first K-tile) computes exactly what the
+    one-tile-per-workgroup form does, for every bf16 epilogue, with M tails and non-temporal
+    stores."""
+    torch.manual_seed(23)
+    x = (torch.rand(M, K, device=cuda) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device=cuda) * 2 - 1) * 0.1).bfloat16()
+    b = torch.randn(N, device=cuda)
+    r = torch.randn(M, N, device=cuda).bfloat16()
+    f = torch.randn(M, N, device=cuda).bfloat16()
+    dy = (torch.rand(M, K, device=cuda) * 2 - 1).bfloat16()
+    wt = w.t().contiguous()  # [K, N]: the dgelu B operand in forward layout is [N, K] = w
+
+    def run():
+        db = torch.zeros(N, device=cuda)
+        return [OPS.gemm(x, w, b, None, False, True, 0), OPS.gemm(x, w, b, r, False, True, 0),
+                *OPS.gemm_gelu(x, w, b), OPS.gemm(x, w, None, None, False, True, 0),
+                OPS.gemm_dgelu(dy, w, f, db, True), db, OPS.gemm(dy, wt, None, None, False, False, 0)]
+
+    monkeypatch.setenv("DEDLOC_GEMM8_PERSIST", "0")
+    base = run()
+    for ctas, nt in ((8, "0"), (5, "1"), (256, "0")):
+        monkeypatch.setenv("DEDLOC_GEMM8_PERSIST", str(ctas))
+        monkeypatch.setenv("DEDLOC_GEMM8_NT", nt)
+        out = run()
+        torch.cuda.synchronize()
+        for i, (o, e) in enumerate(zip(out, base)):
+            if e.dtype == torch.float32:  # dbias: atomics in a different order
+                torch.testing.assert_close(o, e, rtol=1e-5, atol=1e-4)
+            else:
+                assert torch.equal(o, e), (ctas, nt, i, (o.float() - e.float()).abs().max().item())
+    ref = x.float() @ w.float().t() + b
+    assert rel(base[0], ref) < 1e-2
