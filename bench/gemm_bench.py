@@ -1,14 +1,15 @@
-"""ALBERT-large layer GEMMs: the hand-written MFMA kernels vs hipBLASLt (same random bf16 data, one
+"""ALBERT-large layer GEMMs: the hand-written MFMA kernel variants (same random bf16 data, one
 process, interleaved rounds — cdna_hip_programming.md §5.4 rules 24/25).
 
-Variants per GEMM (the dispatch policy is read per call, so one process times them all):
-  gemm8 : csrc/kernels/gemm8.hip (LDS-DMA 8-phase pipeline)         DEDLOC_GEMM=mfma
-  gemm1 : csrc/kernels/gemm.hip (register-staged)                   DEDLOC_GEMM=mfma1
-  lt    : direct hipBLASLt (autotuned) + separate epilogue kernels  DEDLOC_GEMM=lib
+Variants per GEMM (the dispatch knobs are read per call, so one process times them all):
+  gemm8  : csrc/kernels/gemm8.hip, one tile per workgroup (LDS-DMA 8-phase pipeline)
+  g8p    : gemm8's persistent form, deferred output stores             DEDLOC_GEMM8_PERSIST=256
+  g8pnt  : g8p with non-temporal output stores                         + DEDLOC_GEMM8_NT=1
+  gemm1  : csrc/kernels/gemm.hip (register-staged)                     DEDLOC_GEMM=mfma1
 Fused epilogues are timed as the op the model calls (gemm_gelu: bias + GELU; gemm_dgelu: GELU'
-+ bias-gradient column sums), so "lt" includes its separate elementwise kernel.
++ bias-gradient column sums).
 
-usage: T=131072 python bench/gemm_bench.py [--check]
+usage: T=131072 VARIANTS=gemm8,g8p,g8pnt python bench/gemm_bench.py [--check]
 """
 import json
 import os
@@ -20,7 +21,11 @@ import torch
 import dedloc_amd.ops  # noqa: F401
 
 O = torch.ops.dedloc
-VARIANTS = {"gemm8": "mfma", "gemm1": "mfma1", "lt": "lib"}
+VARIANTS = {"gemm8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "0"},
+            "g8p": {"DEDLOC_GEMM8_PERSIST": "256", "DEDLOC_GEMM8_NT": "0"},
+            "g8pnt": {"DEDLOC_GEMM8_PERSIST": "256", "DEDLOC_GEMM8_NT": "1"},
+            "g8nt": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1"},
+            "gemm1": {"DEDLOC_GEMM": "mfma1"}}
 
 
 def timeit(fn, iters=10):
@@ -33,9 +38,15 @@ def timeit(fn, iters=10):
     return (time.perf_counter() - t0) / iters
 
 
+def set_policy(pol):
+    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT"):
+        os.environ.pop(k, None)
+    os.environ.update(pol)
+
+
 def with_policy(pol, fn):
     def run():
-        os.environ["DEDLOC_GEMM"] = pol
+        set_policy(pol)
         return fn()
     return run
 
@@ -48,7 +59,7 @@ def rel(a, b):
 def main():
     T = int(os.environ.get("T", 32768))
     check = "--check" in sys.argv
-    variants = os.environ.get("VARIANTS", "gemm8,lt").split(",")
+    variants = os.environ.get("VARIANTS", "gemm8,g8p").split(",")
     dev = torch.device("cuda")
     H, I = 1024, 4096
     torch.manual_seed(0)
@@ -80,7 +91,7 @@ def main():
             if check:
                 outs = {}
                 for v in variants:
-                    os.environ["DEDLOC_GEMM"] = VARIANTS[v]
+                    set_policy(VARIANTS[v])
                     g.zero_()
                     db.zero_()
                     o = fn()
@@ -102,7 +113,7 @@ def main():
                 row[f"{v}_tflops"] = round(fl / t / 1e12, 1)
             res.append(row)
             print(json.dumps(row), flush=True)
-    os.environ.pop("DEDLOC_GEMM", None)
+    set_policy({})
 
 
 if __name__ == "__main__":

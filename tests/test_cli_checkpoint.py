@@ -126,7 +126,7 @@ def test_run_trainer_single_cpu_peer(tmp_path, sahajbert):
 @pytest.mark.timeout(420)
 def test_launch_collaboration_coordinator_trainers_aux_cpu(tmp_path):
     """The single-node launcher (AWS_runner stand-in, D9): coordinator + 2 trainers + 1 auxiliary peer
-    in one world on CPU/gloo; the trainers finish their global steps and the coordinator's metrics
+    on CPU/gloo (no launch-time world: the peers meet through the coordinator's DHT); the trainers finish their global steps and the coordinator's metrics
     file reports both trainers alive (the aux peer publishes no training metrics)."""
     logs = tmp_path / "logs"
     cmd = [sys.executable, "-m", "dedloc_amd.cli.launch_collaboration", "--n_trainers", "2", "--n_aux", "1",
@@ -143,7 +143,8 @@ def test_launch_collaboration_coordinator_trainers_aux_cpu(tmp_path):
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400, env=env)
     tails = {p.name: p.read_text()[-1500:] for p in logs.glob("*.log")}
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:], tails)
-    assert "coordinator DHT root at" in r.stdout
+    events = [json.loads(x) for x in (logs / "launcher_events.jsonl").read_text().splitlines()]
+    assert any(e["kind"] == "coordinator" and e["dht_root"] for e in events), events
     for t in ("trainer0.log", "trainer1.log"):
         assert "Traceback" not in tails[t], tails[t]
     recs = [json.loads(x) for x in (logs / "coordinator_metrics.jsonl").read_text().splitlines()] \
