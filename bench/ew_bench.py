@@ -1,5 +1,9 @@
 """Memory-bound kernels of the ALBERT layer at the B=256 token count (T=131072): achieved HBM rate,
 v1 (DEDLOC_EW=1) vs v2 (default), interleaved in one process on random data."""
+import os as _os
+import sys as _sys
+
+_sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
 import json
 import os
 import time

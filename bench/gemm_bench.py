@@ -11,6 +11,10 @@ Fused epilogues are timed as the op the model calls (gemm_gelu: bias + GELU; gem
 
 usage: T=131072 VARIANTS=gemm8,g8p,g8pnt python bench/gemm_bench.py [--check]
 """
+import os as _os
+import sys as _sys
+
+_sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
 import json
 import os
 import sys

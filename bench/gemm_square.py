@@ -1,5 +1,9 @@
 """Main-loop comparison at a long reduction (epilogue amortised): gemm8 vs hipBLASLt, M=N=K=8192
 and the ALBERT N=1024/3072 shapes with K=8192 (random data, interleaved, one process)."""
+import os as _os
+import sys as _sys
+
+_sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
 import json
 import os
 import time

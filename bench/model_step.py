@@ -4,6 +4,10 @@
 --impl hf     : HF transformers AlbertForPreTraining, bf16 autocast, PyTorch eager/SDPA —
                 the "PyTorch-eager on MI355X" baseline BASELINE.md asks to record.
 """
+import os as _os
+import sys as _sys
+
+_sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
 import argparse
 import math
 import json
