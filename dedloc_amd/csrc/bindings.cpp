@@ -469,14 +469,32 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
 
 // fp32-accumulating weight gradient c += op(a) op(b) through gemm8: the token (reduction) dimension
 // is split into S slices written as fp32 slabs and summed into c (no atomics); -1 if unsupported.
+// Weight gradients have few output tiles (48 for ALBERT's QKV) and a very long reduction (the
+// tokens), so the reduction is split into S slices; S is chosen for whole waves of workgroups on
+// the 256 CUs (one gemm8 workgroup per CU): 48 tiles x 8 slices = 384 workgroups would leave half
+// the chip idle for the second half of the kernel, 48 x 16 = 768 = 3 full waves does not.  Among
+// the splits with at least 1024 reduction rows per slice, the best wave efficiency wins, the
+// smaller S on ties (fewer slab bytes to sum).
 int wgrad_splits8(const Mat& A, const Mat& B) {
   const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
-  int S = 1;
-  if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) S = std::max(1, std::atoi(e));
-  else
-    while (S < 16 && tiles * S * 2 <= 512 && A.k % (S * 2 * 64) == 0 && A.k / (S * 2) >= 1024) S *= 2;
-  while (S > 1 && A.k % (S * 64)) S /= 2;
-  return S;
+  if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) {
+    int S = std::max(1, std::atoi(e));
+    while (S > 1 && A.k % (S * 64)) S /= 2;
+    return S;
+  }
+  constexpr int64_t kCUs = 256;
+  int best = 1;
+  double best_eff = 0.0;
+  for (int S = 1; S <= 32; S *= 2) {
+    if (A.k % (S * 64) || (S > 1 && A.k / S < 1024)) break;
+    const int64_t wg = tiles * S;
+    const double eff = (double)wg / (double)(kCUs * ((wg + kCUs - 1) / kCUs));
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = S;
+    }
+  }
+  return best;
 }
 
 int own_wgrad(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, at::Tensor c, hipStream_t st) {
