@@ -321,11 +321,14 @@ class DecentralizedAverager:
         return self.get_current_state()
 
     def publish_state_sharing(self, step: int):
+        """Advertise this peer's state server (asynchronous DHT store: the returned future resolves
+        once the record is stored)."""
         if self.state_server is None:
-            return
+            return None
         self.local_step_for_state = step
-        self.dht.store(f"{self.prefix}_state_sharing", {"endpoint": self.state_server.endpoint, "step": int(step)},
-                       get_dht_time() + self.metadata_expiration, subkey=self.peer_id, return_future=True)
+        return self.dht.store(f"{self.prefix}_state_sharing",
+                              {"endpoint": self.state_server.endpoint, "step": int(step)},
+                              get_dht_time() + self.metadata_expiration, subkey=self.peer_id, return_future=True)
 
     def load_state_from_peers(self, timeout: float = 15.0, min_step: int = 0):
         """(metadata, tensors) from the freshest state-sharing peer whose advertised step is at least

@@ -387,8 +387,8 @@ std::tuple<at::Tensor, at::Tensor> attn_softmax_bwd(const at::Tensor& s, const a
 //                  epilogues (bias, residual, bias + GELU, GELU' + bias gradient, fp32 split-K slabs)
 //   gemm.hip       register-staged 256x256 tiles — tiled shapes outside gemm8's contract
 //                  (N % 256 != 0: the SwAV 1x1 convs with 64 / 128 outputs, the stem)
-//   gemm_small.hip any shape and stride, 64x64 tiles — the rest (SwAV prototypes N = K = 3000,
-//                  small heads); a few GFLOP per step at most
+//   gemm_small.hip any shape and stride, 128x128 tiles with a slab-split reduction — the rest
+//                  (N = 128 embedding GEMMs, the tied MLM decoder's gradients, SwAV prototypes)
 // There is no vendor-library or ATen path: a shape no kernel takes is an error, not a fallback.
 // The fp32-accumulating weight-gradient form writes straight into the fp32 gradient buffer, so the
 // shared ALBERT layer's 24 weight-gradient contributions never round through bf16.
@@ -437,15 +437,26 @@ int own_gemm(int akout, int bkout, int epi, const bf16_t* A, long lda, const bf1
   return dl_gemm(akout, bkout, epi, A, lda, B, ldb, M, N, K, C, ldc, Cf, ldcf, bias, R, ldr, H, ldh, dbias, 1, st);
 }
 
+// gemm_small with its reduction split chosen for the shape (fp32 slab workspace from the caching
+// allocator when split)
+void small_gemm(int epi, const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, bf16_t* C, long ldc,
+                float* Cf, long ldcf, int accumulate, const float* bias, const bf16_t* R, long ldr, hipStream_t st) {
+  const int M = (int)A.rows, N = (int)B.rows, K = (int)A.k;
+  const int S = dl_gemm_small_splits(M, N, K);
+  at::Tensor ws;
+  if (S > 1) ws = at::empty({(int64_t)S * M * N}, a.options().dtype(at::kFloat));
+  check(dl_gemm_small(epi, cbf(a), A.srow(), A.sk(), cbf(b), B.srow(), B.sk(), M, N, K, C, ldc, Cf, ldcf, accumulate,
+                      bias, R, ldr, S, S > 1 ? f32(ws) : nullptr, st),
+        "gemm_small");
+}
+
 // C (bf16) = op(A) op(B) (+ bias) (+ R): tiled kernels, else gemm_small.
 void gemm_store(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, bf16_t* C, long ldc,
                 const float* bias, const bf16_t* R, long ldr, hipStream_t st) {
   if (own_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, C, ldc, nullptr,
                0, bias, R, ldr, nullptr, 0, nullptr, st) == 0)
     return;
-  check(dl_gemm_small(0, cbf(a), A.srow(), A.sk(), cbf(b), B.srow(), B.sk(), (int)A.rows, (int)B.rows, (int)A.k, C,
-                      ldc, nullptr, 0, 0, bias, R, ldr, st),
-        "gemm");
+  small_gemm(0, A, B, a, b, C, ldc, nullptr, 0, 0, bias, R, ldr, st);
 }
 
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
@@ -525,9 +536,7 @@ void gemm_acc_f32(const at::Tensor& a, const at::Tensor& b, at::Tensor c, bool t
   if (dl_gemm(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, nullptr, 0,
               f32(c), c.stride(0), nullptr, nullptr, 0, nullptr, 0, nullptr, splits, cur_stream(a)) == 0)
     return;
-  check(dl_gemm_small(1, cbf(a), A.srow(), A.sk(), cbf(b), B.srow(), B.sk(), (int)A.rows, (int)B.rows, (int)A.k,
-                      nullptr, 0, f32(c), c.stride(0), 1, nullptr, nullptr, 0, cur_stream(a)),
-        "gemm_acc_f32");
+  small_gemm(1, A, B, a, b, nullptr, 0, f32(c), c.stride(0), 1, nullptr, nullptr, 0, cur_stream(a));
 }
 
 // Weight gradient of a weight that several consecutive backward calls share (ALBERT's one layer,
@@ -551,11 +560,16 @@ struct SlabKeyHash {
   }
 };
 constexpr size_t kMaxSlabSets = 16;
+struct SlabSet {
+  at::Tensor slabs;
+  uint64_t used = 0;  // LRU clock
+  bool live = false;  // holds partial sums of the current series (not yet added into c)
+};
 std::mutex g_slab_mu;
-std::unordered_map<SlabKey, std::pair<at::Tensor, uint64_t>, SlabKeyHash> g_slabs;
+std::unordered_map<SlabKey, SlabSet, SlabKeyHash> g_slabs;
 uint64_t g_slab_clock = 0;
 
-at::Tensor shared_slabs(const at::Tensor& c, int64_t S) {
+SlabSet& shared_slabs(const at::Tensor& c, int64_t S) {
   std::lock_guard<std::mutex> lock(g_slab_mu);
   const SlabKey key{c.data_ptr(), (int64_t)c.get_device(), S, c.size(0), c.size(1)};
   auto it = g_slabs.find(key);
@@ -563,13 +577,13 @@ at::Tensor shared_slabs(const at::Tensor& c, int64_t S) {
     while (g_slabs.size() >= kMaxSlabSets) {
       auto lru = g_slabs.begin();
       for (auto j = g_slabs.begin(); j != g_slabs.end(); ++j)
-        if (j->second.second < lru->second.second) lru = j;
+        if (j->second.used < lru->second.used) lru = j;
       g_slabs.erase(lru);
     }
-    it = g_slabs.emplace(key, std::make_pair(at::empty({S, c.size(0), c.size(1)}, c.options()), 0)).first;
+    it = g_slabs.emplace(key, SlabSet{at::empty({S, c.size(0), c.size(1)}, c.options())}).first;
   }
-  it->second.second = ++g_slab_clock;
-  return it->second.first;
+  it->second.used = ++g_slab_clock;
+  return it->second;
 }
 
 int64_t clear_workspaces() {
@@ -587,15 +601,20 @@ void gemm_acc_f32_shared(const at::Tensor& a, const at::Tensor& b, at::Tensor c,
   TORCH_CHECK(A.k == B.k && c.size(0) == A.rows && c.size(1) == B.rows, "gemm_acc_f32_shared: shape mismatch");
   const int S = use_gemm8() && c.is_contiguous() ? wgrad_splits8(A, B) : 1;
   if (S > 1) {
-    at::Tensor slabs = shared_slabs(c, S);
+    SlabSet& set = shared_slabs(c, S);
+    if (first) set.live = false;
+    // a shape gemm8 refuses (small heads, odd widths) falls through to the direct fp32 accumulation;
+    // slabs that hold this series' earlier partial sums are still added by the last call
     const int rc = dl_gemm8(A.kouter, B.kouter, 3, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
-                            nullptr, 0, f32(slabs), B.rows, A.rows * B.rows, first ? 0 : 1, nullptr, nullptr, 0,
-                            nullptr, 0, nullptr, S, cur_stream(a));
-    if (rc == 0) {
-      if (last) check(dl_sum_slabs(f32(c), f32(slabs), S, (size_t)c.numel(), cur_stream(a)), "sum_slabs");
-      return;
+                            nullptr, 0, f32(set.slabs), B.rows, A.rows * B.rows, set.live ? 1 : 0, nullptr, nullptr,
+                            0, nullptr, 0, nullptr, S, cur_stream(a));
+    if (rc == 0) set.live = true;
+    else gemm_acc_f32(a, b, c, trans_a, trans_b);
+    if (last && set.live) {
+      check(dl_sum_slabs(f32(c), f32(set.slabs), S, (size_t)c.numel(), cur_stream(a)), "sum_slabs");
+      set.live = false;
     }
-    TORCH_CHECK(first, "gemm_acc_f32_shared: gemm8 refused a shape it accepted for an earlier call");
+    return;
   }
   gemm_acc_f32(a, b, c, trans_a, trans_b);
 }

@@ -130,7 +130,9 @@ int dl_avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream
 int dl_l2norm_fwd(const bf16_t* x, bf16_t* y, float* rinv, int rows, int D, float eps, hipStream_t st);
 int dl_l2norm_bwd(const bf16_t* dy, const bf16_t* y, const float* rinv, bf16_t* dx, int rows, int D, hipStream_t st);
 
-// gemm_small.hip: any-shape / any-stride bf16 MFMA GEMM (epi 0: bf16 C (+bias)(+R); 1: fp32 Cf (+)=)
+// gemm_small.hip: any-shape / any-stride bf16 MFMA GEMM (epi 0: bf16 C (+bias)(+R); 1: fp32 Cf (+)=).
+// splits > 1 splits the reduction into fp32 slabs: ws must hold splits * M * N floats.
+int dl_gemm_small_splits(int M, int N, int K);
 int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B, long sbn, long sbk, int M, int N,
                   int K, bf16_t* C, long ldc, float* Cf, long ldcf, int accumulate, const float* bias, const bf16_t* R,
-                  long ldr, hipStream_t st);
+                  long ldr, int splits, float* ws, hipStream_t st);

@@ -1,18 +1,29 @@
-// General-shape bf16 MFMA GEMM for the shapes outside the tiled kernels' contracts (SURVEY.md
-// §2.7 K20/K23 and the small ALBERT heads): any M, N, K and any element strides — the SwAV
-// prototypes (N = 3000, and K = 3000 in their gradient GEMMs), the 512-row SwAV head, the SOP /
-// pooler heads, the conv stem's column matrix.  Correctness-first and simple: the big GEMMs of
-// both models go to gemm8.hip / gemm.hip; what lands here is a few GFLOP per step at most.
+// General-shape bf16 MFMA GEMM for the shapes outside the 256x256-tiled kernels' contracts
+// (SURVEY.md §2.7 K20/K23): any M, N, K and any element strides.  In ALBERT these are the
+// factorized-embedding GEMMs (hidden 1024 <-> embedding 128: N = 128) and the tied MLM decoder's
+// gradients (vocabulary 30000 on one side, 128 on the other); in SwAV the prototypes (N = K = 3000)
+// and the small heads.  Several of them have a very long reduction and few output tiles (the
+// embedding-mapping weight gradient: 1024 x 128 outputs over 262144 tokens), so the reduction is
+// split over gridDim.z into fp32 slabs that a second pass sums (fixed order: deterministic) and
+// finishes (bias, residual, bf16 rounding, or fp32 (+)= into the gradient).
 //
 //   C[m, n] = sum_k A(m, k) B(n, k)    A(m, k) = A[m*sam + k*sak], B(n, k) = B[n*sbn + k*sbk]
 //
-// Tile 64 x 64 x 32, 256 threads = 4 waves (2 x 2), 32 x 32 outputs per wave = 2 x 2
-// v_mfma_f32_16x16x32_bf16.  Operands are staged element-wise with bounds checks (zero fill) into
-// LDS rows of 32 k (+8 pad, keeps the 16-byte fragment reads aligned and bank-spread); the global
-// walk follows whichever operand stride is unit (k or row), so either layout coalesces.
+// Tile 128 x 128 x 32, 256 threads = 4 waves (2 x 2), 64 x 64 outputs per wave = 4 x 4
+// v_mfma_f32_16x16x32_bf16.  Operands go global -> registers (next K-step prefetched while the
+// current one computes) -> LDS rows of 32 k (+8 pad: 80-byte rows keep the 16-byte fragment reads
+// aligned and spread over the banks).  The global walk follows the unit-stride side of each
+// operand, 16 bytes per lane when it is aligned:
+//   KIN  k is unit stride: 8 consecutive k of one row per lane, one 16-B LDS write
+//   RIN  rows are unit stride (transposed operands: weight-gradient inputs): 8 consecutive rows
+//        of one k per lane, scattered into the k-rows of LDS as eight 2-byte writes
+// A partial 8-chunk at a tile edge (or an operand that is not 16-byte aligned) is read
+// element-wise with bounds checks (zero fill).
 //
 // Epilogues: EPI_STORE C = acc (+ bias[n]) (+ R[m, n])  bf16 (row stride ldc)
 //            EPI_F32   Cf[m, n] = acc  or  += acc        fp32 (row stride ldcf)
+#include <algorithm>
+
 #include "dl_common.h"
 #include "dl_kernels.h"
 
@@ -20,102 +31,234 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int TM = 64, TN = 64, TK = 32, ROW = TK + 8;
+constexpr int TM = 128, TN = 128, TK = 32, ROW = TK + 8, NTH = 256;
+enum { L_KIN = 0, L_RIN = 1 };
 
 struct SmallArgs {
   const bf16_t* A; long sam, sak;
   const bf16_t* B; long sbn, sbk;
-  int M, N, K;
+  int M, N, K, kchunk;
   bf16_t* C; long ldc;
-  float* Cf; long ldcf; int accumulate;
+  float* Cf; long ldcf; long slab; int accumulate;
   const float* bias;
   const bf16_t* R; long ldr;
 };
 
-__device__ __forceinline__ void stage(const bf16_t* __restrict__ p, long srow, long sk, int r0, int k0, int rows,
-                                      int K, bf16_t* img) {
-  // 64 rows x 32 k = 2048 elements, 8 per thread
+// Two 8-element chunks of a 128 x 32 operand tile per thread, into registers.
+template <int L, bool VEC>
+__device__ __forceinline__ void gload(const bf16_t* __restrict__ p, long srow, long sk, int r0, int rows, int k0,
+                                      int kend, uint4 (&v)[2]) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int idx = threadIdx.x + 256 * u;
-    int r, k;
-    if (sk == 1) {
-      r = idx >> 5;
-      k = idx & 31;
+  for (int u = 0; u < 2; ++u) {
+    const int idx = threadIdx.x + NTH * u;
+    int gr, gk;
+    if constexpr (L == L_KIN) {
+      gr = r0 + (idx >> 2);
+      gk = k0 + (idx & 3) * 8;
     } else {
-      k = idx >> 6;
-      r = idx & 63;
+      gr = r0 + (idx & 15) * 8;
+      gk = k0 + (idx >> 4);
     }
-    const int gr = r0 + r, gk = k0 + k;
-    bf16_t v = 0;
-    if (gr < rows && gk < K) v = p[(long)gr * srow + (long)gk * sk];
-    img[r * ROW + k] = v;
+    const bool whole = L == L_KIN ? (gr < rows && gk + 8 <= kend) : (gk < kend && gr + 8 <= rows);
+    if (VEC && whole) {
+      v[u] = *reinterpret_cast<const uint4*>(p + (long)gr * srow + (long)gk * sk);
+    } else {
+      uint16_t e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = L == L_KIN ? gr : gr + j, k = L == L_KIN ? gk + j : gk;
+        e[j] = (r < rows && k < kend) ? p[(long)r * srow + (long)k * sk] : (uint16_t)0;
+      }
+      v[u] = uint4{e[0] | ((uint32_t)e[1] << 16), e[2] | ((uint32_t)e[3] << 16), e[4] | ((uint32_t)e[5] << 16),
+                   e[6] | ((uint32_t)e[7] << 16)};
+    }
   }
 }
 
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_small_kernel(SmallArgs p) {
+template <int L>
+__device__ __forceinline__ void lds_put(bf16_t* img, const uint4 (&v)[2]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int idx = threadIdx.x + NTH * u;
+    if constexpr (L == L_KIN) {
+      *reinterpret_cast<uint4*>(img + (idx >> 2) * ROW + (idx & 3) * 8) = v[u];
+    } else {
+      const int r = (idx & 15) * 8, k = idx >> 4;
+      const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        img[(r + 2 * j) * ROW + k] = (bf16_t)(w[j] & 0xffff);
+        img[(r + 2 * j + 1) * ROW + k] = (bf16_t)(w[j] >> 16);
+      }
+    }
+  }
+}
+
+template <int EPI, int LA, bool VA, int LB, bool VB>
+__global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
   __shared__ __attribute__((aligned(16))) bf16_t sa[TM * ROW];
   __shared__ __attribute__((aligned(16))) bf16_t sb[TN * ROW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
-  floatx4 acc[2][2];
+  const int kbeg = blockIdx.z * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  floatx4 acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < p.K; k0 += TK) {
-    stage(p.A, p.sam, p.sak, m0, k0, p.M, p.K, sa);
-    stage(p.B, p.sbn, p.sbk, n0, k0, p.N, p.K, sb);
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[2], rb[2];
+  gload<LA, VA>(p.A, p.sam, p.sak, m0, p.M, kbeg, kend, ra);
+  gload<LB, VB>(p.B, p.sbn, p.sbk, n0, p.N, kbeg, kend, rb);
+  for (int k0 = kbeg; k0 < kend; k0 += TK) {
+    lds_put<LA>(sa, ra);
+    lds_put<LB>(sb, rb);
     __syncthreads();
-    bf16x8 af[2], bfr[2];
+    if (k0 + TK < kend) {  // next K-step's loads are in flight during this one's MFMAs
+      gload<LA, VA>(p.A, p.sam, p.sak, m0, p.M, k0 + TK, kend, ra);
+      gload<LB, VB>(p.B, p.sbn, p.sbk, n0, p.N, k0 + TK, kend, rb);
+    }
+    bf16x8 af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      af[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * 32 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
-      bfr[i] = *reinterpret_cast<const bf16x8*>(sb + (wn * 32 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
+    for (int i = 0; i < 4; ++i) {
+      af[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * 64 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
+      bfr[i] = *reinterpret_cast<const bf16x8*>(sb + (wn * 64 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+      if (n >= p.N) continue;
+      float bv = 0.f;
+      if constexpr (EPI == 0)
+        if (p.bias) bv = p.bias[n];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + e;
-        const int n = n0 + wn * 32 + j * 16 + (lane & 15);
-        if (m >= p.M || n >= p.N) continue;
+        const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + e;
+        if (m >= p.M) continue;
         float v = acc[i][j][e];
         if constexpr (EPI == 0) {
-          if (p.bias) v += p.bias[n];
+          v += bv;
           if (p.R) v += bf2f(p.R[(long)m * p.ldr + n]);
           p.C[(long)m * p.ldc + n] = f2bf(v);
         } else {
-          float* dst = p.Cf + (long)m * p.ldcf + n;
+          float* dst = p.Cf + (long)blockIdx.z * p.slab + (long)m * p.ldcf + n;
           *dst = p.accumulate ? *dst + v : v;
         }
       }
+    }
+}
+
+// out = finish(sum_z ws[z][m, n]): bf16 (+ bias)(+ R) or fp32 (+)=
+template <bool TO_BF16>
+__global__ __launch_bounds__(256) void slab_finish_kernel(const float* __restrict__ ws, int S, int M, int N,
+                                                          bf16_t* C, long ldc, const float* bias, const bf16_t* R,
+                                                          long ldr, float* Cf, long ldcf, int accumulate) {
+  const long total = (long)M * N;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int m = (int)(idx / N), n = (int)(idx % N);
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += ws[(long)z * total + idx];
+    if constexpr (TO_BF16) {
+      if (bias) s += bias[n];
+      if (R) s += bf2f(R[(long)m * ldr + n]);
+      C[(long)m * ldc + n] = f2bf(s);
+    } else {
+      float* dst = Cf + (long)m * ldcf + n;
+      *dst = accumulate ? *dst + s : s;
+    }
+  }
+}
+
+template <int EPI, int LA, bool VA>
+void launch_b(const SmallArgs& a, int LB, bool VB, dim3 grid, hipStream_t st) {
+  if (LB == L_KIN) {
+    if (VB) gemm_small_kernel<EPI, LA, VA, L_KIN, true><<<grid, NTH, 0, st>>>(a);
+    else gemm_small_kernel<EPI, LA, VA, L_KIN, false><<<grid, NTH, 0, st>>>(a);
+  } else {
+    if (VB) gemm_small_kernel<EPI, LA, VA, L_RIN, true><<<grid, NTH, 0, st>>>(a);
+    else gemm_small_kernel<EPI, LA, VA, L_RIN, false><<<grid, NTH, 0, st>>>(a);
+  }
+}
+
+template <int EPI>
+void launch(const SmallArgs& a, int LA, bool VA, int LB, bool VB, dim3 grid, hipStream_t st) {
+  if (LA == L_KIN) {
+    if (VA) launch_b<EPI, L_KIN, true>(a, LB, VB, grid, st);
+    else launch_b<EPI, L_KIN, false>(a, LB, VB, grid, st);
+  } else {
+    if (VA) launch_b<EPI, L_RIN, true>(a, LB, VB, grid, st);
+    else launch_b<EPI, L_RIN, false>(a, LB, VB, grid, st);
+  }
+}
+
+// walk layout of an operand and whether its 8-chunks can be read as 16-byte vectors
+void walk(const bf16_t* p, long srow, long sk, int* L, bool* vec) {
+  const bool aligned = ((uintptr_t)p & 15) == 0;
+  if (sk == 1) {
+    *L = L_KIN;
+    *vec = aligned && srow % 8 == 0;
+  } else if (srow == 1) {
+    *L = L_RIN;
+    *vec = aligned && sk % 8 == 0;
+  } else {
+    *L = L_KIN;
+    *vec = false;
+  }
 }
 
 }  // namespace
 
+int dl_gemm_small_splits(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0) return 1;
+  const long tiles = (long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  // ~4 workgroups per CU (40 KiB of LDS each), at least 512 reduction rows per slice, and at most
+  // 256 MiB of fp32 slabs
+  long S = std::min<long>((1024 + tiles - 1) / tiles, std::max(1, K / 512));
+  while (S > 1 && S * (long)M * N > (64L << 20)) --S;
+  if (S <= 1) return 1;
+  const int kchunk = ((K + S - 1) / S + TK - 1) / TK * TK;
+  return (K + kchunk - 1) / kchunk;
+}
+
 int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B, long sbn, long sbk, int M, int N,
                   int K, bf16_t* C, long ldc, float* Cf, long ldcf, int accumulate, const float* bias, const bf16_t* R,
-                  long ldr, hipStream_t st) {
-  if (M <= 0 || N <= 0 || K <= 0) return -1;
+                  long ldr, int splits, float* ws, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return -1;
   if (epi == 0 && !C) return -1;
   if (epi == 1 && !Cf) return -1;
-  SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, C, ldc, Cf, ldcf, accumulate, bias, R, ldr};
-  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM);
-  if (grid.y > 65535) return -1;
+  if (splits > 1 && !ws) return -1;
+  const int kchunk = splits > 1 ? ((K + splits - 1) / splits + TK - 1) / TK * TK : K;
+  const int S = (K + kchunk - 1) / kchunk;
+  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, S);
+  if (grid.y > 65535 || S > 65535) return -1;
+  int LA, LB;
+  bool VA, VB;
+  walk(A, sam, sak, &LA, &VA);
+  walk(B, sbn, sbk, &LB, &VB);
+  if (S == 1) {
+    SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, C, ldc, Cf, ldcf, 0, accumulate, bias, R, ldr};
+    if (epi == 0) launch<0>(a, LA, VA, LB, VB, grid, st);
+    else launch<1>(a, LA, VA, LB, VB, grid, st);
+    return 0;
+  }
+  SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, nullptr, 0, ws, N, (long)M * N, 0, nullptr, nullptr, 0};
+  launch<1>(a, LA, VA, LB, VB, grid, st);
+  const long total = (long)M * N;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   if (epi == 0)
-    gemm_small_kernel<0><<<grid, 256, 0, st>>>(a);
+    slab_finish_kernel<true><<<blocks, 256, 0, st>>>(ws, S, M, N, C, ldc, bias, R, ldr, nullptr, 0, 0);
   else
-    gemm_small_kernel<1><<<grid, 256, 0, st>>>(a);
+    slab_finish_kernel<false><<<blocks, 256, 0, st>>>(ws, S, M, N, nullptr, 0, nullptr, nullptr, 0, Cf, ldcf,
+                                                      accumulate);
   return 0;
 }

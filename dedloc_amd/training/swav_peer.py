@@ -153,13 +153,10 @@ class SwavPeer:
             def forward(self, *xs):
                 return self.m(list(xs))
 
-        from ..models.resnet_swav import BNAct, ConvNHWC
-
         for m in self.model.modules():  # captured backward must hand every weight grad to autograd
-            if isinstance(m, ConvNHWC):
-                m.inplace_wgrad = False
-            if isinstance(m, BNAct):
-                m.inplace_grad = False
+            for flag in ("inplace_wgrad", "inplace_grad"):  # convs, BN, head linears / BN1d
+                if hasattr(m, flag):
+                    setattr(m, flag, False)
         grads = self.flat.grad.clone()
         bufs = {k: v.clone() for k, v in self.model.named_buffers()}
         sample = tuple(c.detach().clone() for c in crops)

@@ -218,7 +218,10 @@ def test_resnet_trunk_hip_kernels_match_fp32(cuda):
 def test_bottleneck_grads_match_fp32(cuda, cin, planes, stride, H):
     """One Bottleneck (incl. the stride-2 downsample variant), identical x and dY: dX and every
     parameter gradient (flat buffer, in-place fp32 wgrad) of the hand-written path match the fp32
-    PyTorch module's."""
+    PyTorch module's as closely as stock PyTorch bf16 autocast does.  Through three BN backwards
+    (each re-centres the gradient) bf16 rounding alone leaves 5-9e-2 relative difference on the
+    gradients — stock bf16 measured 0.071 / 0.072 / 0.073 on dX for these three blocks
+    (bench/diag_bottleneck.py) — so the bound is relative to that stock-bf16 twin."""
     from dedloc_amd.models.resnet_swav import BNAct, Bottleneck, ConvNHWC
     from dedloc_amd.utils.flat import FlatParams
 
@@ -228,6 +231,7 @@ def test_bottleneck_grads_match_fp32(cuda, cin, planes, stride, H):
         down = torch.nn.Sequential(ConvNHWC(cin, planes * 4, 1, stride=stride, bias=False), BNAct(planes * 4))
     m = Bottleneck(cin, planes, stride, down)
     ref = _fp32_twin(m, cuda).train()
+    stock = _fp32_twin(m, cuda).train()
     m = m.to(cuda).train()
     torch.manual_seed(1)
     x = torch.randn(4, cin, H, H, device=cuda).bfloat16().contiguous(memory_format=CL)
@@ -240,10 +244,17 @@ def test_bottleneck_grads_match_fp32(cuda, cin, planes, stride, H):
     xr = x.float().requires_grad_(True)
     yr = ref(xr)
     yr.backward(dy.float())
-    # bf16 vs fp32 (each op within 1e-2, kernel tests above): the block's BN backward re-centres the
-    # gradient, so the relative difference grows to a few 1e-2 on dX
+    xs = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ys = stock(xs)
+    ys.backward(dy)
+
+    def bound(stock_err):
+        return 1.3 * stock_err + 5e-3
+
     assert _rel(y.float(), yr) < 1e-2
-    assert _rel(xx.grad.float(), xr.grad) < 4e-2
-    rp = dict(ref.named_parameters())
+    assert _rel(xx.grad.float(), xr.grad) < bound(_rel(xs.grad, xr.grad))
+    rp, sp = dict(ref.named_parameters()), dict(stock.named_parameters())
     for n, _ in m.named_parameters():
-        assert _rel(flat.view(flat.grad, n), rp[n].grad) < 3e-2, (n, _rel(flat.view(flat.grad, n), rp[n].grad))
+        ours, theirs = _rel(flat.view(flat.grad, n), rp[n].grad), _rel(sp[n].grad, rp[n].grad)
+        assert ours < bound(theirs), (n, ours, theirs)

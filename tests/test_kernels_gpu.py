@@ -636,11 +636,14 @@ def test_gemm_register_staged_backend(cuda, monkeypatch):
     assert rel(OPS.gemm(a, w, None, None, False, True, 0), a.float() @ w.float().t()) < 1e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 3000, 128), (1000, 128, 3000), (37, 70, 96), (3000, 128, 512)])
+@pytest.mark.parametrize("M,N,K", [(512, 3000, 128), (1000, 128, 3000), (37, 70, 96), (3000, 128, 512),
+                                   (65576, 128, 1024), (2048, 30000, 128)])
 def test_gemm_small_odd_shapes(cuda, M, N, K):
     """Shapes outside the tiled kernels' contracts (the SwAV prototypes: N = 3000; their gradient
-    GEMMs: K = 3000) run on gemm_small.hip: forward with bias, dgrad (K-outer B) and the fp32
-    accumulating weight gradient, against fp32 references."""
+    GEMMs: K = 3000; ALBERT's N = 128 embedding mapping over many tokens and the tied decoder's
+    30000-wide gradients, whose long reductions split into fp32 slabs) run on gemm_small.hip:
+    forward with bias, dgrad (K-outer B) and the fp32 accumulating weight gradient, against fp32
+    references."""
     torch.manual_seed(19)
     a = torch.randn(M, K, device=cuda).bfloat16()
     w = torch.randn(N, K, device=cuda).bfloat16()
@@ -651,6 +654,20 @@ def test_gemm_small_odd_shapes(cuda, M, N, K):
     g = torch.full((N, K), 0.25, device=cuda)
     OPS.gemm_acc_f32(dy, a, g, True, False)
     assert rel(g, 0.25 + dy.float().t() @ a.float()) < 1e-3
+
+
+def test_gemm_small_strided_views(cuda):
+    """Operands that are column slices of wider tensors (row stride != width), aligned and not."""
+    torch.manual_seed(23)
+    for off in (0, 3):
+        big_a = torch.randn(300, 200, device=cuda).bfloat16()
+        big_w = torch.randn(90, 200, device=cuda).bfloat16()
+        a, w = big_a[:, off:off + 136], big_w[:, off:off + 136]
+        assert rel(OPS.gemm(a, w, None, None, False, True, 0), a.float() @ w.float().t()) < 1e-2
+        g = torch.zeros(90, 136, device=cuda)
+        dy = torch.randn(300, 90, device=cuda).bfloat16()
+        OPS.gemm_acc_f32(dy, a, g, True, False)
+        assert rel(g, dy.float().t() @ a.float()) < 1e-3
 
 
 @pytest.mark.timeout(240)

@@ -65,7 +65,7 @@ CHILD = textwrap.dedent("""
     m = torch.randn(3_000_000, device=dev)
     donor = DecentralizedAverager([x, m], root, "rccl-test", peer_id=b"donor", device=dev,
                                   listen_on="127.0.0.1:*")
-    donor.publish_state_sharing(5)
+    donor.publish_state_sharing(5).result(timeout=30)
     rx = DecentralizedAverager([torch.zeros_like(x), torch.zeros_like(m)], root, "rccl-test", peer_id=b"rx",
                                device=dev, listen_on="127.0.0.1:*", allow_state_sharing=False)
     meta, tensors = rx.load_state_from_peers(timeout=30)
