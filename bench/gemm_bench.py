@@ -80,11 +80,15 @@ def main():
         kinds = [("fwd", lambda: O.gemm(x, w, b, None, False, True, 0)),
                  ("dgrad", lambda: O.gemm(dy, w, None, None, False, False, 0)),
                  ("wgrad", lambda: O.gemm_acc_f32(dy, x, g, True, False))]
-        if os.environ.get("DGRAD_T"):  # dgrad against a transposed weight copy: the forward's layout
-            wt = w.t().contiguous()
-            kinds.insert(2, ("dgrad_wT", lambda: O.gemm(dy, wt, None, None, False, True, 0)))
+        wt = w.t().contiguous()
+        if os.environ.get("DGRAD_T"):  # the other weight layout: W^T [in, out] copies (B K-outer
+            # in the forward, K-inner in the data gradient)
+            kinds.insert(1, ("fwd_wT", lambda: O.gemm(x, wt, b, None, False, False, 0)))
+            kinds.insert(3, ("dgrad_wT", lambda: O.gemm(dy, wt, None, None, False, True, 0)))
         if name == "ffn1":
             kinds.append(("fwd_gelu", lambda: O.gemm_gelu(x, w, b)))
+            if os.environ.get("DGRAD_T"):
+                kinds.append(("fwd_gelu_wT", lambda: O.gemm_gelu(x, wt, b, True)))
         if name == "ffn2":
             f = (torch.randn(T, K, device=dev)).bfloat16()
             kinds.append(("dgrad_dgelu", lambda: O.gemm_dgelu(dy, w, f, db)))

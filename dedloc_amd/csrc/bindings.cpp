@@ -619,16 +619,20 @@ void gemm_acc_f32_shared(const at::Tensor& a, const at::Tensor& b, at::Tensor c,
   gemm_acc_f32(a, b, c, trans_a, trans_b);
 }
 
-// fused FFN-up: H = x W^T + b (pre-activation, kept for backward), G = gelu_new(H)
-std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias) {
+// fused FFN-up: H = x W^T + b (pre-activation, kept for backward), G = gelu_new(H).  trans_w: w
+// holds W^T ([in, out]: a K-outer B operand) instead of W ([out, in], K-inner)
+std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias,
+                                             bool trans_w) {
   expect_operands(x, w);
-  auto H = at::empty({x.size(0), w.size(0)}, x.options());
+  const int64_t nout = trans_w ? w.size(1) : w.size(0);
+  auto H = at::empty({x.size(0), nout}, x.options());
   auto G = at::empty_like(H);
   const at::Tensor bias32 = f32_bias(bias);
-  if (own_gemm(0, 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)w.size(0), (int)x.size(1),
-               bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1), nullptr, cur_stream(x)) == 0)
+  if (own_gemm(0, trans_w ? 1 : 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)nout,
+               (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1), nullptr,
+               cur_stream(x)) == 0)
     return {H, G};
-  const Mat A = a_view(x, false), B = b_view(w, true);
+  const Mat A = a_view(x, false), B = b_view(w, !trans_w);
   gemm_store(A, B, x, w, bf(H), H.size(1), f32(bias32), nullptr, 0, cur_stream(x));
   check(dl_gelu_fwd(cbf(H), bf(G), H.numel(), cur_stream(H)), "gelu_fwd");
   return {H, G};

@@ -197,9 +197,9 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_kernel(GemmArgs p) {
         } else if constexpr (EPI == EPI_GELU) {
           const bf16_t hb = f2bf(v + bv);
           p.H[(long)m * p.ldh + n] = hb;
-          p.C[(long)m * p.ldc + n] = f2bf(gelu_tanh(bf2f(hb)));
+          p.C[(long)m * p.ldc + n] = f2bf(gelu_tanh_sig(bf2f(hb)));
         } else if constexpr (EPI == EPI_DGELU) {
-          const bf16_t cb = f2bf(v * gelu_tanh_grad(bf2f(p.R[(long)m * p.ldr + n])));
+          const bf16_t cb = f2bf(v * gelu_tanh_grad_sig(bf2f(p.R[(long)m * p.ldr + n])));
           p.C[(long)m * p.ldc + n] = cb;
           colsum[ni] += bf2f(cb);
         } else {

@@ -35,7 +35,7 @@
 //   EPI_STORE  C = acc (+ bias[n]) (+ R[m,n])                                 bf16
 //   EPI_GELU   H = bf16(acc + bias); C = gelu_new(H)                          bf16 x2
 //   EPI_DGELU  C = bf16(acc) * gelu_new'(R[m,n]); dbias[n] += sum_m C         bf16 (+ fp32 atomics)
-//   EPI_F32    Cf[z][m,n] = acc  or  += acc (split z = blockIdx.y)            fp32
+//   EPI_F32    Cf[z][m,n] = acc  or  += acc (reduction split z)                fp32
 #include <cstdlib>
 #include <type_traits>
 
@@ -66,6 +66,30 @@ __device__ __forceinline__ int half_to_tile(int l, int h) {
   return ISB ? ((l >> 5) << 6) + (h << 5) + (l & 31) : ((l >> 6) << 7) + (h << 6) + (l & 63);
 }
 
+// Column permutation of a K-outer B tile (swap bits 5 and 6 of the tile column).  A B half-tile
+// holds the 32-column blocks with bit 5 == half (the waves' N quadrants); K-outer, a 32-column
+// block of a k-row is only 64 bytes, so each half-tile DMA would fetch half cache lines (and every
+// line twice, one half per phase).  Tile column c is therefore mapped to global column
+// colperm(c): the blocks of one half land on two 64-column (128-byte, whole-line) runs of global
+// columns.  The epilogue writes column colperm(c) for the accumulator of tile column c, so the
+// permutation is invisible outside the kernel.  K-inner B tiles are not permuted (P = false).
+template <bool P>
+__device__ __forceinline__ int colperm(int c) {
+  return P ? (c & ~0x60) | ((c >> 1) & 0x20) | ((c << 1) & 0x40) : c;
+}
+
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4; M0 = the wave's LDS destination), issued
+// from inline asm.  With __builtin_amdgcn_global_load_lds the compiler's wait-count pass cannot
+// tell the half-tile slots apart and, in front of every ds_read_b64_tr_b16 that follows an
+// in-flight DMA, inserts s_waitcnt vmcnt(0) — three full drains of the prefetch per K-tile in
+// every kernel with a K-outer operand (the weight gradients ran ~30% below the K-inner forms).
+// Hidden in asm, the DMAs are ordered only by the pipeline's own counted vmcnt waits; the
+// compiler's waits for its own loads can only get stricter.
+__device__ __forceinline__ void dma16(const bf16_t* src, uint8_t* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_void*)lds_dst);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(src) : "memory", "m0");
+}
+
 // Issue the two LDS-DMA pieces of this thread for one half-tile.
 template <bool KO, bool ISB>
 __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ g, long ld, int r0, int rows_valid, int k0,
@@ -83,10 +107,10 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ g, long ld
     } else {
       const int k = region * 4 + (lane >> 4);
       const int c = (lane & 15) ^ kout_swz(k);
-      const int tcol = half_to_tile<ISB>(c * 8, half);  // 8-column chunks never straddle a block
+      const int tcol = colperm<ISB>(half_to_tile<ISB>(c * 8, half));  // 8-column chunks never straddle a block
       src = g + (long)(k0 + k) * ld + r0 + tcol;
     }
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(slot + region * 1024), 16, 0, 0);
+    dma16(src, slot + region * 1024);
   }
 }
 
@@ -156,9 +180,15 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   const int wm = w >> 2, wn = w & 3;
   const int tiles_n = p.N / BN;
   const int tiles_m = (p.M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  // one linear grid over (split, tile), remapped so that each XCD runs whole splits: the
+  // workgroups sharing an XCD's L2 then read the same token range (weight gradients: every tile of
+  // a split reads the same rows of both operands), so each operand byte comes from HBM about once
+  // instead of once per XCD
+  const int tiles = tiles_m * tiles_n;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);  // grid = tiles * splits
+  const int split = lid / tiles, bid = lid % tiles;
   const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
-  const int kbase = blockIdx.y * p.K;
+  const int kbase = split * p.K;
   const int nk = p.K / BK;
 
   floatx4 acc[2][2][4][2];
@@ -297,7 +327,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     for (int ni = 0; ni < 2; ++ni) {
       bias_v[qn][ni] = 0.f;
       if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
-        if (p.bias) bias_v[qn][ni] = p.bias[n0 + wn * 64 + qn * 32 + ni * 16 + ccol];
+        if (p.bias) bias_v[qn][ni] = p.bias[n0 + colperm<BKO>(wn * 64 + qn * 32 + ni * 16 + ccol)];
     }
   float colsum[8];
 #pragma unroll
@@ -327,7 +357,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       const int gm = m0 + wm * 128 + qm * 64 + r;
-      const int gn = n0 + wn * 64 + rch * 8;
+      const int gn = n0 + colperm<BKO>(wn * 64 + rch * 8);
 #ifdef GEMM8_PROBE_NO_STORE  // measurement build only (bench/gemm8_probe.hip): skip the output writes
       if (gm < 0) {
 #else
@@ -347,19 +377,19 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
           for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
           store8_bf16(p.H + (long)gm * p.ldh + gn, h, p.nt);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = gelu_tanh(h[j]);
+          for (int j = 0; j < 8; ++j) h[j] = gelu_tanh_sig(h[j]);
           store8_bf16(p.C + (long)gm * p.ldc + gn, h, p.nt);
         } else if constexpr (EPI == EPI_DGELU) {
           float f[8];
           load_bf16<8>(p.R + (long)gm * p.ldr + gn, f);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad(f[j]));
+            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(f[j]));
             colsum[j] += v[j];
           }
           store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
         } else {
-          float* dst = p.Cf + (long)blockIdx.y * p.slab + (long)gm * p.ldcf + gn;
+          float* dst = p.Cf + (long)split * p.slab + (long)gm * p.ldcf + gn;
           if (p.accumulate) {
             const float4 o0 = *reinterpret_cast<const float4*>(dst);
             const float4 o1 = *reinterpret_cast<const float4*>(dst + 4);
@@ -384,7 +414,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       }
       if (lane < 8) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + wn * 64 + lane * 8 + j], colsum[j]);
+        for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + colperm<BKO>(wn * 64 + lane * 8) + j], colsum[j]);
       }
     }
   }
@@ -442,7 +472,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
   int lane = lane0;
   auto out_off = [&](int dn0, int qm, int j) -> unsigned {
     const int rch = lane & 7, rr = lane >> 3;
-    return (unsigned)((((long)(wm * 128 + qm * 64 + j * 8 + rr)) * p.ldc + dn0 + wn * 64 + rch * 8) * 2);
+    return (unsigned)((((long)(wm * 128 + qm * 64 + j * 8 + rr)) * p.ldc + dn0 + colperm<BKO>(wn * 64 + rch * 8)) * 2);
   };
   int dn0 = 0;
 
@@ -587,7 +617,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
       for (int ni = 0; ni < 2; ++ni) {
         bias_v[qn][ni] = 0.f;
         if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
-          if (p.bias) bias_v[qn][ni] = p.bias[n0 + wn * 64 + qn * 32 + ni * 16 + ccol];
+          if (p.bias) bias_v[qn][ni] = p.bias[n0 + colperm<BKO>(wn * 64 + qn * 32 + ni * 16 + ccol)];
       }
     float colsum[8];
 #pragma unroll
@@ -616,7 +646,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
         const int gm = m0 + wm * 128 + qm * 64 + r;
         const int gmc = min(gm, p.M - 1);  // rows past M: computed, then dropped by the range check
-        const int gn = n0 + wn * 64 + rch * 8;
+        const int gn = n0 + colperm<BKO>(wn * 64 + rch * 8);
         if constexpr (EPI == EPI_STORE) {
           if (p.R) {
             float rv[8];
@@ -631,13 +661,13 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
           bstore(tile_rsrc(p.H, p.ldh, m0, p.M),
                  (unsigned)((((long)(wm * 128 + qm * 64 + r)) * p.ldh + gn) * 2), pack8_bf16(h), nt);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(h[j]);
+          for (int j = 0; j < 8; ++j) v[j] = gelu_tanh_sig(h[j]);
         } else {  // EPI_DGELU
           float f[8];
           load_bf16<8>(p.R + (long)gmc * p.ldr + gn, f);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad(f[j]));
+            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(f[j]));
             if (gm < p.M) colsum[j] += v[j];
           }
         }
@@ -658,7 +688,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
         }
         if (lane < 8) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + wn * 64 + lane * 8 + j], colsum[j]);
+          for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + colperm<BKO>(wn * 64 + lane * 8) + j], colsum[j]);
         }
       }
     }
@@ -699,7 +729,7 @@ int launch8(const Args& a, int splits, hipStream_t st) {
       return 0;
     }
   }
-  gemm8_kernel<AKO, BKO, EPI><<<dim3(tiles, splits), NT, 0, st>>>(a);
+  gemm8_kernel<AKO, BKO, EPI><<<dim3(tiles * splits), NT, 0, st>>>(a);
   return 0;
 }
 
@@ -726,14 +756,17 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
     if (epi == EPI_DGELU && !R) return -1;
     if (splits != 1) return -1;
   }
+  // non-temporal bf16 output stores by default (+4..17% on the store-bound epilogues, gemm_bench);
+  // DEDLOC_GEMM8_NT=0 for A/B runs
   const char* nte = std::getenv("DEDLOC_GEMM8_NT");
-  const int nt = nte ? std::atoi(nte) : 0;
+  const int nt = nte ? std::atoi(nte) : 1;
   Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt};
 #define DL_GEMM8_CASE(AK, BK_, E) \
   if (a_kouter == AK && b_kouter == BK_ && epi == E) return launch8<AK, BK_, E>(a, splits, st);
   DL_GEMM8_CASE(0, 0, EPI_STORE)
   DL_GEMM8_CASE(0, 0, EPI_GELU)
   DL_GEMM8_CASE(0, 1, EPI_STORE)
+  DL_GEMM8_CASE(0, 1, EPI_GELU)
   DL_GEMM8_CASE(0, 1, EPI_DGELU)
   DL_GEMM8_CASE(0, 0, EPI_DGELU)
   DL_GEMM8_CASE(1, 1, EPI_F32)

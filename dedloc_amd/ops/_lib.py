@@ -46,7 +46,7 @@ _SCHEMAS = [
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
     "gemm_acc_f32_shared(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b, bool first, bool last) -> ()",
-    "gemm_gelu(Tensor x, Tensor w, Tensor bias) -> (Tensor, Tensor)",
+    "gemm_gelu(Tensor x, Tensor w, Tensor bias, bool trans_w=False) -> (Tensor, Tensor)",
     "sinkhorn(Tensor scores, int bs, float eps, int iters) -> Tensor",
     "swav_ce(Tensor scores, Tensor q, Tensor(a!) dscores, Tensor(b!) loss, float temperature, float scale) -> ()",
     "row_normalize_(Tensor(a!) w) -> ()",
@@ -431,8 +431,8 @@ def _gemm_cpu(a, b, bias, residual, trans_a, trans_b, epilogue):
 
 
 @_impl("gemm_gelu")
-def _gemm_gelu_cpu(x, w, bias):
-    h = _bf(x.float() @ w.float().t() + bias.float())
+def _gemm_gelu_cpu(x, w, bias, trans_w=False):
+    h = _bf(x.float() @ (w.float() if trans_w else w.float().t()) + bias.float())
     return h, _bf(_gelu_tanh(h.float()))
 
 
