@@ -450,11 +450,17 @@ void small_gemm(int epi, const Mat& A, const Mat& B, const at::Tensor& a, const 
         "gemm_small");
 }
 
-// C (bf16) = op(A) op(B) (+ bias) (+ R): tiled kernels, else gemm_small.
+// C (bf16) = op(A) op(B) (+ bias) (+ R): gemm8 where its contract holds; outputs of at most 192
+// columns (1x1 convs with 64 / 128 channels, the stem, ALBERT's 128-wide embedding side) on
+// gemm_small's 128x64 / 128x128 tiles (a 256-wide tile would waste half to three quarters of its
+// MFMAs); the register-staged 256x256 gemm.hip for the remaining wide shapes; gemm_small last.
 void gemm_store(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, bf16_t* C, long ldc,
                 const float* bias, const bf16_t* R, long ldr, hipStream_t st) {
-  if (own_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, C, ldc, nullptr,
-               0, bias, R, ldr, nullptr, 0, nullptr, st) == 0)
+  if (use_gemm8() && dl_gemm8(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k,
+                              C, ldc, nullptr, 0, 0, 0, bias, R, ldr, nullptr, 0, nullptr, 1, st) == 0)
+    return;
+  if (B.rows > 192 && dl_gemm(A.kouter, B.kouter, 0, cbf(a), A.ld, cbf(b), B.ld, (int)A.rows, (int)B.rows, (int)A.k, C,
+                              ldc, nullptr, 0, bias, R, ldr, nullptr, 0, nullptr, 1, st) == 0)
     return;
   small_gemm(0, A, B, a, b, C, ldc, nullptr, 0, 0, bias, R, ldr, st);
 }
@@ -493,11 +499,17 @@ int wgrad_splits8(const Mat& A, const Mat& B) {
     while (S > 1 && A.k % (S * 64)) S /= 2;
     return S;
   }
+  // any S dividing the K-tile count (SwAV's 14x14 maps: 25088 tokens = 392 K-tiles = 2^3 7^2, so
+  // S = 56 puts 224 workgroups on the chip where powers of two stop at 32), each slice at least 4
+  // K-tiles (8 while S > 32)
   constexpr int64_t kCUs = 256;
+  const int64_t ktiles = A.k / 64;
+  if (A.k % 64) return 1;
   int best = 1;
   double best_eff = 0.0;
-  for (int S = 1; S <= 32; S *= 2) {
-    if (A.k % (S * 64) || (S > 1 && A.k / S < 1024)) break;
+  for (int S = 1; S <= 64; ++S) {
+    if (ktiles % S) continue;
+    if (S > 1 && ktiles / S < (S > 32 ? 8 : 4)) break;
     const int64_t wg = tiles * S;
     const double eff = (double)wg / (double)(kCUs * ((wg + kCUs - 1) / kCUs));
     if (eff > best_eff + 1e-9) {
@@ -890,9 +902,9 @@ inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t
   return col;
 }
 
-// Convolutions that are plain GEMMs run on the tiled GEMM kernels (gemm8.hip / gemm.hip): 1x1
+// Convolutions that are plain GEMMs run on the GEMM kernels (gemm8.hip / gemm_small.hip): 1x1
 // stride-1 unpadded convs over NHWC tensors (x[N*H*W, C] x W[K, C]^T; dgrad dY[N*H*W, K] x W
-// against the transposed weight [C, K], a K-inner operand) and the stem's column-matrix GEMM; their
+// with the KRSC weight as a K-outer operand) and the stem's column-matrix GEMM; their
 // weight gradients use gemm8's split-K slabs where both channel counts are multiples of 256 and the
 // implicit-GEMM conv.hip wgrad otherwise.  DEDLOC_CONV_GEMM=hip routes the 1x1 convs through
 // conv.hip too (kernel tests).
@@ -963,7 +975,9 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
   auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);  // [K, R, S, C]
   if (is_pointwise(R, S, stride, pad) && H == P && W == Q && conv_gemm()) {
-    gemm_plain(rows2d(dy), wk.view({K, C}).t().contiguous(), bf(dx), C, cur_stream(dy));
+    // dX[M, C] = dY[M, K] W[K, C]: the weight as a K-outer B operand, no transposed copy
+    const at::Tensor dyr = rows2d(dy), wkc = wk.view({K, C});
+    gemm_store(a_view(dyr, false), b_view(wkc, false), dyr, wkc, bf(dx), C, nullptr, nullptr, 0, cur_stream(dy));
     return dx;
   }
   for (int64_t a = 0; a < stride; ++a) {

@@ -9,8 +9,8 @@
 //
 //   C[m, n] = sum_k A(m, k) B(n, k)    A(m, k) = A[m*sam + k*sak], B(n, k) = B[n*sbn + k*sbk]
 //
-// Tile 128 x 128 x 32, 256 threads = 4 waves (2 x 2), 64 x 64 outputs per wave = 4 x 4
-// v_mfma_f32_16x16x32_bf16.  Operands go global -> registers (next K-step prefetched while the
+// Tile 128 x 128 x 32 (128 x 64 when N <= 64), 256 threads = 4 waves (2 x 2), 64 x 64 (64 x 32)
+// outputs per wave = 4 x 4 (4 x 2) v_mfma_f32_16x16x32_bf16.  Operands go global -> registers (next K-step prefetched while the
 // current one computes) -> LDS rows of 32 k (+8 pad: 80-byte rows keep the 16-byte fragment reads
 // aligned and spread over the banks).  The global walk follows the unit-stride side of each
 // operand, 16 bytes per lane when it is aligned:
@@ -31,7 +31,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int TM = 128, TN = 128, TK = 32, ROW = TK + 8, NTH = 256;
+constexpr int TM = 128, TK = 32, ROW = TK + 8, NTH = 256;
 enum { L_KIN = 0, L_RIN = 1 };
 
 struct SmallArgs {
@@ -44,20 +44,20 @@ struct SmallArgs {
   const bf16_t* R; long ldr;
 };
 
-// Two 8-element chunks of a 128 x 32 operand tile per thread, into registers.
-template <int L, bool VEC>
+// U 8-element chunks of a (64 U) x 32 operand tile per thread, into registers.
+template <int L, bool VEC, int U>
 __device__ __forceinline__ void gload(const bf16_t* __restrict__ p, long srow, long sk, int r0, int rows, int k0,
-                                      int kend, uint4 (&v)[2]) {
+                                      int kend, uint4 (&v)[U]) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int idx = threadIdx.x + NTH * u;
     int gr, gk;
     if constexpr (L == L_KIN) {
       gr = r0 + (idx >> 2);
       gk = k0 + (idx & 3) * 8;
-    } else {
-      gr = r0 + (idx & 15) * 8;
-      gk = k0 + (idx >> 4);
+    } else {  // 8 U row chunks of 8 per k
+      gr = r0 + (idx & (8 * U - 1)) * 8;
+      gk = k0 + idx / (8 * U);
     }
     const bool whole = L == L_KIN ? (gr < rows && gk + 8 <= kend) : (gk < kend && gr + 8 <= rows);
     if (VEC && whole) {
@@ -75,15 +75,15 @@ __device__ __forceinline__ void gload(const bf16_t* __restrict__ p, long srow, l
   }
 }
 
-template <int L>
-__device__ __forceinline__ void lds_put(bf16_t* img, const uint4 (&v)[2]) {
+template <int L, int U>
+__device__ __forceinline__ void lds_put(bf16_t* img, const uint4 (&v)[U]) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int idx = threadIdx.x + NTH * u;
     if constexpr (L == L_KIN) {
       *reinterpret_cast<uint4*>(img + (idx >> 2) * ROW + (idx & 3) * 8) = v[u];
     } else {
-      const int r = (idx & 15) * 8, k = idx >> 4;
+      const int r = (idx & (8 * U - 1)) * 8, k = idx / (8 * U);
       const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -94,8 +94,11 @@ __device__ __forceinline__ void lds_put(bf16_t* img, const uint4 (&v)[2]) {
   }
 }
 
-template <int EPI, int LA, bool VA, int LB, bool VB>
+// TN = 128: 4 waves as 2 x 2 of 64 x 64; TN = 64 (outputs of at most 64 columns, e.g. the
+// ResNet stem and 64-channel 1x1 convs): 2 x 2 of 64 x 32, half the B tile and no wasted MFMAs
+template <int EPI, int TN, int LA, bool VA, int LB, bool VB>
 __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
+  constexpr int UB = TN / 64, NJ = TN / 32;
   __shared__ __attribute__((aligned(16))) bf16_t sa[TM * ROW];
   __shared__ __attribute__((aligned(16))) bf16_t sb[TN * ROW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -103,40 +106,41 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
   const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
   const int kbeg = blockIdx.z * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
-  floatx4 acc[4][4];
+  floatx4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[2], rb[2];
-  gload<LA, VA>(p.A, p.sam, p.sak, m0, p.M, kbeg, kend, ra);
-  gload<LB, VB>(p.B, p.sbn, p.sbk, n0, p.N, kbeg, kend, rb);
+  uint4 ra[2], rb[UB];
+  gload<LA, VA, 2>(p.A, p.sam, p.sak, m0, p.M, kbeg, kend, ra);
+  gload<LB, VB, UB>(p.B, p.sbn, p.sbk, n0, p.N, kbeg, kend, rb);
   for (int k0 = kbeg; k0 < kend; k0 += TK) {
-    lds_put<LA>(sa, ra);
-    lds_put<LB>(sb, rb);
+    lds_put<LA, 2>(sa, ra);
+    lds_put<LB, UB>(sb, rb);
     __syncthreads();
     if (k0 + TK < kend) {  // next K-step's loads are in flight during this one's MFMAs
-      gload<LA, VA>(p.A, p.sam, p.sak, m0, p.M, k0 + TK, kend, ra);
-      gload<LB, VB>(p.B, p.sbn, p.sbk, n0, p.N, k0 + TK, kend, rb);
+      gload<LA, VA, 2>(p.A, p.sam, p.sak, m0, p.M, k0 + TK, kend, ra);
+      gload<LB, VB, UB>(p.B, p.sbn, p.sbk, n0, p.N, k0 + TK, kend, rb);
     }
-    bf16x8 af[4], bfr[4];
+    bf16x8 af[4], bfr[NJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i)
       af[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * 64 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
-      bfr[i] = *reinterpret_cast<const bf16x8*>(sb + (wn * 64 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
-    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (wn * (TN / 2) + j * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     __syncthreads();
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * (TN / 2) + j * 16 + (lane & 15);
       if (n >= p.N) continue;
       float bv = 0.f;
       if constexpr (EPI == 0)
@@ -179,26 +183,33 @@ __global__ __launch_bounds__(256) void slab_finish_kernel(const float* __restric
   }
 }
 
-template <int EPI, int LA, bool VA>
+template <int EPI, int TN, int LA, bool VA>
 void launch_b(const SmallArgs& a, int LB, bool VB, dim3 grid, hipStream_t st) {
   if (LB == L_KIN) {
-    if (VB) gemm_small_kernel<EPI, LA, VA, L_KIN, true><<<grid, NTH, 0, st>>>(a);
-    else gemm_small_kernel<EPI, LA, VA, L_KIN, false><<<grid, NTH, 0, st>>>(a);
+    if (VB) gemm_small_kernel<EPI, TN, LA, VA, L_KIN, true><<<grid, NTH, 0, st>>>(a);
+    else gemm_small_kernel<EPI, TN, LA, VA, L_KIN, false><<<grid, NTH, 0, st>>>(a);
   } else {
-    if (VB) gemm_small_kernel<EPI, LA, VA, L_RIN, true><<<grid, NTH, 0, st>>>(a);
-    else gemm_small_kernel<EPI, LA, VA, L_RIN, false><<<grid, NTH, 0, st>>>(a);
+    if (VB) gemm_small_kernel<EPI, TN, LA, VA, L_RIN, true><<<grid, NTH, 0, st>>>(a);
+    else gemm_small_kernel<EPI, TN, LA, VA, L_RIN, false><<<grid, NTH, 0, st>>>(a);
+  }
+}
+
+template <int EPI, int TN>
+void launch(const SmallArgs& a, int LA, bool VA, int LB, bool VB, dim3 grid, hipStream_t st) {
+  if (LA == L_KIN) {
+    if (VA) launch_b<EPI, TN, L_KIN, true>(a, LB, VB, grid, st);
+    else launch_b<EPI, TN, L_KIN, false>(a, LB, VB, grid, st);
+  } else {
+    if (VA) launch_b<EPI, TN, L_RIN, true>(a, LB, VB, grid, st);
+    else launch_b<EPI, TN, L_RIN, false>(a, LB, VB, grid, st);
   }
 }
 
 template <int EPI>
-void launch(const SmallArgs& a, int LA, bool VA, int LB, bool VB, dim3 grid, hipStream_t st) {
-  if (LA == L_KIN) {
-    if (VA) launch_b<EPI, L_KIN, true>(a, LB, VB, grid, st);
-    else launch_b<EPI, L_KIN, false>(a, LB, VB, grid, st);
-  } else {
-    if (VA) launch_b<EPI, L_RIN, true>(a, LB, VB, grid, st);
-    else launch_b<EPI, L_RIN, false>(a, LB, VB, grid, st);
-  }
+void launch_tn(const SmallArgs& a, int LA, bool VA, int LB, bool VB, int tn, int S, hipStream_t st) {
+  const dim3 grid((a.N + tn - 1) / tn, (a.M + TM - 1) / TM, S);
+  if (tn == 64) launch<EPI, 64>(a, LA, VA, LB, VB, grid, st);
+  else launch<EPI, 128>(a, LA, VA, LB, VB, grid, st);
 }
 
 // walk layout of an operand and whether its 8-chunks can be read as 16-byte vectors
@@ -220,7 +231,8 @@ void walk(const bf16_t* p, long srow, long sk, int* L, bool* vec) {
 
 int dl_gemm_small_splits(int M, int N, int K) {
   if (M <= 0 || N <= 0 || K <= 0) return 1;
-  const long tiles = (long)((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+  const int tn = N <= 64 ? 64 : 128;
+  const long tiles = (long)((M + TM - 1) / TM) * ((N + tn - 1) / tn);
   // ~4 workgroups per CU (40 KiB of LDS each), at least 512 reduction rows per slice, and at most
   // 256 MiB of fp32 slabs
   long S = std::min<long>((1024 + tiles - 1) / tiles, std::max(1, K / 512));
@@ -239,20 +251,20 @@ int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B,
   if (splits > 1 && !ws) return -1;
   const int kchunk = splits > 1 ? ((K + splits - 1) / splits + TK - 1) / TK * TK : K;
   const int S = (K + kchunk - 1) / kchunk;
-  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, S);
-  if (grid.y > 65535 || S > 65535) return -1;
+  const int tn = N <= 64 ? 64 : 128;
+  if ((M + TM - 1) / TM > 65535 || S > 65535) return -1;
   int LA, LB;
   bool VA, VB;
   walk(A, sam, sak, &LA, &VA);
   walk(B, sbn, sbk, &LB, &VB);
   if (S == 1) {
     SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, C, ldc, Cf, ldcf, 0, accumulate, bias, R, ldr};
-    if (epi == 0) launch<0>(a, LA, VA, LB, VB, grid, st);
-    else launch<1>(a, LA, VA, LB, VB, grid, st);
+    if (epi == 0) launch_tn<0>(a, LA, VA, LB, VB, tn, 1, st);
+    else launch_tn<1>(a, LA, VA, LB, VB, tn, 1, st);
     return 0;
   }
   SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, nullptr, 0, ws, N, (long)M * N, 0, nullptr, nullptr, 0};
-  launch<1>(a, LA, VA, LB, VB, grid, st);
+  launch_tn<1>(a, LA, VA, LB, VB, tn, S, st);
   const long total = (long)M * N;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
   if (epi == 0)
