@@ -158,6 +158,16 @@ __device__ __forceinline__ void load_bf16(const bf16_t* p, float* out) {
   }
 }
 
+// 8 bf16 already in registers (a prefetched 16-byte row chunk) -> fp32
+__device__ __forceinline__ void unpack8_bf16(const uint4& v, float* out) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    out[2 * i] = __uint_as_float(w[i] << 16);
+    out[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
 template <int VW>
 __device__ __forceinline__ void store_bf16(bf16_t* p, const float* in) {
   if constexpr (VW == 8) {

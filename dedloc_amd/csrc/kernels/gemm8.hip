@@ -334,6 +334,22 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
   const int rch = lane & 7;   // 8-column chunk handled in the row phase
   const int rr = lane >> 3;   // row within a pass of 8 rows
+  const int gn = n0 + colperm<BKO>(wn * 64 + rch * 8);
+
+  // The residual (STORE) / pre-activation (DGELU) rows are read ahead: all 8 of a row half before
+  // its passes, and the next half's row j right after pass j consumed this half's — ahead of that
+  // pass's store.  Loaded inside each pass instead, every pass waited (vmcnt(0)) for its load's full
+  // HBM latency and, the counter being in issue order, for every store before it.
+  const bool has_r = EPI == EPI_DGELU || (EPI == EPI_STORE && p.R != nullptr);
+  auto rrow = [&](int qm, int pass) -> uint4 {
+    const int gm = min(m0 + wm * 128 + qm * 64 + pass * 8 + rr, p.M - 1);  // tail rows: clamped, unused
+    return *reinterpret_cast<const uint4*>(p.R + (long)gm * p.ldr + gn);
+  };
+  uint4 rbuf[8];
+  if (has_r) {
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) rbuf[pass] = rrow(0, pass);
+  }
 
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm) {
@@ -357,16 +373,18 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       const int gm = m0 + wm * 128 + qm * 64 + r;
-      const int gn = n0 + colperm<BKO>(wn * 64 + rch * 8);
+      float rv[8];
+      if (has_r) {
+        unpack8_bf16(rbuf[pass], rv);
+        if (qm == 0) rbuf[pass] = rrow(1, pass);
+      }
 #ifdef GEMM8_PROBE_NO_STORE  // measurement build only (bench/gemm8_probe.hip): skip the output writes
       if (gm < 0) {
 #else
       if (gm < p.M) {
 #endif
         if constexpr (EPI == EPI_STORE) {
-          if (p.R) {
-            float rv[8];
-            load_bf16<8>(p.R + (long)gm * p.ldr + gn, rv);
+          if (has_r) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] += rv[j];
           }
@@ -380,11 +398,9 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
           for (int j = 0; j < 8; ++j) h[j] = gelu_tanh_sig(h[j]);
           store8_bf16(p.C + (long)gm * p.ldc + gn, h, p.nt);
         } else if constexpr (EPI == EPI_DGELU) {
-          float f[8];
-          load_bf16<8>(p.R + (long)gm * p.ldr + gn, f);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(f[j]));
+            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(rv[j]));
             colsum[j] += v[j];
           }
           store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
