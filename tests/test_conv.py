@@ -221,7 +221,7 @@ def test_bottleneck_grads_match_fp32(cuda, cin, planes, stride, H):
     PyTorch module's as closely as stock PyTorch bf16 autocast does.  Through three BN backwards
     (each re-centres the gradient) bf16 rounding alone leaves 5-9e-2 relative difference on the
     gradients — stock bf16 measured 0.071 / 0.072 / 0.073 on dX for these three blocks
-    (bench/diag_bottleneck.py) — so the bound is relative to that stock-bf16 twin."""
+    (profiles/bottleneck_bf16_drift_diag.log) — so the bound is relative to that stock-bf16 twin."""
     from dedloc_amd.models.resnet_swav import BNAct, Bottleneck, ConvNHWC
     from dedloc_amd.utils.flat import FlatParams
 
