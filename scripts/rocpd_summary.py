@@ -1,0 +1,69 @@
+"""Per-kernel summary of a rocprofv3 ``--kernel-trace`` database (``*_results.db``).
+
+Takes the dispatches of the last ``--window_ms`` milliseconds of GPU time (the steady-state tail of a
+benchmark loop; 0 = everything) and prints / writes one CSV row per kernel name:
+calls, total ms, share of the window's kernel time, mean us, grid, VGPR / AGPR / LDS.
+
+usage: python scripts/rocpd_summary.py gpurun_out/prof/run_results.db [--window_ms 600] [--csv out.csv]
+"""
+import argparse
+import csv
+import re
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
+    if name.startswith("void "):
+        name = name[5:]
+    return re.sub(r"\(.*$", "", name)[:110]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--window_ms", type=float, default=0.0)
+    ap.add_argument("--csv", default=None)
+    ap.add_argument("--top", type=int, default=30)
+    a = ap.parse_args(argv)
+    c = sqlite3.connect(a.db)
+    rows = c.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x, vgpr_count, accum_vgpr_count, "
+                     "lds_size from kernels order by start").fetchall()
+    if not rows:
+        print("no kernels")
+        return 1
+    t_end = max(r[2] for r in rows)
+    t0 = t_end - a.window_ms * 1e6 if a.window_ms > 0 else min(r[1] for r in rows)
+    agg = defaultdict(lambda: [0, 0.0, None])
+    busy = 0.0
+    for name, s, e, gx, gy, gz, wx, vg, ag, lds in rows:
+        if s < t0:
+            continue
+        k = short(name)
+        d = (e - s) / 1e3  # us
+        agg[k][0] += 1
+        agg[k][1] += d
+        agg[k][2] = (gx * gy * gz // max(wx, 1), wx, vg, ag, lds)
+        busy += d
+    span_ms = (t_end - t0) / 1e6
+    out = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    print(f"window {span_ms:.1f} ms, kernel time {busy / 1e3:.1f} ms ({100 * busy / 1e3 / span_ms:.1f}% busy), "
+          f"{sum(v[0] for v in agg.values())} dispatches")
+    print(f"{'ms':>9} {'%':>6} {'calls':>6} {'us/call':>9}  {'wgs':>7} {'wg':>4} {'vgpr':>4} {'agpr':>4} {'lds':>6}  kernel")
+    for k, (n, tot, meta) in out[:a.top]:
+        wgs, wx, vg, ag, lds = meta
+        print(f"{tot / 1e3:9.2f} {100 * tot / busy:6.2f} {n:6d} {tot / n:9.1f}  {wgs:7d} {wx:4d} {vg:4d} {ag:4d} {lds:6d}  {k}")
+    if a.csv:
+        with open(a.csv, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "calls", "total_ms", "pct", "us_per_call", "workgroups", "wg_size", "vgpr", "agpr",
+                        "lds"])
+            for k, (n, tot, meta) in out:
+                w.writerow([k, n, f"{tot / 1e3:.3f}", f"{100 * tot / busy:.2f}", f"{tot / n:.1f}", *meta])
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
