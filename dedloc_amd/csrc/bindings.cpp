@@ -465,6 +465,24 @@ void gemm_store(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tenso
   small_gemm(0, A, B, a, b, C, ldc, nullptr, 0, 0, bias, R, ldr, st);
 }
 
+// gemm_store plus the BatchNorm statistics of the stored values (stats [M / stat_rows][2N], fp32,
+// accumulated): in the GEMM epilogue where the kernel takes it (gemm8 EPI 4 for N % 256 == 0,
+// gemm_small for the narrow outputs), else one statistics pass over C afterwards
+void gemm_store_stats(const Mat& A, const Mat& B, const at::Tensor& a, const at::Tensor& b, bf16_t* C, long ldc,
+                      float* stats, long stat_rows, hipStream_t st) {
+  const int M = (int)A.rows, N = (int)B.rows, K = (int)A.k;
+  if (use_gemm8() && dl_gemm8(A.kouter, B.kouter, 4, cbf(a), A.ld, cbf(b), B.ld, M, N, K, C, ldc, nullptr, 0, 0, 0,
+                              nullptr, nullptr, 0, nullptr, 0, nullptr, 1, st, stats, stat_rows) == 0)
+    return;
+  if (N <= 192 && dl_gemm_small_splits(M, N, K) == 1 &&
+      dl_gemm_small(0, cbf(a), A.srow(), A.sk(), cbf(b), B.srow(), B.sk(), M, N, K, C, ldc, nullptr, 0, 0, nullptr,
+                    nullptr, 0, 1, nullptr, st, stats, stat_rows) == 0)
+    return;
+  gemm_store(A, B, a, b, C, ldc, nullptr, nullptr, 0, st);
+  TORCH_CHECK(ldc == N, "gemm_store_stats: the statistics pass needs a dense C");
+  check(dl_bn_stats(C, stats, stat_rows, N, (int)(M / stat_rows), st), "bn_stats");
+}
+
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& residual, bool trans_a, bool trans_b, int64_t epilogue) {
   expect_operands(a, b);
@@ -736,8 +754,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& x, const
                                                       const c10::optional<at::Tensor>& running_mean,
                                                       const c10::optional<at::Tensor>& running_var, double eps,
                                                       double momentum, bool relu, int64_t groups,
-                                                      const c10::optional<at::Tensor>& sums) {
+                                                      const c10::optional<at::Tensor>& sums, bool stats_ready) {
   expect_nhwc(x, "x");
+  TORCH_CHECK(!stats_ready || sums.has_value(), "bn_fwd: stats_ready needs the sums tensor");
   if (res.has_value()) expect_nhwc(*res, "res");
   expect(gamma, at::kFloat, "gamma");
   expect(beta, at::kFloat, "beta");
@@ -756,7 +775,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> bn_fwd(const at::Tensor& x, const
   }
   check(dl_bn_fwd(cbf(x), res.has_value() ? cbf(*res) : nullptr, bf(y), f32(gamma), f32(beta), sp,
                   f32(stats) + 2 * G * C, f32(stats) + 3 * G * C, rm, rv, R, (int)C, (int)G, (float)eps,
-                  (float)momentum, relu, cur_stream(x), sums.has_value() ? 1 : 0),
+                  (float)momentum, relu, cur_stream(x), sums.has_value() ? 1 : 0, stats_ready ? 1 : 0),
         "bn_fwd (channels must be 64..2048, a power-of-two multiple of 8)");
   return {y, stats.narrow(0, 2 * G * C, G * C).view({G, C}), stats.narrow(0, 3 * G * C, G * C).view({G, C})};
 }
@@ -930,7 +949,45 @@ inline DlConvGeom geom(const bf16_t* img, int64_t N, int64_t H, int64_t W, int64
                     (int)TR, (int)TS, (int)dh0, (int)dhs, (int)dw0, (int)dws};
 }
 
-at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad) {
+// stats (optional, fp32 [groups][2 Cout], accumulated): the BatchNorm statistics of the output per
+// statistics group of the batch (the producing epilogue computes them where the kernel allows,
+// otherwise one statistics pass runs after the conv)
+// cols (optional): the stem's column matrix from im2col_stem (computed once per pass and kept for the
+// weight gradient instead of being rebuilt there)
+at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad, float* stats,
+                           int64_t groups, const c10::optional<at::Tensor>& cols);
+
+at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad,
+                      const c10::optional<at::Tensor>& cols) {
+  return conv2d_fwd_impl(x, w, stride, pad, nullptr, 1, cols);
+}
+
+at::Tensor conv2d_fwd_stats(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad, at::Tensor sums,
+                            int64_t groups, const c10::optional<at::Tensor>& cols) {
+  expect(sums, at::kFloat, "sums");
+  TORCH_CHECK(groups >= 1 && x.size(0) % groups == 0, "conv2d_fwd_stats: batch must split into `groups`");
+  TORCH_CHECK(sums.numel() == 2 * groups * w.size(0), "conv2d_fwd_stats: sums must hold 2 * groups * Cout floats");
+  return conv2d_fwd_impl(x, w, stride, pad, f32(sums), groups, cols);
+}
+
+// the stem's column matrix [N*P*Q, Kp] (see stem_cols) for conv2d_fwd / conv2d_wgrad(cols=...)
+at::Tensor im2col_stem(const at::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad) {
+  expect_nhwc(x, "x");
+  const int64_t P = conv_out(x.size(2), R, stride, pad), Q = conv_out(x.size(3), S, stride, pad);
+  return stem_im2col(x, R, S, stride, pad, P, Q, stem_cols(R, S, x.size(1), false));
+}
+
+inline at::Tensor stem_cols_checked(const c10::optional<at::Tensor>& cols, const at::Tensor& x, int64_t R, int64_t S,
+                                    int64_t stride, int64_t pad, int64_t P, int64_t Q, const StemCols& sc) {
+  if (!cols.has_value()) return stem_im2col(x, R, S, stride, pad, P, Q, sc);
+  TORCH_CHECK(cols->scalar_type() == at::kBFloat16 && cols->is_contiguous() && cols->dim() == 2 &&
+                  cols->size(0) == x.size(0) * P * Q && cols->size(1) == sc.Kp,
+              "cols must be the stem's im2col_stem matrix for this input");
+  return *cols;
+}
+
+at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t stride, int64_t pad, float* stats,
+                           int64_t groups, const c10::optional<at::Tensor>& cols) {
   expect_nhwc(x, "x");
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4, "w must be a bf16 [Cout,Cin,R,S] GPU tensor");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -939,30 +996,40 @@ at::Tensor conv2d_fwd(const at::Tensor& x, const at::Tensor& w, int64_t stride, 
   const int64_t P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
   auto y = at::empty({N, K, P, Q}, x.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);
+  const long stat_rows = N / groups * P * Q;  // output rows per statistics group
   if (is_pointwise(R, S, stride, pad) && conv_gemm()) {
-    gemm_plain(rows2d(x), wk.view({K, C}), bf(y), K, cur_stream(x));
+    const at::Tensor xr = rows2d(x), wr = wk.view({K, C});
+    if (stats) gemm_store_stats(a_view(xr, false), b_view(wr, true), xr, wr, bf(y), K, stats, stat_rows, cur_stream(x));
+    else gemm_plain(xr, wr, bf(y), K, cur_stream(x));
     return y;
   }
   if (C % 64 == 0) {
-    check(dl_conv_fwd(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(wk), R * S * C,
-                      (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x)),
+    const DlConvGeom gm = geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1);
+    if (stats && dl_conv_fwd(gm, cbf(wk), R * S * C, (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x),
+                             stats, stat_rows) == 0)
+      return y;
+    check(dl_conv_fwd(gm, cbf(wk), R * S * C, (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x)),
           "conv2d_fwd");
+    if (stats) check(dl_bn_stats(cbf(y), stats, stat_rows, (int)K, (int)groups, cur_stream(x)), "bn_stats");
     return y;
   }
   // stem (3 input channels): im2col into a column matrix padded to a multiple of 64 columns, then
   // one GEMM against the equally padded weight rows
   const StemCols sc = stem_cols(R, S, C, false);
-  const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
+  const at::Tensor col = stem_cols_checked(cols, x, R, S, stride, pad, P, Q, sc);
   auto wp = at::zeros({K, sc.Kp}, w.options());
   wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
-  gemm_plain(col, wp, bf(y), K, cur_stream(x));
+  if (stats) gemm_store_stats(a_view(col, false), b_view(wp, true), col, wp, bf(y), K, stats, stat_rows, cur_stream(x));
+  else gemm_plain(col, wp, bf(y), K, cur_stream(x));
   return y;
 }
 
 // dX = conv^T(dY): for each output parity class (a, b) of the stride, a dense sub-convolution over
 // the taps r = r0, r0 + stride, ... that reach it (dY row = i + dh0 - tr), weights [Cin][tr][ts][Cout]
+// residual (optional, [N, C, H, W] channels-last bf16): added to dX — in the GEMM epilogue on the
+// 1x1 stride-1 path (a Bottleneck's conv1 taking the identity branch's gradient), afterwards otherwise
 at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t stride, int64_t pad, int64_t H,
-                        int64_t W) {
+                        int64_t W, const c10::optional<at::Tensor>& residual) {
   const at::Tensor dy = dy_in.is_contiguous(at::MemoryFormat::ChannelsLast)
                             ? dy_in
                             : dy_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -973,11 +1040,16 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
   TORCH_CHECK(w.size(0) == K, "conv2d_dgrad: weight/grad channel mismatch");
   TORCH_CHECK(K % 64 == 0, "conv2d_dgrad needs Cout % 64 == 0");
   auto dx = at::empty({N, C, H, W}, dy.options(), at::MemoryFormat::ChannelsLast);
+  if (residual.has_value()) {
+    expect_nhwc(*residual, "residual");
+    TORCH_CHECK(residual->sizes() == dx.sizes(), "conv2d_dgrad: residual must have the input's shape");
+  }
   const at::Tensor wk = krsc_view(w);  // [K, R, S, C]
   if (is_pointwise(R, S, stride, pad) && H == P && W == Q && conv_gemm()) {
-    // dX[M, C] = dY[M, K] W[K, C]: the weight as a K-outer B operand, no transposed copy
+    // dX[M, C] = dY[M, K] W[K, C] (+ residual): the weight as a K-outer B operand, no transposed copy
     const at::Tensor dyr = rows2d(dy), wkc = wk.view({K, C});
-    gemm_store(a_view(dyr, false), b_view(wkc, false), dyr, wkc, bf(dx), C, nullptr, nullptr, 0, cur_stream(dy));
+    gemm_store(a_view(dyr, false), b_view(wkc, false), dyr, wkc, bf(dx), C, nullptr,
+               residual.has_value() ? cbf(*residual) : nullptr, C, cur_stream(dy));
     return dx;
   }
   for (int64_t a = 0; a < stride; ++a) {
@@ -1000,20 +1072,23 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
             "conv2d_dgrad");
     }
   }
+  if (residual.has_value()) dx.add_(*residual);
   return dx;
 }
 
 // dW (fp32 [Cout, Cin, R, S] with KRSC memory, e.g. the flat-buffer grad view) += conv wgrad
-void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, int64_t stride, int64_t pad) {
+void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, int64_t stride, int64_t pad,
+                  const c10::optional<at::Tensor>& cols) {
   const at::Tensor dy = dy_in.is_contiguous(at::MemoryFormat::ChannelsLast)
                             ? dy_in
                             : dy_in.contiguous(at::MemoryFormat::ChannelsLast);
   expect_nhwc(dy, "dy");
-  expect_nhwc(x, "x");
+  if (!cols.has_value()) expect_nhwc(x, "x");  // with the stem's cols only x's shape is read
   TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.dim() == 4, "dw must be an fp32 4-D GPU tensor");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t K = dy.size(1), P = dy.size(2), Q = dy.size(3), R = dw.size(2), S = dw.size(3);
   TORCH_CHECK(dw.size(0) == K && dw.size(1) == C, "conv2d_wgrad: dw shape mismatch");
+  TORCH_CHECK(!cols.has_value() || C % 64 != 0, "conv2d_wgrad: cols are the stem's (C not a multiple of 64) only");
   at::Tensor dk = dw.permute({0, 2, 3, 1});  // [K, R, S, C]
   const bool direct = dk.is_contiguous();
   at::Tensor acc = direct ? dk : at::zeros({K, R, S, C}, dw.options());
@@ -1028,7 +1103,7 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
     // stem: wgrad over the padded column matrix into a [K, R, SCp] slab, then the real columns
     const StemCols sc = stem_cols(R, S, C, false);
     const int64_t M = N * P * Q;
-    const at::Tensor col = stem_im2col(x, R, S, stride, pad, P, Q, sc);
+    const at::Tensor col = stem_cols_checked(cols, x, R, S, stride, pad, P, Q, sc);
     auto slab = at::zeros({K, R, sc.SCp}, dw.options());
     rc = dl_conv_wgrad(geom(cbf(col), M, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1), cbf(dy), K, (int)K,
                        f32(slab), R * sc.SCp, (int)(R * sc.SCp), cur_stream(dy));
@@ -1042,6 +1117,8 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
 
 TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("conv2d_fwd", &conv2d_fwd);
+  m.impl("conv2d_fwd_stats", &conv2d_fwd_stats);
+  m.impl("im2col_stem", &im2col_stem);
   m.impl("conv2d_dgrad", &conv2d_dgrad);
   m.impl("conv2d_wgrad", &conv2d_wgrad);
   m.impl("bn_fwd", &bn_fwd);

@@ -64,10 +64,12 @@ int dl_gemm(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, cons
             long ldh, float* dbias, int splits, hipStream_t st);
 
 // gemm8.hip (LDS-DMA 8-phase MFMA GEMM; epi as dl_gemm; EPI 3 writes fp32 slab blockIdx.y of
-// Cf (+= when accumulate); splits > 1 only for EPI 3)
+// Cf (+= when accumulate); splits > 1 only for EPI 3; EPI 4 = EPI 0 plus BatchNorm statistics of
+// the stored values: stats[m / stat_rows][0..N) += column sums, [N..2N) += sums of squares)
 int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N,
              int K, bf16_t* C, long ldc, float* Cf, long ldcf, long slab, int accumulate, const float* bias,
-             const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st);
+             const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st,
+             float* stats = nullptr, long stat_rows = 0);
 
 // swav.hip
 int dl_sinkhorn(const float* scores, float* P, float* Q, float* ws, int n, int K, int bs, float eps, int iters,
@@ -81,7 +83,10 @@ int dl_multicrop(const float* pool, int P, int Hp, int Wp, const float* params, 
                  const float* stdv, float* ws, bf16_t* out, hipStream_t st);
 int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta, float* sums,
               float* mean, float* rstd, float* run_mean, float* run_var, long R, int C, int G, float eps,
-              float momentum, int relu, hipStream_t st, int sums_zeroed = 0);
+              float momentum, int relu, hipStream_t st, int sums_zeroed = 0, int stats_ready = 0);
+// BatchNorm forward statistics alone (sums [G][2C] += per-group channel sums / sums of squares of
+// x [G*R, C]); dl_bn_fwd with stats_ready = 1 then skips its own statistics pass
+int dl_bn_stats(const bf16_t* x, float* sums, long R, int C, int G, hipStream_t st);
 int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
               const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
               int G, int relu, hipStream_t st, int sums_zeroed = 0, int accumulate = 0, const float* beta = nullptr);
@@ -96,8 +101,10 @@ struct DlConvGeom {
   int TR, TS, dh0, dhs, dw0, dws;
 };
 // out[(n, i*osh+oh0, j*osw+ow0), 0..N) (NHWC, row stride ldo) = sum_{t,c} img(pixel(m,t), c) * w[n][t*C + c]
+// stats (optional): BatchNorm statistics of the stored output as in dl_gemm8 EPI 4 (stat_rows a
+// multiple of 128 dividing M; -1 otherwise)
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                int oh0, int ow0, long ldo, hipStream_t st);
+                int oh0, int ow0, long ldo, hipStream_t st, float* stats = nullptr, long stat_rows = 0);
 // dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols)
 int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,
                   hipStream_t st);
@@ -133,6 +140,8 @@ int dl_l2norm_bwd(const bf16_t* dy, const bf16_t* y, const float* rinv, bf16_t* 
 // gemm_small.hip: any-shape / any-stride bf16 MFMA GEMM (epi 0: bf16 C (+bias)(+R); 1: fp32 Cf (+)=).
 // splits > 1 splits the reduction into fp32 slabs: ws must hold splits * M * N floats.
 int dl_gemm_small_splits(int M, int N, int K);
+// stats (epi 0, splits 1 only): BatchNorm statistics of the stored values as in dl_gemm8 EPI 4
+// (stat_rows a multiple of 128 dividing M)
 int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B, long sbn, long sbk, int M, int N,
                   int K, bf16_t* C, long ldc, float* Cf, long ldcf, int accumulate, const float* bias, const bf16_t* R,
-                  long ldr, int splits, float* ws, hipStream_t st);
+                  long ldr, int splits, float* ws, hipStream_t st, float* stats = nullptr, long stat_rows = 0);

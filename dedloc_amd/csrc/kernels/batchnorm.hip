@@ -384,15 +384,25 @@ inline int apply_blocks(long nvec) {
 // BatchNorm's workspace instead of one hipMemsetAsync — a ~5 us launch — per call)
 int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta, float* sums,
               float* mean, float* rstd, float* run_mean, float* run_var, long R, int C, int G, float eps,
-              float momentum, int relu, hipStream_t st, int sums_zeroed) {
+              float momentum, int relu, hipStream_t st, int sums_zeroed, int stats_ready) {
   if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
-  if (!sums_zeroed) DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
-  long rpb;
-  const int nb = stats_blocks(R, C, rpb);
-  bn_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(x, sums, R, C, rpb);
+  if (!stats_ready) {  // else: the producing conv / GEMM epilogue already accumulated them
+    if (!sums_zeroed) DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
+    long rpb;
+    const int nb = stats_blocks(R, C, rpb);
+    bn_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(x, sums, R, C, rpb);
+  }
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
   bn_apply_kernel<<<dim3(na, G), kThreads, 0, st>>>(x, res, y, sums, gamma, beta, mean, rstd, run_mean, run_var, R, C,
                                                     eps, momentum, relu);
+  return 0;
+}
+
+int dl_bn_stats(const bf16_t* x, float* sums, long R, int C, int G, hipStream_t st) {
+  if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
+  long rpb;
+  const int nb = stats_blocks(R, C, rpb);
+  bn_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(x, sums, R, C, rpb);
   return 0;
 }
 

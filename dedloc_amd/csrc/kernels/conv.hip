@@ -25,6 +25,7 @@
 // register stage sets keep two k-tiles of loads in flight.  The forward kernel swaps the MFMA
 // operand roles so each lane owns 4 consecutive output channels of one pixel (8-byte NHWC stores).
 #include <algorithm>
+#include <cstdlib>
 
 #include "dl_common.h"
 #include "dl_kernels.h"
@@ -127,6 +128,8 @@ struct FwdArgs {
   int M, K;
   unsigned img_bytes, w_bytes;
   int tpw;  // output tiles per workgroup
+  float* stats;    // optional BatchNorm statistics [M / stat_rows][2N] of the stored output
+  long stat_rows;
 };
 
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
@@ -238,6 +241,10 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
+    // thread tid always writes channel chunk tid & 15 (8 channels) of rows (tid >> 4) + 16 u
+    float csum[8], csq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = csq[e] = 0.f;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int idx = tid + NT * u, row = idx >> 4, c = idx & 15;
@@ -248,7 +255,42 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
         const int i = r / g.J, j = r - i * g.J;
         bf16_t* orow = p.out + ((long)(n * p.OH + i * p.osh + p.oh0) * p.OW + j * p.osw + p.ow0) * p.ldo;
         *reinterpret_cast<uint4*>(orow + ch) = v;
+        if (p.stats) {
+          float f[8];
+          unpack8_bf16(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            csum[e] += f[e];
+            csq[e] = fmaf(f[e], f[e], csq[e]);
+          }
+        }
       }
+    }
+    if (p.stats) {
+      // Atomics are issue-bound (one wave-instruction per ~50 ns per CU, MI355X_MICROARCH.md), so
+      // the tile's 256 statistics are folded before they leave: lanes l, l^16, l^32, l^48 share a
+      // chunk (shuffles), the 4 waves meet in the (drained) staging buffer, and every thread adds
+      // one value — 4 wave-instructions per tile.
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        csum[e] += __shfl_xor(csum[e], 16, 64);
+        csq[e] += __shfl_xor(csq[e], 16, 64);
+        csum[e] += __shfl_xor(csum[e], 32, 64);
+        csq[e] += __shfl_xor(csq[e], 32, 64);
+      }
+      __syncthreads();  // every staged row has been read: the buffer is free
+      float* red = reinterpret_cast<float*>(stage);  // [wave][moment][128 channels]
+      if (lane < 16) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[wv * 256 + lane * 8 + e] = csum[e];
+          red[wv * 256 + 128 + lane * 8 + e] = csq[e];
+        }
+      }
+      __syncthreads();
+      const float v = red[tid] + red[256 + tid] + red[512 + tid] + red[768 + tid];
+      const int chl = tid & 127, mom = tid >> 7;
+      if (n0 + chl < p.N) atomicAdd(p.stats + (m0 / p.stat_rows) * 2L * p.N + (long)mom * p.N + n0 + chl, v);
     }
     __syncthreads();  // the staging buffer is restaged by the pipeline right after
   };
@@ -470,9 +512,11 @@ void set_lds(Kern k) {
 }  // namespace
 
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                int oh0, int ow0, long ldo, hipStream_t st) {
+                int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows) {
   if (g.C % BK || N % 4 || ldw % 8 || ldo % 4 || g.I < 0 || g.J < 0) return -1;
   const long M = (long)g.Nimg * g.I * g.J;
+  // statistics: every 128-row tile inside one group, whole 8-channel chunks
+  if (stats && (stat_rows < BM || stat_rows % BM || M % stat_rows || N % 8)) return -1;
   if (M >= (1L << 31)) return -1;
   if (M == 0 || N == 0) return 0;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * ldw;
@@ -481,7 +525,7 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
   // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
   const int tpw = std::max(1, tiles / 1024);
   FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C,
-            (unsigned)img_bytes, (unsigned)w_bytes, tpw};
+            (unsigned)img_bytes, (unsigned)w_bytes, tpw, stats, stat_rows};
   static bool attr = false;
   if (!attr) {
     set_lds(conv_fwd_kernel);
@@ -499,10 +543,17 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
   if (M >= (1L << 24)) return -1;  // fdiv exactness bound
   if (M == 0 || Ncols == 0) return 0;
   const int tiles = ((Cout + BM - 1) / BM) * ((Ncols + BN - 1) / BN);
-  // split the (long) pixel reduction so that ~4 workgroups per CU exist; each split is a
-  // multiple of the 64-deep k-step and at least 8 k-steps long
+  // split the (long) pixel reduction so that ~`target` workgroups exist (default 256: one per CU;
+  // SwAV b=64 iteration 1990-1997 samples/s at 1024, 2051-2061 at 256, 2041 at 512);
+  // each split is a multiple of the 64-deep k-step and at least 8 k-steps long.  Every split adds
+  // its 128x128 fp32 tile with atomics (256 wave-instructions per tile), so fewer, longer splits
+  // trade parallelism for atomic traffic (DEDLOC_CONV_WGRAD_WGS: A/B measurements)
+  static const long target = [] {
+    const char* e = std::getenv("DEDLOC_CONV_WGRAD_WGS");
+    return e ? std::max(1L, std::atol(e)) : 256L;
+  }();
   const long ksteps = (M + BK - 1) / BK;
-  long splits = std::max(1L, std::min<long>((1024 + tiles - 1) / tiles, ksteps / 8));
+  long splits = std::max(1L, std::min<long>((target + tiles - 1) / tiles, ksteps / 8));
   const long steps_per = (ksteps + splits - 1) / splits;
   splits = (ksteps + steps_per - 1) / steps_per;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, dy_bytes = 2L * M * ldy;

@@ -36,6 +36,10 @@
 //   EPI_GELU   H = bf16(acc + bias); C = gelu_new(H)                          bf16 x2
 //   EPI_DGELU  C = bf16(acc) * gelu_new'(R[m,n]); dbias[n] += sum_m C         bf16 (+ fp32 atomics)
 //   EPI_F32    Cf[z][m,n] = acc  or  += acc (reduction split z)                fp32
+//   EPI_STATS  EPI_STORE, plus per-column sum and sum of squares of the stored bf16 values into
+//              stats[g][0..N) / stats[g][N..2N) (fp32 atomics), g = m / stat_rows: the batch
+//              statistics of a BatchNorm over this output (SwAV's 1x1 convs), so the BN forward
+//              does not re-read the tensor
 #include <cstdlib>
 #include <type_traits>
 
@@ -49,7 +53,7 @@ typedef short s4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4_t lds_s4;
 typedef __attribute__((address_space(3))) void lds_void;
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3 };
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_STATS = 4 };
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
 constexpr int HALF = 16384;     // one half-tile image
@@ -159,6 +163,7 @@ struct Args {
   bf16_t* H; long ldh;           // pre-activation out (GELU)
   float* dbias;                  // column sums out (DGELU)
   int nt;                        // non-temporal output stores (bf16 epilogues)
+  float* stats; long stat_rows;  // EPI_STATS: [M / stat_rows][2N] column sums / sums of squares
 };
 
 #define DL_MFMA_QUAD(QM, QN)                                                          \
@@ -326,12 +331,12 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       bias_v[qn][ni] = 0.f;
-      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
+      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_STATS)
         if (p.bias) bias_v[qn][ni] = p.bias[n0 + colperm<BKO>(wn * 64 + qn * 32 + ni * 16 + ccol)];
     }
-  float colsum[8];
+  float colsum[8], colsq[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
+  for (int j = 0; j < 8; ++j) colsum[j] = colsq[j] = 0.f;
   const int rch = lane & 7;   // 8-column chunk handled in the row phase
   const int rr = lane >> 3;   // row within a pass of 8 rows
   const int gn = n0 + colperm<BKO>(wn * 64 + rch * 8);
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   // its passes, and the next half's row j right after pass j consumed this half's — ahead of that
   // pass's store.  Loaded inside each pass instead, every pass waited (vmcnt(0)) for its load's full
   // HBM latency and, the counter being in issue order, for every store before it.
-  const bool has_r = EPI == EPI_DGELU || (EPI == EPI_STORE && p.R != nullptr);
+  const bool has_r = EPI == EPI_DGELU || ((EPI == EPI_STORE || EPI == EPI_STATS) && p.R != nullptr);
   auto rrow = [&](int qm, int pass) -> uint4 {
     const int gm = min(m0 + wm * 128 + qm * 64 + pass * 8 + rr, p.M - 1);  // tail rows: clamped, unused
     return *reinterpret_cast<const uint4*>(p.R + (long)gm * p.ldr + gn);
@@ -389,6 +394,18 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
             for (int j = 0; j < 8; ++j) v[j] += rv[j];
           }
           store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
+        } else if constexpr (EPI == EPI_STATS) {
+          if (has_r) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += rv[j];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[j] = round_bf16(v[j]);
+            colsum[j] += v[j];
+            colsq[j] = fmaf(v[j], v[j], colsq[j]);
+          }
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
         } else if constexpr (EPI == EPI_GELU) {
           float h[8];
 #pragma unroll
@@ -433,6 +450,34 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
         for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + colperm<BKO>(wn * 64 + lane * 8) + j], colsum[j]);
       }
     }
+  }
+  if constexpr (EPI == EPI_STATS) {
+    // lanes with the same 8-column chunk (lane & 7) hold disjoint rows: fold them, then one atomic
+    // per column and moment from lanes 0..7
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float s = colsum[j], q = colsq[j];
+      s += __shfl_xor(s, 8, 64);
+      q += __shfl_xor(q, 8, 64);
+      s += __shfl_xor(s, 16, 64);
+      q += __shfl_xor(q, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      colsum[j] = s;
+      colsq[j] = q;
+    }
+    // every lane now holds its chunk's eight totals; lane l adds column (l & 7) * 8 + (l >> 3):
+    // 64 distinct columns, one wave-instruction per moment (atomics are issue-bound)
+    const int jl = lane >> 3;
+    float s = colsum[0], q = colsq[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      s = jl == j ? colsum[j] : s;
+      q = jl == j ? colsq[j] : q;
+    }
+    float* st = p.stats + (m0 / p.stat_rows) * 2L * p.N + n0 + colperm<BKO>(wn * 64 + rch * 8) + jl;
+    atomicAdd(st, s);
+    atomicAdd(st + p.N, q);
   }
 }
 
@@ -736,7 +781,7 @@ int persistent_ctas() {  // read per call: tests and benchmarks A/B the two form
 template <bool AKO, bool BKO, int EPI>
 int launch8(const Args& a, int splits, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
-  if constexpr (EPI != EPI_F32) {
+  if constexpr (EPI != EPI_F32 && EPI != EPI_STATS) {
     // DEDLOC_GEMM8_PERSIST=n: the persistent deferred-store form on min(tiles, n) workgroups
     // (n = 256: one per CU of an MI355X)
     const int ctas = persistent_ctas();
@@ -758,7 +803,8 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // pointer 16-byte aligned.
 int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N,
              int K, bf16_t* C, long ldc, float* Cf, long ldcf, long slab, int accumulate, const float* bias,
-             const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st) {
+             const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st, float* stats,
+             long stat_rows) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return -1;
   if (N % BN || K % (BK * splits)) return -1;
   if (a_kouter && M % BM) return -1;
@@ -771,12 +817,15 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
     if (epi == EPI_GELU && (!H || ldh % 8 || !aligned16(H))) return -1;
     if (epi == EPI_DGELU && !R) return -1;
     if (splits != 1) return -1;
+    // EPI_STATS: every 256-row tile inside one statistics group
+    if (epi == EPI_STATS && (!stats || stat_rows < BM || stat_rows % BM || M % stat_rows)) return -1;
   }
   // non-temporal bf16 output stores by default (+4..17% on the store-bound epilogues, gemm_bench);
   // DEDLOC_GEMM8_NT=0 for A/B runs
   const char* nte = std::getenv("DEDLOC_GEMM8_NT");
   const int nt = nte ? std::atoi(nte) : 1;
-  Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt};
+  Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt,
+         stats, stat_rows};
 #define DL_GEMM8_CASE(AK, BK_, E) \
   if (a_kouter == AK && b_kouter == BK_ && epi == E) return launch8<AK, BK_, E>(a, splits, st);
   DL_GEMM8_CASE(0, 0, EPI_STORE)
@@ -787,6 +836,7 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
   DL_GEMM8_CASE(0, 0, EPI_DGELU)
   DL_GEMM8_CASE(1, 1, EPI_F32)
   DL_GEMM8_CASE(0, 0, EPI_F32)
+  DL_GEMM8_CASE(0, 0, EPI_STATS)
 #undef DL_GEMM8_CASE
   return -1;
 }

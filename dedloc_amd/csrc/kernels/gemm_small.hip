@@ -22,6 +22,9 @@
 //
 // Epilogues: EPI_STORE C = acc (+ bias[n]) (+ R[m, n])  bf16 (row stride ldc)
 //            EPI_F32   Cf[m, n] = acc  or  += acc        fp32 (row stride ldcf)
+// EPI_STORE with `stats`: also the per-column sum / sum of squares of the stored bf16 values into
+// stats[m / stat_rows][0..N) / [N..2N) (BatchNorm statistics of a 64 / 128-channel 1x1 conv or the
+// stem, fp32 atomics; a tile's rows never straddle two groups: stat_rows % 128 == 0)
 #include <algorithm>
 
 #include "dl_common.h"
@@ -42,6 +45,7 @@ struct SmallArgs {
   float* Cf; long ldcf; long slab; int accumulate;
   const float* bias;
   const bf16_t* R; long ldr;
+  float* stats; long stat_rows;
 };
 
 // U 8-element chunks of a (64 U) x 32 operand tile per thread, into registers.
@@ -136,6 +140,9 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
       for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     __syncthreads();
   }
+  float csum[NJ], csq[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) csum[j] = csq[j] = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -153,13 +160,43 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
         if constexpr (EPI == 0) {
           v += bv;
           if (p.R) v += bf2f(p.R[(long)m * p.ldr + n]);
-          p.C[(long)m * p.ldc + n] = f2bf(v);
+          const bf16_t o = f2bf(v);
+          p.C[(long)m * p.ldc + n] = o;
+          const float r = bf2f(o);
+          csum[j] += r;
+          csq[j] = fmaf(r, r, csq[j]);
         } else {
           float* dst = p.Cf + (long)blockIdx.z * p.slab + (long)m * p.ldcf + n;
           *dst = p.accumulate ? *dst + v : v;
         }
       }
     }
+  if constexpr (EPI == 0) {
+    if (p.stats) {
+      // lanes l, l^16, l^32, l^48 hold the same columns: fold them, then lane l adds column block
+      // j = l >> 4, column l & 15 — one wave-instruction per moment (atomics are issue-bound)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        csum[j] += __shfl_xor(csum[j], 16, 64);
+        csq[j] += __shfl_xor(csq[j], 16, 64);
+        csum[j] += __shfl_xor(csum[j], 32, 64);
+        csq[j] += __shfl_xor(csq[j], 32, 64);
+      }
+      const int jl = lane >> 4;
+      float s = csum[0], q = csq[0];
+#pragma unroll
+      for (int j = 1; j < NJ; ++j) {
+        s = jl == j ? csum[j] : s;
+        q = jl == j ? csq[j] : q;
+      }
+      const int n = n0 + wn * (TN / 2) + jl * 16 + (lane & 15);
+      if (jl < NJ && n < p.N) {
+        float* st = p.stats + (m0 / p.stat_rows) * 2L * p.N;
+        atomicAdd(st + n, s);
+        atomicAdd(st + p.N + n, q);
+      }
+    }
+  }
 }
 
 // out = finish(sum_z ws[z][m, n]): bf16 (+ bias)(+ R) or fp32 (+)=
@@ -244,8 +281,9 @@ int dl_gemm_small_splits(int M, int N, int K) {
 
 int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B, long sbn, long sbk, int M, int N,
                   int K, bf16_t* C, long ldc, float* Cf, long ldcf, int accumulate, const float* bias, const bf16_t* R,
-                  long ldr, int splits, float* ws, hipStream_t st) {
+                  long ldr, int splits, float* ws, hipStream_t st, float* stats, long stat_rows) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return -1;
+  if (stats && (epi != 0 || splits != 1 || stat_rows < TM || stat_rows % TM || M % stat_rows)) return -1;
   if (epi == 0 && !C) return -1;
   if (epi == 1 && !Cf) return -1;
   if (splits > 1 && !ws) return -1;
@@ -258,12 +296,14 @@ int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B,
   walk(A, sam, sak, &LA, &VA);
   walk(B, sbn, sbk, &LB, &VB);
   if (S == 1) {
-    SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, C, ldc, Cf, ldcf, 0, accumulate, bias, R, ldr};
+    SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, C, ldc, Cf, ldcf, 0, accumulate, bias, R, ldr, stats,
+                stat_rows};
     if (epi == 0) launch_tn<0>(a, LA, VA, LB, VB, tn, 1, st);
     else launch_tn<1>(a, LA, VA, LB, VB, tn, 1, st);
     return 0;
   }
-  SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, nullptr, 0, ws, N, (long)M * N, 0, nullptr, nullptr, 0};
+  SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, nullptr, 0, ws, N, (long)M * N, 0, nullptr, nullptr, 0,
+              nullptr, 0};
   launch_tn<1>(a, LA, VA, LB, VB, tn, S, st);
   const long total = (long)M * N;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);

@@ -28,6 +28,23 @@ from torch.utils.checkpoint import checkpoint
 # BN+ReLU (no residual) backward reads only dy and x: the ReLU mask is recomputed from x
 # (DEDLOC_BN_XMASK=0: read y instead — A/B measurement switch)
 _BN_XMASK = os.environ.get("DEDLOC_BN_XMASK", "1") != "0"
+# BatchNorm forward statistics accumulated in the producing conv's epilogue (DEDLOC_CONV_STATS=0:
+# a separate statistics pass per BN — A/B measurement switch)
+_CONV_STATS = os.environ.get("DEDLOC_CONV_STATS", "1") != "0"
+# identity-branch gradient added in conv1's data-gradient epilogue (DEDLOC_RES_LINK=0: autograd's add)
+_RES_LINK = os.environ.get("DEDLOC_RES_LINK", "1") != "0"
+
+
+class _GradLink:
+    """Hands the identity-branch gradient of a Bottleneck from bn3's backward (the residual input's
+    gradient, which autograd would otherwise add to conv1's data gradient with a separate kernel) to
+    conv1's backward, whose data-gradient GEMM adds it in its epilogue.  bn3's backward always runs
+    first: conv1's backward depends on it through conv3 -> bn2 -> conv2 -> bn1."""
+
+    __slots__ = ("g",)
+
+    def __init__(self):
+        self.g = None
 
 
 class _BNAct(torch.autograd.Function):
@@ -40,11 +57,13 @@ class _BNAct(torch.autograd.Function):
     so autograd launches no per-pass accumulation adds."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, res, running_mean, running_var, relu, eps, momentum, groups, ws, module):
+    def forward(ctx, x, gamma, beta, res, running_mean, running_var, relu, eps, momentum, groups, ws, module,
+                stats_ready=False, link=None):
         y, mean, rstd = torch.ops.dedloc.bn_fwd(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu,
-                                                groups, None if ws is None else ws[0])
+                                                groups, None if ws is None else ws[0], stats_ready)
         ctx.save_for_backward(x, y, mean, rstd, gamma, beta)
         ctx.relu, ctx.has_res, ctx.ws, ctx.module = relu, res is not None, ws, module
+        ctx.link = link if res is not None else None
         return y
 
     @staticmethod
@@ -61,7 +80,10 @@ class _BNAct(torch.autograd.Function):
                                                           beta if (_BN_XMASK and ctx.relu and not ctx.has_res) else None)
         if acc:
             dgamma = dbeta = None
-        return (dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None)
+        if ctx.link is not None:  # the residual's gradient rides in conv1's data-gradient epilogue
+            ctx.link.g, dres = dres, None
+        return (dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None,
+                None, None)
 
 
 class _ConvNHWC(torch.autograd.Function):
@@ -70,7 +92,7 @@ class _ConvNHWC(torch.autograd.Function):
     bound ``.grad`` (the flat gradient buffer, KRSC layout) when there is one, like the ALBERT layer."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, module):
+    def forward(ctx, x, weight, stride, pad, module, stats=None, groups=1, link=None):
         # bf16 copy of the weight (keeps the channels-last KRSC strides), shared by the trunk passes
         # of one SwAVModel.forward (one cast per iteration instead of one per resolution group); the
         # model clears the cache at the start and end of every forward, so an optimizer update
@@ -80,30 +102,45 @@ class _ConvNHWC(torch.autograd.Function):
             wb = weight.detach().to(torch.bfloat16)
             if module._wb_share:
                 module._wb_cache = wb
-        ctx.save_for_backward(x, wb)
+        # the stem (3 input channels): its im2col column matrix is built once here and kept for the
+        # weight gradient (the input image needs no gradient, so the matrix replaces it)
+        cols = None
+        if x.shape[1] % 64 and not x.requires_grad:
+            cols = torch.ops.dedloc.im2col_stem(x, wb.shape[2], wb.shape[3], stride, pad)
+        ctx.save_for_backward(x if cols is None else cols, wb)
         ctx.stride, ctx.pad, ctx.module = stride, pad, module
-        return torch.ops.dedloc.conv2d_fwd(x, wb, stride, pad)
+        ctx.has_cols, ctx.xshape, ctx.link = cols is not None, tuple(x.shape), link
+        if stats is not None:  # the consuming BatchNorm's statistics, accumulated by the conv's epilogue
+            return torch.ops.dedloc.conv2d_fwd_stats(x, wb, stride, pad, stats, groups, cols)
+        return torch.ops.dedloc.conv2d_fwd(x, wb, stride, pad, cols)
 
     @staticmethod
     def backward(ctx, dy):
         x, wb = ctx.saved_tensors
+        cols = None
+        if ctx.has_cols:  # stem: x is only consulted for its shape
+            cols = x
+            x = torch.empty((), dtype=torch.bfloat16, device=dy.device).expand(ctx.xshape)
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3])
+            res = None
+            if ctx.link is not None:  # + the block's identity-branch gradient (see _GradLink)
+                res, ctx.link.g = ctx.link.g, None
+            dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3], res)
         dw = None
         if ctx.needs_input_grad[1]:
             weight = ctx.module.weight
             g = weight.grad
             if (g is not None and ctx.module.inplace_wgrad and g.dtype == torch.float32
                     and g.permute(0, 2, 3, 1).is_contiguous()):
-                torch.ops.dedloc.conv2d_wgrad(dy, x, g, ctx.stride, ctx.pad)  # in place, no AccumulateGrad
+                torch.ops.dedloc.conv2d_wgrad(dy, x, g, ctx.stride, ctx.pad, cols)  # in place, no AccumulateGrad
             else:
                 dw = torch.zeros(weight.shape, dtype=torch.float32, device=weight.device).contiguous(
                     memory_format=torch.channels_last)
-                torch.ops.dedloc.conv2d_wgrad(dy, x, dw, ctx.stride, ctx.pad)
+                torch.ops.dedloc.conv2d_wgrad(dy, x, dw, ctx.stride, ctx.pad, cols)
                 dw = dw.to(weight.dtype)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 class ConvNHWC(nn.Conv2d):
@@ -119,7 +156,11 @@ class ConvNHWC(nn.Conv2d):
     # (HIP-graph capture via make_graphed_callables needs every parameter to receive an autograd grad)
     inplace_wgrad = True
 
-    def forward(self, x):
+    def forward(self, x, bn=None, link=None):
+        """``bn``: the BNAct that consumes this output.  When it will take its fused path with a
+        pass workspace, the conv's epilogue accumulates that BatchNorm's batch statistics and the BN
+        forward skips its own statistics pass over the tensor.  ``link``: a _GradLink whose gradient the
+        data-gradient epilogue adds (Bottleneck conv1)."""
         if not x.is_cuda:
             return super().forward(x)
         if not (self.bias is None and self.groups == 1 and self.dilation == (1, 1)
@@ -128,7 +169,11 @@ class ConvNHWC(nn.Conv2d):
             raise NotImplementedError("ConvNHWC: only the ResNet-50 conv forms (no bias, groups 1, square "
                                       "stride/padding) have GPU kernels")
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self)
+        if bn is not None and bn.takes_conv_stats():
+            bn.stats_ready = True
+            return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, bn.pass_ws[0],
+                                   bn.stat_groups, link)
+        return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, None, 1, link)
 
 
 class BNAct(nn.BatchNorm2d):
@@ -150,8 +195,14 @@ class BNAct(nn.BatchNorm2d):
         self.stat_groups = 1  # >1: the batch holds that many crops, each normalised with its own stats
         self.pass_ws = None   # set by ResNet50Trunk.forward: (fwd sums, bwd sums) slices, pre-zeroed
         self.count_deferred = False  # num_batches_tracked is advanced by the trunk, one launch per pass
+        self.stats_ready = False  # the producing conv accumulated this call's statistics into pass_ws[0]
 
-    def forward(self, x, res=None):
+    def takes_conv_stats(self) -> bool:
+        """True when this BN's next forward runs the fused kernels over a pre-zeroed pass workspace,
+        so the conv producing its input can accumulate the batch statistics in its epilogue."""
+        return self.fused and self.training and self.pass_ws is not None and _CONV_STATS
+
+    def forward(self, x, res=None, link=None):
         G = self.stat_groups if self.training else 1
         if (self.fused and self.training and x.is_cuda and x.dtype == torch.bfloat16
                 and x.is_contiguous(memory_format=torch.channels_last)
@@ -160,8 +211,10 @@ class BNAct(nn.BatchNorm2d):
             if not self.count_deferred:
                 self.num_batches_tracked.add_(G)
             ws, self.pass_ws = self.pass_ws, None
+            ready, self.stats_ready = self.stats_ready and ws is not None, False
             return _BNAct.apply(x, self.weight, self.bias, res, self.running_mean, self.running_var, self.relu,
-                                self.eps, self.momentum, G, ws, self)
+                                self.eps, self.momentum, G, ws, self, ready, link)
+        self.stats_ready = False
         if G > 1:  # reference semantics without the fused kernel: one BN call per crop chunk
             y = torch.cat([super(BNAct, self).forward(c) for c in x.chunk(G)])
         else:
@@ -232,10 +285,17 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), idt)
+        link = None
+        if self.downsample is None:
+            idt = x
+            if _RES_LINK and x.is_cuda and x.requires_grad and torch.is_grad_enabled():
+                link = _GradLink()
+        else:
+            conv, bn = self.downsample[0], self.downsample[1]
+            idt = bn(conv(x, bn))
+        out = self.bn1(self.conv1(x, self.bn1, link))
+        out = self.bn2(self.conv2(out, self.bn2))
+        return self.bn3(self.conv3(out, self.bn3), idt, link)
 
 
 class ResNet50Trunk(nn.Module):
@@ -301,7 +361,7 @@ class ResNet50Trunk(nn.Module):
 
     def forward(self, x):
         self._prepare_bn_pass(x)
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.maxpool(self.bn1(self.conv1(x, self.bn1)))
         for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
             if self.checkpoint_stages and self.training and x.requires_grad:
                 x = checkpoint(stage, x, use_reentrant=False)
@@ -317,7 +377,7 @@ class _HeadLinearFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, module):
-        wb = weight.detach().to(torch.bfloat16)
+        wb = module._wb_cache if module._wb_cache is not None else weight.detach().to(torch.bfloat16)
         ctx.save_for_backward(x, wb)
         ctx.module, ctx.has_bias = module, bias is not None
         return torch.ops.dedloc.gemm(x, wb, None if bias is None else bias.detach(), None, False, True, 0)
@@ -351,6 +411,7 @@ class HeadLinear(nn.Linear):
     """``nn.Linear`` (same parameters / keys) on the dedloc GEMM kernels for GPU inputs."""
 
     inplace_grad = True
+    _wb_cache = None  # bf16 weight view set by SwAVModel.forward (the flat buffer's bf16 mirror)
 
     def forward(self, x):
         if x.is_cuda:
@@ -424,8 +485,16 @@ class SwAVModel(nn.Module):
         self.trunk = ResNet50Trunk(checkpoint_stages=checkpoint_stages)
         self.heads = nn.ModuleList([SwAVPrototypesHead(num_prototypes=num_prototypes)])
         self.single_pass_every_crop = single_pass_every_crop
+        self._flat = None  # FlatParams with a bf16 mirror (bind_flat)
         if conv_impl not in (None, "hip", "auto"):  # "auto": round-2 configs (it chose MIOpen per shape)
             raise ValueError(f"conv backend must be 'hip' (the hand-written kernels), got {conv_impl!r}")
+
+    def bind_flat(self, flat):
+        """Take the GEMM / conv weights of every forward from ``flat``'s bf16 mirror: one cast
+        kernel over the whole flat buffer per iteration instead of one per conv and linear layer."""
+        self._flat = flat if getattr(flat, "bf16", None) is not None else None
+        self._wb_names = [(m, f"{n}.weight") for n, m in self.named_modules()
+                          if isinstance(m, (ConvNHWC, HeadLinear))]
 
     def set_bn_stat_groups(self, g: int):
         for m in self.trunk.modules():
@@ -444,11 +513,19 @@ class SwAVModel(nn.Module):
         convs = [m for m in self.trunk.modules() if isinstance(m, ConvNHWC)]
         for m in convs:
             m._wb_cache, m._wb_share = None, True
+        flat = self._flat
+        if flat is not None and flat.bf16.device == crops[0].device:
+            flat.refresh_bf16()
+            for m, n in self._wb_names:
+                m._wb_cache = flat.w(n)
         try:
             return self._forward(crops)
         finally:
             for m in convs:
                 m._wb_cache, m._wb_share = None, False
+            for m in self.heads.modules():
+                if isinstance(m, HeadLinear):
+                    m._wb_cache = None
 
     def _forward(self, crops):
         feats, i = [], 0

@@ -58,14 +58,18 @@ _SCHEMAS = [
     "l2norm_bwd(Tensor dy, Tensor y, Tensor rinv) -> Tensor",
     "multicrop(Tensor pool, Tensor params, int size, int rad, float[] mean, float[] std) -> Tensor",
     "bn_fwd(Tensor x, Tensor? res, Tensor gamma, Tensor beta, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-    "float eps, float momentum, bool relu, int groups=1, Tensor(c!)? sums=None) -> (Tensor, Tensor, Tensor)",
+    "float eps, float momentum, bool relu, int groups=1, Tensor(c!)? sums=None, bool stats_ready=False) "
+    "-> (Tensor, Tensor, Tensor)",
     "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres, "
     "Tensor(a!)? sums=None, Tensor(b!)? dgamma_acc=None, Tensor(c!)? dbeta_acc=None, Tensor? beta=None) "
     "-> (Tensor, Tensor, Tensor, Tensor)",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
-    "conv2d_fwd(Tensor x, Tensor w, int stride, int pad) -> Tensor",
-    "conv2d_dgrad(Tensor dy, Tensor w, int stride, int pad, int H, int W) -> Tensor",
-    "conv2d_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad) -> ()",
+    "conv2d_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? cols=None) -> Tensor",
+    "conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor(a!) sums, int groups, Tensor? cols=None) "
+    "-> Tensor",
+    "im2col_stem(Tensor x, int R, int S, int stride, int pad) -> Tensor",
+    "conv2d_dgrad(Tensor dy, Tensor w, int stride, int pad, int H, int W, Tensor? residual=None) -> Tensor",
+    "conv2d_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, Tensor? cols=None) -> ()",
 ]
 for _s in _SCHEMAS:
     LIB.define(_s)
@@ -529,7 +533,8 @@ def _multicrop_cpu(pool, params, size, rad, mean, std):
 
 
 @_impl("bn_fwd")
-def _bn_fwd_cpu(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, groups=1, sums=None):
+def _bn_fwd_cpu(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, groups=1, sums=None,
+                stats_ready=False):  # the reference recomputes the statistics from x either way
     G = groups
     xf = x.float().reshape(G, x.shape[0] // G, *x.shape[1:])
     R = xf[0].numel() // xf.shape[2]
@@ -550,20 +555,30 @@ def _bn_fwd_cpu(x, res, gamma, beta, running_mean, running_var, eps, momentum, r
 
 
 @_impl("conv2d_fwd")
-def _conv2d_fwd_cpu(x, w, stride, pad):
+def _conv2d_fwd_cpu(x, w, stride, pad, cols=None):  # cols: a GPU-side stem cache, unused here
     y = F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
     return y.to(x.dtype).contiguous(memory_format=torch.channels_last)
 
 
+@_impl("conv2d_fwd_stats")
+def _conv2d_fwd_stats_cpu(x, w, stride, pad, sums, groups, cols=None):
+    y = _conv2d_fwd_cpu(x, w, stride, pad)
+    yg = y.float().reshape(groups, -1, *y.shape[1:])
+    sums.view(groups, 2, -1).add_(torch.stack([yg.sum(dim=(1, 3, 4)), (yg * yg).sum(dim=(1, 3, 4))], 1))
+    return y
+
+
 @_impl("conv2d_dgrad")
-def _conv2d_dgrad_cpu(dy, w, stride, pad, H, W):
+def _conv2d_dgrad_cpu(dy, w, stride, pad, H, W, residual=None):
     shape = (dy.shape[0], w.shape[1], H, W)
     dx = torch.nn.grad.conv2d_input(shape, w.float(), dy.float(), stride=stride, padding=pad)
+    if residual is not None:
+        dx = dx + residual.float()
     return dx.to(dy.dtype).contiguous(memory_format=torch.channels_last)
 
 
 @_impl("conv2d_wgrad")
-def _conv2d_wgrad_cpu(dy, x, dw, stride, pad):
+def _conv2d_wgrad_cpu(dy, x, dw, stride, pad, cols=None):
     dw.add_(torch.nn.grad.conv2d_weight(x.float(), dw.shape, dy.float(), stride=stride, padding=pad))
 
 

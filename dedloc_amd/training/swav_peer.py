@@ -75,8 +75,10 @@ class SwavPeer:
         self.log_frequency = max(1, int(cfg.get("LOG_FREQUENCY", 10)))
         # vissl PerfTimer/LogPerfTimeMetricsHook (V20): HIP-event phase timers, reported per global step
         self.perf = PerfStats(self.device, enabled=bool(hooks.get("PERF_STATS", True)))
-        self.flat = FlatParams(self.model.named_parameters(), device=self.device, with_bf16=False, autograd=True,
+        self.flat = FlatParams(self.model.named_parameters(), device=self.device,
+                               with_bf16=self.device.type == "cuda", autograd=True,
                                channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
+        self.model.bind_flat(self.flat)  # GEMM / conv weights read from the flat buffer's bf16 mirror
         self.model.normalize_prototypes()
         larc = ocfg.larc_config
         assert ocfg.use_larc, "we can't use collab sgd without larc (sgd_collaborative.py:138)"

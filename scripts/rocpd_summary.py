@@ -27,6 +27,8 @@ def main(argv=None):
     ap.add_argument("--window_ms", type=float, default=0.0)
     ap.add_argument("--csv", default=None)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--from_ms", type=float, default=None, help="window start, ms after the first dispatch")
+    ap.add_argument("--to_ms", type=float, default=None, help="window end, ms after the first dispatch")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x, vgpr_count, accum_vgpr_count, "
@@ -34,8 +36,12 @@ def main(argv=None):
     if not rows:
         print("no kernels")
         return 1
-    t_end = max(r[2] for r in rows)
-    t0 = t_end - a.window_ms * 1e6 if a.window_ms > 0 else min(r[1] for r in rows)
+    t_first = min(r[1] for r in rows)
+    t_end = max(r[2] for r in rows) if a.to_ms is None else t_first + a.to_ms * 1e6
+    t0 = t_end - a.window_ms * 1e6 if a.window_ms > 0 else t_first
+    if a.from_ms is not None:
+        t0 = t_first + a.from_ms * 1e6
+    rows = [r for r in rows if r[1] < t_end]
     agg = defaultdict(lambda: [0, 0.0, None])
     busy = 0.0
     for name, s, e, gx, gy, gz, wx, vg, ag, lds in rows:

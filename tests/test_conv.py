@@ -185,7 +185,7 @@ def _fp32_twin(m, device):
     ref = copy.deepcopy(m).float().to(device)
     for mod in ref.modules():
         if isinstance(mod, ConvNHWC):
-            mod.forward = lambda x, _m=mod: F.conv2d(x, _m.weight, None, _m.stride, _m.padding)
+            mod.forward = lambda x, *_, _m=mod: F.conv2d(x, _m.weight, None, _m.stride, _m.padding)
         if isinstance(mod, BNAct):
             mod.fused = False
     return ref
@@ -258,3 +258,18 @@ def test_bottleneck_grads_match_fp32(cuda, cin, planes, stride, H):
     for n, _ in m.named_parameters():
         ours, theirs = _rel(flat.view(flat.grad, n), rp[n].grad), _rel(sp[n].grad, rp[n].grad)
         assert ours < bound(theirs), (n, ours, theirs)
+
+
+def test_conv_fwd_stats_cpu_reference():
+    """CPU reference of conv2d_fwd_stats: the conv output and per-group channel sums / sums of
+    squares of the stored values, accumulated into `sums`."""
+    torch.manual_seed(0)
+    x = torch.randn(4, 8, 6, 6).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(16, 8, 3, 3)
+    sums = torch.ones(2 * 2 * 16)
+    y = torch.ops.dedloc.conv2d_fwd_stats(x, w, 1, 1, sums, 2)
+    yr = F.conv2d(x, w, padding=1)
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-4)
+    g = yr.reshape(2, 2, 16, 36)
+    ref = torch.stack([g.sum((1, 3)), (g * g).sum((1, 3))], 1).reshape(-1) + 1
+    torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-3)

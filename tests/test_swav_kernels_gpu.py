@@ -19,6 +19,7 @@ def _distinct(N, C, H, W, dev, seed=0):
 def test_maxpool_matches_torch(cuda, hw):
     H, W = hw
     N, C = 3, 64
+    torch.manual_seed(H * 1000 + W)
     if H * W <= 1024:
         x = _distinct(N, C, H, W, cuda)
     else:  # large planes: random values (ties only among equal values, whose routing is then ambiguous)
@@ -74,3 +75,81 @@ def test_swav_trunk_uses_native_pools(cuda):
     assert z.shape == (2, 64) and z.grad_fn.__class__.__name__ == "_AvgPoolBackward"
     z.float().sum().backward()
     assert x.grad is not None and torch.isfinite(x.grad.float()).all()
+
+
+# Conv output + BatchNorm batch statistics (conv2d_fwd_stats): the epilogues of gemm_small (64 / 128
+# outputs), gemm8 (N % 256 == 0), conv.hip (3x3 / strided) and the stem column GEMM, plus the
+# fallback statistics pass when a tile would straddle two statistics groups (stat_rows not a
+# multiple of the tile height).  Reference: fp32 F.conv2d, then per-group sums of the bf16-rounded
+# output (the values BN would read back).
+@pytest.mark.parametrize("cin,cout,k,stride,hw,groups", [
+    (256, 64, 1, 1, 16, 2),     # gemm_small epilogue
+    (64, 128, 1, 1, 16, 1),     # gemm_small, TN = 128
+    (64, 256, 1, 1, 16, 2),     # gemm8 EPI_STATS
+    (128, 512, 1, 1, 8, 2),     # gemm8, 2 N-tiles
+    (64, 64, 3, 1, 16, 2),      # conv.hip epilogue
+    (128, 256, 1, 2, 16, 2),    # strided 1x1 (downsample) on conv.hip
+    (512, 2048, 1, 1, 3, 2),    # 2 x 9 rows per group: fallback statistics pass
+    (3, 64, 7, 2, 32, 2),       # stem: im2col + gemm_small epilogue
+])
+def test_conv_fwd_stats_match_fp32(cuda, cin, cout, k, stride, hw, groups):
+    torch.manual_seed(3)
+    N = 8
+    pad = k // 2
+    x = torch.randn(N, cin, hw, hw, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, k, k, device=cuda) / (cin * k * k) ** 0.5).bfloat16()
+    w = w.contiguous(memory_format=torch.channels_last)
+    sums = torch.zeros(groups * 2 * cout, device=cuda)
+    y = torch.ops.dedloc.conv2d_fwd_stats(x, w, stride, pad, sums, groups)
+    y0 = torch.ops.dedloc.conv2d_fwd(x, w, stride, pad)
+    assert torch.equal(y, y0)  # the statistics do not change the stored output
+    yr = F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    yg = y.float().reshape(groups, N // groups, cout, -1)
+    ref = torch.stack([yg.sum((1, 3)), (yg * yg).sum((1, 3))], 1).reshape(-1)
+    torch.testing.assert_close(sums, ref, rtol=1e-4, atol=1e-2)
+
+
+def test_bottleneck_conv_stats_match_separate_pass(cuda, monkeypatch):
+    """A Bottleneck (identity and downsample variants) with the BN statistics from the conv
+    epilogues computes what it computes with the separate statistics pass: outputs within bf16
+    rounding noise (the sums differ only in fp32 summation order).  Whole random-init trunks are no
+    test for this: run-to-run fp32-atomics noise alone grows through their 16 blocks to O(1)
+    differences at layer4 (scripts/diag_trunk_paths.py, either path against itself)."""
+    from dedloc_amd.models import resnet_swav as rs
+
+    torch.manual_seed(0)
+    for cin, planes, stride in ((256, 64, 1), (256, 128, 2)):
+        down = None
+        if stride != 1 or cin != planes * 4:
+            down = torch.nn.Sequential(rs.ConvNHWC(cin, planes * 4, 1, stride=stride, bias=False),
+                                       rs.BNAct(planes * 4))
+        m = rs.Bottleneck(cin, planes, stride, down).to(cuda).train()
+        bns = [mod for mod in m.modules() if isinstance(mod, rs.BNAct)]
+        x = torch.randn(4, cin, 16, 16, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+        outs = []
+        for flag in (True, False):
+            monkeypatch.setattr(rs, "_CONV_STATS", flag)
+            ws = torch.zeros(sum(4 * 2 * b.num_features for b in bns), device=cuda)
+            off = 0
+            for b in bns:  # the trunk's per-pass workspace, as ResNet50Trunk._prepare_bn_pass lays it out
+                n = 2 * 2 * b.num_features
+                b.stat_groups, b.pass_ws, b.count_deferred = 2, (ws[off:off + n], ws[off + n:off + 2 * n]), True
+                off += 2 * n
+            with torch.no_grad():
+                outs.append(m(x).float())
+        torch.testing.assert_close(outs[0], outs[1], rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("cin,cout", [(256, 64), (512, 128), (1024, 256)])
+def test_conv_dgrad_residual_epilogue(cuda, cin, cout):
+    """conv2d_dgrad(..., residual): the 1x1 data gradient plus the identity branch's gradient, added
+    in the GEMM epilogue (one rounding), against fp32 PyTorch."""
+    torch.manual_seed(5)
+    CLF = torch.channels_last
+    dy = torch.randn(4, cout, 14, 14, device=cuda).bfloat16().contiguous(memory_format=CLF)
+    w = (torch.randn(cout, cin, 1, 1, device=cuda) / cout ** 0.5).bfloat16().contiguous(memory_format=CLF)
+    r = torch.randn(4, cin, 14, 14, device=cuda).bfloat16().contiguous(memory_format=CLF)
+    dx = torch.ops.dedloc.conv2d_dgrad(dy, w, 1, 0, 14, 14, r)
+    ref = torch.nn.grad.conv2d_input((4, cin, 14, 14), w.float(), dy.float()) + r.float()
+    torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2)
