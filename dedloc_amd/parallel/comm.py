@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import datetime
 import logging
+import os
 import threading
 import time
 from collections import OrderedDict
@@ -215,10 +216,21 @@ class GroupCommunicators:
         self._lock = threading.RLock()
         self.created = 0
         self.aborted = 0
+        self.rccl_create_failures = 0  # consecutive RCCL communicators that never came up
 
     # ------------------------------------------------------------------ matchmaking info
+    # After this many consecutive RCCL communicators failed to come up (a broken RCCL install or
+    # transport on this host), the peer announces gloo: every later group it joins runs over
+    # host-staged gloo — slower, but the collaboration keeps averaging instead of losing every
+    # round to the bootstrap deadline.  DEDLOC_DATA_PLANE=gloo forces that from the start.
+    RCCL_FALLBACK_AFTER = 3
+
     @property
     def backend(self) -> str:
+        if os.environ.get("DEDLOC_DATA_PLANE", "").lower() == "gloo":
+            return "gloo"
+        if self.rccl_create_failures >= self.RCCL_FALLBACK_AFTER:
+            return "gloo"
         return "rccl" if rccl_available(self.device) else "gloo"
 
     def announce(self) -> Dict:
@@ -281,7 +293,16 @@ class GroupCommunicators:
                 self._publish(tok, {"uid": uid})
             else:
                 uid = bytes(self._await(tok, deadline)["uid"])
-            return RcclGroupComm.create(uid, n, rank, self.device, deadline)
+            try:
+                comm = RcclGroupComm.create(uid, n, rank, self.device, deadline)
+            except Exception:  # CommError (deadline) or an RCCL init error raised by the op
+                self.rccl_create_failures += 1
+                if self.rccl_create_failures == self.RCCL_FALLBACK_AFTER:
+                    logger.warning(f"{self.rccl_create_failures} RCCL group communicators in a row did not come "
+                                   f"up; this peer now averages over host-staged gloo groups")
+                raise
+            self.rccl_create_failures = 0
+            return comm
         timeout = max(1.0, _left(deadline))
         store_td = datetime.timedelta(seconds=timeout)
         if leader:

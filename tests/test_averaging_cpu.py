@@ -246,3 +246,34 @@ def test_comm_reuse_requires_every_member_to_hold_it():
     for d in dhts:
         d.shutdown()
     root.shutdown()
+
+
+def test_group_comms_fall_back_to_gloo_after_rccl_bootstrap_failures(monkeypatch):
+    """A peer whose RCCL communicators keep failing to come up announces gloo (host-staged groups)
+    from then on; DEDLOC_DATA_PLANE=gloo forces that; a successful bootstrap resets the count."""
+    import torch
+
+    from dedloc_amd.parallel import comm as C
+
+    monkeypatch.setattr(C, "rccl_available", lambda dev: True)
+    g = C.GroupCommunicators(dht=None, prefix="t", peer_id=b"a", device=torch.device("cpu"))
+    assert g.backend == "rccl"
+    monkeypatch.setenv("DEDLOC_DATA_PLANE", "gloo")
+    assert g.backend == "gloo"
+    monkeypatch.delenv("DEDLOC_DATA_PLANE")
+
+    def boom(*a, **k):
+        raise C.CommError("bootstrap deadline")
+
+    monkeypatch.setattr(C.RcclGroupComm, "create", classmethod(lambda cls, *a, **k: boom()))
+    monkeypatch.setattr(g, "_await", lambda tok, deadline: {"uid": b"\0" * 128})
+    for i in range(C.GroupCommunicators.RCCL_FALLBACK_AFTER):
+        assert g.backend == "rccl"
+        try:
+            g._create("tok%d" % i, "rccl", 2, 1, deadline=None)
+        except C.CommError:
+            pass
+    assert g.backend == "gloo"
+    monkeypatch.setattr(C.RcclGroupComm, "create", classmethod(lambda cls, *a, **k: object()))
+    g._create("ok", "rccl", 2, 1, deadline=None)
+    assert g.rccl_create_failures == 0 and g.backend == "rccl"
