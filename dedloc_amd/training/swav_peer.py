@@ -138,44 +138,65 @@ class SwavPeer:
     # ------------------------------------------------------------------ one local iteration
     # ------------------------------------------------------------------ HIP-graph capture
     def _build_graph(self, crops):
-        """Capture the trunk+head forward and backward as HIP graphs (torch make_graphed_callables).
-
-        Opt-in (MODEL.CUDA_GRAPH): with batched equal-resolution trunk passes and the fused BN
-        kernels the iteration is GPU-bound and replaying the graph measured slower than eager
-        (1462 vs 1689 samples/s, b=64; with the HIP convs 1685 vs 1976) because of the static-input/grad
-        copies.  The loss (Sinkhorn + CE, global-step-dependent queue), the collaborative step
-        and the prototype normalisation stay eager.  Warm-up iterations run inside the capture
-        helper, so grads and BN statistics are restored afterwards."""
-
-        class _Fwd(torch.nn.Module):
-            def __init__(self, m):
-                super().__init__()
-                self.m = m
-
-            def forward(self, *xs):
-                return self.m(list(xs))
-
-        for m in self.model.modules():  # captured backward must hand every weight grad to autograd
-            for flag in ("inplace_wgrad", "inplace_grad"):  # convs, BN, head linears / BN1d
-                if hasattr(m, flag):
-                    setattr(m, flag, False)
+        """Capture the trunk+head forward and its backward as two HIP graphs sharing one memory pool
+        (MODEL.CUDA_GRAPH).  The iteration launches ~1100 kernels, many of them a few microseconds
+        long, so eager launching leaves the GPU idle between them; a replay issues each graph with
+        one call.  Unlike ``make_graphed_callables`` nothing changes in the gradient flow: every
+        conv / BN / linear weight gradient is still written in place into the flat gradient buffer
+        (the captured kernels hold its fixed address), so no per-parameter grads are materialised
+        or accumulated.  The SwAV loss (Sinkhorn over a queue that switches on at a global step,
+        host-side ring pointer) stays eager between the two replays: the forward graph's
+        embeddings / scores are its inputs and the gradient w.r.t. the scores is copied into the
+        backward graph's static seed.  Warm-up iterations run on a side stream first (first-call
+        allocations, kernel attributes), after which gradients and BN statistics are restored."""
+        model = self.model
+        static = [c.detach().clone() for c in crops]
         grads = self.flat.grad.clone()
-        bufs = {k: v.clone() for k, v in self.model.named_buffers()}
-        sample = tuple(c.detach().clone() for c in crops)
-        with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False):
-            graphed = torch.cuda.make_graphed_callables(_Fwd(self.model), sample, num_warmup_iters=3)
+        bufs = {k: v.clone() for k, v in model.named_buffers()}
+
+        def fwd():
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False):
+                return model(static)
+
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                emb, scores = fwd()
+                torch.autograd.backward([scores], [torch.ones_like(scores)])
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        g_fwd, g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        # thread_local: the averager / DHT threads may touch the device while the trainer captures
+        with torch.cuda.graph(g_fwd, capture_error_mode="thread_local"):
+            emb, scores = fwd()
+        seed = torch.zeros_like(scores)
+        with torch.cuda.graph(g_bwd, pool=g_fwd.pool(), capture_error_mode="thread_local"):
+            torch.autograd.backward([scores], [seed])
         with torch.no_grad():
             self.flat.grad.copy_(grads)
-            for k, v in self.model.named_buffers():
+            for k, v in model.named_buffers():
                 v.copy_(bufs[k])
         self.flat.rebind_grads()
-        return graphed
+        return {"fwd": g_fwd, "bwd": g_bwd, "in": static, "emb": emb, "scores": scores, "seed": seed}
+
+    def _graph_iteration(self, crops):
+        """One forward + loss + backward through the captured graphs (see _build_graph)."""
+        gr = self._graphed
+        for s, c in zip(gr["in"], crops):
+            s.copy_(c)
+        with self.perf.phase("fwd"):
+            gr["fwd"].replay()
+        with self.perf.phase("loss_bwd"):
+            scores = gr["scores"].detach().requires_grad_(True)
+            proto = self.model.heads[0].prototypes0.weight
+            loss = self.loss_fn(gr["emb"].detach().float(), scores, proto,
+                                training_iterations=int(self.collab_opt.local_step))
+            loss.backward()
+            gr["seed"].copy_(scores.grad)
+            gr["bwd"].replay()
+        return loss
 
     def _forward(self, crops):
-        if self.use_graph and self.iteration >= self.graph_warmup:
-            if self._graphed is None:
-                self._graphed = self._build_graph(crops)
-            return self._graphed(*crops)
         with torch.autocast(device_type=self.device.type, dtype=torch.bfloat16,
                             enabled=self.device.type == "cuda"):
             return self.model(crops)
@@ -183,12 +204,17 @@ class SwavPeer:
     def train_step(self, crops=None):
         with self.perf.phase("data"):
             crops = crops if crops is not None else self.data.next_batch()
-        with self.perf.phase("fwd"):
-            emb, scores = self._forward(crops)
-        with self.perf.phase("loss_bwd"):
-            proto = self.model.heads[0].prototypes0.weight
-            loss = self.loss_fn(emb.float(), scores, proto, training_iterations=int(self.collab_opt.local_step))
-            loss.backward()
+        if self.use_graph and self.iteration >= self.graph_warmup:
+            if self._graphed is None:
+                self._graphed = self._build_graph(crops)
+            loss = self._graph_iteration(crops)
+        else:
+            with self.perf.phase("fwd"):
+                emb, scores = self._forward(crops)
+            with self.perf.phase("loss_bwd"):
+                proto = self.model.heads[0].prototypes0.weight
+                loss = self.loss_fn(emb.float(), scores, proto, training_iterations=int(self.collab_opt.local_step))
+                loss.backward()
         for name, iters in self.frozen:  # FreezeParametersHook (state_update_hooks.py:235-280)
             if self.iteration < iters:
                 name = name[len("module."):] if name.startswith("module.") else name

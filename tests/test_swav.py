@@ -300,8 +300,8 @@ def test_swav_loss_gpu_matches_cpu(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize("graph", [False, True])
 def test_swav_peer_gpu_step(cuda, tmp_path, graph):
-    """Eager and HIP-graph (MODEL.CUDA_GRAPH: forward/backward replayed after 3 eager iterations;
-    the hand-written convs then return their weight grads through autograd) peer iterations."""
+    """Eager and HIP-graph (MODEL.CUDA_GRAPH: forward and backward graphs replayed after 3 eager
+    iterations, weight gradients still written in place into the flat buffer) peer iterations."""
     from dedloc_amd.dht import DHT
     from dedloc_amd.training.swav_peer import SwavPeer
 
@@ -322,6 +322,40 @@ def test_swav_peer_gpu_step(cuda, tmp_path, graph):
     finally:
         peer.shutdown()
         dht.shutdown()
+
+
+@pytest.mark.gpu
+def test_swav_peer_graph_matches_eager(cuda, tmp_path):
+    """The graph-replayed iteration computes what the eager one does: two peers from the same
+    initialisation, fed the same crops, with the queue active, through collaborative LARC steps
+    (every second iteration).  Losses agree to the run-to-run noise of the fp32 statistics atomics."""
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.training.swav_peer import SwavPeer
+
+    peers, dhts = [], []
+    for graph in (False, True):
+        cfg = load_config("swav_1node_resnet_submit", [
+            "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=16", "config.DATA.TRAIN.SYNTHETIC_POOL_SIZE=32",
+            "config.LOSS.swav_loss.queue.start_iter=0", "config.LOSS.swav_loss.queue.queue_length=64",
+            "config.OPTIMIZER.target_batch_size=32", "config.OPTIMIZER.batch_size_for_tracking=16",
+            f"config.CHECKPOINT.DIR={tmp_path}/{graph}", f"config.MODEL.CUDA_GRAPH={graph}",
+            "config.MODEL.CUDA_GRAPH_WARMUP=2"])
+        dhts.append(DHT(start=True))
+        peers.append(SwavPeer(cfg, cuda, dht=dhts[-1]))
+    try:
+        for it in range(7):
+            crops = peers[0].data.next_batch()
+            la = float(peers[0].train_step([c.clone() for c in crops]))
+            lb = float(peers[1].train_step([c.clone() for c in crops]))
+            assert math.isfinite(la) and abs(la - lb) <= 2e-2 * abs(la), (it, la, lb)
+        assert peers[1]._graphed is not None
+        pa, pb = peers[0].flat.fp32, peers[1].flat.fp32
+        assert ((pa - pb).norm() / pa.norm()).item() < 1e-2
+    finally:
+        for p in peers:
+            p.shutdown()
+        for d in dhts:
+            d.shutdown()
 
 
 @pytest.mark.gpu
