@@ -57,6 +57,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--no_miopen", action="store_true", help="time the hand-written kernels only")
     args = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     dev = torch.device("cuda", 0)
@@ -72,13 +73,16 @@ def main():
         flop = 2.0 * N * P * P * Cout * Cin * k * k
         res = {"shape": [N, Cin, H, Cout, k, stride, pad], "count": count, "gflop": flop / 1e9}
         res["ours_fwd_us"] = timeit(lambda: ops.conv2d_fwd(x, w, stride, pad), args.iters)
-        res["miopen_fwd_us"] = timeit(lambda: torch.nn.functional.conv2d(x, w, stride=stride, padding=pad), args.iters)
+        if not args.no_miopen:
+            res["miopen_fwd_us"] = timeit(lambda: torch.nn.functional.conv2d(x, w, stride=stride, padding=pad), args.iters)
         if Cin % 64 == 0:
             res["ours_dgrad_us"] = timeit(lambda: ops.conv2d_dgrad(dy, w, stride, pad, H, H), args.iters)
-            res["miopen_dgrad_us"] = timeit(lambda: torch.ops.aten.convolution_backward(
+            if not args.no_miopen:
+                res["miopen_dgrad_us"] = timeit(lambda: torch.ops.aten.convolution_backward(
                 dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [True, False, False]), args.iters)
         res["ours_wgrad_us"] = timeit(lambda: ops.conv2d_wgrad(dy, x, dw32, stride, pad), args.iters)
-        res["miopen_wgrad_us"] = timeit(lambda: torch.ops.aten.convolution_backward(
+        if not args.no_miopen:
+            res["miopen_wgrad_us"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [False, True, False]), args.iters)
         for k_, v in list(res.items()):
             if k_.endswith("_us"):
