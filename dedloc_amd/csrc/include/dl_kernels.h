@@ -63,13 +63,27 @@ int dl_gemm(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, cons
             int K, bf16_t* C, long ldc, float* Cf, long ldcf, const float* bias, const bf16_t* R, long ldr, bf16_t* H,
             long ldh, float* dbias, int splits, hipStream_t st);
 
+// BatchNorm+ReLU backward preparation fused into a data-gradient GEMM epilogue (gemm8 EPI 5,
+// gemm_small): the GEMM's output is dY of the BN's output; the epilogue masks it by the ReLU
+// (Y > 0, or the forward's pre-activation X*gamma*rstd + beta - mean*gamma*rstd > 0 when Y is null),
+// stores the masked g and accumulates stats[m / stat_rows][n] += g and [N + n] += g*(X - mean)*rstd.
+struct DlBnBwdEpi {
+  const bf16_t* X;      // BN input [M, N], row stride ldx
+  const bf16_t* Y;      // optional BN output (ReLU mask source when the BN had a residual), stride ldx
+  long ldx;
+  const float* mean;    // [G][N]
+  const float* rstd;    // [G][N]
+  const float* gamma;   // [N] (mask from X)
+  const float* beta;    // [N]
+};
+
 // gemm8.hip (LDS-DMA 8-phase MFMA GEMM; epi as dl_gemm; EPI 3 writes fp32 slab blockIdx.y of
 // Cf (+= when accumulate); splits > 1 only for EPI 3; EPI 4 = EPI 0 plus BatchNorm statistics of
 // the stored values: stats[m / stat_rows][0..N) += column sums, [N..2N) += sums of squares)
 int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N,
              int K, bf16_t* C, long ldc, float* Cf, long ldcf, long slab, int accumulate, const float* bias,
              const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st,
-             float* stats = nullptr, long stat_rows = 0);
+             float* stats = nullptr, long stat_rows = 0, const DlBnBwdEpi* bn = nullptr);
 
 // swav.hip
 int dl_sinkhorn(const float* scores, float* P, float* Q, float* ws, int n, int K, int bs, float eps, int iters,
@@ -144,4 +158,5 @@ int dl_gemm_small_splits(int M, int N, int K);
 // (stat_rows a multiple of 128 dividing M)
 int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B, long sbn, long sbk, int M, int N,
                   int K, bf16_t* C, long ldc, float* Cf, long ldcf, int accumulate, const float* bias, const bf16_t* R,
-                  long ldr, int splits, float* ws, hipStream_t st, float* stats = nullptr, long stat_rows = 0);
+                  long ldr, int splits, float* ws, hipStream_t st, float* stats = nullptr, long stat_rows = 0,
+                  const DlBnBwdEpi* bn = nullptr);

@@ -40,6 +40,11 @@
 //              stats[g][0..N) / stats[g][N..2N) (fp32 atomics), g = m / stat_rows: the batch
 //              statistics of a BatchNorm over this output (SwAV's 1x1 convs), so the BN forward
 //              does not re-read the tensor
+//   EPI_BNBWD  the data gradient dY of a BatchNorm+ReLU's output (+ R: the identity-branch
+//              gradient), prepared for that BN's backward: g = bf16(acc + R) masked by the ReLU
+//              (y = Y[m,n] > 0, or x*gamma*rstd + beta - mean*gamma*rstd > 0 from the BN input X),
+//              stored; stats[grp][n] += g, stats[grp][N + n] += g * (X[m,n] - mean) * rstd — the
+//              BN backward's two column sums, so it skips its statistics pass over dY and X
 #include <cstdlib>
 #include <type_traits>
 
@@ -53,7 +58,7 @@ typedef short s4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4_t lds_s4;
 typedef __attribute__((address_space(3))) void lds_void;
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_STATS = 4 };
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_STATS = 4, EPI_BNBWD = 5 };
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
 constexpr int HALF = 16384;     // one half-tile image
@@ -164,6 +169,7 @@ struct Args {
   float* dbias;                  // column sums out (DGELU)
   int nt;                        // non-temporal output stores (bf16 epilogues)
   float* stats; long stat_rows;  // EPI_STATS: [M / stat_rows][2N] column sums / sums of squares
+  DlBnBwdEpi bn;                 // EPI_BNBWD operands (BN input, ReLU mask source, mean / rstd)
 };
 
 #define DL_MFMA_QUAD(QM, QN)                                                          \
@@ -345,7 +351,21 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   // its passes, and the next half's row j right after pass j consumed this half's — ahead of that
   // pass's store.  Loaded inside each pass instead, every pass waited (vmcnt(0)) for its load's full
   // HBM latency and, the counter being in issue order, for every store before it.
-  const bool has_r = EPI == EPI_DGELU || ((EPI == EPI_STORE || EPI == EPI_STATS) && p.R != nullptr);
+  const bool has_r =
+      EPI == EPI_DGELU || ((EPI == EPI_STORE || EPI == EPI_STATS || EPI == EPI_BNBWD) && p.R != nullptr);
+  // EPI_BNBWD: this lane's eight columns of the tile's statistics group
+  float bmu[8], brs[8], bsc[8], bsh[8];
+  if constexpr (EPI == EPI_BNBWD) {
+    const long go = (long)(m0 / p.stat_rows) * p.N;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = n0 + colperm<BKO>(wn * 64 + rch * 8) + j;
+      bmu[j] = p.bn.mean[go + c];
+      brs[j] = p.bn.rstd[go + c];
+      bsc[j] = p.bn.Y ? 0.f : p.bn.gamma[c] * brs[j];
+      bsh[j] = p.bn.Y ? 0.f : p.bn.beta[c] - bmu[j] * bsc[j];
+    }
+  }
   auto rrow = [&](int qm, int pass) -> uint4 {
     const int gm = min(m0 + wm * 128 + qm * 64 + pass * 8 + rr, p.M - 1);  // tail rows: clamped, unused
     return *reinterpret_cast<const uint4*>(p.R + (long)gm * p.ldr + gn);
@@ -406,6 +426,23 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
             colsq[j] = fmaf(v[j], v[j], colsq[j]);
           }
           store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
+        } else if constexpr (EPI == EPI_BNBWD) {
+          float xv[8], yv[8];
+          load_bf16<8>(p.bn.X + (long)gm * p.bn.ldx + gn, xv);
+          if (p.bn.Y) load_bf16<8>(p.bn.Y + (long)gm * p.bn.ldx + gn, yv);
+          if (has_r) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += rv[j];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const bool live = p.bn.Y ? yv[j] > 0.f : fmaf(xv[j], bsc[j], bsh[j]) > 0.f;
+            const float g = live ? round_bf16(v[j]) : 0.f;
+            v[j] = g;
+            colsum[j] += g;
+            colsq[j] = fmaf(g, (xv[j] - bmu[j]) * brs[j], colsq[j]);
+          }
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
         } else if constexpr (EPI == EPI_GELU) {
           float h[8];
 #pragma unroll
@@ -451,7 +488,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       }
     }
   }
-  if constexpr (EPI == EPI_STATS) {
+  if constexpr (EPI == EPI_STATS || EPI == EPI_BNBWD) {
     // lanes with the same 8-column chunk (lane & 7) hold disjoint rows: fold them, then one atomic
     // per column and moment from lanes 0..7
 #pragma unroll
@@ -781,7 +818,7 @@ int persistent_ctas() {  // read per call: tests and benchmarks A/B the two form
 template <bool AKO, bool BKO, int EPI>
 int launch8(const Args& a, int splits, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
-  if constexpr (EPI != EPI_F32 && EPI != EPI_STATS) {
+  if constexpr (EPI != EPI_F32 && EPI != EPI_STATS && EPI != EPI_BNBWD) {
     // DEDLOC_GEMM8_PERSIST=n: the persistent deferred-store form on min(tiles, n) workgroups
     // (n = 256: one per CU of an MI355X)
     const int ctas = persistent_ctas();
@@ -804,7 +841,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N,
              int K, bf16_t* C, long ldc, float* Cf, long ldcf, long slab, int accumulate, const float* bias,
              const bf16_t* R, long ldr, bf16_t* H, long ldh, float* dbias, int splits, hipStream_t st, float* stats,
-             long stat_rows) {
+             long stat_rows, const DlBnBwdEpi* bn) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return -1;
   if (N % BN || K % (BK * splits)) return -1;
   if (a_kouter && M % BM) return -1;
@@ -818,14 +855,19 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
     if (epi == EPI_DGELU && !R) return -1;
     if (splits != 1) return -1;
     // EPI_STATS: every 256-row tile inside one statistics group
-    if (epi == EPI_STATS && (!stats || stat_rows < BM || stat_rows % BM || M % stat_rows)) return -1;
+    if ((epi == EPI_STATS || epi == EPI_BNBWD) && (!stats || stat_rows < BM || stat_rows % BM || M % stat_rows))
+      return -1;
+    if (epi == EPI_BNBWD && (!bn || !bn->X || bn->ldx % 8 || !aligned16(bn->X) || (bn->Y && !aligned16(bn->Y)) ||
+                             (!bn->Y && (!bn->gamma || !bn->beta))))
+      return -1;
   }
   // non-temporal bf16 output stores by default (+4..17% on the store-bound epilogues, gemm_bench);
   // DEDLOC_GEMM8_NT=0 for A/B runs
   const char* nte = std::getenv("DEDLOC_GEMM8_NT");
   const int nt = nte ? std::atoi(nte) : 1;
   Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt,
-         stats, stat_rows};
+         stats, stat_rows, DlBnBwdEpi{}};
+  if (epi == EPI_BNBWD) a.bn = *bn;  // by value: the kernel reads it from its argument buffer
 #define DL_GEMM8_CASE(AK, BK_, E) \
   if (a_kouter == AK && b_kouter == BK_ && epi == E) return launch8<AK, BK_, E>(a, splits, st);
   DL_GEMM8_CASE(0, 0, EPI_STORE)
@@ -837,6 +879,8 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
   DL_GEMM8_CASE(1, 1, EPI_F32)
   DL_GEMM8_CASE(0, 0, EPI_F32)
   DL_GEMM8_CASE(0, 0, EPI_STATS)
+  DL_GEMM8_CASE(0, 1, EPI_BNBWD)
+  DL_GEMM8_CASE(0, 0, EPI_BNBWD)
 #undef DL_GEMM8_CASE
   return -1;
 }

@@ -46,6 +46,8 @@ struct SmallArgs {
   const float* bias;
   const bf16_t* R; long ldr;
   float* stats; long stat_rows;
+  DlBnBwdEpi bn; int bnbwd;  // BN backward preparation (dl_kernels.h DlBnBwdEpi): stats are then the
+                             // BN backward's sums and the stored values the ReLU-masked gradient
 };
 
 // U 8-element chunks of a (64 U) x 32 operand tile per thread, into registers.
@@ -160,11 +162,29 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
         if constexpr (EPI == 0) {
           v += bv;
           if (p.R) v += bf2f(p.R[(long)m * p.ldr + n]);
-          const bf16_t o = f2bf(v);
-          p.C[(long)m * p.ldc + n] = o;
-          const float r = bf2f(o);
-          csum[j] += r;
-          csq[j] = fmaf(r, r, csq[j]);
+          if (p.bnbwd) {
+            const long go = (long)(m0 / p.stat_rows) * p.N + n;
+            const float x = bf2f(p.bn.X[(long)m * p.bn.ldx + n]);
+            const float mu = p.bn.mean[go], rs = p.bn.rstd[go];
+            bool live;
+            if (p.bn.Y) {
+              live = bf2f(p.bn.Y[(long)m * p.bn.ldx + n]) > 0.f;
+            } else {
+              const float sc = p.bn.gamma[n] * rs;
+              live = fmaf(x, sc, p.bn.beta[n] - mu * sc) > 0.f;
+            }
+            const bf16_t o = live ? f2bf(v) : (bf16_t)0;
+            p.C[(long)m * p.ldc + n] = o;
+            const float g = bf2f(o);
+            csum[j] += g;
+            csq[j] = fmaf(g, (x - mu) * rs, csq[j]);
+          } else {
+            const bf16_t o = f2bf(v);
+            p.C[(long)m * p.ldc + n] = o;
+            const float r = bf2f(o);
+            csum[j] += r;
+            csq[j] = fmaf(r, r, csq[j]);
+          }
         } else {
           float* dst = p.Cf + (long)blockIdx.z * p.slab + (long)m * p.ldcf + n;
           *dst = p.accumulate ? *dst + v : v;
@@ -281,9 +301,11 @@ int dl_gemm_small_splits(int M, int N, int K) {
 
 int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B, long sbn, long sbk, int M, int N,
                   int K, bf16_t* C, long ldc, float* Cf, long ldcf, int accumulate, const float* bias, const bf16_t* R,
-                  long ldr, int splits, float* ws, hipStream_t st, float* stats, long stat_rows) {
+                  long ldr, int splits, float* ws, hipStream_t st, float* stats, long stat_rows,
+                  const DlBnBwdEpi* bn) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return -1;
   if (stats && (epi != 0 || splits != 1 || stat_rows < TM || stat_rows % TM || M % stat_rows)) return -1;
+  if (bn && (!stats || !bn->X || (!bn->Y && (!bn->gamma || !bn->beta)))) return -1;
   if (epi == 0 && !C) return -1;
   if (epi == 1 && !Cf) return -1;
   if (splits > 1 && !ws) return -1;
@@ -297,13 +319,14 @@ int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B,
   walk(B, sbn, sbk, &LB, &VB);
   if (S == 1) {
     SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, C, ldc, Cf, ldcf, 0, accumulate, bias, R, ldr, stats,
-                stat_rows};
+                stat_rows, bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0};
     if (epi == 0) launch_tn<0>(a, LA, VA, LB, VB, tn, 1, st);
     else launch_tn<1>(a, LA, VA, LB, VB, tn, 1, st);
     return 0;
   }
+  if (bn) return -1;  // the BN preparation needs the single-pass (unsplit) epilogue
   SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, nullptr, 0, ws, N, (long)M * N, 0, nullptr, nullptr, 0,
-              nullptr, 0};
+              nullptr, 0, DlBnBwdEpi{}, 0};
   launch_tn<1>(a, LA, VA, LB, VB, tn, S, st);
   const long total = (long)M * N;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
