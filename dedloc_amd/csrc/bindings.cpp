@@ -787,8 +787,13 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
                                                                   const c10::optional<at::Tensor>& sums,
                                                                   const c10::optional<at::Tensor>& dgamma_acc,
                                                                   const c10::optional<at::Tensor>& dbeta_acc,
-                                                                  const c10::optional<at::Tensor>& beta) {
+                                                                  const c10::optional<at::Tensor>& beta,
+                                                                  bool stats_ready) {
   const int64_t G = mean.dim() == 2 ? mean.size(0) : 1;
+  // stats_ready: dy is already masked by the ReLU and `sums` holds the backward column sums (a
+  // conv data-gradient epilogue prepared them, conv2d_dgrad_bn); the residual's gradient is then dy
+  // itself, returned without a copy
+  TORCH_CHECK(!stats_ready || sums.has_value(), "bn_bwd: stats_ready needs the sums tensor");
   expect_nhwc(x, "x");
   expect_nhwc(y, "y");
   const at::Tensor g = dy.is_contiguous(at::MemoryFormat::ChannelsLast) ? dy
@@ -796,7 +801,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
   expect_nhwc(g, "dy");
   const int64_t C = x.size(1), R = x.numel() / C / G;
   auto dx = at::empty_like(x);
-  auto dres = want_dres ? at::empty_like(x) : at::Tensor();
+  auto dres = want_dres && !stats_ready ? at::empty_like(x) : at::Tensor();
   auto ws = at::empty({2 * G * C + 2 * C}, gamma.options());  // sums[G,2C] | dgamma[C] | dbeta[C]
   float* sp = f32(ws);
   if (sums.has_value()) {  // caller's pre-zeroed [G, 2C] slice: no memset per call
@@ -815,15 +820,17 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> bn_bwd(const at::Tens
   float* dgp = acc ? f32(*dgamma_acc) : f32(ws) + 2 * G * C;
   float* dbp = acc ? f32(*dbeta_acc) : f32(ws) + 2 * G * C + C;
   // beta (BatchNorm+ReLU without a residual branch only): the ReLU mask comes from x, y is not read
-  const bool xmask = beta.has_value() && relu && !want_dres;
+  const bool xmask = beta.has_value() && relu && !want_dres && !stats_ready;
   if (xmask) {
     expect(*beta, at::kFloat, "beta");
     TORCH_CHECK(beta->numel() == C, "beta size mismatch");
   }
   check(dl_bn_bwd(cbf(g), cbf(y), cbf(x), f32(mean), f32(rstd), f32(gamma), sp, bf(dx),
-                  want_dres ? bf(dres) : nullptr, dgp, dbp, R, (int)C, (int)G, relu, cur_stream(x),
-                  sums.has_value() ? 1 : 0, acc ? 1 : 0, xmask ? f32(*beta) : nullptr),
+                  want_dres && !stats_ready ? bf(dres) : nullptr, dgp, dbp, R, (int)C, (int)G,
+                  stats_ready ? 0 : relu, cur_stream(x), sums.has_value() ? 1 : 0, acc ? 1 : 0,
+                  xmask ? f32(*beta) : nullptr, stats_ready ? 1 : 0),
         "bn_bwd");
+  if (want_dres && stats_ready) dres = g;
   if (acc) return {dx, want_dres ? dres : at::empty({0}, x.options()), at::empty({0}, gamma.options()),
                    at::empty({0}, gamma.options())};
   return {dx, want_dres ? dres : at::empty({0}, x.options()), ws.narrow(0, 2 * G * C, C),
@@ -1076,6 +1083,79 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
   return dx;
 }
 
+// The data gradient of a conv whose input is the output of a BatchNorm+ReLU, prepared for that BN's
+// backward (which then skips its statistics pass, bn_bwd(stats_ready)): returns g = dX (+ residual)
+// masked by the ReLU — mask from y > 0 when y is given (the BN had a residual branch), else from
+// the forward's pre-activation over x (the BN input) — and adds sums[grp][c] += g, sums[grp][C + c]
+// += g * (x - mean) * rstd, in the GEMM epilogue of a 1x1 stride-1 data gradient (gemm8 EPI 5;
+// gemm_small's per-element epilogue with DEDLOC_BN_BWD_SMALL=1).  Returns (dx, fused): where the
+// epilogue cannot take it, dx is the plain data gradient (+ residual), unmasked, and fused is false —
+// the BN backward then runs its own statistics pass (a separate preparation pass here would cost
+// more than that pass: it writes the masked gradient too).
+std::tuple<at::Tensor, bool> conv2d_dgrad_bn(const at::Tensor& dy, const at::Tensor& w, int64_t stride, int64_t pad, int64_t H,
+                           int64_t W, const c10::optional<at::Tensor>& residual, const at::Tensor& x,
+                           const c10::optional<at::Tensor>& y, const at::Tensor& mean, const at::Tensor& rstd,
+                           const at::Tensor& gamma, const at::Tensor& beta, at::Tensor sums, int64_t groups) {
+  expect_nhwc(x, "x");
+  if (y.has_value()) expect_nhwc(*y, "y");
+  expect(mean, at::kFloat, "mean");
+  expect(rstd, at::kFloat, "rstd");
+  expect(gamma, at::kFloat, "gamma");
+  expect(beta, at::kFloat, "beta");
+  expect(sums, at::kFloat, "sums");
+  const int64_t N = x.size(0), C = x.size(1);
+  TORCH_CHECK(groups >= 1 && N % groups == 0 && mean.numel() == groups * C && rstd.numel() == groups * C &&
+                  sums.numel() == 2 * groups * C,
+              "conv2d_dgrad_bn: statistics shapes");
+  TORCH_CHECK(x.size(2) == H && x.size(3) == W && w.size(1) == C, "conv2d_dgrad_bn: x must be the conv input");
+  const long stat_rows = N / groups * H * W;
+  const DlBnBwdEpi bn{cbf(x), y.has_value() ? cbf(*y) : nullptr, (long)C, f32(mean), f32(rstd), f32(gamma),
+                      f32(beta)};
+  const at::Tensor gdy = dy.is_contiguous(at::MemoryFormat::ChannelsLast) ? dy
+                                                                           : dy.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t K = w.size(0), R = w.size(2), S = w.size(3);
+  if (is_pointwise(R, S, stride, pad) && gdy.size(2) == H && gdy.size(3) == W && conv_gemm()) {
+    expect_nhwc(gdy, "dy");
+    if (residual.has_value()) {
+      expect_nhwc(*residual, "residual");
+      TORCH_CHECK(residual->sizes() == x.sizes(), "conv2d_dgrad_bn: residual must have the input's shape");
+    }
+    auto dx = at::empty_like(x);
+    const at::Tensor wk = krsc_view(w);
+    const at::Tensor dyr = rows2d(gdy), wkc = wk.view({K, C});
+    const Mat A = a_view(dyr, false), B = b_view(wkc, false);
+    const bf16_t* rp = residual.has_value() ? cbf(*residual) : nullptr;
+    const int M = (int)A.rows;
+    const hipStream_t st = cur_stream(dy);
+    if (use_gemm8() && dl_gemm8(A.kouter, B.kouter, 5, cbf(dyr), A.ld, cbf(wkc), B.ld, M, (int)C, (int)A.k, bf(dx), C,
+                                nullptr, 0, 0, 0, nullptr, rp, C, nullptr, 0, nullptr, 1, st, f32(sums), stat_rows,
+                                &bn) == 0)
+      return {dx, true};
+    static const bool small_ok = [] {
+      const char* e = std::getenv("DEDLOC_BN_BWD_SMALL");
+      return e && e[0] == '1';
+    }();
+    if (small_ok && C <= 192 && dl_gemm_small_splits(M, (int)C, (int)A.k) == 1 &&
+        dl_gemm_small(0, cbf(dyr), A.srow(), A.sk(), cbf(wkc), B.srow(), B.sk(), M, (int)C, (int)A.k, bf(dx), C,
+                      nullptr, 0, 0, nullptr, rp, C, 1, nullptr, st, f32(sums), stat_rows, &bn) == 0)
+      return {dx, true};
+  }
+  return {conv2d_dgrad(gdy, w, stride, pad, H, W, residual), false};
+}
+
+// the preparation as its own pass (tests; the fallback the fused epilogues are checked against)
+at::Tensor bn_bwd_prep(at::Tensor g, const at::Tensor& x, const c10::optional<at::Tensor>& y, const at::Tensor& mean,
+                       const at::Tensor& rstd, const at::Tensor& gamma, const at::Tensor& beta, at::Tensor sums,
+                       int64_t groups) {
+  expect_nhwc(g, "g");
+  expect_nhwc(x, "x");
+  const int64_t C = x.size(1);
+  check(dl_bn_bwd_prep(bf(g), y.has_value() ? cbf(*y) : nullptr, cbf(x), f32(mean), f32(rstd), f32(gamma), f32(beta),
+                       f32(sums), x.numel() / C / groups, (int)C, (int)groups, cur_stream(g)),
+        "bn_bwd_prep");
+  return g;
+}
+
 // dW (fp32 [Cout, Cin, R, S] with KRSC memory, e.g. the flat-buffer grad view) += conv wgrad
 void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, int64_t stride, int64_t pad,
                   const c10::optional<at::Tensor>& cols) {
@@ -1119,6 +1199,8 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("conv2d_fwd", &conv2d_fwd);
   m.impl("conv2d_fwd_stats", &conv2d_fwd_stats);
   m.impl("im2col_stem", &im2col_stem);
+  m.impl("conv2d_dgrad_bn", &conv2d_dgrad_bn);
+  m.impl("bn_bwd_prep", &bn_bwd_prep);
   m.impl("conv2d_dgrad", &conv2d_dgrad);
   m.impl("conv2d_wgrad", &conv2d_wgrad);
   m.impl("bn_fwd", &bn_fwd);

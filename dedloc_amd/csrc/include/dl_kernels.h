@@ -103,7 +103,10 @@ int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
 int dl_bn_stats(const bf16_t* x, float* sums, long R, int C, int G, hipStream_t st);
 int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
               const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
-              int G, int relu, hipStream_t st, int sums_zeroed = 0, int accumulate = 0, const float* beta = nullptr);
+              int G, int relu, hipStream_t st, int sums_zeroed = 0, int accumulate = 0, const float* beta = nullptr,
+              int stats_ready = 0);
+int dl_bn_bwd_prep(bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
+                   const float* gamma, const float* beta, float* sums, long R, int C, int G, hipStream_t st);
 
 // conv.hip — implicit-GEMM NHWC convolutions.  The gathered operand is an NHWC image
 // [Nimg, H, W, C]; GEMM rows m = (n, i, j) over [Nimg, I, J]; tap t = (tr < TR, ts < TS) reads

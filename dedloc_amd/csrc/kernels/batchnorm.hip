@@ -170,7 +170,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
                                                                 const float* __restrict__ rstd, float* __restrict__ sums,
                                                                 long R, int C, long rpb, int relu,
                                                                 const float* __restrict__ gamma,
-                                                                const float* __restrict__ beta) {
+                                                                const float* __restrict__ beta,
+                                                                bf16_t* gout) {
   __shared__ float red[kThreads * 16];
   const int CV = C >> 3, rpi = kThreads / CV;
   const int cv = threadIdx.x % CV, rsub = threadIdx.x / CV;
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
   dy += base;
   x += base;
   if (y != nullptr) y += base;
+  if (gout != nullptr) gout += base;  // optional: the masked gradient written back (may alias dy)
   mean += (long)blockIdx.y * C;
   rstd += (long)blockIdx.y * C;
   sums += (long)blockIdx.y * 2 * C;
@@ -205,14 +207,17 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
       if (relu && !xmask) ld8(y + off, yv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const bool live = !relu || (xmask ? fmaf(xv[u][j], sc[j], sh[j]) > 0.f : yv[u][j] > 0.f);
         const float gg = live ? g[u][j] : 0.f;
+        g[u][j] = gg;
         sg[j] += gg;
         sgx[j] = fmaf(gg, (xv[u][j] - mu[j]) * rs[j], sgx[j]);
       }
+      if (gout != nullptr) store_bf16<8>(gout + (r + u * rpi) * C + cv * 8, g[u]);
+    }
   }
   for (; r < r1; r += rpi) {
     const long off = r * C + cv * 8;
@@ -233,6 +238,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
       sg[j] += g[j];
       sgx[j] = fmaf(g[j], (xv[j] - mu[j]) * rs[j], sgx[j]);
     }
+    if (gout != nullptr) store_bf16<8>(gout + off, g);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -406,17 +412,34 @@ int dl_bn_stats(const bf16_t* x, float* sums, long R, int C, int G, hipStream_t 
   return 0;
 }
 
+// BatchNorm+ReLU backward preparation as a separate pass (the fallback of the fused data-gradient
+// epilogues): dy (in place) <- dy masked by the ReLU (y > 0, or from x with beta), sums += the two
+// backward column sums; then dl_bn_bwd(..., relu = 0, stats_ready = 1)
+int dl_bn_bwd_prep(bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
+                   const float* gamma, const float* beta, float* sums, long R, int C, int G, hipStream_t st) {
+  if (!bn_shape_ok(C) || R < 1 || G < 1 || (!y && !beta)) return -1;
+  long rpb;
+  const int nb = stats_blocks(R, C, rpb);
+  bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, 1, gamma,
+                                                         y ? nullptr : beta, dy);
+  return 0;
+}
+
 // accumulate: dgamma / dbeta += (the parameters' gradient buffers) instead of =
 // beta: non-null -> the ReLU mask is recomputed from x (BatchNorm+ReLU without a residual branch;
 // y is then not read at all)
 int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* mean, const float* rstd,
               const float* gamma, float* sums, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, long R, int C,
-              int G, int relu, hipStream_t st, int sums_zeroed, int accumulate, const float* beta) {
+              int G, int relu, hipStream_t st, int sums_zeroed, int accumulate, const float* beta, int stats_ready) {
   if (!bn_shape_ok(C) || R < 1 || G < 1) return -1;
-  if (!sums_zeroed) DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
   long rpb;
   const int nb = stats_blocks(R, C, rpb);
-  bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu, gamma, beta);
+  if (!stats_ready) {  // else: a data-gradient epilogue (or dl_bn_bwd_prep) accumulated the sums and
+                       // already masked dy by the ReLU (the caller then passes relu = 0)
+    if (!sums_zeroed) DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
+    bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu, gamma, beta,
+                                                           nullptr);
+  }
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
   bn_bwd_dx_kernel<<<dim3(na, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
                                                      relu, accumulate, beta);

@@ -33,6 +33,9 @@ _BN_XMASK = os.environ.get("DEDLOC_BN_XMASK", "1") != "0"
 _CONV_STATS = os.environ.get("DEDLOC_CONV_STATS", "1") != "0"
 # identity-branch gradient added in conv1's data-gradient epilogue (DEDLOC_RES_LINK=0: autograd's add)
 _RES_LINK = os.environ.get("DEDLOC_RES_LINK", "1") != "0"
+# BatchNorm+ReLU backward statistics accumulated in the consuming 1x1 conv's data-gradient epilogue
+# (DEDLOC_BN_BWD_EPI=0: the BN backward's own statistics pass)
+_BN_BWD_EPI = os.environ.get("DEDLOC_BN_BWD_EPI", "1") != "0"
 
 
 class _GradLink:
@@ -47,6 +50,24 @@ class _GradLink:
         self.g = None
 
 
+class _BnBwdLink:
+    """Hands a BatchNorm+ReLU's backward preparation to the 1x1 conv that consumes its output.
+
+    The BN forward records what its backward needs (its input, mean / rstd, gamma / beta, the
+    pass workspace's backward sums); the consumer conv's backward then computes its data gradient
+    with conv2d_dgrad_bn — the ReLU mask applied and the BN backward's two column sums accumulated in
+    the GEMM epilogue — and marks the link done, so the BN backward skips its statistics pass over
+    dY and X.  The BN backward always runs after that conv's: its incoming gradient is that
+    conv's data gradient.  For bn3 (ReLU after the residual add) the mask comes from the BN output,
+    which is the consumer's own input (the next block's conv1)."""
+
+    __slots__ = ("bn", "done")
+
+    def __init__(self):
+        self.bn = None
+        self.done = False
+
+
 class _BNAct(torch.autograd.Function):
     """Training-mode BN (+ residual) (+ ReLU) on channels-last bf16 via the fused HIP kernels.
 
@@ -58,12 +79,17 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, res, running_mean, running_var, relu, eps, momentum, groups, ws, module,
-                stats_ready=False, link=None):
+                stats_ready=False, link=None, bwd_link=None):
         y, mean, rstd = torch.ops.dedloc.bn_fwd(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu,
                                                 groups, None if ws is None else ws[0], stats_ready)
         ctx.save_for_backward(x, y, mean, rstd, gamma, beta)
         ctx.relu, ctx.has_res, ctx.ws, ctx.module = relu, res is not None, ws, module
         ctx.link = link if res is not None else None
+        ctx.bwd_link = None
+        if bwd_link is not None and relu and ws is not None:
+            bwd_link.bn = (x, mean, rstd, gamma, beta, ws[1], groups, res is not None)
+            bwd_link.done = False
+            ctx.bwd_link = bwd_link
         return y
 
     @staticmethod
@@ -73,17 +99,22 @@ class _BNAct(torch.autograd.Function):
         gw, gb = (m.weight.grad, m.bias.grad) if m is not None else (None, None)
         acc = (m is not None and m.inplace_grad and gw is not None and gb is not None
                and gw.dtype == torch.float32 and gb.dtype == torch.float32)
+        # the consuming conv's epilogue prepared dy (ReLU-masked) and the backward sums (_BnBwdLink)
+        ready = ctx.bwd_link is not None and ctx.bwd_link.done
+        if ready:
+            ctx.bwd_link.done = False
         dx, dres, dgamma, dbeta = torch.ops.dedloc.bn_bwd(dy, y, x, mean, rstd, gamma, ctx.relu, ctx.has_res,
                                                           None if ctx.ws is None else ctx.ws[1],
                                                           gw if acc else None, gb if acc else None,
                                                           # BN+ReLU without a residual: ReLU mask from x, y unread
-                                                          beta if (_BN_XMASK and ctx.relu and not ctx.has_res) else None)
+                                                          beta if (_BN_XMASK and ctx.relu and not ctx.has_res) else None,
+                                                          ready)
         if acc:
             dgamma = dbeta = None
         if ctx.link is not None:  # the residual's gradient rides in conv1's data-gradient epilogue
             ctx.link.g, dres = dres, None
         return (dx, dgamma, dbeta, (dres if ctx.has_res else None), None, None, None, None, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 class _ConvNHWC(torch.autograd.Function):
@@ -92,7 +123,7 @@ class _ConvNHWC(torch.autograd.Function):
     bound ``.grad`` (the flat gradient buffer, KRSC layout) when there is one, like the ALBERT layer."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, module, stats=None, groups=1, link=None):
+    def forward(ctx, x, weight, stride, pad, module, stats=None, groups=1, link=None, bn_link=None):
         # bf16 copy of the weight (keeps the channels-last KRSC strides), shared by the trunk passes
         # of one SwAVModel.forward (one cast per iteration instead of one per resolution group); the
         # model clears the cache at the start and end of every forward, so an optimizer update
@@ -109,7 +140,7 @@ class _ConvNHWC(torch.autograd.Function):
             cols = torch.ops.dedloc.im2col_stem(x, wb.shape[2], wb.shape[3], stride, pad)
         ctx.save_for_backward(x if cols is None else cols, wb)
         ctx.stride, ctx.pad, ctx.module = stride, pad, module
-        ctx.has_cols, ctx.xshape, ctx.link = cols is not None, tuple(x.shape), link
+        ctx.has_cols, ctx.xshape, ctx.link, ctx.bn_link = cols is not None, tuple(x.shape), link, bn_link
         if stats is not None:  # the consuming BatchNorm's statistics, accumulated by the conv's epilogue
             return torch.ops.dedloc.conv2d_fwd_stats(x, wb, stride, pad, stats, groups, cols)
         return torch.ops.dedloc.conv2d_fwd(x, wb, stride, pad, cols)
@@ -127,7 +158,14 @@ class _ConvNHWC(torch.autograd.Function):
             res = None
             if ctx.link is not None:  # + the block's identity-branch gradient (see _GradLink)
                 res, ctx.link.g = ctx.link.g, None
-            dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3], res)
+            bl = ctx.bn_link
+            if bl is not None and bl.bn is not None:  # + the producing BN's backward preparation (_BnBwdLink)
+                bx, mean, rstd, gamma, beta, sums, G, has_res = bl.bn
+                dx, bl.done = torch.ops.dedloc.conv2d_dgrad_bn(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3],
+                                                               res, bx, x if has_res else None, mean, rstd, gamma,
+                                                               beta, sums, G)
+            else:
+                dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3], res)
         dw = None
         if ctx.needs_input_grad[1]:
             weight = ctx.module.weight
@@ -140,7 +178,7 @@ class _ConvNHWC(torch.autograd.Function):
                     memory_format=torch.channels_last)
                 torch.ops.dedloc.conv2d_wgrad(dy, x, dw, ctx.stride, ctx.pad, cols)
                 dw = dw.to(weight.dtype)
-        return dx, dw, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None
 
 
 class ConvNHWC(nn.Conv2d):
@@ -156,11 +194,13 @@ class ConvNHWC(nn.Conv2d):
     # (HIP-graph capture via make_graphed_callables needs every parameter to receive an autograd grad)
     inplace_wgrad = True
 
-    def forward(self, x, bn=None, link=None):
+    def forward(self, x, bn=None, link=None, bn_link=None):
         """``bn``: the BNAct that consumes this output.  When it will take its fused path with a
         pass workspace, the conv's epilogue accumulates that BatchNorm's batch statistics and the BN
         forward skips its own statistics pass over the tensor.  ``link``: a _GradLink whose gradient the
-        data-gradient epilogue adds (Bottleneck conv1)."""
+        data-gradient epilogue adds (Bottleneck conv1).  ``bn_link``: the _BnBwdLink of the
+        BatchNorm+ReLU that produced ``x`` (its backward preparation rides in this conv's data
+        gradient)."""
         if not x.is_cuda:
             return super().forward(x)
         if not (self.bias is None and self.groups == 1 and self.dilation == (1, 1)
@@ -172,8 +212,8 @@ class ConvNHWC(nn.Conv2d):
         if bn is not None and bn.takes_conv_stats():
             bn.stats_ready = True
             return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, bn.pass_ws[0],
-                                   bn.stat_groups, link)
-        return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, None, 1, link)
+                                   bn.stat_groups, link, bn_link)
+        return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, None, 1, link, bn_link)
 
 
 class BNAct(nn.BatchNorm2d):
@@ -202,7 +242,7 @@ class BNAct(nn.BatchNorm2d):
         so the conv producing its input can accumulate the batch statistics in its epilogue."""
         return self.fused and self.training and self.pass_ws is not None and _CONV_STATS
 
-    def forward(self, x, res=None, link=None):
+    def forward(self, x, res=None, link=None, bwd_link=None):
         G = self.stat_groups if self.training else 1
         if (self.fused and self.training and x.is_cuda and x.dtype == torch.bfloat16
                 and x.is_contiguous(memory_format=torch.channels_last)
@@ -213,7 +253,7 @@ class BNAct(nn.BatchNorm2d):
             ws, self.pass_ws = self.pass_ws, None
             ready, self.stats_ready = self.stats_ready and ws is not None, False
             return _BNAct.apply(x, self.weight, self.bias, res, self.running_mean, self.running_var, self.relu,
-                                self.eps, self.momentum, G, ws, self, ready, link)
+                                self.eps, self.momentum, G, ws, self, ready, link, bwd_link)
         self.stats_ready = False
         if G > 1:  # reference semantics without the fused kernel: one BN call per crop chunk
             y = torch.cat([super(BNAct, self).forward(c) for c in x.chunk(G)])
@@ -286,6 +326,10 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         link = None
+        # the previous block's bn3 backward preparation can ride in conv1's data gradient only when
+        # that gradient is the whole gradient of x: identity block, identity gradient linked in
+        in_link = getattr(x, "_dedloc_bn_link", None)
+        fused_bwd = _BN_BWD_EPI and x.is_cuda and x.requires_grad and torch.is_grad_enabled()
         if self.downsample is None:
             idt = x
             if _RES_LINK and x.is_cuda and x.requires_grad and torch.is_grad_enabled():
@@ -293,9 +337,14 @@ class Bottleneck(nn.Module):
         else:
             conv, bn = self.downsample[0], self.downsample[1]
             idt = bn(conv(x, bn))
-        out = self.bn1(self.conv1(x, self.bn1, link))
-        out = self.bn2(self.conv2(out, self.bn2))
-        return self.bn3(self.conv3(out, self.bn3), idt, link)
+        out = self.bn1(self.conv1(x, self.bn1, link, in_link if link is not None else None))
+        l2 = _BnBwdLink() if fused_bwd else None
+        out = self.bn2(self.conv2(out, self.bn2), bwd_link=l2)
+        l3 = _BnBwdLink() if fused_bwd else None
+        y = self.bn3(self.conv3(out, self.bn3, bn_link=l2), idt, link, bwd_link=l3)
+        if l3 is not None:
+            y._dedloc_bn_link = l3
+        return y
 
 
 class ResNet50Trunk(nn.Module):

@@ -61,8 +61,12 @@ _SCHEMAS = [
     "float eps, float momentum, bool relu, int groups=1, Tensor(c!)? sums=None, bool stats_ready=False) "
     "-> (Tensor, Tensor, Tensor)",
     "bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor rstd, Tensor gamma, bool relu, bool want_dres, "
-    "Tensor(a!)? sums=None, Tensor(b!)? dgamma_acc=None, Tensor(c!)? dbeta_acc=None, Tensor? beta=None) "
-    "-> (Tensor, Tensor, Tensor, Tensor)",
+    "Tensor(a!)? sums=None, Tensor(b!)? dgamma_acc=None, Tensor(c!)? dbeta_acc=None, Tensor? beta=None, "
+    "bool stats_ready=False) -> (Tensor, Tensor, Tensor, Tensor)",
+    "conv2d_dgrad_bn(Tensor dy, Tensor w, int stride, int pad, int H, int W, Tensor? residual, Tensor x, Tensor? y, "
+    "Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, Tensor(a!) sums, int groups) -> (Tensor, bool)",
+    "bn_bwd_prep(Tensor(a!) g, Tensor x, Tensor? y, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, "
+    "Tensor(b!) sums, int groups) -> Tensor",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
     "conv2d_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? cols=None) -> Tensor",
     "conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor(a!) sums, int groups, Tensor? cols=None) "
@@ -577,6 +581,39 @@ def _conv2d_dgrad_cpu(dy, w, stride, pad, H, W, residual=None):
     return dx.to(dy.dtype).contiguous(memory_format=torch.channels_last)
 
 
+@_impl("conv2d_dgrad_bn")
+def _conv2d_dgrad_bn_cpu(dy, w, stride, pad, H, W, residual, x, y, mean, rstd, gamma, beta, sums, groups):
+    g = _conv2d_dgrad_cpu(dy, w, stride, pad, H, W, residual).float()
+    G, C = groups, x.shape[1]
+    shp = (G, x.shape[0] // G, C, H, W)
+    xf = x.float().reshape(shp)
+    mu, rs = mean.reshape(G, 1, C, 1, 1), rstd.reshape(G, 1, C, 1, 1)
+    if y is not None:
+        live = y.float().reshape(shp) > 0
+    else:
+        sc = gamma.view(1, 1, C, 1, 1) * rs
+        live = xf * sc + (beta.view(1, 1, C, 1, 1) - mu * sc) > 0
+    gg = torch.where(live, g.reshape(shp), torch.zeros((), dtype=torch.float32))
+    sums.view(G, 2, C).add_(torch.stack([gg.sum((1, 3, 4)), (gg * (xf - mu) * rs).sum((1, 3, 4))], 1))
+    return gg.reshape(x.shape).to(dy.dtype).contiguous(memory_format=torch.channels_last), True
+
+
+@_impl("bn_bwd_prep")
+def _bn_bwd_prep_cpu(g, x, y, mean, rstd, gamma, beta, sums, groups):
+    G, C, H, W = groups, x.shape[1], x.shape[2], x.shape[3]
+    shp = (G, x.shape[0] // G, C, H, W)
+    xf, mu, rs = x.float().reshape(shp), mean.reshape(G, 1, C, 1, 1), rstd.reshape(G, 1, C, 1, 1)
+    if y is not None:
+        live = y.float().reshape(shp) > 0
+    else:
+        sc = gamma.view(1, 1, C, 1, 1) * rs
+        live = xf * sc + (beta.view(1, 1, C, 1, 1) - mu * sc) > 0
+    gg = torch.where(live, g.float().reshape(shp), torch.zeros((), dtype=torch.float32))
+    sums.view(G, 2, C).add_(torch.stack([gg.sum((1, 3, 4)), (gg * (xf - mu) * rs).sum((1, 3, 4))], 1))
+    g.copy_(gg.reshape(g.shape))
+    return g
+
+
 @_impl("conv2d_wgrad")
 def _conv2d_wgrad_cpu(dy, x, dw, stride, pad, cols=None):
     dw.add_(torch.nn.grad.conv2d_weight(x.float(), dw.shape, dy.float(), stride=stride, padding=pad))
@@ -584,7 +621,8 @@ def _conv2d_wgrad_cpu(dy, x, dw, stride, pad, cols=None):
 
 @_impl("bn_bwd")
 def _bn_bwd_cpu(dy, y, x, mean, rstd, gamma, relu, want_dres, sums=None, dgamma_acc=None, dbeta_acc=None,
-                beta=None):  # beta: the GPU kernels' ReLU mask from x; the reference reads y
+                beta=None, stats_ready=False):  # beta: the GPU kernels' ReLU mask from x; the reference reads y
+    # (stats_ready: dy arrives masked — masking it again by y > 0 changes nothing)
     mean2 = mean.reshape(-1, x.shape[1])
     rstd2 = rstd.reshape(-1, x.shape[1])
     G = mean2.shape[0]

@@ -185,7 +185,7 @@ def _fp32_twin(m, device):
     ref = copy.deepcopy(m).float().to(device)
     for mod in ref.modules():
         if isinstance(mod, ConvNHWC):
-            mod.forward = lambda x, *_, _m=mod: F.conv2d(x, _m.weight, None, _m.stride, _m.padding)
+            mod.forward = lambda x, *_, _m=mod, **__: F.conv2d(x, _m.weight, None, _m.stride, _m.padding)
         if isinstance(mod, BNAct):
             mod.fused = False
     return ref
@@ -273,3 +273,56 @@ def test_conv_fwd_stats_cpu_reference():
     g = yr.reshape(2, 2, 16, 36)
     ref = torch.stack([g.sum((1, 3)), (g * g).sum((1, 3))], 1).reshape(-1) + 1
     torch.testing.assert_close(sums, ref, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,planes,stride", [(256, 64, 1), (512, 128, 2)])
+def test_chained_bottlenecks_grads_match_fp32(cuda, cin, planes, stride):
+    """Three chained Bottlenecks (the second and third identity blocks), so every fused backward path
+    runs: bn2's backward statistics in conv3's data-gradient epilogue, bn3's in the NEXT block's
+    conv1 epilogue (ReLU mask from that conv's input, identity gradient added), and the first
+    block's bn3 through its own pass (a downsample block follows nothing here).  dX and every
+    parameter gradient against the fp32 PyTorch twin, bounded relative to stock bf16 autocast."""
+    from dedloc_amd.models.resnet_swav import BNAct, Bottleneck, ConvNHWC
+    from dedloc_amd.utils.flat import FlatParams
+
+    torch.manual_seed(0)
+    down = None
+    if stride != 1 or cin != planes * 4:
+        down = torch.nn.Sequential(ConvNHWC(cin, planes * 4, 1, stride=stride, bias=False), BNAct(planes * 4))
+    m = torch.nn.Sequential(Bottleneck(cin, planes, stride, down), Bottleneck(planes * 4, planes),
+                            Bottleneck(planes * 4, planes))
+    ref = _fp32_twin(m, cuda).train()
+    stock = _fp32_twin(m, cuda).train()
+    m = m.to(cuda).train()
+    H = 16
+    torch.manual_seed(1)
+    x = torch.randn(8, cin, H, H, device=cuda).bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(8, planes * 4, H // stride, H // stride, device=cuda).bfloat16().contiguous(memory_format=CL)
+    flat = FlatParams(m.named_parameters(), device=cuda, with_bf16=False, autograd=True, channels_last=True)
+    bns = [mod for mod in m.modules() if isinstance(mod, BNAct)]
+    ws = torch.zeros(sum(2 * 2 * b.num_features for b in bns), device=cuda)
+    off = 0
+    for b in bns:  # the trunk's per-pass workspace (fused forward statistics and backward preparation)
+        n = 2 * b.num_features
+        b.pass_ws, b.count_deferred = (ws[off:off + n], ws[off + n:off + 2 * n]), True
+        off += 2 * n
+    xx = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(xx)
+    y.backward(dy)
+    xr = x.float().requires_grad_(True)
+    ref(xr).backward(dy.float())
+    xs = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ys = stock(xs)
+    ys.backward(dy)
+
+    def bound(stock_err):
+        return 1.3 * stock_err + 5e-3
+
+    assert _rel(xx.grad.float(), xr.grad) < bound(_rel(xs.grad, xr.grad))
+    rp, sp = dict(ref.named_parameters()), dict(stock.named_parameters())
+    for n, _ in m.named_parameters():
+        ours, theirs = _rel(flat.view(flat.grad, n), rp[n].grad), _rel(sp[n].grad, rp[n].grad)
+        assert ours < bound(theirs), (n, ours, theirs)
