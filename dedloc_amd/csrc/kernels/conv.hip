@@ -132,13 +132,35 @@ struct FwdArgs {
   long stat_rows;
 };
 
+// Tile shapes: TM_ x TN_ = 128 x 128 (four 64 x 64 waves as 2 x 2) or 256 x 64 (4 x 1) for
+// outputs of at most 64 channels — the 64-channel 3x3 convs of the first stage would leave half of
+// a 128-wide channel tile empty.  The per-wave MFMA work is the same 64 x 64 in both.
+template <int U>
+struct StageN {
+  uint4 v[U];
+};
+// thread `tid`, slot u: K-inner tiles put chunk (tid&7) of row (tid>>3)+32u
+template <int U>
+__device__ __forceinline__ void st_kin_n(const StageN<U>& s, uint8_t* img) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int idx = threadIdx.x + NT * u;
+    *reinterpret_cast<uint4*>(img + kin_off(idx >> 3, idx & 7)) = s.v[u];
+  }
+}
+
+template <int TM_, int TN_>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
+  constexpr int WN = TN_ / 64, UA = TM_ / 32, UB = TN_ / 32;
+  constexpr int CPR = TN_ / 8;            // 16-byte chunks per staged output row
+  constexpr int AIMG = TM_ * 128;         // A image bytes (64 k per row)
+  constexpr int SBYTES = (TM_ + TN_) * 128;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const DlConvGeom& g = p.g;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int tiles_n = (p.N + BN - 1) / BN;
-  const int tiles_m = (p.M + BM - 1) / BM;
+  const int wm = wv / WN, wn = wv % WN;
+  const int tiles_n = (p.N + TN_ - 1) / TN_;
+  const int tiles_m = (p.M + TM_ - 1) / TM_;
   const int ntiles = tiles_m * tiles_n;
   // persistent over `tpw` consecutive output tiles (same pixel rows, successive channel blocks
   // first): the load stream runs on across tile boundaries, so short-K convs (1x1 over 64-256
@@ -152,12 +174,12 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
 
   // load cursor: per-thread decoded gathered rows of the tile being loaded
   int dec_tile = -1;
-  int hb[4], wb[4], nb[4], brow[4];
+  int hb[UA], wb[UA], nb[UA], brow[UB];
   auto decode = [&](int tile) {
     dec_tile = tile;
-    const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+    const int m0 = (tile / tiles_n) * TM_, n0 = (tile % tiles_n) * TN_;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < UA; ++u) {
       const int m = m0 + (tid >> 3) + 32 * u;
       if (m < p.M) {
         const int n = m / IJ, r = m - n * IJ;
@@ -170,15 +192,16 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
         wb[u] = 0;
         nb[u] = 0;
       }
-      brow[u] = min(n0 + (tid >> 3) + 32 * u, p.N - 1);
     }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) brow[u] = min(n0 + (tid >> 3) + 32 * u, p.N - 1);
   };
 
   const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, p.w_bytes);
   const int nsteps = mytiles * nk;
   // stage step s (clamped: steps past the end reload the last one; staged, never computed)
-  auto load_step = [&](Stage& sa, Stage& sb, int s) {
+  auto load_step = [&](StageN<UA>& sa, StageN<UB>& sb, int s) {
     s = min(s, nsteps - 1);
     const int tile = tile0 + s / nk, k0 = (s % nk) * BK;
     if (tile != dec_tile) decode(tile);
@@ -186,14 +209,14 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     const int tr = t / g.TS, ts = t - tr * g.TS;
     const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < UA; ++u) {
       const int h = hb[u] + dh, w = wb[u] + dw;
       const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
       const unsigned off = 2u * ((unsigned)((nb[u] + h) * g.W + w) * (unsigned)g.C + (unsigned)(c0 + cofs));
       sa.v[u] = bload(rimg, ok ? off : OOB);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) sb.v[u] = bload(rw, 2u * ((unsigned)brow[u] * (unsigned)p.ldw + (unsigned)(k0 + cofs)));
+    for (int u = 0; u < UB; ++u) sb.v[u] = bload(rw, 2u * ((unsigned)brow[u] * (unsigned)p.ldw + (unsigned)(k0 + cofs)));
   };
 
   floatx4 acc[4][4];
@@ -203,7 +226,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](const uint8_t* Ai) {
-    const uint8_t* Bi = Ai + TILE;
+    const uint8_t* Bi = Ai + AIMG;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[4];
@@ -219,11 +242,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   };
 
   // acc[ni][mi][i] = out[pixel m0+wm*64+mi*16+(lane&15)][channel n0+wn*64+ni*16+4*(lane>>4)+i].
-  // The 128x128 bf16 tile is staged through the LDS buffer the pipeline is not using (`stage`,
-  // 32 KiB: [128 pixels][16 chunks of 16 B], chunk c of row r at c ^ (r & 15)) and written back as
-  // whole 256-byte pixel rows (16 B per lane), instead of 8-byte pieces scattered over 16 rows.
+  // The TM_ x TN_ bf16 tile (32 KiB) is staged through the LDS buffer the pipeline is not using
+  // (`stage`: [TM_ pixels][CPR chunks of 16 B], chunk c of row r at c ^ (r & (CPR-1))) and written
+  // back as whole pixel rows (16 B per lane), instead of 8-byte pieces scattered over 16 rows.
   auto epilogue = [&](int tile, uint8_t* stage) {
-    const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+    const int m0 = (tile / tiles_n) * TM_, n0 = (tile % tiles_n) * TN_;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const int row = wm * 64 + mi * 16 + (lane & 15);
@@ -233,7 +256,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
         uint2 v;
         v.x = (uint32_t)f2bf(acc[ni][mi][0]) | ((uint32_t)f2bf(acc[ni][mi][1]) << 16);
         v.y = (uint32_t)f2bf(acc[ni][mi][2]) | ((uint32_t)f2bf(acc[ni][mi][3]) << 16);
-        *reinterpret_cast<uint2*>(stage + row * 256 + (((col >> 3) ^ (row & 15)) << 4) + ((col & 7) << 1)) = v;
+        *reinterpret_cast<uint2*>(stage + row * (CPR * 16) + (((col >> 3) ^ (row & (CPR - 1))) << 4) +
+                                  ((col & 7) << 1)) = v;
       }
     }
 #pragma unroll
@@ -241,15 +265,15 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
-    // thread tid always writes channel chunk tid & 15 (8 channels) of rows (tid >> 4) + 16 u
+    // thread tid always writes channel chunk tid % CPR (8 channels) of rows tid / CPR + (NT / CPR) u
     float csum[8], csq[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = csq[e] = 0.f;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = tid + NT * u, row = idx >> 4, c = idx & 15;
+    for (int u = 0; u < TM_ * CPR / NT; ++u) {
+      const int idx = tid + NT * u, row = idx / CPR, c = idx % CPR;
       const int m = m0 + row, ch = n0 + c * 8;
-      const uint4 v = *reinterpret_cast<const uint4*>(stage + row * 256 + ((c ^ (row & 15)) << 4));
+      const uint4 v = *reinterpret_cast<const uint4*>(stage + row * (CPR * 16) + ((c ^ (row & (CPR - 1))) << 4));
       if (m < p.M && ch < p.N) {
         const int n = m / IJ, r = m - n * IJ;
         const int i = r / g.J, j = r - i * g.J;
@@ -268,29 +292,32 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     }
     if (p.stats) {
       // Atomics are issue-bound (one wave-instruction per ~50 ns per CU, MI355X_MICROARCH.md), so
-      // the tile's 256 statistics are folded before they leave: lanes l, l^16, l^32, l^48 share a
-      // chunk (shuffles), the 4 waves meet in the (drained) staging buffer, and every thread adds
-      // one value — 4 wave-instructions per tile.
+      // the tile's 2 x TN_ statistics are folded before they leave: the lanes of a wave that share
+      // a chunk (shuffles), then the 4 waves in the (drained) staging buffer, and one thread per
+      // value adds it — 2-4 wave-instructions per tile.
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        csum[e] += __shfl_xor(csum[e], 16, 64);
-        csq[e] += __shfl_xor(csq[e], 16, 64);
-        csum[e] += __shfl_xor(csum[e], 32, 64);
-        csq[e] += __shfl_xor(csq[e], 32, 64);
+#pragma unroll
+        for (int d = CPR; d < 64; d *= 2) {
+          csum[e] += __shfl_xor(csum[e], d, 64);
+          csq[e] += __shfl_xor(csq[e], d, 64);
+        }
       }
       __syncthreads();  // every staged row has been read: the buffer is free
-      float* red = reinterpret_cast<float*>(stage);  // [wave][moment][128 channels]
-      if (lane < 16) {
+      float* red = reinterpret_cast<float*>(stage);  // [wave][moment][TN_ channels]
+      if (lane < CPR) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          red[wv * 256 + lane * 8 + e] = csum[e];
-          red[wv * 256 + 128 + lane * 8 + e] = csq[e];
+          red[wv * 2 * TN_ + lane * 8 + e] = csum[e];
+          red[wv * 2 * TN_ + TN_ + lane * 8 + e] = csq[e];
         }
       }
       __syncthreads();
-      const float v = red[tid] + red[256 + tid] + red[512 + tid] + red[768 + tid];
-      const int chl = tid & 127, mom = tid >> 7;
-      if (n0 + chl < p.N) atomicAdd(p.stats + (m0 / p.stat_rows) * 2L * p.N + (long)mom * p.N + n0 + chl, v);
+      if (tid < 2 * TN_) {
+        const float v = red[tid] + red[2 * TN_ + tid] + red[4 * TN_ + tid] + red[6 * TN_ + tid];
+        const int chl = tid % TN_, mom = tid / TN_;
+        if (n0 + chl < p.N) atomicAdd(p.stats + (m0 / p.stat_rows) * 2L * p.N + (long)mom * p.N + n0 + chl, v);
+      }
     }
     __syncthreads();  // the staging buffer is restaged by the pipeline right after
   };
@@ -305,27 +332,28 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   // stores, so the compiler's wait counting sees the true issue order and waits only for the set
   // it is about to store.
   uint8_t* buf0 = smem;
-  uint8_t* buf1 = smem + 2 * TILE;
-  Stage xa, xb, ya, yb;
+  uint8_t* buf1 = smem + SBYTES;
+  StageN<UA> xa, ya;
+  StageN<UB> xb, yb;
   load_step(xa, xb, 0);
   load_step(ya, yb, 1);
-  st_kin(xa, buf0);
-  st_kin(xb, buf0 + TILE);
+  st_kin_n(xa, buf0);
+  st_kin_n(xb, buf0 + AIMG);
   load_step(xa, xb, 2);
   __syncthreads();
   for (int s = 0; s < nsteps; s += 2) {
     compute(buf0);  // step s
     if (s % nk == nk - 1) epilogue(tile0 + s / nk, buf1);  // buf1: drained, not yet restaged
-    st_kin(ya, buf1);
-    st_kin(yb, buf1 + TILE);
+    st_kin_n(ya, buf1);
+    st_kin_n(yb, buf1 + AIMG);
     load_step(ya, yb, s + 3);
     __syncthreads();
     if (s + 1 < nsteps) {
       compute(buf1);  // step s + 1
       if ((s + 1) % nk == nk - 1) epilogue(tile0 + (s + 1) / nk, buf0);
     }
-    st_kin(xa, buf0);
-    st_kin(xb, buf0 + TILE);
+    st_kin_n(xa, buf0);
+    st_kin_n(xb, buf0 + AIMG);
     load_step(xa, xb, s + 4);
     __syncthreads();
   }
@@ -521,17 +549,29 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
   if (M == 0 || N == 0) return 0;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * ldw;
   if (img_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
-  const int tiles = (int)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  // outputs of at most 64 channels: 256 x 64 tiles (DEDLOC_CONV_NARROW=0: always 128 x 128)
+  static const bool narrow_ok = [] {
+    const char* e = std::getenv("DEDLOC_CONV_NARROW");
+    return !(e && e[0] == '0');
+  }();
+  const bool narrow = narrow_ok && N <= 64 && (!stats || stat_rows % 256 == 0);
+  const int TMv = narrow ? 256 : BM, TNv = narrow ? 64 : BN;
+  const int tiles = (int)((M + TMv - 1) / TMv) * ((N + TNv - 1) / TNv);
   // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
   const int tpw = std::max(1, tiles / 1024);
   FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C,
             (unsigned)img_bytes, (unsigned)w_bytes, tpw, stats, stat_rows};
+  const int lds = 2 * (TMv + TNv) * 128;
   static bool attr = false;
   if (!attr) {
-    set_lds(conv_fwd_kernel);
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
     attr = true;
   }
-  conv_fwd_kernel<<<dim3((tiles + tpw - 1) / tpw), NT, LDS_BYTES, st>>>(a);
+  if (narrow) conv_fwd_kernel<256, 64><<<dim3((tiles + tpw - 1) / tpw), NT, lds, st>>>(a);
+  else conv_fwd_kernel<BM, BN><<<dim3((tiles + tpw - 1) / tpw), NT, lds, st>>>(a);
   return 0;
 }
 
