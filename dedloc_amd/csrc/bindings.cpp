@@ -1026,6 +1026,24 @@ at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t str
   const at::Tensor col = stem_cols_checked(cols, x, R, S, stride, pad, P, Q, sc);
   auto wp = at::zeros({K, sc.Kp}, w.options());
   wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
+  // the column-matrix GEMM as a 1x1 conv over the [N*P*Q, 1, 1, Kp] "image" on conv.hip (its
+  // 256x64 tiles for the 64 stem channels, with the statistics epilogue); the tiled GEMM kernels
+  // otherwise (DEDLOC_STEM_GEMM=1)
+  static const bool stem_gemm = [] {
+    const char* e = std::getenv("DEDLOC_STEM_GEMM");
+    return e && e[0] == '1';
+  }();
+  const int64_t Mc = col.size(0);
+  if (!stem_gemm && sc.Kp % 64 == 0) {
+    const DlConvGeom gc = geom(cbf(col), Mc, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1);
+    if (stats && dl_conv_fwd(gc, cbf(wp), sc.Kp, (int)K, bf(y), 1, 1, 1, 1, 0, 0, K, cur_stream(x), stats,
+                             stat_rows) == 0)
+      return y;
+    if (dl_conv_fwd(gc, cbf(wp), sc.Kp, (int)K, bf(y), 1, 1, 1, 1, 0, 0, K, cur_stream(x)) == 0) {
+      if (stats) check(dl_bn_stats(cbf(y), stats, stat_rows, (int)K, (int)groups, cur_stream(x)), "bn_stats");
+      return y;
+    }
+  }
   if (stats) gemm_store_stats(a_view(col, false), b_view(wp, true), col, wp, bf(y), K, stats, stat_rows, cur_stream(x));
   else gemm_plain(col, wp, bf(y), K, cur_stream(x));
   return y;
