@@ -941,6 +941,16 @@ bool conv_gemm() {
 inline bool is_pointwise(int64_t R, int64_t S, int64_t stride, int64_t pad) {
   return R == 1 && S == 1 && stride == 1 && pad == 0;
 }
+// 1x1 convs whose GEMM output has at most this many columns (forward: output channels; data
+// gradient: input channels) run on conv.hip's implicit-GEMM kernel (256x64 / 128x128 tiles, 2-deep
+// register prefetch) instead of gemm_small (DEDLOC_CONV_NARROW_1X1 = 0 / 64 / 128)
+inline int64_t narrow_1x1_max() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("DEDLOC_CONV_NARROW_1X1");
+    return e ? (int64_t)std::atol(e) : (int64_t)128;
+  }();
+  return v;
+}
 inline at::Tensor rows2d(const at::Tensor& t) {  // channels-last [N, C, H, W] -> [N*H*W, C] view
   return t.permute({0, 2, 3, 1}).reshape({-1, t.size(1)});
 }
@@ -1004,7 +1014,7 @@ at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t str
   auto y = at::empty({N, K, P, Q}, x.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);
   const long stat_rows = N / groups * P * Q;  // output rows per statistics group
-  if (is_pointwise(R, S, stride, pad) && conv_gemm()) {
+  if (is_pointwise(R, S, stride, pad) && conv_gemm() && !(K <= narrow_1x1_max() && C % 64 == 0)) {
     const at::Tensor xr = rows2d(x), wr = wk.view({K, C});
     if (stats) gemm_store_stats(a_view(xr, false), b_view(wr, true), xr, wr, bf(y), K, stats, stat_rows, cur_stream(x));
     else gemm_plain(xr, wr, bf(y), K, cur_stream(x));
@@ -1070,7 +1080,8 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
     TORCH_CHECK(residual->sizes() == dx.sizes(), "conv2d_dgrad: residual must have the input's shape");
   }
   const at::Tensor wk = krsc_view(w);  // [K, R, S, C]
-  if (is_pointwise(R, S, stride, pad) && H == P && W == Q && conv_gemm()) {
+  if (is_pointwise(R, S, stride, pad) && H == P && W == Q && conv_gemm() &&
+      !(C <= narrow_1x1_max() && K % 64 == 0)) {
     // dX[M, C] = dY[M, K] W[K, C] (+ residual): the weight as a K-outer B operand, no transposed copy
     const at::Tensor dyr = rows2d(dy), wkc = wk.view({K, C});
     gemm_store(a_view(dyr, false), b_view(wkc, false), dyr, wkc, bf(dx), C, nullptr,
