@@ -20,12 +20,17 @@
 // normalises every crop with its own statistics — exactly the reference's SINGLE_PASS_EVERY_CROP
 // semantics (one trunk pass per crop) with 8x fewer, 6x larger kernels; the running statistics
 // take the G momentum updates in crop order.
+#include <cstdlib>
+
 #include "dl_common.h"
 #include "dl_kernels.h"
 
 namespace {
 
 constexpr int kThreads = 256;
+// 16-byte vectors (rows) in flight per thread in the streaming passes (apply, backward statistics,
+// dx): template parameter BN_U, DEDLOC_BN_UNROLL = 2 (default) or 4.  4 needs 116-190 VGPRs and
+// halves the resident waves: SwAV iteration 2186-2191 vs 2202-2212 samples/s with 2 (same box)
 
 __device__ __forceinline__ void ld8(const bf16_t* p, float (&v)[8]) { load_bf16<8>(p, v); }
 
@@ -77,6 +82,7 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------------------------- forward apply
+template <int BN_U>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __restrict__ x,
                                                             const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
                                                             const float* __restrict__ sums,
@@ -123,15 +129,15 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
   // iteration keep two independent load chains in flight per thread
   const long stride = (long)gridDim.x * kThreads;
   long i = blockIdx.x * (long)kThreads + threadIdx.x;
-  for (; i + stride < nvec; i += 2 * stride) {
-    float v[2][8], rr[2][8];
+  for (; i + (BN_U - 1) * stride < nvec; i += BN_U * stride) {
+    float v[BN_U][8], rr[BN_U][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < BN_U; ++u) {
       ld8(x + (i + u * stride) * 8, v[u]);
       if (res != nullptr) ld8(res + (i + u * stride) * 8, rr[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < BN_U; ++u) {
       const int c0 = ((int)(i + u * stride) & (CV - 1)) * 8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -163,6 +169,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
 // pre-activation fmaf(x, gamma*rstd, beta - mean*gamma*rstd) > 0 — the forward's own expression over
 // the saved mean / rstd — so with `beta` given the backward passes read dy and x only (2 of 3
 // streams; with a residual the mask depends on it and y is read).
+template <int BN_U>
 __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __restrict__ dy,
                                                                 const bf16_t* __restrict__ y,
                                                                 const bf16_t* __restrict__ x,
@@ -197,17 +204,17 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
   }
   float sg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sgx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   long r = r0 + rsub;
-  for (; r + rpi < r1; r += 2 * rpi) {  // two rows (up to six 16-byte loads) in flight per thread
-    float g[2][8], xv[2][8], yv[2][8];
+  for (; r + (BN_U - 1) * rpi < r1; r += BN_U * rpi) {  // BN_U rows (2-3 loads each) in flight per thread
+    float g[BN_U][8], xv[BN_U][8], yv[BN_U][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < BN_U; ++u) {
       const long off = (r + u * rpi) * C + cv * 8;
       ld8(dy + off, g[u]);
       ld8(x + off, xv[u]);
       if (relu && !xmask) ld8(y + off, yv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < BN_U; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const bool live = !relu || (xmask ? fmaf(xv[u][j], sc[j], sh[j]) > 0.f : yv[u][j] > 0.f);
@@ -255,6 +262,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
 }
 
 // ---------------------------------------------------------------------------------- backward dx
+template <int BN_U>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ y,
                                                              const bf16_t* __restrict__ x,
@@ -303,16 +311,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
   const long nvec = R * CV;
   const long stride = (long)gridDim.x * kThreads;
   long i = blockIdx.x * (long)kThreads + threadIdx.x;
-  for (; i + stride < nvec; i += 2 * stride) {
-    float g[2][8], xv[2][8], yv[2][8];
+  for (; i + (BN_U - 1) * stride < nvec; i += BN_U * stride) {
+    float g[BN_U][8], xv[BN_U][8], yv[BN_U][8];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < BN_U; ++u) {
       ld8(dy + (i + u * stride) * 8, g[u]);
       ld8(x + (i + u * stride) * 8, xv[u]);
       if (relu && !xmask) ld8(y + (i + u * stride) * 8, yv[u]);
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < BN_U; ++u) {
       const long iv = i + u * stride;
       const int c0 = ((int)iv & (CV - 1)) * 8;
       if (xmask) {
@@ -359,6 +367,21 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
   }
 }
 
+inline int bn_unroll() {
+  static const int u = [] {
+    const char* e = std::getenv("DEDLOC_BN_UNROLL");
+    return e && std::atoi(e) == 4 ? 4 : 2;
+  }();
+  return u;
+}
+
+// launch KERNEL<2> or KERNEL<4> by the unroll knob
+#define DL_BN_LAUNCH(KERNEL, GRID, ...)                                     \
+  do {                                                                      \
+    if (bn_unroll() == 2) KERNEL<2><<<GRID, kThreads, 0, st>>>(__VA_ARGS__); \
+    else KERNEL<4><<<GRID, kThreads, 0, st>>>(__VA_ARGS__);                  \
+  } while (0)
+
 inline bool bn_shape_ok(int C) {
   if (C % 8 || C > 2048) return false;
   const int CV = C / 8;
@@ -399,7 +422,7 @@ int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
     bn_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(x, sums, R, C, rpb);
   }
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
-  bn_apply_kernel<<<dim3(na, G), kThreads, 0, st>>>(x, res, y, sums, gamma, beta, mean, rstd, run_mean, run_var, R, C,
+  DL_BN_LAUNCH(bn_apply_kernel, dim3(na, G), x, res, y, sums, gamma, beta, mean, rstd, run_mean, run_var, R, C,
                                                     eps, momentum, relu);
   return 0;
 }
@@ -420,7 +443,7 @@ int dl_bn_bwd_prep(bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* me
   if (!bn_shape_ok(C) || R < 1 || G < 1 || (!y && !beta)) return -1;
   long rpb;
   const int nb = stats_blocks(R, C, rpb);
-  bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, 1, gamma,
+  DL_BN_LAUNCH(bn_bwd_stats_kernel, dim3(nb, G), dy, y, x, mean, rstd, sums, R, C, rpb, 1, gamma,
                                                          y ? nullptr : beta, dy);
   return 0;
 }
@@ -437,11 +460,11 @@ int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* m
   if (!stats_ready) {  // else: a data-gradient epilogue (or dl_bn_bwd_prep) accumulated the sums and
                        // already masked dy by the ReLU (the caller then passes relu = 0)
     if (!sums_zeroed) DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
-    bn_bwd_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu, gamma, beta,
+    DL_BN_LAUNCH(bn_bwd_stats_kernel, dim3(nb, G), dy, y, x, mean, rstd, sums, R, C, rpb, relu, gamma, beta,
                                                            nullptr);
   }
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
-  bn_bwd_dx_kernel<<<dim3(na, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
+  DL_BN_LAUNCH(bn_bwd_dx_kernel, dim3(na, G), dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
                                                      relu, accumulate, beta);
   return 0;
 }
