@@ -10,6 +10,7 @@
 
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <unordered_map>
 
 #include "dl_kernels.h"
@@ -1059,12 +1060,30 @@ at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t str
   return y;
 }
 
+// Tap-transposed data-gradient weights of every parity class of a strided conv, in (a, b) order:
+// [C, TR, TS, K] per class (an empty tensor for a class with no contributing tap).  The SwAV
+// model computes them once per iteration and passes them to every data-gradient call of that conv
+// (both trunk passes), instead of one copy kernel per class per call.
+std::vector<at::Tensor> conv2d_dgrad_weights(const at::Tensor& w, int64_t stride, int64_t pad) {
+  const at::Tensor wk = krsc_view(w);
+  const int64_t R = wk.size(1), S = wk.size(2);
+  std::vector<at::Tensor> out;
+  for (int64_t a = 0; a < stride; ++a)
+    for (int64_t b = 0; b < stride; ++b) {
+      const int64_t r0 = (a + pad) % stride, s0 = (b + pad) % stride;
+      if (r0 < R && s0 < S) out.push_back(wk.slice(1, r0, R, stride).slice(2, s0, S, stride).permute({3, 1, 2, 0}).contiguous());
+      else out.push_back(at::empty({0}, w.options()));  // no contributing tap
+    }
+  return out;
+}
+
 // dX = conv^T(dY): for each output parity class (a, b) of the stride, a dense sub-convolution over
 // the taps r = r0, r0 + stride, ... that reach it (dY row = i + dh0 - tr), weights [Cin][tr][ts][Cout]
 // residual (optional, [N, C, H, W] channels-last bf16): added to dX — in the GEMM epilogue on the
 // 1x1 stride-1 path (a Bottleneck's conv1 taking the identity branch's gradient), afterwards otherwise
 at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t stride, int64_t pad, int64_t H,
-                        int64_t W, const c10::optional<at::Tensor>& residual) {
+                        int64_t W, const c10::optional<at::Tensor>& residual,
+                        const c10::optional<std::vector<at::Tensor>>& wds) {
   const at::Tensor dy = dy_in.is_contiguous(at::MemoryFormat::ChannelsLast)
                             ? dy_in
                             : dy_in.contiguous(at::MemoryFormat::ChannelsLast);
@@ -1097,11 +1116,18 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
       const int64_t s0 = (b + pad) % stride, TS = s0 < S ? (S - 1 - s0) / stride + 1 : 0;
       const int64_t dw0 = (b + pad - s0) / stride;
       if (I <= 0 || J <= 0) continue;
-      at::Tensor wd;
-      if (TR > 0 && TS > 0)
-        wd = wk.slice(1, r0, R, stride).slice(2, s0, S, stride).permute({3, 1, 2, 0}).contiguous();  // [C, TR, TS, K]
-      else
-        wd = at::zeros({C, 8}, w.options());  // no contributing tap: the class is all zeros
+      // [C, TR, TS, K] tap-transposed weights of this parity class (precomputed ones when given); a
+      // class with no contributing tap runs the kernel's zero-tile path, which reads no weights
+      at::Tensor wd = wk;
+      if (TR > 0 && TS > 0) {
+        const size_t cls = (size_t)(a * stride + b);
+        if (wds.has_value() && cls < wds->size() && (*wds)[cls].numel() > 0) {
+          wd = (*wds)[cls];
+          TORCH_CHECK(wd.is_contiguous() && wd.numel() == C * TR * TS * K, "conv2d_dgrad: wds shape");
+        } else {
+          wd = wk.slice(1, r0, R, stride).slice(2, s0, S, stride).permute({3, 1, 2, 0}).contiguous();
+        }
+      }
       check(dl_conv_fwd(geom(cbf(dy), N, P, Q, K, I, J, 1, 1, TR, TS, dh0, -1, dw0, -1), cbf(wd),
                         std::max<int64_t>(8, TR * TS * K), (int)C, bf(dx), (int)H, (int)W, (int)stride, (int)stride,
                         (int)a, (int)b, C, cur_stream(dy)),
@@ -1124,7 +1150,8 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
 std::tuple<at::Tensor, bool> conv2d_dgrad_bn(const at::Tensor& dy, const at::Tensor& w, int64_t stride, int64_t pad, int64_t H,
                            int64_t W, const c10::optional<at::Tensor>& residual, const at::Tensor& x,
                            const c10::optional<at::Tensor>& y, const at::Tensor& mean, const at::Tensor& rstd,
-                           const at::Tensor& gamma, const at::Tensor& beta, at::Tensor sums, int64_t groups) {
+                           const at::Tensor& gamma, const at::Tensor& beta, at::Tensor sums, int64_t groups,
+                           const c10::optional<std::vector<at::Tensor>>& wds) {
   expect_nhwc(x, "x");
   if (y.has_value()) expect_nhwc(*y, "y");
   expect(mean, at::kFloat, "mean");
@@ -1169,7 +1196,7 @@ std::tuple<at::Tensor, bool> conv2d_dgrad_bn(const at::Tensor& dy, const at::Ten
                       nullptr, 0, 0, nullptr, rp, C, 1, nullptr, st, f32(sums), stat_rows, &bn) == 0)
       return {dx, true};
   }
-  return {conv2d_dgrad(gdy, w, stride, pad, H, W, residual), false};
+  return {conv2d_dgrad(gdy, w, stride, pad, H, W, residual, wds), false};
 }
 
 // the preparation as its own pass (tests; the fallback the fused epilogues are checked against)
@@ -1229,6 +1256,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("conv2d_fwd_stats", &conv2d_fwd_stats);
   m.impl("im2col_stem", &im2col_stem);
   m.impl("conv2d_dgrad_bn", &conv2d_dgrad_bn);
+  m.impl("conv2d_dgrad_weights", &conv2d_dgrad_weights);
   m.impl("bn_bwd_prep", &bn_bwd_prep);
   m.impl("conv2d_dgrad", &conv2d_dgrad);
   m.impl("conv2d_wgrad", &conv2d_wgrad);

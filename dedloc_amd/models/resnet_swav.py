@@ -154,6 +154,7 @@ class _ConvNHWC(torch.autograd.Function):
             x = torch.empty((), dtype=torch.bfloat16, device=dy.device).expand(ctx.xshape)
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
+        wds = _dgrad_weights(ctx.module, wb, ctx.stride, ctx.pad) if ctx.needs_input_grad[0] else None
         if ctx.needs_input_grad[0]:
             res = None
             if ctx.link is not None:  # + the block's identity-branch gradient (see _GradLink)
@@ -163,9 +164,9 @@ class _ConvNHWC(torch.autograd.Function):
                 bx, mean, rstd, gamma, beta, sums, G, has_res = bl.bn
                 dx, bl.done = torch.ops.dedloc.conv2d_dgrad_bn(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3],
                                                                res, bx, x if has_res else None, mean, rstd, gamma,
-                                                               beta, sums, G)
+                                                               beta, sums, G, wds)
             else:
-                dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3], res)
+                dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3], res, wds)
         dw = None
         if ctx.needs_input_grad[1]:
             weight = ctx.module.weight
@@ -179,6 +180,25 @@ class _ConvNHWC(torch.autograd.Function):
                 torch.ops.dedloc.conv2d_wgrad(dy, x, dw, ctx.stride, ctx.pad, cols)
                 dw = dw.to(weight.dtype)
         return dx, dw, None, None, None, None, None, None, None
+
+
+def _dgrad_weights(module, wb, stride, pad):
+    """The tap-transposed data-gradient weights of a conv that takes the implicit-GEMM data-gradient
+    path (3x3 and strided convs, 1x1 convs with at most 128 input channels), computed once per
+    SwAVModel iteration (``module._wd_token``, renewed by every SwAVModel.forward) and shared by the
+    backward of both trunk passes; None elsewhere (the op then transposes per call)."""
+    k = wb.shape[2]
+    if k == 1 and stride == 1 and (wb.shape[1] > 128 or wb.shape[0] % 64):
+        return None  # the 1x1 GEMM route reads the weight as it is
+    token = getattr(module, "_wd_token", None)
+    if token is None:
+        return None
+    cached = getattr(module, "_wd_cache", None)
+    if cached is not None and cached[0] is token:
+        return cached[1]
+    wds = torch.ops.dedloc.conv2d_dgrad_weights(wb, stride, pad)
+    module._wd_cache = (token, wds)
+    return wds
 
 
 class ConvNHWC(nn.Conv2d):
@@ -560,8 +580,9 @@ class SwAVModel(nn.Module):
         statistics span the whole resolution group (original SwAV's idx_crops grouping).
         """
         convs = [m for m in self.trunk.modules() if isinstance(m, ConvNHWC)]
+        token = object()  # this iteration's weights: the data-gradient weight cache key (_dgrad_weights)
         for m in convs:
-            m._wb_cache, m._wb_share = None, True
+            m._wb_cache, m._wb_share, m._wd_token = None, True, token
         flat = self._flat
         if flat is not None and flat.bf16.device == crops[0].device:
             flat.refresh_bf16()

@@ -64,7 +64,8 @@ _SCHEMAS = [
     "Tensor(a!)? sums=None, Tensor(b!)? dgamma_acc=None, Tensor(c!)? dbeta_acc=None, Tensor? beta=None, "
     "bool stats_ready=False) -> (Tensor, Tensor, Tensor, Tensor)",
     "conv2d_dgrad_bn(Tensor dy, Tensor w, int stride, int pad, int H, int W, Tensor? residual, Tensor x, Tensor? y, "
-    "Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, Tensor(a!) sums, int groups) -> (Tensor, bool)",
+    "Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, Tensor(a!) sums, int groups, Tensor[]? wds=None) "
+    "-> (Tensor, bool)",
     "bn_bwd_prep(Tensor(a!) g, Tensor x, Tensor? y, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, "
     "Tensor(b!) sums, int groups) -> Tensor",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
@@ -72,7 +73,9 @@ _SCHEMAS = [
     "conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor(a!) sums, int groups, Tensor? cols=None) "
     "-> Tensor",
     "im2col_stem(Tensor x, int R, int S, int stride, int pad) -> Tensor",
-    "conv2d_dgrad(Tensor dy, Tensor w, int stride, int pad, int H, int W, Tensor? residual=None) -> Tensor",
+    "conv2d_dgrad(Tensor dy, Tensor w, int stride, int pad, int H, int W, Tensor? residual=None, "
+    "Tensor[]? wds=None) -> Tensor",
+    "conv2d_dgrad_weights(Tensor w, int stride, int pad) -> Tensor[]",
     "conv2d_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, Tensor? cols=None) -> ()",
 ]
 for _s in _SCHEMAS:
@@ -573,7 +576,7 @@ def _conv2d_fwd_stats_cpu(x, w, stride, pad, sums, groups, cols=None):
 
 
 @_impl("conv2d_dgrad")
-def _conv2d_dgrad_cpu(dy, w, stride, pad, H, W, residual=None):
+def _conv2d_dgrad_cpu(dy, w, stride, pad, H, W, residual=None, wds=None):  # wds: GPU-side cache
     shape = (dy.shape[0], w.shape[1], H, W)
     dx = torch.nn.grad.conv2d_input(shape, w.float(), dy.float(), stride=stride, padding=pad)
     if residual is not None:
@@ -582,7 +585,7 @@ def _conv2d_dgrad_cpu(dy, w, stride, pad, H, W, residual=None):
 
 
 @_impl("conv2d_dgrad_bn")
-def _conv2d_dgrad_bn_cpu(dy, w, stride, pad, H, W, residual, x, y, mean, rstd, gamma, beta, sums, groups):
+def _conv2d_dgrad_bn_cpu(dy, w, stride, pad, H, W, residual, x, y, mean, rstd, gamma, beta, sums, groups, wds=None):
     g = _conv2d_dgrad_cpu(dy, w, stride, pad, H, W, residual).float()
     G, C = groups, x.shape[1]
     shp = (G, x.shape[0] // G, C, H, W)
