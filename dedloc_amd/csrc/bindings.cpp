@@ -1232,8 +1232,18 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
   if (is_pointwise(R, S, stride, pad) && conv_gemm() && K % 256 == 0 && C % 256 == 0) {
     gemm_acc_f32(rows2d(dy), rows2d(x), acc.view({K, C}), true, false);
   } else if (C % 8 == 0 && C >= 8 && C % 64 == 0) {
-    rc = dl_conv_wgrad(geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1), cbf(dy), K, (int)K,
-                       f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy));
+    const DlConvGeom gm = geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1);
+    // DEDLOC_CONV_WGRAD_SLAB=1: split partials as fp32 slabs summed in one pass instead of fp32
+    // atomics (SwAV b=64, interleaved on one box: slabs 2168 / 2141, atomics 2226 / 2104 samples/s —
+    // no consistent gain, atomics stay the default)
+    static const bool slabs = [] {
+      const char* e = std::getenv("DEDLOC_CONV_WGRAD_SLAB");
+      return e && e[0] == '1';
+    }();
+    const size_t nws = slabs ? dl_conv_wgrad_ws_floats(gm, (int)K, (int)(R * S * C)) : 0;
+    at::Tensor ws = nws ? at::empty({(int64_t)nws}, dw.options()) : at::Tensor();
+    rc = dl_conv_wgrad(gm, cbf(dy), K, (int)K, f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy),
+                       nws ? f32(ws) : nullptr, nws);
     check(rc, "conv2d_wgrad");
   } else {
     // stem: wgrad over the padded column matrix into a [K, R, SCp] slab, then the real columns
