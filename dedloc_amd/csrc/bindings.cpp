@@ -1236,10 +1236,8 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
     // DEDLOC_CONV_WGRAD_SLAB=1: split partials as fp32 slabs summed in one pass instead of fp32
     // atomics (SwAV b=64, interleaved on one box: slabs 2168 / 2141, atomics 2226 / 2104 samples/s —
     // no consistent gain, atomics stay the default)
-    static const bool slabs = [] {
-      const char* e = std::getenv("DEDLOC_CONV_WGRAD_SLAB");
-      return e && e[0] == '1';
-    }();
+    const char* slab_env = std::getenv("DEDLOC_CONV_WGRAD_SLAB");  // read per call: tests A/B both forms
+    const bool slabs = slab_env && slab_env[0] == '1';
     const size_t nws = slabs ? dl_conv_wgrad_ws_floats(gm, (int)K, (int)(R * S * C)) : 0;
     at::Tensor ws = nws ? at::empty({(int64_t)nws}, dw.options()) : at::Tensor();
     rc = dl_conv_wgrad(gm, cbf(dy), K, (int)K, f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy),

@@ -326,3 +326,25 @@ def test_chained_bottlenecks_grads_match_fp32(cuda, cin, planes, stride):
     for n, _ in m.named_parameters():
         ours, theirs = _rel(flat.view(flat.grad, n), rp[n].grad), _rel(sp[n].grad, rp[n].grad)
         assert ours < bound(theirs), (n, ours, theirs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8, 64, 28, 64, 3, 1, 1), (4, 128, 28, 256, 3, 2, 1), (8, 64, 28, 256, 1, 1, 0)])
+def test_conv_wgrad_slab_mode_matches_atomics(cuda, monkeypatch, shape):
+    """The split weight gradient's slab form (per-split fp32 partials + a summing pass) equals the
+    atomic-add form up to fp32 summation order, accumulating into the existing gradient."""
+    N, Cin, H, Cout, k, stride, pad = shape
+    torch.manual_seed(4)
+    x = torch.randn(N, Cin, H, H, device=cuda).bfloat16().contiguous(memory_format=CL)
+    P = (H + 2 * pad - k) // stride + 1
+    dy = torch.randn(N, Cout, P, P, device=cuda).bfloat16().contiguous(memory_format=CL)
+    outs = []
+    for slab in ("0", "1"):
+        monkeypatch.setenv("DEDLOC_CONV_WGRAD_SLAB", slab)
+        monkeypatch.setenv("DEDLOC_CONV_GEMM", "hip")
+        dw = torch.ones(Cout, Cin, k, k, device=cuda).contiguous(memory_format=CL)
+        torch.ops.dedloc.conv2d_wgrad(dy, x, dw, stride, pad)
+        outs.append(dw)
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-3)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, Cin, k, k), dy.float(), stride=stride, padding=pad) + 1
+    assert _rel(outs[1], ref) < 1e-2
