@@ -293,8 +293,9 @@ class GroupCommunicators:
                 self._publish(tok, {"uid": uid})
             else:
                 uid = bytes(self._await(tok, deadline)["uid"])
-            try:
-                comm = RcclGroupComm.create(uid, n, rank, self.device, deadline)
+            try:  # a healthy bootstrap takes seconds: a broken one should not hold the whole round
+                boot = min(deadline, time.monotonic() + float(os.environ.get("DEDLOC_RCCL_BOOTSTRAP_S", "30")))
+                comm = RcclGroupComm.create(uid, n, rank, self.device, boot)
             except Exception:  # CommError (deadline) or an RCCL init error raised by the op
                 self.rccl_create_failures += 1
                 if self.rccl_create_failures == self.RCCL_FALLBACK_AFTER:
