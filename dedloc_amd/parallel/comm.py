@@ -294,7 +294,8 @@ class GroupCommunicators:
             else:
                 uid = bytes(self._await(tok, deadline)["uid"])
             try:  # a healthy bootstrap takes seconds: a broken one should not hold the whole round
-                boot = min(deadline, time.monotonic() + float(os.environ.get("DEDLOC_RCCL_BOOTSTRAP_S", "30")))
+                boot = time.monotonic() + float(os.environ.get("DEDLOC_RCCL_BOOTSTRAP_S", "30"))
+                boot = boot if deadline is None else min(deadline, boot)
                 comm = RcclGroupComm.create(uid, n, rank, self.device, boot)
             except Exception:  # CommError (deadline) or an RCCL init error raised by the op
                 self.rccl_create_failures += 1
