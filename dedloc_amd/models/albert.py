@@ -138,8 +138,9 @@ def _layer_prefix(g: int, i: int) -> str:
 # DEDLOC_RESIDUAL=ln keeps the residual add inside the LayerNorm kernel (A/B measurement)
 _RESIDUAL_IN_GEMM = os.environ.get("DEDLOC_RESIDUAL", "gemm") != "ln"
 # The backward's data-gradient GEMMs (dX = dY W) run against transposed weight copies made once per
-# encoder call (the 24 layers share them): hipBLASLt's "NT" kernels (the forward's layout) beat the
-# "NN" ones by 10-15% on these shapes (profiles/README.md).  DEDLOC_DGRAD_WT=0: plain weights.
+# encoder call (the 24 layers share them): gemm8 with both operands K-inner beats the K-outer-B form
+# by 5-10% on these shapes (profiles/gemm8_asm_dma_layouts_T131072.log).  DEDLOC_DGRAD_WT=0: plain
+# weights.
 _DGRAD_WT = os.environ.get("DEDLOC_DGRAD_WT", "1") != "0"
 # Weight gradients of the shared layer keep their token-split fp32 slabs across the layer
 # applications and add them into the flat gradient once, at the last backward call

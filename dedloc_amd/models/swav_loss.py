@@ -82,7 +82,7 @@ class SwAVLoss(nn.Module):
             for i, crop_id in enumerate(self.crops_for_assign):
                 s = scores[bs * crop_id: bs * (crop_id + 1)].float()
                 if self.use_queue:  # queue rows first, current batch last (the kernel emits the last bs rows)
-                    s = torch.cat([self.queue[i] @ prototypes.detach().float().t(), s])
+                    s = torch.cat([self._queue_scores(i, prototypes), s])
                 q = self._sinkhorn(s.contiguous(), bs)
                 if self.num_iteration < self.temp_hard_assignment_iters:
                     q = torch.zeros_like(q).scatter_(1, q.argmax(dim=1, keepdim=True), 1.0)
@@ -92,6 +92,16 @@ class SwAVLoss(nn.Module):
         if self.use_queue:
             self._update_queue(embedding.detach())
         return loss
+
+    def _queue_scores(self, i, prototypes):
+        """Scores of queue i against the prototypes, [L, K] fp32: on the GPU the own GEMM kernels
+        (bf16 operands like the batch's prototype scores, fp32 accumulation and output)."""
+        q = self.queue[i]
+        if not q.is_cuda:
+            return q @ prototypes.detach().float().t()
+        out = torch.zeros(q.shape[0], prototypes.shape[0], dtype=torch.float32, device=q.device)
+        torch.ops.dedloc.gemm_acc_f32(q.to(torch.bfloat16), prototypes.detach().to(torch.bfloat16), out, False, True)
+        return out
 
     def _sinkhorn(self, s, bs):
         return torch.ops.dedloc.sinkhorn(s, bs, self.epsilon, self.num_iters)

@@ -127,7 +127,7 @@ class SwavPeer:
         self.frozen = [(name, int(iters)) for name, iters in (mcfg.get("TEMP_FROZEN_PARAMS_ITER_MAP") or [])]
         self.use_graph = bool(mcfg.get("CUDA_GRAPH", False)) and self.device.type == "cuda" and \
             not bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING)
-        self.graph_warmup = int(mcfg.get("CUDA_GRAPH_WARMUP", 3))  # eager iterations first (MIOpen find)
+        self.graph_warmup = int(mcfg.get("CUDA_GRAPH_WARMUP", 3))  # eager iterations before the capture
         self._graphed = None
         self.iteration = 0
         self._loss_sum = torch.zeros((), device=self.device)

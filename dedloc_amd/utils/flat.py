@@ -29,8 +29,8 @@ class FlatParams:
       * ``autograd=True`` (torch-module models such as the SwAV ResNet): parameters keep
         ``requires_grad`` and their ``.grad`` is pre-bound to the ``grad`` view, so autograd's
         AccumulateGrad adds in place into the flat buffer.  With ``channels_last=True`` every 4-D
-        parameter (conv weight) is laid out NHWC inside the flat buffer, matching channels-last
-        activations so MIOpen never transposes weights.
+        parameter (conv weight) is laid out NHWC (KRSC) inside the flat buffer, the layout the
+        implicit-GEMM conv kernels read, so weights are never transposed for the forward.
     """
 
     def __init__(self, named_params: Iterable[Tuple[str, torch.nn.Parameter]], device=None,

@@ -186,3 +186,17 @@ def test_conv_dgrad_bn_matches_reference(cuda, cin, cout, ymask, res):
                                                 mean.cpu(), rstd.cpu(), gamma.cpu(), beta.cpu(), sums_ref, G)
     torch.testing.assert_close(g.float().cpu(), g_ref.float(), rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(sums.cpu(), sums_ref, rtol=2e-2, atol=2.0)
+
+
+def test_swav_queue_scores_on_own_gemm(cuda):
+    """The SwAV loss's queue-vs-prototype scores run on the own GEMM kernels (bf16 operands, fp32
+    accumulation) and match the fp32 product to bf16 operand rounding."""
+    from dedloc_amd.models.swav_loss import SwAVLoss
+
+    torch.manual_seed(0)
+    loss = SwAVLoss(queue_length=3840, num_prototypes=3000, embedding_dim=128).to(cuda)
+    proto = torch.nn.functional.normalize(torch.randn(3000, 128, device=cuda), dim=1)
+    s = loss._queue_scores(0, proto)
+    ref = loss.queue[0] @ proto.t()
+    assert s.dtype == torch.float32 and s.shape == (3840, 3000)
+    torch.testing.assert_close(s, ref, rtol=2e-2, atol=2e-2)
