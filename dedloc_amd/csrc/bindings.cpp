@@ -484,6 +484,24 @@ void gemm_store_stats(const Mat& A, const Mat& B, const at::Tensor& a, const at:
   check(dl_bn_stats(C, stats, stat_rows, N, (int)(M / stat_rows), st), "bn_stats");
 }
 
+// out[b] = a[b] @ b[b] (torch.bmm semantics; any element strides, e.g. transposed views, read in
+// place) on gemm_small's batched launch: bf16 out, or fp32 with out_f32 (the composed attention's
+// scores).  One launch for the whole batch.
+at::Tensor bmm(const at::Tensor& a, const at::Tensor& b, bool out_f32) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
+              "bmm: bf16 GPU operands");
+  TORCH_CHECK(a.dim() == 3 && b.dim() == 3 && a.size(0) == b.size(0) && a.size(2) == b.size(1), "bmm: shapes");
+  const int64_t Bn = a.size(0), M = a.size(1), K = a.size(2), N = b.size(2);
+  auto out = at::empty({Bn, M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  if (Bn == 0 || M == 0 || N == 0) return out;
+  if (K == 0) return out.zero_();
+  check(dl_gemm_small_batched(out_f32 ? 1 : 0, cbf(a), a.stride(1), a.stride(2), a.stride(0), cbf(b), b.stride(2),
+                              b.stride(1), b.stride(0), (int)M, (int)N, (int)K, out_f32 ? nullptr : bf(out), N,
+                              out_f32 ? f32(out) : nullptr, N, M * N, (int)Bn, cur_stream(a)),
+        "bmm");
+  return out;
+}
+
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                 const c10::optional<at::Tensor>& residual, bool trans_a, bool trans_b, int64_t epilogue) {
   expect_operands(a, b);
@@ -1304,6 +1322,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("attn_softmax_fwd", &attn_softmax_fwd);
   m.impl("attn_softmax_bwd", &attn_softmax_bwd);
   m.impl("gemm", &gemm);
+  m.impl("bmm", &bmm);
   m.impl("gemm_acc_f32", &gemm_acc_f32);
   m.impl("gemm_acc_f32_shared", &gemm_acc_f32_shared);
   m.impl("gemm_gelu", &gemm_gelu);

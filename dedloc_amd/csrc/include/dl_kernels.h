@@ -160,6 +160,10 @@ int dl_l2norm_bwd(const bf16_t* dy, const bf16_t* y, const float* rinv, bf16_t* 
 // gemm_small.hip: any-shape / any-stride bf16 MFMA GEMM (epi 0: bf16 C (+bias)(+R); 1: fp32 Cf (+)=).
 // splits > 1 splits the reduction into fp32 slabs: ws must hold splits * M * N floats.
 int dl_gemm_small_splits(int M, int N, int K);
+// batch GEMMs in one launch (entry b: A + b*sab, B + b*sbb, C / Cf + b*scb); epi 0 bf16, 1 fp32 (=)
+int dl_gemm_small_batched(int epi, const bf16_t* A, long sam, long sak, long sab, const bf16_t* B, long sbn, long sbk,
+                          long sbb, int M, int N, int K, bf16_t* C, long ldc, float* Cf, long ldcf, long scb,
+                          int batch, hipStream_t st);
 // stats (epi 0, splits 1 only): BatchNorm statistics of the stored values as in dl_gemm8 EPI 4
 // (stat_rows a multiple of 128 dividing M)
 int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B, long sbn, long sbk, int M, int N,

@@ -48,6 +48,8 @@ struct SmallArgs {
   float* stats; long stat_rows;
   DlBnBwdEpi bn; int bnbwd;  // BN backward preparation (dl_kernels.h DlBnBwdEpi): stats are then the
                              // BN backward's sums and the stored values the ReLU-masked gradient
+  long sab, sbb, scb; int batched;  // batched mode: gridDim.z = batch, operand / output strides per
+                                    // batch entry (fp32 outputs use `slab` as theirs), no K split
 };
 
 // U 8-element chunks of a (64 U) x 32 operand tile per thread, into registers.
@@ -110,8 +112,11 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
-  const int kbeg = blockIdx.z * p.kchunk;
+  const int kbeg = p.batched ? 0 : blockIdx.z * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
+  const bf16_t* __restrict__ Ap = p.A + (p.batched ? (long)blockIdx.z * p.sab : 0L);
+  const bf16_t* __restrict__ Bp = p.B + (p.batched ? (long)blockIdx.z * p.sbb : 0L);
+  bf16_t* Cp = p.C + (p.batched ? (long)blockIdx.z * p.scb : 0L);
   floatx4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -119,15 +124,15 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
     for (int j = 0; j < NJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[2], rb[UB];
-  gload<LA, VA, 2>(p.A, p.sam, p.sak, m0, p.M, kbeg, kend, ra);
-  gload<LB, VB, UB>(p.B, p.sbn, p.sbk, n0, p.N, kbeg, kend, rb);
+  gload<LA, VA, 2>(Ap, p.sam, p.sak, m0, p.M, kbeg, kend, ra);
+  gload<LB, VB, UB>(Bp, p.sbn, p.sbk, n0, p.N, kbeg, kend, rb);
   for (int k0 = kbeg; k0 < kend; k0 += TK) {
     lds_put<LA, 2>(sa, ra);
     lds_put<LB, UB>(sb, rb);
     __syncthreads();
     if (k0 + TK < kend) {  // next K-step's loads are in flight during this one's MFMAs
-      gload<LA, VA, 2>(p.A, p.sam, p.sak, m0, p.M, k0 + TK, kend, ra);
-      gload<LB, VB, UB>(p.B, p.sbn, p.sbk, n0, p.N, k0 + TK, kend, rb);
+      gload<LA, VA, 2>(Ap, p.sam, p.sak, m0, p.M, k0 + TK, kend, ra);
+      gload<LB, VB, UB>(Bp, p.sbn, p.sbk, n0, p.N, k0 + TK, kend, rb);
     }
     bf16x8 af[4], bfr[NJ];
 #pragma unroll
@@ -174,13 +179,13 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
               live = fmaf(x, sc, p.bn.beta[n] - mu * sc) > 0.f;
             }
             const bf16_t o = live ? f2bf(v) : (bf16_t)0;
-            p.C[(long)m * p.ldc + n] = o;
+            Cp[(long)m * p.ldc + n] = o;
             const float g = bf2f(o);
             csum[j] += g;
             csq[j] = fmaf(g, (x - mu) * rs, csq[j]);
           } else {
             const bf16_t o = f2bf(v);
-            p.C[(long)m * p.ldc + n] = o;
+            Cp[(long)m * p.ldc + n] = o;
             const float r = bf2f(o);
             csum[j] += r;
             csq[j] = fmaf(r, r, csq[j]);
@@ -286,6 +291,28 @@ void walk(const bf16_t* p, long srow, long sk, int* L, bool* vec) {
 
 }  // namespace
 
+// batch independent GEMMs C_b = A_b B_b^T (same strides in every entry; entry b at A + b*sab,
+// B + b*sbb, and C + b*scb (epi 0) or Cf + b*scb (epi 1)): one launch, gridDim.z = batch
+int dl_gemm_small_batched(int epi, const bf16_t* A, long sam, long sak, long sab, const bf16_t* B, long sbn, long sbk,
+                          long sbb, int M, int N, int K, bf16_t* C, long ldc, float* Cf, long ldcf, long scb,
+                          int batch, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || batch < 1 || batch > 65535) return -1;
+  if ((epi == 0 && !C) || (epi == 1 && !Cf) || (M + TM - 1) / TM > 65535) return -1;
+  int LA, LB;
+  bool VA, VB;
+  walk(A, sam, sak, &LA, &VA);
+  walk(B, sbn, sbk, &LB, &VB);
+  // the 16-byte vector walk also needs every batch entry's base aligned
+  VA = VA && sab % 8 == 0;
+  VB = VB && sbb % 8 == 0;
+  SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, K, C, ldc, Cf, ldcf, scb, 0, nullptr, nullptr, 0,
+              nullptr, 0, DlBnBwdEpi{}, 0, sab, sbb, scb, 1};
+  const int tn = N <= 64 ? 64 : 128;
+  if (epi == 0) launch_tn<0>(a, LA, VA, LB, VB, tn, batch, st);
+  else launch_tn<1>(a, LA, VA, LB, VB, tn, batch, st);
+  return 0;
+}
+
 int dl_gemm_small_splits(int M, int N, int K) {
   if (M <= 0 || N <= 0 || K <= 0) return 1;
   const int tn = N <= 64 ? 64 : 128;
@@ -319,14 +346,14 @@ int dl_gemm_small(int epi, const bf16_t* A, long sam, long sak, const bf16_t* B,
   walk(B, sbn, sbk, &LB, &VB);
   if (S == 1) {
     SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, C, ldc, Cf, ldcf, 0, accumulate, bias, R, ldr, stats,
-                stat_rows, bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0};
+                stat_rows, bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0, 0, 0, 0, 0};
     if (epi == 0) launch_tn<0>(a, LA, VA, LB, VB, tn, 1, st);
     else launch_tn<1>(a, LA, VA, LB, VB, tn, 1, st);
     return 0;
   }
   if (bn) return -1;  // the BN preparation needs the single-pass (unsplit) epilogue
   SmallArgs a{A, sam, sak, B, sbn, sbk, M, N, K, kchunk, nullptr, 0, ws, N, (long)M * N, 0, nullptr, nullptr, 0,
-              nullptr, 0, DlBnBwdEpi{}, 0};
+              nullptr, 0, DlBnBwdEpi{}, 0, 0, 0, 0, 0};
   launch_tn<1>(a, LA, VA, LB, VB, tn, S, st);
   const long total = (long)M * N;
   const int blocks = (int)std::min<long>((total + 255) / 256, 4096);

@@ -108,31 +108,17 @@ def add_layernorm(x, res, gamma, beta, ggamma=None, gbeta=None, eps=1e-12):
 
 
 _LOG2E = math.log2(math.e)
-_BMM_OUT_F32 = None  # torch.bmm(..., out_dtype=float32) supported for bf16 on this build? (probed once)
-
-
-def _bmm_out_f32_supported(device) -> bool:
-    """One tiny probe: only an unsupported-signature/dtype error disables the bf16-in / fp32-out
-    path; errors of real calls (an OutOfMemoryError on the [B*H, S, S] scores) propagate."""
-    global _BMM_OUT_F32
-    if _BMM_OUT_F32 is None:
-        x = torch.zeros(1, 2, 2, dtype=torch.bfloat16, device=device)
-        try:
-            _BMM_OUT_F32 = torch.bmm(x, x, out_dtype=torch.float32).dtype == torch.float32
-        except (TypeError, NotImplementedError):
-            _BMM_OUT_F32 = False
-        except RuntimeError as e:
-            if isinstance(e, torch.OutOfMemoryError):
-                raise
-            _BMM_OUT_F32 = False
-    return _BMM_OUT_F32
 
 
 def _bmm_f32(a, b):
-    """[N, M, K] x [N, K, P] bf16 -> fp32 without rounding the product through bf16."""
-    if a.is_cuda and _bmm_out_f32_supported(a.device):
-        return torch.bmm(a, b, out_dtype=torch.float32)
-    return torch.bmm(a.float(), b.float())
+    """[N, M, K] x [N, K, P] bf16 -> fp32 without rounding the product through bf16 (the own
+    batched GEMM kernel; transposed operands are read in place)."""
+    return OPS.bmm(a, b, True)
+
+
+def _bmm(a, b):
+    """[N, M, K] x [N, K, P] bf16 -> bf16 on the own batched GEMM kernel."""
+    return OPS.bmm(a, b, False)
 
 
 def _attn_split(qkv, H, S):
@@ -152,7 +138,7 @@ def attn_composed_fwd(qkv, mbias, H, S, scale):
     s = _bmm_f32(q, k.transpose(1, 2))
     p, lse = OPS.attn_softmax_fwd(s, mbias, H, scale * _LOG2E)
     del s
-    o = torch.bmm(p, v)
+    o = _bmm(p, v)
     return o.view(B, H, S, D).transpose(1, 2).reshape(B * S, H * D), lse.view(B, H, S)
 
 
@@ -169,9 +155,9 @@ def attn_composed_bwd(qkv, mbias, out, dout, lse, H, S, scale, dbias=None):
     p, ds = OPS.attn_softmax_bwd(s, dp, mbias, lse.reshape(-1).contiguous(), delta.reshape(-1), H,
                                  scale * _LOG2E, scale)
     del s, dp
-    dv = torch.bmm(p.transpose(1, 2), do)
-    dq = torch.bmm(ds, k)
-    dk = torch.bmm(ds.transpose(1, 2), q)
+    dv = _bmm(p.transpose(1, 2), do)
+    dq = _bmm(ds, k)
+    dk = _bmm(ds.transpose(1, 2), q)
     g = torch.stack([dq, dk, dv], 0).view(3, B, H, S, D).permute(1, 3, 0, 2, 4).reshape(B * S, 3 * H * D)
     if dbias is not None:  # query: colsum dQ; key: 0 (softmax shift invariance); value: colsum dout
         HD = H * D

@@ -44,6 +44,7 @@ _SCHEMAS = [
     "attn_softmax_bwd(Tensor s, Tensor dp, Tensor? mbias, Tensor lse, Tensor delta, int H, float c, float scale) "
     "-> (Tensor, Tensor)",
     "gemm(Tensor a, Tensor b, Tensor? bias, Tensor? residual, bool trans_a, bool trans_b, int epilogue) -> Tensor",
+    "bmm(Tensor a, Tensor b, bool out_f32=False) -> Tensor",
     "gemm_acc_f32(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b) -> ()",
     "gemm_acc_f32_shared(Tensor a, Tensor b, Tensor(a!) c, bool trans_a, bool trans_b, bool first, bool last) -> ()",
     "gemm_gelu(Tensor x, Tensor w, Tensor bias, bool trans_w=False) -> (Tensor, Tensor)",
@@ -537,6 +538,12 @@ def _multicrop_cpu(pool, params, size, rad, mean, std):
     from dedloc_amd.data.multicrop import augment_reference
 
     return augment_reference(pool, params, size, rad, mean, std)
+
+
+@_impl("bmm")
+def _bmm_cpu(a, b, out_f32=False):
+    c = torch.bmm(a.float(), b.float())
+    return c if out_f32 else c.to(a.dtype)
 
 
 @_impl("bn_fwd")

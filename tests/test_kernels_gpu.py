@@ -670,6 +670,24 @@ def test_gemm_small_strided_views(cuda):
         assert rel(g, dy.float().t() @ a.float()) < 1e-3
 
 
+@pytest.mark.parametrize("Bn,M,N,K", [(48, 512, 512, 64), (6, 192, 64, 192), (5, 37, 70, 96)])
+def test_gemm_small_batched_bmm(cuda, Bn, M, N, K):
+    """OPS.bmm (gemm_small's batched launch, gridDim.z = batch) against fp32 torch.bmm: plain,
+    transposed-view operands read in place (the composed attention's K^T, P^T, dS^T), bf16 and fp32
+    outputs."""
+    torch.manual_seed(29)
+    a = torch.randn(Bn, M, K, device=cuda).bfloat16()
+    b = torch.randn(Bn, K, N, device=cuda).bfloat16()
+    ref = torch.bmm(a.float(), b.float())
+    out32 = OPS.bmm(a, b, True)
+    assert out32.dtype == torch.float32 and rel(out32, ref) < 1e-5
+    assert rel(OPS.bmm(a, b, False), ref) < 1e-2
+    at = torch.randn(Bn, K, M, device=cuda).bfloat16().transpose(1, 2)
+    bt = torch.randn(Bn, N, K, device=cuda).bfloat16().transpose(1, 2)
+    assert rel(OPS.bmm(at, bt, True), torch.bmm(at.float(), bt.float())) < 1e-5
+    assert rel(OPS.bmm(at, b, False), torch.bmm(at.float(), b.float())) < 1e-2
+
+
 @pytest.mark.timeout(240)
 def test_albert_pretraining_converges_on_gpu(cuda):
     """End to end through the HIP kernels: a small shared-layer ALBERT memorises one fixed MLM+SOP batch
