@@ -9,7 +9,7 @@ Variants per GEMM (the dispatch knobs are read per call, so one process times th
 Fused epilogues are timed as the op the model calls (gemm_gelu: bias + GELU; gemm_dgelu: GELU'
 + bias-gradient column sums).
 
-usage: T=131072 VARIANTS=gemm8,g8p,g8pnt python bench/gemm_bench.py [--check]
+usage: T=131072 VARIANTS=gemm8,g8p,g8pnt [KINDS=fwd,dgrad_wT] python bench/gemm_bench.py [--check]
 """
 import os as _os
 import sys as _sys
@@ -29,7 +29,12 @@ VARIANTS = {"gemm8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "0"},
             "g8p": {"DEDLOC_GEMM8_PERSIST": "256", "DEDLOC_GEMM8_NT": "0"},
             "g8pnt": {"DEDLOC_GEMM8_PERSIST": "256", "DEDLOC_GEMM8_NT": "1"},
             "g8nt": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1"},
-            "gemm1": {"DEDLOC_GEMM": "mfma1"}}
+            "gemm1": {"DEDLOC_GEMM": "mfma1"},
+            # tile order: bands of G row blocks walked column by column (gemm8.hip tile_of)
+            "g8g2": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "2"},
+            "g8g4": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "4"},
+            "g8g8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "8"},
+            "g8g16": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "16"}}
 
 
 def timeit(fn, iters=10):
@@ -43,7 +48,7 @@ def timeit(fn, iters=10):
 
 
 def set_policy(pol):
-    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT"):
+    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT", "DEDLOC_GEMM8_GROUP"):
         os.environ.pop(k, None)
     os.environ.update(pol)
 
@@ -76,6 +81,8 @@ def main():
         dy = (torch.rand(T, N, device=dev) * 2 - 1).bfloat16()
         g = torch.zeros(N, K, device=dev)
         db = torch.zeros(N, device=dev)
+        if name == "ffn2":  # gemm_dgelu's bias gradient spans its K (= 4096) output columns
+            db = torch.zeros(K, device=dev)
         fl = 2.0 * T * N * K
         kinds = [("fwd", lambda: O.gemm(x, w, b, None, False, True, 0)),
                  ("dgrad", lambda: O.gemm(dy, w, None, None, False, False, 0)),
@@ -95,7 +102,10 @@ def main():
             if os.environ.get("DGRAD_T"):
                 w2t = w.t().contiguous()
                 kinds.append(("dgrad_dgelu_wT", lambda: O.gemm_dgelu(dy, w2t, f, db, True)))
+        only = os.environ.get("KINDS")  # e.g. KINDS=fwd,dgrad_wT: time only these
         for kind, fn in kinds:
+            if only and kind not in only.split(","):
+                continue
             if check:
                 outs = {}
                 for v in variants:

@@ -423,8 +423,9 @@ inline void expect_operands(const at::Tensor& a, const at::Tensor& b) {
               "gemm operands must be 2-D with unit inner stride");
 }
 
-inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias) {
+inline at::Tensor f32_bias(const c10::optional<at::Tensor>& bias, int64_t n) {
   if (!bias.has_value()) return at::Tensor();
+  TORCH_CHECK(bias->numel() == n, "gemm bias must hold one value per output column");
   return bias->scalar_type() == at::kFloat ? bias->contiguous() : bias->to(at::kFloat).contiguous();
 }
 
@@ -513,7 +514,7 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
                 "gemm residual must be a contiguous bf16 [M, N] tensor");
   }
   auto c = at::empty({A.rows, B.rows}, a.options());
-  const at::Tensor bias32 = f32_bias(bias);
+  const at::Tensor bias32 = f32_bias(bias, B.rows);
   const float* bp = bias32.defined() ? f32(bias32) : nullptr;
   const bf16_t* rp = residual.has_value() ? cbf(*residual) : nullptr;
   gemm_store(A, B, a, b, bf(c), B.rows, bp, rp, B.rows, cur_stream(a));
@@ -676,7 +677,7 @@ std::tuple<at::Tensor, at::Tensor> gemm_gelu(const at::Tensor& x, const at::Tens
   const int64_t nout = trans_w ? w.size(1) : w.size(0);
   auto H = at::empty({x.size(0), nout}, x.options());
   auto G = at::empty_like(H);
-  const at::Tensor bias32 = f32_bias(bias);
+  const at::Tensor bias32 = f32_bias(bias, nout);
   if (own_gemm(0, trans_w ? 1 : 0, 1, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0), (int)nout,
                (int)x.size(1), bf(G), G.size(1), nullptr, 0, f32(bias32), nullptr, 0, bf(H), H.size(1), nullptr,
                cur_stream(x)) == 0)
@@ -695,6 +696,8 @@ at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tenso
   expect(F, at::kBFloat16, "F");
   expect(dbias, at::kFloat, "dbias");
   const int64_t nout = trans_w ? w.size(0) : w.size(1);
+  TORCH_CHECK(dbias.is_contiguous() && dbias.numel() == nout, "gemm_dgelu: dbias must hold one fp32 per output column");
+  TORCH_CHECK(F.dim() == 2 && F.size(0) == dy.size(0) && F.size(1) == nout, "gemm_dgelu: F shape");
   auto C = at::empty({dy.size(0), nout}, dy.options());
   if (own_gemm(0, trans_w ? 0 : 1, 2, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0), (int)nout,
                (int)dy.size(1), bf(C), C.size(1), nullptr, 0, nullptr, cbf(F), F.size(1), nullptr, 0, f32(dbias),
@@ -1095,6 +1098,54 @@ std::vector<at::Tensor> conv2d_dgrad_weights(const at::Tensor& w, int64_t stride
   return out;
 }
 
+// The implicit-GEMM data gradient dX[n, h, w, c] of a conv (dy NHWC, wk the KRSC weight view): a
+// stride-s conv splits into s^2 parity classes (h = i*s + a), each a dense stride-1 sub-convolution
+// over its contributing taps.  bn (with sums [groups][2C]): conv.hip's BN-backward epilogue on every
+// class; returns false without launching anything when a class's rows do not split into whole
+// 256-row tiles per statistics group.
+bool conv_dgrad_classes(const at::Tensor& dy, const at::Tensor& wk, int64_t stride, int64_t pad, int64_t H, int64_t W,
+                        at::Tensor& dx, const c10::optional<std::vector<at::Tensor>>& wds, float* sums,
+                        int64_t groups, const DlBnBwdEpi* bn) {
+  const int64_t N = dy.size(0), K = dy.size(1), P = dy.size(2), Q = dy.size(3);
+  const int64_t R = wk.size(1), S = wk.size(2), C = wk.size(3);
+  if (bn) {
+    if (groups < 1 || N % groups || C % 8) return false;
+    for (int64_t a = 0; a < stride; ++a)
+      for (int64_t b = 0; b < stride; ++b) {
+        const int64_t I = (H - a + stride - 1) / stride, J = (W - b + stride - 1) / stride;
+        if (I > 0 && J > 0 && (N / groups * I * J) % 256) return false;
+      }
+  }
+  for (int64_t a = 0; a < stride; ++a) {
+    const int64_t I = (H - a + stride - 1) / stride;
+    const int64_t r0 = (a + pad) % stride, TR = r0 < R ? (R - 1 - r0) / stride + 1 : 0;
+    const int64_t dh0 = (a + pad - r0) / stride;
+    for (int64_t b = 0; b < stride; ++b) {
+      const int64_t J = (W - b + stride - 1) / stride;
+      const int64_t s0 = (b + pad) % stride, TS = s0 < S ? (S - 1 - s0) / stride + 1 : 0;
+      const int64_t dw0 = (b + pad - s0) / stride;
+      if (I <= 0 || J <= 0) continue;
+      // [C, TR, TS, K] tap-transposed weights of this parity class (precomputed ones when given); a
+      // class with no contributing tap runs the kernel's zero-tile path, which reads no weights
+      at::Tensor wd = wk;
+      if (TR > 0 && TS > 0) {
+        const size_t cls = (size_t)(a * stride + b);
+        if (wds.has_value() && cls < wds->size() && (*wds)[cls].numel() > 0) {
+          wd = (*wds)[cls];
+          TORCH_CHECK(wd.is_contiguous() && wd.numel() == C * TR * TS * K, "conv2d_dgrad: wds shape");
+        } else {
+          wd = wk.slice(1, r0, R, stride).slice(2, s0, S, stride).permute({3, 1, 2, 0}).contiguous();
+        }
+      }
+      check(dl_conv_fwd(geom(cbf(dy), N, P, Q, K, I, J, 1, 1, TR, TS, dh0, -1, dw0, -1), cbf(wd),
+                        std::max<int64_t>(8, TR * TS * K), (int)C, bf(dx), (int)H, (int)W, (int)stride, (int)stride,
+                        (int)a, (int)b, C, cur_stream(dy), bn ? sums : nullptr, bn ? N / groups * I * J : 0, bn),
+            "conv2d_dgrad");
+    }
+  }
+  return true;
+}
+
 // dX = conv^T(dY): for each output parity class (a, b) of the stride, a dense sub-convolution over
 // the taps r = r0, r0 + stride, ... that reach it (dY row = i + dh0 - tr), weights [Cin][tr][ts][Cout]
 // residual (optional, [N, C, H, W] channels-last bf16): added to dX — in the GEMM epilogue on the
@@ -1125,33 +1176,7 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
                residual.has_value() ? cbf(*residual) : nullptr, C, cur_stream(dy));
     return dx;
   }
-  for (int64_t a = 0; a < stride; ++a) {
-    const int64_t I = (H - a + stride - 1) / stride;
-    const int64_t r0 = (a + pad) % stride, TR = r0 < R ? (R - 1 - r0) / stride + 1 : 0;
-    const int64_t dh0 = (a + pad - r0) / stride;
-    for (int64_t b = 0; b < stride; ++b) {
-      const int64_t J = (W - b + stride - 1) / stride;
-      const int64_t s0 = (b + pad) % stride, TS = s0 < S ? (S - 1 - s0) / stride + 1 : 0;
-      const int64_t dw0 = (b + pad - s0) / stride;
-      if (I <= 0 || J <= 0) continue;
-      // [C, TR, TS, K] tap-transposed weights of this parity class (precomputed ones when given); a
-      // class with no contributing tap runs the kernel's zero-tile path, which reads no weights
-      at::Tensor wd = wk;
-      if (TR > 0 && TS > 0) {
-        const size_t cls = (size_t)(a * stride + b);
-        if (wds.has_value() && cls < wds->size() && (*wds)[cls].numel() > 0) {
-          wd = (*wds)[cls];
-          TORCH_CHECK(wd.is_contiguous() && wd.numel() == C * TR * TS * K, "conv2d_dgrad: wds shape");
-        } else {
-          wd = wk.slice(1, r0, R, stride).slice(2, s0, S, stride).permute({3, 1, 2, 0}).contiguous();
-        }
-      }
-      check(dl_conv_fwd(geom(cbf(dy), N, P, Q, K, I, J, 1, 1, TR, TS, dh0, -1, dw0, -1), cbf(wd),
-                        std::max<int64_t>(8, TR * TS * K), (int)C, bf(dx), (int)H, (int)W, (int)stride, (int)stride,
-                        (int)a, (int)b, C, cur_stream(dy)),
-            "conv2d_dgrad");
-    }
-  }
+  conv_dgrad_classes(dy, wk, stride, pad, H, W, dx, wds, nullptr, 1, nullptr);
   if (residual.has_value()) dx.add_(*residual);
   return dx;
 }
@@ -1161,8 +1186,9 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
 // masked by the ReLU — mask from y > 0 when y is given (the BN had a residual branch), else from
 // the forward's pre-activation over x (the BN input) — and adds sums[grp][c] += g, sums[grp][C + c]
 // += g * (x - mean) * rstd, in the GEMM epilogue of a 1x1 stride-1 data gradient (gemm8 EPI 5;
-// gemm_small's per-element epilogue with DEDLOC_BN_BWD_SMALL=1).  Returns (dx, fused): where the
-// epilogue cannot take it, dx is the plain data gradient (+ residual), unmasked, and fused is false —
+// gemm_small's per-element epilogue with DEDLOC_BN_BWD_SMALL=1) or in conv.hip's epilogue on every
+// parity class of the others (no residual; whole 256-row tiles per statistics group).  Returns
+// (dx, fused): where the epilogue cannot take it, dx is the plain data gradient (+ residual), unmasked, and fused is false —
 // the BN backward then runs its own statistics pass (a separate preparation pass here would cost
 // more than that pass: it writes the masked gradient too).
 std::tuple<at::Tensor, bool> conv2d_dgrad_bn(const at::Tensor& dy, const at::Tensor& w, int64_t stride, int64_t pad, int64_t H,
@@ -1213,6 +1239,13 @@ std::tuple<at::Tensor, bool> conv2d_dgrad_bn(const at::Tensor& dy, const at::Ten
         dl_gemm_small(0, cbf(dyr), A.srow(), A.sk(), cbf(wkc), B.srow(), B.sk(), M, (int)C, (int)A.k, bf(dx), C,
                       nullptr, 0, 0, nullptr, rp, C, 1, nullptr, st, f32(sums), stat_rows, &bn) == 0)
       return {dx, true};
+  }
+  // 3x3 / strided data gradients (Bottleneck conv2 <- bn1) and the 1x1 ones gemm8 does not take
+  // (at most 128 input channels: conv3 <- bn2 in the first stages): conv.hip's epilogue
+  if (!residual.has_value() && K % 64 == 0) {
+    expect_nhwc(gdy, "dy");
+    auto dx = at::empty_like(x);
+    if (conv_dgrad_classes(gdy, krsc_view(w), stride, pad, H, W, dx, wds, f32(sums), groups, &bn)) return {dx, true};
   }
   return {conv2d_dgrad(gdy, w, stride, pad, H, W, residual, wds), false};
 }

@@ -121,7 +121,8 @@ struct DlConvGeom {
 // stats (optional): BatchNorm statistics of the stored output as in dl_gemm8 EPI 4 (stat_rows a
 // multiple of 128 dividing M; -1 otherwise)
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                int oh0, int ow0, long ldo, hipStream_t st, float* stats = nullptr, long stat_rows = 0);
+                int oh0, int ow0, long ldo, hipStream_t st, float* stats = nullptr, long stat_rows = 0,
+                const DlBnBwdEpi* bn = nullptr);  // bn (needs stats): BN-backward preparation epilogue
 // dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols)
 // ws (optional, >= dl_conv_wgrad_ws_floats floats): per-split slabs summed into a dense dw instead
 // of fp32 atomics

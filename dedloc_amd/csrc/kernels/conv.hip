@@ -130,6 +130,9 @@ struct FwdArgs {
   int tpw;  // output tiles per workgroup
   float* stats;    // optional BatchNorm statistics [M / stat_rows][2N] of the stored output
   long stat_rows;
+  DlBnBwdEpi bn;   // bnbwd: the stored output is the data gradient of a BatchNorm+ReLU's output,
+  int bnbwd;       // prepared for that BN's backward (as gemm8's EPI_BNBWD): ReLU-masked, and
+                   // `stats` receives its two column sums (sum g, sum g * xhat)
 };
 
 // Tile shapes: TM_ x TN_ = 128 x 128 (four 64 x 64 waves as 2 x 2) or 256 x 64 (4 x 1) for
@@ -269,17 +272,49 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     float csum[8], csq[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = csq[e] = 0.f;
+    // bnbwd: this thread's 8 channels of the tile's statistics group (mean / rstd, and the ReLU
+    // mask's scale / shift when it comes from the BN input X)
+    float bmu[8], brs[8], bsc[8], bsh[8];
+    if (p.bnbwd) {
+      const int ch0 = min(n0 + (tid % CPR) * 8, p.N - 8);
+      const long go = (long)(m0 / p.stat_rows) * p.N + ch0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bmu[e] = p.bn.mean[go + e];
+        brs[e] = p.bn.rstd[go + e];
+        bsc[e] = p.bn.Y ? 0.f : p.bn.gamma[ch0 + e] * brs[e];
+        bsh[e] = p.bn.Y ? 0.f : p.bn.beta[ch0 + e] - bmu[e] * bsc[e];
+      }
+    }
 #pragma unroll
     for (int u = 0; u < TM_ * CPR / NT; ++u) {
       const int idx = tid + NT * u, row = idx / CPR, c = idx % CPR;
       const int m = m0 + row, ch = n0 + c * 8;
-      const uint4 v = *reinterpret_cast<const uint4*>(stage + row * (CPR * 16) + ((c ^ (row & (CPR - 1))) << 4));
+      uint4 v = *reinterpret_cast<const uint4*>(stage + row * (CPR * 16) + ((c ^ (row & (CPR - 1))) << 4));
       if (m < p.M && ch < p.N) {
         const int n = m / IJ, r = m - n * IJ;
         const int i = r / g.J, j = r - i * g.J;
-        bf16_t* orow = p.out + ((long)(n * p.OH + i * p.osh + p.oh0) * p.OW + j * p.osw + p.ow0) * p.ldo;
-        *reinterpret_cast<uint4*>(orow + ch) = v;
-        if (p.stats) {
+        const long pix = (long)(n * p.OH + i * p.osh + p.oh0) * p.OW + j * p.osw + p.ow0;
+        bf16_t* orow = p.out + pix * p.ldo;
+        if (p.bnbwd) {  // g = dY masked by the BN's ReLU; the BN backward's two sums
+          float f[8], xv[8], yv[8];
+          unpack8_bf16(v, f);
+          load_bf16<8>(p.bn.X + pix * p.bn.ldx + ch, xv);
+          if (p.bn.Y) load_bf16<8>(p.bn.Y + pix * p.bn.ldx + ch, yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bool live = p.bn.Y ? yv[e] > 0.f : fmaf(xv[e], bsc[e], bsh[e]) > 0.f;
+            const float gg = live ? f[e] : 0.f;  // f is bf16 already: the masked store is exact
+            f[e] = gg;
+            csum[e] += gg;
+            csq[e] = fmaf(gg, (xv[e] - bmu[e]) * brs[e], csq[e]);
+          }
+          v = pack8_bf16(f);
+          *reinterpret_cast<uint4*>(orow + ch) = v;
+        } else {
+          *reinterpret_cast<uint4*>(orow + ch) = v;
+        }
+        if (p.stats && !p.bnbwd) {
           float f[8];
           unpack8_bf16(v, f);
 #pragma unroll
@@ -549,8 +584,9 @@ void set_lds(Kern k) {
 }  // namespace
 
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows) {
+                int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows, const DlBnBwdEpi* bn) {
   if (g.C % BK || N % 4 || ldw % 8 || ldo % 4 || g.I < 0 || g.J < 0) return -1;
+  if (bn && (!stats || !bn->X || bn->ldx % 8 || (!bn->Y && (!bn->gamma || !bn->beta)))) return -1;
   const long M = (long)g.Nimg * g.I * g.J;
   // statistics: every 128-row tile inside one group, whole 8-channel chunks
   if (stats && (stat_rows < BM || stat_rows % BM || M % stat_rows || N % 8)) return -1;
@@ -569,7 +605,7 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
   // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
   const int tpw = std::max(1, tiles / 1024);
   FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C,
-            (unsigned)img_bytes, (unsigned)w_bytes, tpw, stats, stat_rows};
+            (unsigned)img_bytes, (unsigned)w_bytes, tpw, stats, stat_rows, bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0};
   const int lds = 2 * (TMv + TNv) * 128;
   static bool attr = false;
   if (!attr) {

@@ -45,6 +45,7 @@
 //              (y = Y[m,n] > 0, or x*gamma*rstd + beta - mean*gamma*rstd > 0 from the BN input X),
 //              stored; stats[grp][n] += g, stats[grp][N + n] += g * (X[m,n] - mean) * rstd — the
 //              BN backward's two column sums, so it skips its statistics pass over dY and X
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -170,7 +171,22 @@ struct Args {
   int nt;                        // non-temporal output stores (bf16 epilogues)
   float* stats; long stat_rows;  // EPI_STATS: [M / stat_rows][2N] column sums / sums of squares
   DlBnBwdEpi bn;                 // EPI_BNBWD operands (BN input, ReLU mask source, mean / rstd)
+  int group_m;                   // tile order: column-major inside bands of group_m row blocks
 };
+
+// Tile (m0, n0) of linear tile index bid.  group_m = 1: row-major (all column tiles of one row
+// block, then the next).  group_m = G: bands of G row blocks walked column by column, so the 32
+// consecutive tiles one XCD runs at a time cover ~G row blocks x 32/G column blocks instead of
+// ~2.7 x 12 (QKV): fewer distinct operand panels per L2 (e.g. 6 MiB instead of 7.3 for QKV's
+// 3072-column weight, which does not fit one XCD's 4 MiB L2).
+__device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int G, int& m0, int& n0) {
+  const int band = G * tiles_n;
+  const int first = (bid / band) * G;
+  const int gsz = min(tiles_m - first, G);
+  const int r = bid % band;
+  m0 = (first + r % gsz) * BM;
+  n0 = (r / gsz) * BN;
+}
 
 #define DL_MFMA_QUAD(QM, QN)                                                          \
   do {                                                                                \
@@ -198,7 +214,8 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   const int tiles = tiles_m * tiles_n;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);  // grid = tiles * splits
   const int split = lid / tiles, bid = lid % tiles;
-  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  int m0, n0;
+  tile_of(bid, tiles_m, tiles_n, p.group_m, m0, n0);
   const int kbase = split * p.K;
   const int nk = p.K / BK;
 
@@ -585,7 +602,8 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
     asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
     const int rch = lane & 7, rr = lane >> 3;
     const int bid = xcd_remap(tix, total);
-    const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+    int m0, n0;
+    tile_of(bid, tiles_m, tiles_n, p.group_m, m0, n0);
 #define DL_STAGEP(T, KSLOT)                                                                         \
   do {                                                                                              \
     uint8_t* slot_ = smem + ((T) & 1) * BUF + (KSLOT) * HALF;                                       \
@@ -865,8 +883,13 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
   // DEDLOC_GEMM8_NT=0 for A/B runs
   const char* nte = std::getenv("DEDLOC_GEMM8_NT");
   const int nt = nte ? std::atoi(nte) : 1;
+  // tile order (tile_of): DEDLOC_GEMM8_GROUP row blocks per band.  Default 4: against row-major
+  // (1) at T = 262144 the QKV forward 1507 -> 1468 us, FFN-up + GELU 2409 -> 2324 us, FFN-down data
+  // gradient 2027 -> 1970 us, the rest within +-1.5% (profiles/r3_gemm8_tile_order_T262144.jsonl)
+  const char* ge = std::getenv("DEDLOC_GEMM8_GROUP");
+  const int group_m = ge ? std::max(1, std::atoi(ge)) : 4;
   Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt,
-         stats, stat_rows, DlBnBwdEpi{}};
+         stats, stat_rows, DlBnBwdEpi{}, group_m};
   if (epi == EPI_BNBWD) a.bn = *bn;  // by value: the kernel reads it from its argument buffer
 #define DL_GEMM8_CASE(AK, BK_, E) \
   if (a_kouter == AK && b_kouter == BK_ && epi == E) return launch8<AK, BK_, E>(a, splits, st);

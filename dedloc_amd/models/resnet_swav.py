@@ -36,6 +36,11 @@ _RES_LINK = os.environ.get("DEDLOC_RES_LINK", "1") != "0"
 # BatchNorm+ReLU backward statistics accumulated in the consuming 1x1 conv's data-gradient epilogue
 # (DEDLOC_BN_BWD_EPI=0: the BN backward's own statistics pass)
 _BN_BWD_EPI = os.environ.get("DEDLOC_BN_BWD_EPI", "1") != "0"
+# the same for bn1 in the 3x3 conv2's data gradient (conv.hip epilogue, DEDLOC_BN_BWD_EPI_3X3=1).
+# Off by default: same-box A/B of the b=64 iteration 2142 / 2095 samples/s on vs 2136 / 2139 off
+# (profiles/r3_swav_bn_bwd_epi_3x3_ab.log) — the epilogue's extra X reads and statistics reduction
+# cost what the 32 removed statistics passes saved
+_BN_BWD_EPI_3X3 = os.environ.get("DEDLOC_BN_BWD_EPI_3X3", "0") == "1"
 
 
 class _GradLink:
@@ -51,7 +56,8 @@ class _GradLink:
 
 
 class _BnBwdLink:
-    """Hands a BatchNorm+ReLU's backward preparation to the 1x1 conv that consumes its output.
+    """Hands a BatchNorm+ReLU's backward preparation to the conv that consumes its output (1x1: the
+    GEMM epilogues; 3x3 / strided: conv.hip's data-gradient epilogue).
 
     The BN forward records what its backward needs (its input, mean / rstd, gamma / beta, the
     pass workspace's backward sums); the consumer conv's backward then computes its data gradient
@@ -357,9 +363,10 @@ class Bottleneck(nn.Module):
         else:
             conv, bn = self.downsample[0], self.downsample[1]
             idt = bn(conv(x, bn))
-        out = self.bn1(self.conv1(x, self.bn1, link, in_link if link is not None else None))
+        l1 = _BnBwdLink() if fused_bwd and _BN_BWD_EPI_3X3 else None
+        out = self.bn1(self.conv1(x, self.bn1, link, in_link if link is not None else None), bwd_link=l1)
         l2 = _BnBwdLink() if fused_bwd else None
-        out = self.bn2(self.conv2(out, self.bn2), bwd_link=l2)
+        out = self.bn2(self.conv2(out, self.bn2, bn_link=l1), bwd_link=l2)
         l3 = _BnBwdLink() if fused_bwd else None
         y = self.bn3(self.conv3(out, self.bn3, bn_link=l2), idt, link, bwd_link=l3)
         if l3 is not None:

@@ -14,7 +14,7 @@ import torch
 pytestmark = pytest.mark.multiproc
 
 
-def _peer(rank, world, dht_ep, out_q, cfg, mode="", compression="NONE"):
+def _peer(rank, world, dht_ep, out_q, cfg, mode="", compression="NONE", barrier=None):
     torch.set_num_threads(1)
     import logging
 
@@ -54,6 +54,8 @@ def _peer(rank, world, dht_ep, out_q, cfg, mode="", compression="NONE"):
     if late:
         time.sleep(2.0)  # late joiner: must download state
     peer = AlbertPeer(targs, dargs, cargs, dev, rank=rank, auxiliary=aux)
+    if barrier is not None:  # both peers in the DHT before either trains (spawn start-up skew under
+        barrier.wait(timeout=120)  # load let one peer finish its steps alone)
     res = {"rank": rank}
     try:
         if aux:
@@ -107,7 +109,8 @@ def _run(world, tmp_path, mode="", expect=None, compression="NONE"):
     cfg = _tiny_cfg(tmp_path)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_peer, args=(r, world, root.endpoint, q, cfg, mode, compression))
+    bar = ctx.Barrier(world) if world == 2 and mode == "" else None
+    procs = [ctx.Process(target=_peer, args=(r, world, root.endpoint, q, cfg, mode, compression, bar))
              for r in range(world)]
     for p in procs:
         p.start()

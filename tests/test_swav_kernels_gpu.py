@@ -155,34 +155,37 @@ def test_conv_dgrad_residual_epilogue(cuda, cin, cout):
     torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("cin,cout,ymask,res", [(64, 256, False, False),    # bn2 -> conv3 (gemm_small, N=64)
-                                                 (256, 1024, False, False),  # bn2 -> conv3 (gemm8, N=256)
-                                                 (256, 64, True, True),      # bn3 -> next conv1 (gemm8, N=256)
-                                                 (64, 64, False, False)])    # 3x3: not fused -> prep pass
-def test_conv_dgrad_bn_matches_reference(cuda, cin, cout, ymask, res):
+@pytest.mark.parametrize("cin,cout,k,stride,N,ymask,res,expect_fused", [
+    (64, 256, 1, 1, 4, False, False, True),    # bn2 -> conv3 (1x1 on conv.hip / gemm_small, N=64)
+    (256, 1024, 1, 1, 4, False, False, True),  # bn2 -> conv3 (gemm8, N=256)
+    (256, 64, 1, 1, 4, True, True, True),      # bn3 -> next conv1 (gemm8, N=256)
+    (64, 64, 3, 1, 4, False, False, True),     # bn1 -> conv2 3x3 (conv.hip epilogue, 256x64 tiles)
+    (128, 128, 3, 2, 8, False, False, True),   # bn1 -> strided conv2: four parity classes, one workspace
+    (64, 64, 3, 2, 4, False, False, False)])   # class rows per group 128: not fused -> prep pass
+def test_conv_dgrad_bn_matches_reference(cuda, cin, cout, k, stride, N, ymask, res, expect_fused):
     """conv2d_dgrad_bn (BN+ReLU backward preparation in the data-gradient epilogue; where it reports
     not fused, the plain gradient followed by the separate bn_bwd_prep pass) against the op's fp32
     CPU reference: the ReLU-masked gradient and the two backward sums."""
     torch.manual_seed(7)
     CLF = torch.channels_last
-    G, N, H = 2, 4, 16
-    k = 3 if (cin, cout) == (64, 64) else 1
+    G, H = 2, 16
+    P = H // stride
     x = (torch.randn(N, cin, H, H, device=cuda) + 0.3).bfloat16().contiguous(memory_format=CLF)
     y = torch.relu(torch.randn(N, cin, H, H, device=cuda)).bfloat16().contiguous(memory_format=CLF) if ymask else None
     w = (torch.randn(cout, cin, k, k, device=cuda) / (cin * k * k) ** 0.5).bfloat16().contiguous(memory_format=CLF)
-    dy = torch.randn(N, cout, H, H, device=cuda).bfloat16().contiguous(memory_format=CLF)
+    dy = torch.randn(N, cout, P, P, device=cuda).bfloat16().contiguous(memory_format=CLF)
     r = torch.randn(N, cin, H, H, device=cuda).bfloat16().contiguous(memory_format=CLF) if res else None
     mean = torch.randn(G, cin, device=cuda) * 0.1 + 0.3
     rstd = torch.rand(G, cin, device=cuda) + 0.5
     gamma, beta = torch.rand(cin, device=cuda) + 0.5, torch.randn(cin, device=cuda) * 0.1
     sums = torch.zeros(G * 2 * cin, device=cuda)
-    g, fused = torch.ops.dedloc.conv2d_dgrad_bn(dy, w, 1, k // 2, H, H, r, x, y, mean, rstd, gamma, beta, sums, G)
-    assert fused == (cout != cin or k == 1) or not fused
+    g, fused = torch.ops.dedloc.conv2d_dgrad_bn(dy, w, stride, k // 2, H, H, r, x, y, mean, rstd, gamma, beta, sums, G)
+    assert fused == expect_fused
     if not fused:
         g = torch.ops.dedloc.bn_bwd_prep(g, x, y, mean, rstd, gamma, beta, sums, G)
     cpu = lambda t: None if t is None else t.cpu()  # noqa: E731
     sums_ref = torch.zeros(G * 2 * cin)
-    g_ref, _ = torch.ops.dedloc.conv2d_dgrad_bn(dy.cpu(), w.cpu(), 1, k // 2, H, H, cpu(r), x.cpu(), cpu(y),
+    g_ref, _ = torch.ops.dedloc.conv2d_dgrad_bn(dy.cpu(), w.cpu(), stride, k // 2, H, H, cpu(r), x.cpu(), cpu(y),
                                                 mean.cpu(), rstd.cpu(), gamma.cpu(), beta.cpu(), sums_ref, G)
     torch.testing.assert_close(g.float().cpu(), g_ref.float(), rtol=2e-2, atol=3e-2)
     torch.testing.assert_close(sums.cpu(), sums_ref, rtol=2e-2, atol=2.0)
