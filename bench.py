@@ -203,6 +203,13 @@ def main():
     if world > 1:
         dist.barrier()
     base = co.local_step
+    first_s = None
+    if args.warmup > 0:  # the first micro-step alone: lazy start-up (module loads, allocations) cost
+        sync()
+        t_first = time.perf_counter()
+        peer.train_step()
+        sync()
+        first_s = time.perf_counter() - t_first
     run_until(base + args.warmup)
     sync()
     if world > 1:
@@ -232,6 +239,7 @@ def main():
         out = dict(describe(value, world), n_gpus=world, steps=args.steps, warmup=args.warmup,
                    ms_per_step=round(max_dt / args.steps * 1e3, 2))
         out.update({
+               "first_microstep_s": None if first_s is None else round(first_s, 3),
                "ema_samples_per_s_sum": round(ema_sum, 2), "averaging_rounds": co.stats["averaging_rounds"],
                "averaging_failed": co.stats["averaging_failed"],
                # timed-region breakdown, mean over peers: host seconds per global step in the state

@@ -90,6 +90,7 @@ class _BNAct(torch.autograd.Function):
                                                 groups, None if ws is None else ws[0], stats_ready)
         ctx.save_for_backward(x, y, mean, rstd, gamma, beta)
         ctx.relu, ctx.has_res, ctx.ws, ctx.module = relu, res is not None, ws, module
+        ctx.gslot = getattr(module, "_gslot", None)  # a concurrent second pass's gradient buffers
         ctx.link = link if res is not None else None
         ctx.bwd_link = None
         if bwd_link is not None and relu and ws is not None:
@@ -103,6 +104,8 @@ class _BNAct(torch.autograd.Function):
         x, y, mean, rstd, gamma, beta = ctx.saved_tensors
         m = ctx.module
         gw, gb = (m.weight.grad, m.bias.grad) if m is not None else (None, None)
+        if ctx.gslot is not None:  # a concurrent trunk pass: its own gradient buffer (SwAVModel)
+            gw, gb = ctx.gslot
         acc = (m is not None and m.inplace_grad and gw is not None and gb is not None
                and gw.dtype == torch.float32 and gb.dtype == torch.float32)
         # the consuming conv's epilogue prepared dy (ReLU-masked) and the backward sums (_BnBwdLink)
@@ -147,6 +150,7 @@ class _ConvNHWC(torch.autograd.Function):
         ctx.save_for_backward(x if cols is None else cols, wb)
         ctx.stride, ctx.pad, ctx.module = stride, pad, module
         ctx.has_cols, ctx.xshape, ctx.link, ctx.bn_link = cols is not None, tuple(x.shape), link, bn_link
+        ctx.gslot = getattr(module, "_gslot", None)  # a concurrent second pass's weight-gradient buffer
         if stats is not None:  # the consuming BatchNorm's statistics, accumulated by the conv's epilogue
             return torch.ops.dedloc.conv2d_fwd_stats(x, wb, stride, pad, stats, groups, cols)
         return torch.ops.dedloc.conv2d_fwd(x, wb, stride, pad, cols)
@@ -176,7 +180,7 @@ class _ConvNHWC(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             weight = ctx.module.weight
-            g = weight.grad
+            g = weight.grad if ctx.gslot is None else ctx.gslot
             if (g is not None and ctx.module.inplace_wgrad and g.dtype == torch.float32
                     and g.permute(0, 2, 3, 1).is_contiguous()):
                 torch.ops.dedloc.conv2d_wgrad(dy, x, g, ctx.stride, ctx.pad, cols)  # in place, no AccumulateGrad
@@ -216,6 +220,7 @@ class ConvNHWC(nn.Conv2d):
 
     _wb_cache = None    # bf16 weight shared across the trunk passes of one model forward
     _wb_share = False   # set by SwAVModel.forward for the duration of that forward
+    _gslot = None       # weight-gradient target of a concurrent second trunk pass (SwAVModel)
     # False: return the weight gradient through autograd instead of adding it into the bound .grad
     # (HIP-graph capture via make_graphed_callables needs every parameter to receive an autograd grad)
     inplace_wgrad = True
@@ -254,6 +259,8 @@ class BNAct(nn.BatchNorm2d):
     # False: return dgamma / dbeta through autograd (HIP-graph capture needs an autograd grad for
     # every parameter); True: accumulate into the bound fp32 .grad buffers in the kernel
     inplace_grad = True
+    _gslot = None        # (dgamma, dbeta) targets of a concurrent second trunk pass (SwAVModel)
+    _rs_override = None  # (running_mean, running_var) stand-ins of that pass (deferred update)
 
     def __init__(self, num_features, relu: bool = False, fused: bool = True):
         super().__init__(num_features)
@@ -278,7 +285,8 @@ class BNAct(nn.BatchNorm2d):
                 self.num_batches_tracked.add_(G)
             ws, self.pass_ws = self.pass_ws, None
             ready, self.stats_ready = self.stats_ready and ws is not None, False
-            return _BNAct.apply(x, self.weight, self.bias, res, self.running_mean, self.running_var, self.relu,
+            rm, rv = self._rs_override or (self.running_mean, self.running_var)
+            return _BNAct.apply(x, self.weight, self.bias, res, rm, rv, self.relu,
                                 self.eps, self.momentum, G, ws, self, ready, link, bwd_link)
         self.stats_ready = False
         if G > 1:  # reference semantics without the fused kernel: one BN call per crop chunk
@@ -409,25 +417,34 @@ class ResNet50Trunk(nn.Module):
         layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
-    def _prepare_bn_pass(self, x):
-        """One zeroed workspace for every BatchNorm's forward and backward statistics sums of this
-        pass, and one multi-tensor add for their num_batches_tracked counters (instead of two
-        memsets and one add launch per BatchNorm; each is a ~5 us kernel at b=64)."""
+    def alloc_bn_pass(self, x):
+        """One zeroed workspace for every BatchNorm's forward and backward statistics sums of the
+        pass over ``x`` (with the BatchNorms' current stat_groups), and one multi-tensor add for their
+        num_batches_tracked counters (instead of two memsets and one add launch per BatchNorm; each
+        is a ~5 us kernel at b=64).  Returns the per-BatchNorm workspace slices for ``forward``'s
+        ``prepared`` (None: the per-call path)."""
         if (not self.pass_workspace or not self.training or self.checkpoint_stages or not x.is_cuda
                 or x.dtype != torch.bfloat16 or not x.is_contiguous(memory_format=torch.channels_last)):
-            for m in self._bn_modules():
-                m.count_deferred, m.pass_ws = False, None
-            return
+            return None
         bns = self._bn_modules()
         G = bns[0].stat_groups
         sizes = [2 * G * m.num_features for m in bns]
         ws = torch.zeros(2 * sum(sizes), dtype=torch.float32, device=x.device)
-        off = 0
-        for m, n in zip(bns, sizes):
-            m.pass_ws = (ws[off:off + n], ws[off + n:off + 2 * n])
-            m.count_deferred = True
+        out, off = [], 0
+        for n in sizes:
+            out.append((ws[off:off + n], ws[off + n:off + 2 * n]))
             off += 2 * n
         torch._foreach_add_([m.num_batches_tracked for m in bns], G)
+        return out
+
+    def _prepare_bn_pass(self, x, prepared=None):
+        if prepared is None:
+            prepared = self.alloc_bn_pass(x)
+        for i, m in enumerate(self._bn_modules()):
+            if prepared is None:
+                m.count_deferred, m.pass_ws = False, None
+            else:
+                m.count_deferred, m.pass_ws = True, prepared[i]
 
     def _bn_modules(self):
         bns = getattr(self, "_bns", None)
@@ -435,8 +452,10 @@ class ResNet50Trunk(nn.Module):
             bns = self._bns = [m for m in self.modules() if isinstance(m, BNAct)]
         return bns
 
-    def forward(self, x):
-        self._prepare_bn_pass(x)
+    def forward(self, x, prepared=None):
+        """``prepared``: this pass's BatchNorm workspaces from ``alloc_bn_pass`` (allocated ahead,
+        e.g. on another stream); None allocates them here."""
+        self._prepare_bn_pass(x, prepared)
         x = self.maxpool(self.bn1(self.conv1(x, self.bn1)))
         for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
             if self.checkpoint_stages and self.training and x.requires_grad:
@@ -565,12 +584,107 @@ class SwAVModel(nn.Module):
         if conv_impl not in (None, "hip", "auto"):  # "auto": round-2 configs (it chose MIOpen per shape)
             raise ValueError(f"conv backend must be 'hip' (the hand-written kernels), got {conv_impl!r}")
 
+    # Two concurrent trunk passes (set by a trainer that calls ``after_backward`` after every
+    # backward): the resolution groups (2x224 and 6x96 crops) are independent through the trunk, and
+    # at b=64 many of their kernels leave most of the chip idle, so the second pass runs on a side
+    # stream (forward and, through autograd's per-op streams, backward).  What the passes share is
+    # made race-free: the bf16 weights and the data-gradient weights are prepared before the fork;
+    # both passes' BatchNorm workspaces and counters are allocated ahead on this stream; the second
+    # pass writes its weight / BN-parameter gradients into a buffer of its own (added into the flat
+    # gradient by after_backward) and its running-statistics updates into zeroed stand-ins (merged
+    # after the join: the update is affine, rm <- (1-m)^G rm + D, so the crop order is kept).
+    concurrent_passes = False
+
     def bind_flat(self, flat):
         """Take the GEMM / conv weights of every forward from ``flat``'s bf16 mirror: one cast
         kernel over the whole flat buffer per iteration instead of one per conv and linear layer."""
         self._flat = flat if getattr(flat, "bf16", None) is not None else None
         self._wb_names = [(m, f"{n}.weight") for n, m in self.named_modules()
                           if isinstance(m, (ConvNHWC, HeadLinear))]
+        self._conc = None
+
+    def _conc_state(self):
+        c = getattr(self, "_conc", None)
+        if c is None:
+            flat = self._flat
+            gb = torch.zeros_like(flat.grad)
+            slots = []
+            for n, m in self.trunk.named_modules():
+                if isinstance(m, ConvNHWC):
+                    slots.append((m, flat.view(gb, f"trunk.{n}.weight")))
+                elif isinstance(m, BNAct):
+                    slots.append((m, (flat.view(gb, f"trunk.{n}.weight"), flat.view(gb, f"trunk.{n}.bias"))))
+            bns = self.trunk._bn_modules()
+            rs = torch.zeros(2 * sum(m.num_features for m in bns), dtype=torch.float32, device=gb.device)
+            views, off = [], 0
+            for m in bns:
+                C = m.num_features
+                views.append((rs[off:off + C], rs[off + C:off + 2 * C]))
+                off += 2 * C
+            c = self._conc = {"grad_b": gb, "slots": slots, "rs": rs, "rs_views": views,
+                              "stream": torch.cuda.Stream(gb.device), "pending": False}
+        return c
+
+    def _concurrent_ok(self, groups) -> bool:
+        x = groups[0][0]
+        return (self.concurrent_passes and len(groups) == 2 and self._flat is not None and x.is_cuda
+                and self.training and torch.is_grad_enabled() and ResNet50Trunk.pass_workspace
+                and not self.trunk.checkpoint_stages and BNAct.inplace_grad and ConvNHWC.inplace_wgrad
+                and all(m.momentum is not None for m in self.trunk._bn_modules())
+                and all(g.is_contiguous(memory_format=torch.channels_last) and g.dtype == torch.bfloat16
+                        for g, _ in groups))
+
+    def _trunk_concurrent(self, groups):
+        c = self._conc_state()
+        cur, side = torch.cuda.current_stream(), c["stream"]
+        convs = [m for m in self.trunk.modules() if isinstance(m, ConvNHWC)]
+        for m in convs:  # shared by both passes' backward: made here, before the fork
+            _dgrad_weights(m, m._wb_cache, m.stride[0], m.padding[0])
+        (xa, ga), (xb, gb) = groups
+        self.set_bn_stat_groups(ga)
+        prep_a = self.trunk.alloc_bn_pass(xa)
+        self.set_bn_stat_groups(gb)
+        prep_b = self.trunk.alloc_bn_pass(xb)
+        side.wait_stream(cur)
+        self.set_bn_stat_groups(ga)
+        fa = self.trunk(xa, prep_a)
+        bns = self.trunk._bn_modules()
+        self.set_bn_stat_groups(gb)
+        for m, g in c["slots"]:
+            m._gslot = g
+        for m, r in zip(bns, c["rs_views"]):
+            m._rs_override = r
+        try:
+            with torch.cuda.stream(side):
+                fb = self.trunk(xb, prep_b)
+        finally:
+            for m, _ in c["slots"]:
+                m._gslot = None
+            for m in bns:
+                m._rs_override = None
+        cur.wait_stream(side)
+        fb.record_stream(cur)
+        with torch.no_grad():  # the second pass's running-statistics updates, in crop order
+            torch._foreach_mul_([m.running_mean for m in bns], [(1.0 - m.momentum) ** gb for m in bns])
+            torch._foreach_add_([m.running_mean for m in bns], [v[0] for v in c["rs_views"]])
+            torch._foreach_mul_([m.running_var for m in bns], [(1.0 - m.momentum) ** gb for m in bns])
+            torch._foreach_add_([m.running_var for m in bns], [v[1] for v in c["rs_views"]])
+            c["rs"].zero_()
+        c["pending"] = True
+        return [fa, fb]
+
+    def after_backward(self):
+        """Add the concurrent second pass's gradients into the flat gradient (after every backward
+        of a forward that ran the passes concurrently; a no-op otherwise)."""
+        c = getattr(self, "_conc", None)
+        if c is not None and c["pending"]:
+            # the second pass's backward ran on the side stream and ends there (its gradients are
+            # written in place, nothing flows back): join it before reading its gradients (this also
+            # joins the side stream's work into a HIP-graph capture of the backward)
+            torch.cuda.current_stream().wait_stream(c["stream"])
+            self._flat.grad.add_(c["grad_b"])
+            c["grad_b"].zero_()
+            c["pending"] = False
 
     def set_bn_stat_groups(self, g: int):
         for m in self.trunk.modules():
@@ -605,14 +719,21 @@ class SwAVModel(nn.Module):
                     m._wb_cache = None
 
     def _forward(self, crops):
-        feats, i = [], 0
+        groups, i = [], 0
         while i < len(crops):
             j = i
             while j < len(crops) and crops[j].shape[-1] == crops[i].shape[-1]:
                 j += 1
-            self.set_bn_stat_groups(j - i if self.single_pass_every_crop else 1)
-            feats.append(self.trunk(torch.cat(crops[i:j]) if j - i > 1 else crops[i]))
+            groups.append((torch.cat(crops[i:j]) if j - i > 1 else crops[i],
+                           j - i if self.single_pass_every_crop else 1))
             i = j
+        if self._concurrent_ok(groups):
+            feats = self._trunk_concurrent(groups)
+        else:
+            feats = []
+            for x, g in groups:
+                self.set_bn_stat_groups(g)
+                feats.append(self.trunk(x))
         self.set_bn_stat_groups(1)
         return self.heads[0](torch.cat(feats))
 

@@ -79,6 +79,9 @@ class SwavPeer:
                                with_bf16=self.device.type == "cuda", autograd=True,
                                channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
         self.model.bind_flat(self.flat)  # GEMM / conv weights read from the flat buffer's bf16 mirror
+        # the two crop resolutions' trunk passes on two streams (SwAVModel.concurrent_passes; this
+        # trainer calls after_backward after every backward)
+        self.model.concurrent_passes = bool(cfg.MODEL.get("CONCURRENT_PASSES", True))
         self.model.normalize_prototypes()
         larc = ocfg.larc_config
         assert ocfg.use_larc, "we can't use collab sgd without larc (sgd_collaborative.py:138)"
@@ -164,6 +167,7 @@ class SwavPeer:
             for _ in range(2):
                 emb, scores = fwd()
                 torch.autograd.backward([scores], [torch.ones_like(scores)])
+                model.after_backward()
         torch.cuda.current_stream(self.device).wait_stream(side)
         g_fwd, g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         # thread_local: the averager / DHT threads may touch the device while the trainer captures
@@ -172,6 +176,7 @@ class SwavPeer:
         seed = torch.zeros_like(scores)
         with torch.cuda.graph(g_bwd, pool=g_fwd.pool(), capture_error_mode="thread_local"):
             torch.autograd.backward([scores], [seed])
+            model.after_backward()
         with torch.no_grad():
             self.flat.grad.copy_(grads)
             for k, v in model.named_buffers():
@@ -215,6 +220,7 @@ class SwavPeer:
                 proto = self.model.heads[0].prototypes0.weight
                 loss = self.loss_fn(emb.float(), scores, proto, training_iterations=int(self.collab_opt.local_step))
                 loss.backward()
+                self.model.after_backward()
         for name, iters in self.frozen:  # FreezeParametersHook (state_update_hooks.py:235-280)
             if self.iteration < iters:
                 name = name[len("module."):] if name.startswith("module.") else name

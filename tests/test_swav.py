@@ -594,3 +594,49 @@ def test_trunk_bn_pass_workspace_and_inplace_grads(cuda, monkeypatch):
     assert rel(b1, b0) < max(3 * rel(ba, b0), 1e-4), (rel(b1, b0), rel(ba, b0))
     n_tracked = [b for n, b in ResNet50Trunk().named_buffers() if n.endswith("num_batches_tracked")]
     assert len(n_tracked) == 53 and b1[-1].item() == 8.0  # 2 + 6 statistics groups counted
+
+
+@pytest.mark.gpu
+def test_concurrent_trunk_passes_match_sequential(cuda):
+    """SwAVModel.concurrent_passes (the two crop resolutions' trunk passes on two streams, the second
+    pass's parameter gradients in a buffer of its own added by after_backward, its running-statistics
+    updates merged after the join) gives the sequential path's gradients, running statistics and
+    counters.  The sequential path run twice gives the run-to-run spread (fp32 atomics in the BN
+    statistics) the comparison allows for."""
+    from dedloc_amd.models.resnet_swav import SwAVModel
+    from dedloc_amd.utils.flat import FlatParams
+
+    CLF = torch.channels_last
+
+    def run(concurrent):
+        torch.manual_seed(0)
+        model = SwAVModel(num_prototypes=100).to(cuda).to(memory_format=CLF).train()
+        flat = FlatParams(model.named_parameters(), device=cuda, with_bf16=True, autograd=True, channels_last=True)
+        model.bind_flat(flat)
+        model.concurrent_passes = concurrent
+        g = torch.Generator(device="cpu").manual_seed(1)
+        for _ in range(2):  # two iterations: the stand-ins / second-pass gradients are re-zeroed
+            crops = [torch.randn(8, 3, 64, 64, generator=g).to(cuda).bfloat16().contiguous(memory_format=CLF)
+                     for _ in range(2)]
+            crops += [torch.randn(8, 3, 32, 32, generator=g).to(cuda).bfloat16().contiguous(memory_format=CLF)
+                      for _ in range(4)]
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                emb, scores = model(crops)
+            (scores.float().pow(2).mean() + emb.float().pow(2).mean()).backward()
+            model.after_backward()
+        torch.cuda.synchronize()
+        ran = getattr(model, "_conc", None) is not None
+        bufs = torch.cat([b.float().flatten() for _, b in model.named_buffers()])
+        return flat.grad.clone(), bufs, ran
+
+    g0, b0, r0 = run(False)
+    ga, ba, _ = run(False)
+    g1, b1, r1 = run(True)
+    assert not r0 and r1
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+
+    assert torch.isfinite(g1).all()
+    assert rel(g1, g0) < max(3 * rel(ga, g0), 2e-3), (rel(g1, g0), rel(ga, g0))
+    assert rel(b1, b0) < max(3 * rel(ba, b0), 1e-4), (rel(b1, b0), rel(ba, b0))
