@@ -57,8 +57,28 @@ def main():
         cur.wait_stream(s1)
         cur.wait_stream(s2)
 
+    streams = [torch.cuda.Stream() for _ in range(4)]
+
+    def multi(parts):  # parts: [(x, groups)] each on its own stream
+        def run():
+            cur = torch.cuda.current_stream()
+            for st in streams[:len(parts)]:
+                st.wait_stream(cur)
+            for st, (x, g) in zip(streams, parts):
+                m.set_bn_stat_groups(g)
+                with torch.cuda.stream(st):
+                    m.trunk(x)
+            for st in streams[:len(parts)]:
+                cur.wait_stream(st)
+        return run
+
+    x224a, x224b = x224[:64].contiguous(memory_format=cl), x224[64:].contiguous(memory_format=cl)
+    x96a, x96b = x96[:192].contiguous(memory_format=cl), x96[192:].contiguous(memory_format=cl)
     with torch.no_grad():
-        res = {"p224_ms": timeit(p224), "p96_ms": timeit(p96), "seq_ms": timeit(seq), "two_streams_ms": timeit(conc)}
+        res = {"p224_ms": timeit(p224), "p96_ms": timeit(p96), "seq_ms": timeit(seq), "two_streams_ms": timeit(conc),
+               "three_224split_ms": timeit(multi([(x224a, 1), (x224b, 1), (x96, 6)])),
+               "three_96split_ms": timeit(multi([(x224, 2), (x96a, 3), (x96b, 3)])),
+               "four_ms": timeit(multi([(x224a, 1), (x224b, 1), (x96a, 3), (x96b, 3)]))}
     print(json.dumps({k: round(v, 3) for k, v in res.items()}), flush=True)
 
 
