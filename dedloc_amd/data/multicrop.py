@@ -160,3 +160,40 @@ class SyntheticMultiCropStream:
     def next_batch(self) -> List[torch.Tensor]:
         idx = torch.randint(0, self.pool.shape[0], (self.batch_size,), generator=self.gen)
         return self.augment(self.pool, idx, self.gen, self.out_dtype)
+
+
+class StreamPrefetcher:
+    """Overlaps batch generation with training: while the caller's stream computes on batch i,
+    batch i+1 is produced on a side stream (the reference's DataLoader workers prepare batches
+    ahead on the CPU; here the augmentation kernels run ahead on the GPU).  ``next_batch`` makes the
+    caller's stream wait for the batch it returns and records that stream on its tensors, so the
+    caching allocator never hands their memory to the side stream while the caller still reads it."""
+
+    def __init__(self, source, device):
+        self.source = source
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._next = None
+
+    def _launch(self):
+        with torch.cuda.stream(self.stream):
+            batch = self.source.next_batch()
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self._next = (batch, ev)
+
+    def next_batch(self) -> List[torch.Tensor]:
+        if self.stream is None:
+            return self.source.next_batch()
+        if self._next is None:
+            self._launch()
+        batch, ev = self._next
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(ev)
+        for t in batch:
+            t.record_stream(cur)
+        self._launch()  # the following batch, under this iteration's compute
+        return batch
+
+    def __getattr__(self, name):  # pool, batch_size, augment, ... of the wrapped stream
+        return getattr(self.source, name)

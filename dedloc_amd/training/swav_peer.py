@@ -26,7 +26,7 @@ from typing import Optional
 
 import torch
 
-from ..data.multicrop import MultiCropAugment, SyntheticMultiCropStream
+from ..data.multicrop import MultiCropAugment, StreamPrefetcher, SyntheticMultiCropStream
 from ..dht import DHT, get_dht_time
 from ..metrics import LocalMetrics, make_validators
 from ..models.resnet_swav import SwAVModel
@@ -127,6 +127,8 @@ class SwavPeer:
                                              pool_size=int(dcfg.get("SYNTHETIC_POOL_SIZE", 1024)),
                                              image_size=int(dcfg.get("SYNTHETIC_IMAGE_SIZE", 256)), augment=aug,
                                              out_dtype=torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        if self.device.type == "cuda" and bool(dcfg.get("PREFETCH", True)):
+            self.data = StreamPrefetcher(self.data, self.device)  # next batch's crops under this step's compute
         self.frozen = [(name, int(iters)) for name, iters in (mcfg.get("TEMP_FROZEN_PARAMS_ITER_MAP") or [])]
         self.use_graph = bool(mcfg.get("CUDA_GRAPH", False)) and self.device.type == "cuda" and \
             not bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING)
