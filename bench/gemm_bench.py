@@ -34,7 +34,10 @@ VARIANTS = {"gemm8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "0"},
             "g8g2": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "2"},
             "g8g4": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "4"},
             "g8g8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "8"},
-            "g8g16": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "16"}}
+            "g8g16": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "16"},
+            # B0 fragments kept in registers for phase 3 (default) vs read again from LDS
+            "g8kb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "1"},
+            "g8rb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "0"}}
 
 
 def timeit(fn, iters=10):
@@ -48,7 +51,7 @@ def timeit(fn, iters=10):
 
 
 def set_policy(pol):
-    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT", "DEDLOC_GEMM8_GROUP"):
+    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT", "DEDLOC_GEMM8_GROUP", "DEDLOC_GEMM8_KEEPB0"):
         os.environ.pop(k, None)
     os.environ.update(pol)
 

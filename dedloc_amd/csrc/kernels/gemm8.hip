@@ -188,18 +188,22 @@ __device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int G
   n0 = (r / gsz) * BN;
 }
 
-#define DL_MFMA_QUAD(QM, QN)                                                          \
+#define DL_MFMA_QUAD_B(QM, QN, BF)                                                    \
   do {                                                                                \
     __builtin_amdgcn_s_setprio(1);                                                    \
     _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                  \
       _Pragma("unroll") for (int mi = 0; mi < 4; ++mi)                                \
         _Pragma("unroll") for (int ni = 0; ni < 2; ++ni)                              \
           acc[QM][QN][mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(              \
-              af[mi][ks], bfr[ni][ks], acc[QM][QN][mi][ni], 0, 0, 0);                 \
+              af[mi][ks], BF[ni][ks], acc[QM][QN][mi][ni], 0, 0, 0);                  \
     __builtin_amdgcn_s_setprio(0);                                                    \
   } while (0)
+#define DL_MFMA_QUAD(QM, QN) DL_MFMA_QUAD_B(QM, QN, bfr)
 
-template <bool AKO, bool BKO, int EPI>
+// KEEPB0: the B0 fragments read in phase 0 stay in registers for phase 3 (16 more VGPRs) instead of
+// being read again — 24 instead of 28 KiB of LDS reads per wave and K-tile, and phase 3 issues no
+// LDS reads at all
+template <bool AKO, bool BKO, int EPI, bool KEEPB0>
 __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   const int lane = threadIdx.x & 63;
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   if (wm == 1) __builtin_amdgcn_s_barrier();
   const int ra = wm * 64;  // this wave's rows inside an A half-tile image
   const int cb = wn * 32;  // this wave's columns inside a B half-tile image
-  bf16x8 af[4][2], bfr[2][2];
+  bf16x8 af[4][2], bfr[2][2], bf0[2][2];
   for (int t = 0; t < nk; ++t) {
     const uint8_t* buf = smem + (t & 1) * BUF;
     const uint8_t* iA0 = buf;
@@ -278,7 +282,10 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+      for (int ni = 0; ni < 2; ++ni) {
+        if constexpr (KEEPB0) bf0[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+        else bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+      }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -286,7 +293,8 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA0, ra + mi * 16, ks, lane);
     if (more1) DL_STAGE(t + 1, 2);
     __builtin_amdgcn_s_barrier();
-    DL_MFMA_QUAD(0, 0);
+    if constexpr (KEEPB0) DL_MFMA_QUAD_B(0, 0, bf0);
+    else DL_MFMA_QUAD(0, 0);
     __builtin_amdgcn_s_barrier();
 
     // ---- phase 1: quadrant (0,1); prefetch B0 of tile t+1
@@ -310,10 +318,12 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     __builtin_amdgcn_s_barrier();
 
     // ---- phase 3: quadrant (1,0); prefetch B1 of tile t+2; retire tile t+1
+    if constexpr (!KEEPB0) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+    }
     if (more2) {
       DL_STAGE(t + 2, 1);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -321,7 +331,8 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
-    DL_MFMA_QUAD(1, 0);
+    if constexpr (KEEPB0) DL_MFMA_QUAD_B(1, 0, bf0);
+    else DL_MFMA_QUAD(1, 0);
     __builtin_amdgcn_s_barrier();
   }
 #undef DL_STAGE
@@ -827,6 +838,12 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
 }
 
 #undef DL_MFMA_QUAD
+#undef DL_MFMA_QUAD_B
+
+bool keep_b0() {  // read per call (A/B in one process); DEDLOC_GEMM8_KEEPB0=0: re-read B0 in phase 3
+  const char* e = std::getenv("DEDLOC_GEMM8_KEEPB0");
+  return !(e && e[0] == '0');
+}
 
 int persistent_ctas() {  // read per call: tests and benchmarks A/B the two forms in one process
   const char* e = std::getenv("DEDLOC_GEMM8_PERSIST");
@@ -845,7 +862,8 @@ int launch8(const Args& a, int splits, hipStream_t st) {
       return 0;
     }
   }
-  gemm8_kernel<AKO, BKO, EPI><<<dim3(tiles * splits), NT, 0, st>>>(a);
+  if (keep_b0()) gemm8_kernel<AKO, BKO, EPI, true><<<dim3(tiles * splits), NT, 0, st>>>(a);
+  else gemm8_kernel<AKO, BKO, EPI, false><<<dim3(tiles * splits), NT, 0, st>>>(a);
   return 0;
 }
 
