@@ -37,7 +37,10 @@ VARIANTS = {"gemm8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "0"},
             "g8g16": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "16"},
             # B0 fragments kept in registers for phase 3 (default) vs read again from LDS
             "g8kb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "1"},
-            "g8rb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "0"}}
+            "g8rb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "0"},
+            # per-lane DMA source bases computed once + peeled K-loop tail
+            "g8pre": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_PRESRC": "1"},
+            "g8nopre": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_PRESRC": "0"}}
 
 
 def timeit(fn, iters=10):
@@ -51,7 +54,8 @@ def timeit(fn, iters=10):
 
 
 def set_policy(pol):
-    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT", "DEDLOC_GEMM8_GROUP", "DEDLOC_GEMM8_KEEPB0"):
+    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT", "DEDLOC_GEMM8_GROUP", "DEDLOC_GEMM8_KEEPB0",
+              "DEDLOC_GEMM8_PRESRC"):
         os.environ.pop(k, None)
     os.environ.update(pol)
 

@@ -124,6 +124,33 @@ __device__ __forceinline__ void stage_half(const bf16_t* __restrict__ g, long ld
   }
 }
 
+// The per-lane global source of both LDS-DMA pieces of a half-tile at k0 = 0 (stage_half's address
+// math, done once per workgroup): a K-tile's stage is then base + k offset — two 64-bit adds
+// instead of ~12 VALU address instructions per piece in the K loop
+template <bool KO, bool ISB>
+__device__ __forceinline__ void src_base(const bf16_t* __restrict__ g, long ld, int r0, int rows_valid, int half,
+                                         int w, int lane, const bf16_t* (&base)[2]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int region = j * 8 + w;
+    if constexpr (!KO) {
+      const int lrow = region * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ kin_swz(lrow);
+      const int grow = min(r0 + half_to_tile<ISB>(lrow, half), rows_valid - 1);
+      base[j] = g + (long)grow * ld + c * 8;
+    } else {
+      const int k = region * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ kout_swz(k);
+      base[j] = g + (long)k * ld + r0 + colperm<ISB>(half_to_tile<ISB>(c * 8, half));
+    }
+  }
+}
+
+__device__ __forceinline__ void stage_pre(const bf16_t* const (&base)[2], long koff, uint8_t* slot, int w) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) dma16(base[j] + koff, slot + (j * 8 + w) * 1024);
+}
+
 // MFMA operand fragment: 16 rows (r0..) x 32 k (k-step ks) of a half-tile image; lane l holds
 // (row r0 + (l & 15), k = 32 ks + 8 (l >> 4) + j), j = 0..7.
 template <bool KO>
@@ -203,7 +230,8 @@ __device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int G
 // KEEPB0: the B0 fragments read in phase 0 stay in registers for phase 3 (16 more VGPRs) instead of
 // being read again — 24 instead of 28 KiB of LDS reads per wave and K-tile, and phase 3 issues no
 // LDS reads at all
-template <bool AKO, bool BKO, int EPI, bool KEEPB0>
+// PRESRC: DMA source addresses from per-lane bases computed once (src_base / stage_pre)
+template <bool AKO, bool BKO, int EPI, bool KEEPB0, bool PRESRC>
 __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   const int lane = threadIdx.x & 63;
@@ -233,15 +261,33 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
         for (int d = 0; d < 2; ++d) acc[a][b][c][d] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  const bf16_t* bA0[2];
+  const bf16_t* bA1[2];
+  const bf16_t* bB0[2];
+  const bf16_t* bB1[2];
+  if constexpr (PRESRC) {
+    src_base<AKO, false>(p.A, p.lda, m0, p.M, 0, w, lane, bA0);
+    src_base<AKO, false>(p.A, p.lda, m0, p.M, 1, w, lane, bA1);
+    src_base<BKO, true>(p.B, p.ldb, n0, p.N, 0, w, lane, bB0);
+    src_base<BKO, true>(p.B, p.ldb, n0, p.N, 1, w, lane, bB1);
+  }
   // half-tile h = 4 t + k of the stream: k = 0 A0, 1 B1, 2 A1, 3 B0 -> slot k of buffer t & 1
 #define DL_STAGE(T, KSLOT)                                                                          \
   do {                                                                                              \
     uint8_t* slot_ = smem + ((T) & 1) * BUF + (KSLOT) * HALF;                                       \
     const int k0_ = kbase + (T) * BK;                                                               \
-    if ((KSLOT) == 0) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 0, slot_, w, lane);          \
-    else if ((KSLOT) == 1) stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 1, slot_, w, lane);      \
-    else if ((KSLOT) == 2) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 1, slot_, w, lane);     \
-    else stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 0, slot_, w, lane);                        \
+    if constexpr (PRESRC) {                                                                         \
+      const long ka_ = AKO ? (long)k0_ * p.lda : (long)k0_, kb_ = BKO ? (long)k0_ * p.ldb : (long)k0_; \
+      if ((KSLOT) == 0) stage_pre(bA0, ka_, slot_, w);                                              \
+      else if ((KSLOT) == 1) stage_pre(bB1, kb_, slot_, w);                                         \
+      else if ((KSLOT) == 2) stage_pre(bA1, ka_, slot_, w);                                         \
+      else stage_pre(bB0, kb_, slot_, w);                                                           \
+    } else {                                                                                        \
+      if ((KSLOT) == 0) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 0, slot_, w, lane);        \
+      else if ((KSLOT) == 1) stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 1, slot_, w, lane);    \
+      else if ((KSLOT) == 2) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 1, slot_, w, lane);   \
+      else stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 0, slot_, w, lane);                      \
+    }                                                                                               \
   } while (0)
 
 #ifdef GEMM8_PROBE_DESYNC  // measurement build only: offset the first wave of workgroups in time
@@ -270,13 +316,86 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   const int ra = wm * 64;  // this wave's rows inside an A half-tile image
   const int cb = wn * 32;  // this wave's columns inside a B half-tile image
   bf16x8 af[4][2], bfr[2][2], bf0[2][2];
-  for (int t = 0; t < nk; ++t) {
+  // One K-tile; M1 / M2: K-tiles t+1 / t+2 exist (prefetch them).  PRESRC peels the last two K-tiles
+  // so the steady-state loop carries no prefetch conditions (no scalar compare/branch pairs around
+  // the DMAs); otherwise the flags are run-time.
+  auto ktile = [&](int t, auto m1, auto m2) {
+    constexpr bool M1 = decltype(m1)::value, M2 = decltype(m2)::value;
     const uint8_t* buf = smem + (t & 1) * BUF;
     const uint8_t* iA0 = buf;
     const uint8_t* iB1 = buf + HALF;
     const uint8_t* iA1 = buf + 2 * HALF;
     const uint8_t* iB0 = buf + 3 * HALF;
-    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+
+    // ---- phase 0: quadrant (0,0); prefetch A1 of tile t+1
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        if constexpr (KEEPB0) bf0[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+        else bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA0, ra + mi * 16, ks, lane);
+    if constexpr (M1) DL_STAGE(t + 1, 2);
+    __builtin_amdgcn_s_barrier();
+    if constexpr (KEEPB0) DL_MFMA_QUAD_B(0, 0, bf0);
+    else DL_MFMA_QUAD(0, 0);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 1: quadrant (0,1); prefetch B0 of tile t+1
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB1, cb + ni * 16, ks, lane);
+    if constexpr (M1) DL_STAGE(t + 1, 3);
+    __builtin_amdgcn_s_barrier();
+    DL_MFMA_QUAD(0, 1);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 2: quadrant (1,1); prefetch A0 of tile t+2
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA1, ra + mi * 16, ks, lane);
+    if constexpr (M2) DL_STAGE(t + 2, 0);
+    __builtin_amdgcn_s_barrier();
+    DL_MFMA_QUAD(1, 1);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 3: quadrant (1,0); prefetch B1 of tile t+2; retire tile t+1
+    if constexpr (!KEEPB0) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
+    }
+    if constexpr (M2) {
+      DL_STAGE(t + 2, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if constexpr (KEEPB0) DL_MFMA_QUAD_B(1, 0, bf0);
+    else DL_MFMA_QUAD(1, 0);
+    __builtin_amdgcn_s_barrier();
+    };
+  if constexpr (PRESRC) {
+    for (int t = 0; t < nk - 2; ++t) ktile(t, std::true_type{}, std::true_type{});
+    if (nk >= 2) ktile(nk - 2, std::true_type{}, std::false_type{});
+    ktile(nk - 1, std::false_type{}, std::false_type{});
+  } else {
+    for (int t = 0; t < nk; ++t) {
+      const uint8_t* buf = smem + (t & 1) * BUF;
+      const uint8_t* iA0 = buf;
+      const uint8_t* iB1 = buf + HALF;
+      const uint8_t* iA1 = buf + 2 * HALF;
+      const uint8_t* iB0 = buf + 3 * HALF;
+      const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
 
     // ---- phase 0: quadrant (0,0); prefetch A1 of tile t+1
 #pragma unroll
@@ -334,6 +453,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     if constexpr (KEEPB0) DL_MFMA_QUAD_B(1, 0, bf0);
     else DL_MFMA_QUAD(1, 0);
     __builtin_amdgcn_s_barrier();
+      }
   }
 #undef DL_STAGE
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: every wave passes the same barriers
@@ -845,6 +965,15 @@ bool keep_b0() {  // read per call (A/B in one process); DEDLOC_GEMM8_KEEPB0=0: 
   return !(e && e[0] == '0');
 }
 
+// read per call; DEDLOC_GEMM8_PRESRC=0: the per-K-tile source address math and run-time prefetch
+// conditions.  Default on: at T = 262144 the weight gradients run 5-7% and the forward / data-gradient
+// forms 1-3% faster, the B=512 micro-step 924.3 / 926.1 -> 946.6 / 944.7 samples/s same box
+// (profiles/r3_gemm8_presrc_*); the bias+GELU form measured 2% slower and keeps the old loop
+bool pre_src() {
+  const char* e = std::getenv("DEDLOC_GEMM8_PRESRC");
+  return !(e && e[0] == '0');
+}
+
 int persistent_ctas() {  // read per call: tests and benchmarks A/B the two forms in one process
   const char* e = std::getenv("DEDLOC_GEMM8_PERSIST");
   return e ? std::atoi(e) : 0;
@@ -862,8 +991,10 @@ int launch8(const Args& a, int splits, hipStream_t st) {
       return 0;
     }
   }
-  if (keep_b0()) gemm8_kernel<AKO, BKO, EPI, true><<<dim3(tiles * splits), NT, 0, st>>>(a);
-  else gemm8_kernel<AKO, BKO, EPI, false><<<dim3(tiles * splits), NT, 0, st>>>(a);
+  const dim3 grid(tiles * splits);
+  if (!keep_b0()) gemm8_kernel<AKO, BKO, EPI, false, false><<<grid, NT, 0, st>>>(a);
+  else if (EPI != EPI_GELU && pre_src()) gemm8_kernel<AKO, BKO, EPI, true, true><<<grid, NT, 0, st>>>(a);
+  else gemm8_kernel<AKO, BKO, EPI, true, false><<<grid, NT, 0, st>>>(a);
   return 0;
 }
 

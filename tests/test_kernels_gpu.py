@@ -627,7 +627,8 @@ def test_gemm8_pipeline_depths(cuda, force_mfma, M, N, K):
         assert rel(g, 0.5 + dy.float().t() @ a.float()) < 1e-5
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 512, 192), (2048, 768, 1024), (512, 256, 4096)])
+@pytest.mark.parametrize("M,N,K", [(300, 512, 64), (300, 512, 128), (300, 512, 192), (2048, 768, 1024),
+                                   (512, 256, 4096)])
 def test_gemm8_kept_b0_fragments_bitwise(cuda, monkeypatch, M, N, K):
     """gemm8 with the phase-0 B fragments kept in registers for phase 3 (DEDLOC_GEMM8_KEEPB0, the
     default) is the same computation as re-reading them: bitwise equal outputs for the forward
@@ -637,15 +638,18 @@ def test_gemm8_kept_b0_fragments_bitwise(cuda, monkeypatch, M, N, K):
     w = (torch.rand(N, K, device=cuda) * 2 - 1).bfloat16()
     dy = (torch.rand(M, N, device=cuda) * 2 - 1).bfloat16()
     outs = {}
-    for keep in ("1", "0"):
+    for keep, pre in (("1", "1"), ("1", "0"), ("0", "0")):  # + the precomputed-source, peeled-tail loop
         monkeypatch.setenv("DEDLOC_GEMM8_KEEPB0", keep)
+        monkeypatch.setenv("DEDLOC_GEMM8_PRESRC", pre)
         g = torch.zeros(N, K, device=cuda)
         if M % 256 == 0:
             OPS.gemm_acc_f32(dy, a, g, True, False)
-        outs[keep] = (OPS.gemm(a, w, None, None, False, True, 0), OPS.gemm(dy, w, None, None, False, False, 0), g)
-    for x, y in zip(outs["1"], outs["0"]):
-        assert torch.equal(x, y)
-    assert rel(outs["1"][0], a.float() @ w.float().t()) < 8e-3
+        outs[keep + pre] = (OPS.gemm(a, w, None, None, False, True, 0), OPS.gemm(dy, w, None, None, False, False, 0),
+                            g)
+    for v in ("10", "11"):
+        for x, y in zip(outs[v], outs["00"]):
+            assert torch.equal(x, y), v
+    assert rel(outs["11"][0], a.float() @ w.float().t()) < 8e-3
 
 
 def test_gemm_register_staged_backend(cuda, monkeypatch):
