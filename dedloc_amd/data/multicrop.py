@@ -196,4 +196,6 @@ class StreamPrefetcher:
         return batch
 
     def __getattr__(self, name):  # pool, batch_size, augment, ... of the wrapped stream
+        if name == "source":  # not set yet (copy / unpickle): no recursion through __getattr__
+            raise AttributeError(name)
         return getattr(self.source, name)
