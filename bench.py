@@ -12,8 +12,16 @@ A bench "step" = ONE collaborative (global) optimizer step = 4096 samples summed
 The total work per step is fixed as N grows, so scaling is "strong".
 
     python bench.py                         # 1 GPU
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+    python bench.py --gpus 8                # 8 peers, one per GPU: this script starts them itself
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8   # same, launched by torchrun
     python bench.py --model swav            # BASELINE config 3 (collaborative SwAV ResNet-50), same contract
+
+Peers are independent processes, one per GPU, as in the reference's fleet (each AWS worker runs its
+own run_trainer, albert/AWS_runner.ipynb:293-297).  Without a launcher (no WORLD_SIZE in the
+environment) ``--gpus N`` makes this script start the N peer processes itself, before it touches
+the GPU, each with RANK / LOCAL_RANK / WORLD_SIZE set the way torchrun sets them (peer i on GPU i).
+Two peers on one device are refused unless ``--allow_shared_device`` is given; the JSON line then
+reports ``physical_gpus`` (distinct devices actually used) next to ``n_gpus`` (peers).
 """
 from __future__ import annotations
 
@@ -21,6 +29,9 @@ import argparse
 import json
 import logging
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -70,8 +81,59 @@ def parse():
     ap.add_argument("--throttle", type=float, default=0.0,
                     help="emulation only: idle seconds added after every micro-step (with --cpu_test, stands in "
                          "for GPU compute time when studying the collaboration protocol's overheads)")
+    ap.add_argument("--allow_shared_device", action="store_true",
+                    help="let several peers share one GPU (protocol emulation on a small box); the JSON line "
+                         "reports physical_gpus < n_gpus.  Without it, more peers than visible GPUs is an error")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(args) -> int:
+    """Start ``args.gpus`` peer processes (this script again, with torchrun's environment: RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT) and wait for them; rank 0 prints the JSON line.
+    Called before anything initialises the GPU (``device_count`` does not), and the children are
+    started as subprocesses, never by exec."""
+    n = args.gpus
+    if not args.cpu_test:
+        visible = torch.cuda.device_count()
+        if n > visible and not args.allow_shared_device:
+            print(f"bench.py: --gpus {n} needs {n} GPUs but {visible} are visible; one peer per GPU is the "
+                  f"measured configuration (pass --allow_shared_device to emulate {n} peers on "
+                  f"{max(visible, 1)} device(s))", file=sys.stderr)
+            return 2
+    env = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), start_new_session=True))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    print(f"bench.py: peer process {p.pid} exited with {code}; stopping the others", file=sys.stderr)
+                    for q in pending:
+                        os.killpg(q.pid, signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
 
 
 def _protocol_breakdown(gathered, keys):
@@ -166,8 +228,28 @@ def _harness_world(cpu: bool):
     return rank, world, dev
 
 
+def _device_id(dev: torch.device) -> str:
+    if dev.type != "cuda":
+        return "cpu"
+    props = torch.cuda.get_device_properties(dev)
+    uuid = getattr(props, "uuid", None)
+    return str(uuid) if uuid is not None else f"{props.name}:{dev.index}"
+
+
+def _physical_devices(dev, world: int):
+    """Distinct devices used by the peers (gathered over the harness group)."""
+    ids = [None] * world
+    if world > 1:
+        dist.all_gather_object(ids, _device_id(dev))
+    else:
+        ids = [_device_id(dev)]
+    return ids
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_self_launch(args))
     logging.basicConfig(level=logging.INFO if args.verbose else logging.WARNING,
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     rank, world, dev = _harness_world(cpu=bool(args.cpu_test))
@@ -177,6 +259,15 @@ def main():
             torch.cuda.synchronize()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev_ids = _physical_devices(dev, world)
+    physical = len({d for d in dev_ids if d != "cpu"})
+    if dev.type == "cuda" and physical < world and not args.allow_shared_device:
+        if rank == 0:
+            print(f"bench.py: {world} peers on {physical} GPU(s): two peers would share a device; pass "
+                  f"--allow_shared_device to emulate that", file=sys.stderr)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(2)
     from dedloc_amd.dht import DHT
 
     # control plane: rank 0 hosts the DHT root, everyone else bootstraps from it
@@ -239,6 +330,8 @@ def main():
         out = dict(describe(value, world), n_gpus=world, steps=args.steps, warmup=args.warmup,
                    ms_per_step=round(max_dt / args.steps * 1e3, 2))
         out.update({
+               "physical_gpus": physical, "peers": world,
+               "data_plane": (co.last_group or {}).get("backend"),
                "first_microstep_s": None if first_s is None else round(first_s, 3),
                "ema_samples_per_s_sum": round(ema_sum, 2), "averaging_rounds": co.stats["averaging_rounds"],
                "averaging_failed": co.stats["averaging_failed"],

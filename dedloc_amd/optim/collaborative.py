@@ -106,6 +106,7 @@ class CollaborativeOptimizer:
         self.local_step = 0
         self.performance_ema = PerformanceEMA(alpha=performance_ema_alpha)
         self.last_step_time = None
+        self._pending_finite = []  # (host flag, event, batch size, local step) of recent micro-steps
         self.last_group: Optional[Dict] = None
         self.stats = {"global_steps": 0, "averaging_rounds": 0, "averaging_failed": 0, "state_loads": 0,
                       # where a global step's time goes (host clock, seconds, summed over steps): the
@@ -211,8 +212,41 @@ class CollaborativeOptimizer:
     def zero_grad(self, *args, **kwargs):
         self.opt.zero_grad()
 
-    def step(self, batch_size: Optional[int] = None, **kwargs):
-        """Accumulate this step's gradients; run a global step when the collaboration is ready."""
+    def _track_finite(self, finite: torch.Tensor, batch_size: int):
+        """Remember a micro-step's device-side finite flag (1 = finite).  The reference's GradScaler
+        skips ``step()`` for a non-finite step, so its samples never count toward the global batch;
+        here the gradient is already zeroed on the device, and once the flag has reached the host the
+        step's samples and its micro-step are taken back out of the local counts (``_resolve_finite``)
+        — without a per-step host sync."""
+        if not finite.is_cuda:
+            self._pending_finite.append((finite.reshape(-1)[:1].clone(), None, batch_size, self.local_step))
+            return
+        host = torch.empty(1, dtype=finite.dtype, pin_memory=True)
+        host.copy_(finite.reshape(-1)[:1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending_finite.append((host, ev, batch_size, self.local_step))
+
+    def _resolve_finite(self, block: bool):
+        while self._pending_finite:
+            host, ev, bs, step = self._pending_finite[0]
+            if ev is not None:
+                if block:
+                    ev.synchronize()
+                elif not ev.query():
+                    return
+            self._pending_finite.pop(0)
+            if float(host[0]) == 0.0 and step == self.local_step:
+                with self.lock_local_progress:
+                    self.local_samples_accumulated = max(0, self.local_samples_accumulated - bs)
+                    self.local_steps_accumulated = max(0, self.local_steps_accumulated - 1)
+                    self.stats["nonfinite_steps"] = self.stats.get("nonfinite_steps", 0) + 1
+
+    def step(self, batch_size: Optional[int] = None, finite: Optional[torch.Tensor] = None, **kwargs):
+        """Accumulate this step's gradients; run a global step when the collaboration is ready.
+
+        ``finite``: the micro-step's device-side finite flag; a step whose flag reads 0 (its gradient
+        was zeroed by the caller) does not count toward the global batch (``_track_finite``)."""
         if self.batch_size_per_step is None:
             if batch_size is None:
                 raise ValueError("specify batch_size_per_step or pass batch_size")
@@ -233,12 +267,16 @@ class CollaborativeOptimizer:
             self.local_steps_accumulated += 1
             self.performance_ema.update(num_processed=batch_size)
             self.should_report_progress.set()
+        if finite is not None:
+            self._track_finite(finite, batch_size)
+        self._resolve_finite(block=False)
 
         if self._param_round is not None and not self._param_round.is_alive():
             self._finish_param_round()
         if not (self.collaboration_state.ready_for_step or self._ready_exact()
                 or self._ready_within_slack(batch_size)):
             return None
+        self._resolve_finite(block=True)  # the global step's weight counts finite samples only
 
         logger.log(self.status_loglevel, f"beginning global optimizer step #{self.collaboration_state.optimizer_step}")
         self._finish_param_round()

@@ -181,6 +181,7 @@ class AlbertPeer:
                 loss = out["loss"] / ga if ga > 1 else out["loss"]
                 loss.backward()
             self._loss_sum += loss.detach()
+        finite = None
         if self.impl == "eager":
             if a.max_grad_norm:
                 torch.nn.utils.clip_grad_norm_(self.model.module.parameters(), a.max_grad_norm)
@@ -188,8 +189,9 @@ class AlbertPeer:
             torch.ops.dedloc.grad_norm_clip(self._flat.grad, float(a.max_grad_norm or 0.0), self._clip_part,
                                             self._clip_out)
             self._drop_if_nonfinite()
+            finite = self._clip_out[1:2]
         with self.perf.phase("collab_step"):  # accumulate (+ averaging + optimizer on global steps)
-            self.collab_opt.step(batch_size=self.batch_size_per_step)
+            self.collab_opt.step(batch_size=self.batch_size_per_step, finite=finite)
         self.opt.zero_grad()
         self.mini_steps += 1
         self.hf_step += 1

@@ -56,6 +56,46 @@ def test_bench_multi_rank_cpu_plumbing(tmp_path, nproc):
 
 
 @pytest.mark.multiproc
+@pytest.mark.timeout(400)
+def test_bench_self_launches_peers_without_torchrun(tmp_path):
+    """`python bench.py --gpus 3` (no torchrun, no WORLD_SIZE): the script starts its three peer
+    processes itself; they find each other through the DHT, average every global step, and rank 0
+    reports 3 peers."""
+    from dedloc_amd.models.albert import AlbertConfig
+
+    cfg = tmp_path / "cfg"
+    AlbertConfig.tiny(num_hidden_layers=2, max_position_embeddings=64).save_pretrained(str(cfg))
+    cmd = [sys.executable, "bench.py", "--gpus", "3", "--steps", "2", "--warmup", "1", "--cpu_test", str(cfg),
+           "--micro_batch", "2", "--seq_len", "64", "--target_batch_size", "12"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=360, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert KEYS <= set(out)
+    assert out["n_gpus"] == 3 and out["peers"] == 3 and out["physical_gpus"] == 0
+    assert out["averaging_rounds"] >= 3 and out["averaging_failed"] == 0 and out["last_group"]["size"] == 3
+    assert out["data_plane"] == "gloo"
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+def test_bench_refuses_more_peers_than_gpus():
+    """On a box with fewer GPUs than --gpus, bench.py refuses to put two peers on one device unless
+    --allow_shared_device is given (the check runs before any GPU work)."""
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--steps", "1", "--warmup", "0"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=100, env=env)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "--allow_shared_device" in r.stderr
+
+
+@pytest.mark.multiproc
 @pytest.mark.timeout(600)
 def test_bench_swav_mode_two_ranks_cpu():
     """bench.py --model swav (BASELINE config 3): two collaborative SwAV ResNet-50 peers on CPU/gloo run

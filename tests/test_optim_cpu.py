@@ -164,3 +164,39 @@ def test_lamb_weight_decay_zero_keeps_two_groups():
     by_name = {n: topt.state[p] for n, p in named_t}
     for n in flat.names:
         torch.testing.assert_close(flat.view(opt.exp_avg, n), by_name[n]["exp_avg"])
+
+
+def test_nonfinite_microstep_does_not_count_samples(tmp_path):
+    """A micro-step with non-finite gradients is dropped (its gradient zeroed on the device) and,
+    like the reference's GradScaler skipping ``step()``, its samples and micro-step do not count
+    toward the global batch: ``local_samples_accumulated`` stays unchanged."""
+    from dedloc_amd.cli.arguments import AlbertTrainingArguments, CollaborationArguments, DatasetArguments
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.models.albert import AlbertConfig
+    from dedloc_amd.training.albert_peer import AlbertPeer
+
+    cfg = tmp_path / "cfg"
+    AlbertConfig.tiny(num_hidden_layers=2, max_position_embeddings=64).save_pretrained(str(cfg))
+    root = DHT(listen_on="127.0.0.1:*")
+    peer = None
+    try:
+        targs = AlbertTrainingArguments(per_device_train_batch_size=2, gradient_accumulation_steps=1, seq_length=64, save_steps=0,
+                                        output_dir=str(tmp_path / "out"), seed=0)
+        cargs = CollaborationArguments(experiment_prefix="nan", initial_peers=[root.endpoint],
+                                       dht_listen_on="127.0.0.1:*", target_batch_size=64, listen_on="127.0.0.1:*")
+        peer = AlbertPeer(targs, DatasetArguments(config_path=str(cfg)), cargs, torch.device("cpu"))
+        co = peer.collab_opt
+        peer.train_step()
+        assert co.local_samples_accumulated == 2 and co.local_steps_accumulated == 1
+        acc = co.accumulator.clone()
+        with torch.no_grad():  # poison the parameters: the next backward yields NaN gradients
+            peer.model.flat.fp32.fill_(float("nan"))
+            peer.model.flat.refresh_bf16()
+        peer.train_step()
+        assert co.local_samples_accumulated == 2 and co.local_steps_accumulated == 1
+        assert co.stats["nonfinite_steps"] == 1
+        torch.testing.assert_close(co.accumulator, acc)  # the zeroed gradient added nothing
+    finally:
+        if peer is not None:
+            peer.shutdown()
+        root.shutdown()
