@@ -21,6 +21,12 @@ exactly zero.
 Part sizes come from the load-balancing LP; client-mode members own no part (they only send and
 receive), auxiliary members contribute no tensor (weight 0) but reduce a part.
 
+Weights travel on the wire: each contributor sends its own fp32 weight (bit-exact, as 1-2 wire
+elements) to every reducer together with the part, and the reducer reads the weights it applies
+from what it received.  Only ``spec.weights[my_index]`` has to be known when the round starts — so
+matchmaking can run ahead of the last micro-step of a global batch, before a peer knows how many
+samples it will have contributed (``DecentralizedAverager.prejoin``).
+
 Timeouts: completion is polled on the host against a deadline; on expiry the communicator is
 aborted (``ncclCommAbort`` for RCCL) so the operations still posted on it can never be matched by a
 later round, and the round raises ``AllreduceException``; the caller drops the communicator from its
@@ -74,7 +80,7 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
 
     ``sources``: pack these instead of ``tensors`` (same shapes) and add the averaging deltas to
     ``tensors`` — delayed parameter averaging packs a snapshot and collects the delta in a zeroed
-    buffer while the live parameters keep training.  Returns the group's total weight."""
+    buffer while the live parameters keep training."""
     ops = torch.ops.dedloc
     wire = WIRE_DTYPES[compression]
     dev = tensors[0].device
@@ -88,11 +94,13 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
     my_lo, my_hi = starts[me], starts[me + 1]
     P = my_hi - my_lo
     contrib_idx = [j for j in range(spec.size) if spec.contributes[j]]
-    total_w = float(sum(spec.weights[j] for j in contrib_idx))
-    if total_w <= 0:
-        raise AllreduceException("group has no contributing weight")
+    if not contrib_idx:
+        raise AllreduceException("group has no contributing member")
     deadline = time.monotonic() + timeout if timeout else None
     i_contribute = spec.contributes[me]
+    # this contributor's weight as wire elements (the fp32 bits: 1 element of fp32, 2 of fp16/bf16)
+    W = 4 // torch.empty(0, dtype=wire).element_size()
+    my_w = torch.tensor([float(spec.weights[me])], dtype=torch.float32).view(wire).to(dev)
 
     # 1. pack (compressed, unweighted: the reducer applies the weights in fp32)
     send = torch.empty(V if i_contribute else 0, dtype=wire, device=dev)
@@ -103,29 +111,32 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
             o += n
     nc = len(contrib_idx)
     recv = torch.empty((max(1, nc), max(P, 1)), dtype=wire, device=dev)
+    wrecv = torch.empty((max(1, nc), W), dtype=wire, device=dev)
 
-    # 2. reduce-scatter: part j of every contributor's wire goes to member j (one grouped launch)
+    # 2. reduce-scatter: part j of every contributor's wire (and its weight) goes to member j (one
+    #    grouped launch; the two transfers of a pair are matched in order)
     sends, send_peers, recvs, recv_peers = [], [], [], []
     for slot, j in enumerate(contrib_idx):
         if j == me:
             if P:
                 recv[slot, :P].copy_(send[my_lo:my_hi])
+                wrecv[slot].copy_(my_w)
             continue
         if P:
-            recvs.append(recv[slot, :P])
-            recv_peers.append(spec.ranks[j])
+            recvs += [recv[slot, :P], wrecv[slot]]
+            recv_peers += [spec.ranks[j]] * 2
     if i_contribute:
         for j in range(spec.size):
             if j != me and spec.part_sizes[j] > 0:
-                sends.append(send[starts[j]:starts[j + 1]])
-                send_peers.append(spec.ranks[j])
+                sends += [send[starts[j]:starts[j + 1]], my_w]
+                send_peers += [spec.ranks[j]] * 2
     _p2p(comm, sends, send_peers, recvs, recv_peers, deadline, tag=1)
 
     # 3. weighted fp32 average of my part and one delta row per contributor
     deltas = None
     if P:
         parts = recv if recv.shape[1] == P else recv[:, :P].contiguous()
-        w = torch.tensor([float(spec.weights[j]) for j in contrib_idx], dtype=torch.float32, device=dev)
+        w = wrecv.view(torch.float32).reshape(-1)
         deltas = torch.empty_like(parts)
         ops.reduce_delta(parts, w, deltas)
 
@@ -153,4 +164,3 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
         for t, n in zip(tensors, sizes):
             ops.unpack(dbuf[o:o + n], t.reshape(-1), None, True)
             o += n
-    return total_w

@@ -23,13 +23,15 @@ import socket
 import struct
 import threading
 import time
+from concurrent.futures import Future
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 import msgpack
 import torch
 
 from ..dht import DHT, get_dht_time, parse_endpoint
-from ..parallel.comm import CommError, GroupCommunicators, pairwise_rccl, rccl_available, RcclGroupComm
+from ..parallel import comm as _comm
+from ..parallel.comm import CommError, GroupCommunicators, RcclGroupComm, pairwise_rccl, routable_host
 from .allreduce import GroupSpec, WIRE_DTYPES, butterfly_allreduce
 from .load_balancing import load_balance_peers
 
@@ -84,7 +86,8 @@ class StateServer:
         self.sock.bind((bind, port))
         self.sock.listen(16)
         self.port = self.sock.getsockname()[1]
-        self.endpoint = f"{'127.0.0.1' if bind == '0.0.0.0' else bind}:{self.port}"
+        # the address published through the DHT: routable from other machines
+        self.endpoint = f"{routable_host(bind)}:{self.port}"
         self.served = {"R": 0, "T": 0}
         self._stop = threading.Event()
         self.thread = threading.Thread(target=self._loop, daemon=True, name="state-server")
@@ -109,7 +112,8 @@ class StateServer:
                 if self.device.type == "cuda":
                     torch.cuda.set_device(self.device)
                 meta, tensors = self.get_state()
-                rccl = uid is not None and rccl_available(self.device) and all(t.is_cuda for t in tensors)
+                rccl = uid is not None and _comm.rccl_available(self.device) and all(t.device == self.device
+                                                                                     for t in tensors)
                 descs = [(str(t.dtype).replace("torch.", ""), list(t.shape)) for t in tensors]
                 header = msgpack.packb({"metadata": meta, "tensors": descs, "mode": "R" if rccl else "T"},
                                        use_bin_type=True)
@@ -124,17 +128,20 @@ class StateServer:
             logger.warning(f"state transfer failed: {e}")
 
     def _send_rccl(self, uid: bytes, tensors: List[torch.Tensor]):
-        ready = torch.cuda.Event()
-        ready.record()  # the snapshot copies were queued on this thread's current stream
-        stream = torch.cuda.Stream(self.device)
         deadline = time.monotonic() + self.transfer_timeout
-        with torch.cuda.stream(stream):
-            stream.wait_event(ready)
-            comm = pairwise_rccl(uid, 0, self.device, deadline)
-            try:
+        comm = pairwise_rccl(uid, 0, self.device, deadline)
+        try:
+            if self.device.type == "cuda":
+                ready = torch.cuda.Event()
+                ready.record()  # the snapshot clones were queued on this thread's current stream
+                stream = torch.cuda.Stream(self.device)
+                with torch.cuda.stream(stream):
+                    stream.wait_event(ready)
+                    comm.p2p([t.reshape(-1) for t in tensors], [1] * len(tensors), [], [], deadline)
+            else:
                 comm.p2p([t.reshape(-1) for t in tensors], [1] * len(tensors), [], [], deadline)
-            finally:
-                comm.abort()
+        finally:
+            comm.abort()
 
     def _send_tcp(self, conn, tensors: List[torch.Tensor]):
         staging, stream = None, None
@@ -187,7 +194,7 @@ def download_state(endpoint: str, timeout: float = 60.0, device: Optional[torch.
     metadata carries the transfer mode under ``_mode`` ("R" or "T")."""
     host, port = parse_endpoint(endpoint)
     device = torch.device(device) if device is not None else torch.device("cpu")
-    uid = RcclGroupComm.new_unique_id() if allow_rccl and rccl_available(device) else None
+    uid = RcclGroupComm.new_unique_id() if allow_rccl and _comm.rccl_available(device) else None
     deadline = time.monotonic() + timeout
     with socket.create_connection((host, port), timeout=timeout) as s:
         s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
@@ -235,7 +242,7 @@ class DecentralizedAverager:
             device = self.averaged_tensors[0].device if self.averaged_tensors else torch.device("cpu")
         self.device = torch.device(device)
         host = parse_endpoint(listen_on.replace("*", "0").replace("[::]", "0.0.0.0"))[0]
-        self.host = "127.0.0.1" if host in ("0.0.0.0", "") else host
+        self.host = routable_host(host)  # published for gloo rendezvous: reachable by other machines
         self.comms = GroupCommunicators(dht, prefix, self.peer_id, self.device,
                                         timeout_s=max(30.0, 2 * averaging_timeout), max_cached=max_cached_comms,
                                         host=self.host)
@@ -248,29 +255,75 @@ class DecentralizedAverager:
         self.emulate_transfer_delay = emulate_transfer_delay
 
     # ------------------------------------------------------------------ averaging
+    # An RCCL member's link in a mixed group (GPU trainers + CPU peers) for load balancing: one xGMI
+    # link, ~153 GB/s, in the Mbps unit of the reference's --bandwidth.  The CPU member's declared
+    # bandwidth stays as given, so the LP hands it a part in proportion and the GPU members stage
+    # only that share through host memory.
+    XGMI_MBPS = 1.2e6
+
+    def _info(self, weight: Optional[float], gather: Optional[Dict[str, Any]]) -> Dict:
+        bw = 0.0 if self.client_mode else (self.throughput if self.throughput is not None else 1.0)
+        info = {"bandwidth": bw, "weight": weight, "aux": self.auxiliary, "gather": gather or {}}
+        info.update(self.comms.announce())
+        return info
+
+    def _join(self, info: Dict, expected_group_size: int, key_suffix: str):
+        window = self.averaging_expiration
+        t0 = time.perf_counter()
+        ok, gid, members = self.dht.join_group(f"{self.prefix}_averaging{key_suffix}".encode(), self.peer_id, info,
+                                               self.target_group_size, self.min_group_size, expected_group_size,
+                                               window, timeout=window + 10.0)
+        return ok, gid, members, time.perf_counter() - t0
+
+    def prejoin(self, expected_group_size: int = 0, gather: Optional[Dict[str, Any]] = None,
+                key_suffix: str = "") -> Future:
+        """Start matchmaking for the next round in the background and return its future, to be passed
+        to ``step(prejoined=...)``.  The collaborative optimizer calls this when the NEXT micro-step
+        will complete the global batch (``albert/arguments.py:67-70``, batch_size_lead: "begin
+        looking for group in advance"), so the group forms while that micro-step computes.  The
+        weight is not known yet and need not be: weights travel with the data (allreduce.py)."""
+        fut: Future = Future()
+        info = self._info(None if not self.auxiliary else 0.0, gather)
+
+        def run():
+            try:
+                fut.set_result(self._join(info, expected_group_size, key_suffix))
+            except Exception as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+        threading.Thread(target=run, daemon=True, name="prejoin").start()
+        return fut
+
     def step(self, weight: float = 1.0, timeout: Optional[float] = None, expected_group_size: int = 0,
              gather: Optional[Dict[str, Any]] = None, tensors: Optional[Sequence[torch.Tensor]] = None,
-             sources: Optional[Sequence[torch.Tensor]] = None, key_suffix: str = "") -> Optional[Dict]:
+             sources: Optional[Sequence[torch.Tensor]] = None, key_suffix: str = "",
+             prejoined: Optional[Future] = None) -> Optional[Dict]:
         """Matchmake and average.  Returns {"group_id", "size", "gathered"} or None on failure.
 
         ``tensors`` overrides the averaged set for this round (e.g. gradients only), ``sources`` packs
         snapshots instead of the live tensors, ``key_suffix`` selects an independent matchmaking key
-        (so a delayed parameter round never mixes with a gradient round)."""
+        (so a delayed parameter round never mixes with a gradient round), ``prejoined`` is a
+        ``prejoin`` future whose group this round uses (a fresh matchmaking if it failed)."""
         tensors = list(tensors) if tensors is not None else self.averaged_tensors
         weight = 0.0 if self.auxiliary else float(weight)
-        bw = 0.0 if self.client_mode else (self.throughput if self.throughput is not None else 1.0)
-        info = {"bandwidth": bw, "weight": weight, "aux": self.auxiliary, "gather": gather or {}}
-        info.update(self.comms.announce())
-        window = self.averaging_expiration
-        t_join = time.perf_counter()
-        try:
-            ok, gid, members = self.dht.join_group(f"{self.prefix}_averaging{key_suffix}".encode(), self.peer_id, info,
-                                                   self.target_group_size, self.min_group_size,
-                                                   expected_group_size, window, timeout=window + 10.0)
-        except Exception as e:  # noqa: BLE001
-            logger.warning(f"matchmaking failed: {e}")
-            return None
-        t_match = time.perf_counter() - t_join
+        t_wait = time.perf_counter()
+        res = None
+        if prejoined is not None:
+            try:
+                res = prejoined.result(timeout=self.averaging_expiration + 15.0)
+                if not res[0] or len(res[2]) < self.min_group_size:
+                    res = None
+            except Exception as e:  # noqa: BLE001
+                logger.info(f"matchmaking ahead of the step failed ({e}); joining now")
+                res = None
+        if res is None:
+            try:
+                res = self._join(self._info(weight, gather), expected_group_size, key_suffix)
+            except Exception as e:  # noqa: BLE001
+                logger.warning(f"matchmaking failed: {e}")
+                return None
+        ok, gid, members, t_match_total = res
+        t_match = time.perf_counter() - t_wait  # matchmaking time this step actually waited for
         if not ok or len(members) < self.min_group_size:
             logger.info(f"averaging round failed: group of {len(members)} < {self.min_group_size}")
             return None
@@ -278,8 +331,11 @@ class DecentralizedAverager:
         pids = [bytes(m[0]) for m in members]
         my_index = pids.index(self.peer_id)
         V = sum(t.numel() for t in tensors)
-        parts = load_balance_peers(V, [i["bandwidth"] for i in infos], min_size=0)
-        if sum(i["weight"] for i in infos if not i["aux"]) <= 0:
+        bws = [i["bandwidth"] for i in infos]
+        if GroupCommunicators.group_backend(members) == "hybrid":
+            bws = [(self.XGMI_MBPS if b > 0 else 0.0) if i.get("backend") == "rccl" else b for b, i in zip(bws, infos)]
+        parts = load_balance_peers(V, bws, min_size=0)
+        if not any(not i["aux"] for i in infos):
             return None
         t0 = time.perf_counter()
         deadline = time.monotonic() + (timeout or self.averaging_timeout)
@@ -287,8 +343,8 @@ class DecentralizedAverager:
         try:
             comm, rank_of = self.comms.get(members, gid, deadline)
             spec = GroupSpec(ranks=[rank_of[p] for p in pids], part_sizes=list(parts),
-                             weights=[i["weight"] for i in infos], contributes=[not i["aux"] for i in infos],
-                             my_index=my_index)
+                             weights=[weight if k == my_index else 0.0 for k in range(len(pids))],
+                             contributes=[not i["aux"] for i in infos], my_index=my_index)
             with self.lock_averaged_tensors:
                 butterfly_allreduce(tensors, spec, self.compression, comm=comm,
                                     timeout=max(1e-3, deadline - time.monotonic()), sources=sources)
@@ -299,6 +355,7 @@ class DecentralizedAverager:
             if comm is not None:
                 self.comms.invalidate(comm)
             return None
+        bw = bws[my_index]
         if self.emulate_transfer_delay and bw > 0:  # emulate the volunteer's link (AWS_runner wondershaper caps)
             from ..emulation.heterogeneity import emulated_transfer_seconds
 
@@ -308,8 +365,9 @@ class DecentralizedAverager:
             if want > spent:
                 time.sleep(want - spent)
         self.last_group = {"group_id": gid, "size": len(members), "gathered": [i["gather"] for i in infos],
-                           "matchmaking_s": t_match, "allreduce_s": time.perf_counter() - t0, "parts": list(parts),
-                           "backend": comm.backend if comm is not None else None}
+                           "matchmaking_s": t_match, "matchmaking_total_s": t_match_total,
+                           "prejoined": prejoined is not None, "allreduce_s": time.perf_counter() - t0,
+                           "parts": list(parts), "backend": comm.backend if comm is not None else None}
         return self.last_group
 
     # ------------------------------------------------------------------ state sharing
@@ -345,7 +403,7 @@ class DecentralizedAverager:
                 continue
             donors.append((v.value.get("step", 0), v.value["endpoint"]))
         for step, ep in sorted(donors, reverse=True):
-            for rccl in ((True, False) if rccl_available(self.device) else (False,)):
+            for rccl in ((True, False) if _comm.rccl_available(self.device) else (False,)):
                 try:
                     t0 = time.perf_counter()
                     meta, tensors = download_state(ep, timeout=timeout, device=self.device, allow_rccl=rccl)

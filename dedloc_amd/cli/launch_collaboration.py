@@ -62,6 +62,8 @@ class _Proc:
         self.log_path = log_dir / (f"{name}.log" if generation == 0 else f"{name}.gen{generation}.log")
         self.f = open(self.log_path, "w")
         self.p = subprocess.Popen(cmd, stdout=self.f, stderr=subprocess.STDOUT, env=env, start_new_session=True)
+        self.started = time.time()
+        self.killed = False  # ended by the kill schedule (a scripted preemption), not by itself
 
     def alive(self):
         return self.p.poll() is None
@@ -94,6 +96,12 @@ def main(argv=None):
     ap.add_argument("--kill_schedule", default=None, help="T:slot[,T:slot...] — SIGKILL trainer `slot` at T s")
     ap.add_argument("--respawn", action="store_true", help="restart dead trainers as fresh processes")
     ap.add_argument("--respawn_delay", type=float, default=30.0)
+    ap.add_argument("--min_run_s", type=float, default=30.0,
+                    help="a trainer that exits on its own (non-zero) sooner than this after starting is a fast "
+                         "failure: its respawn delay doubles each time (capped at 10 x respawn_delay)")
+    ap.add_argument("--max_fast_failures", type=int, default=5,
+                    help="stop respawning a slot after this many consecutive fast failures (a bad config or "
+                         "import error would otherwise restart forever)")
     ap.add_argument("--log_dir", default="collab_logs")
     ap.add_argument("--sahajbert", action="store_true")
     ap.add_argument("--no_coordinator", action="store_true")
@@ -166,6 +174,7 @@ def main(argv=None):
     # 3. supervise: scripted preemptions, respawn loop, stop at duration / when all trainers finished
     kills = parse_kill_schedule(args.kill_schedule)
     respawn_at = {}
+    fast_failures, gave_up = {}, set()
     rc = 0
     try:
         while True:
@@ -176,15 +185,24 @@ def main(argv=None):
                 proc = trainers.get(slot)
                 if proc is not None and proc.alive():
                     proc.kill(signal.SIGKILL)
+                    proc.killed = True
                     event("kill", slot=slot, pid=proc.p.pid, generation=proc.generation)
             for slot, proc in trainers.items():
-                if proc.alive() or slot in respawn_at:
+                if proc.alive() or slot in respawn_at or slot in gave_up or getattr(proc, "handled", False):
                     continue
+                proc.handled = True
                 code = proc.p.returncode
                 finished = code == 0
                 if args.respawn and not finished:
-                    respawn_at[slot] = now + args.respawn_delay
-                    event("died", slot=slot, returncode=code, respawn_in=args.respawn_delay)
+                    fast = not proc.killed and time.time() - proc.started < args.min_run_s
+                    fast_failures[slot] = fast_failures.get(slot, 0) + 1 if fast else 0
+                    if fast_failures[slot] >= args.max_fast_failures:
+                        gave_up.add(slot)
+                        event("gave_up", slot=slot, returncode=code, fast_failures=fast_failures[slot])
+                        continue
+                    delay = min(args.respawn_delay * 2 ** fast_failures[slot], 10 * args.respawn_delay)
+                    respawn_at[slot] = now + delay
+                    event("died", slot=slot, returncode=code, respawn_in=delay, fast_failures=fast_failures[slot])
             for slot, t in list(respawn_at.items()):
                 if t <= now:
                     del respawn_at[slot]

@@ -79,7 +79,8 @@ class CollaborativeOptimizer:
                  auxiliary: bool = False, allow_state_sharing: bool = True, verbose: bool = False, start: bool = True,
                  compression_type: str = "FLOAT16", compression: Optional[str] = None, throughput: Optional[float] = None,
                  peer_id: Optional[bytes] = None, max_grad_norm: Optional[float] = None,
-                 delay_param_averaging: bool = False, eta_slack: float = 0.0, **averager_kwargs):
+                 delay_param_averaging: bool = False, eta_slack: float = 0.0, prejoin: bool = True,
+                 **averager_kwargs):
         self.opt, self.dht, self.prefix = opt, dht, prefix
         self.flat = opt.flat
         self.scheduler = scheduler
@@ -120,8 +121,16 @@ class CollaborativeOptimizer:
             auxiliary=auxiliary, allow_state_sharing=allow_state_sharing, metadata_expiration=metadata_expiration,
             averaging_timeout=self.averaging_timeout, **averager_kwargs)
         self.averager.get_current_state = self._get_current_state
+        self._snapshot_lock = threading.Lock()
+        self._snapshot_bufs = None
+        self._snapshot_readers = []
+        self._snapshot_ready = None
+        self._snapshot_meta = None
+        self._serve_stream = None
 
         self.eta_slack = float(eta_slack)
+        self._prejoin = None  # background matchmaking for the coming global step (_maybe_prejoin)
+        self.prejoin_enabled = prejoin
         self.delay_param_averaging = delay_param_averaging
         self._param_round: Optional[threading.Thread] = None
         self._param_round_result = None
@@ -138,6 +147,8 @@ class CollaborativeOptimizer:
         self.collaboration_state_updated = threading.Event()
         self._stop = threading.Event()
         self.collaboration_state = self.fetch_collaboration_state()
+        with self.lock_step:
+            self._take_snapshot()
         self._threads = []
         if start:
             for target, name in ((self._report_loop, "progress-reporter"), (self._update_loop, "collab-updater")):
@@ -156,11 +167,58 @@ class CollaborativeOptimizer:
         return not self._stop.is_set()
 
     # ------------------------------------------------------------------ state
+    def _take_snapshot(self):
+        """Copy the state a joiner downloads (parameters + optimizer state + step metadata) into the
+        snapshot buffers.  Called with ``lock_step`` held, at the end of every global step and state
+        load: one device copy on the trainer's stream (~200 MB for ALBERT-large, well under a
+        millisecond).  ``_get_current_state`` serves from it without taking ``lock_step``, so a peer
+        joining while this one is in the middle of an averaging round gets the last global step's
+        state at once instead of waiting for the round (which holds ``lock_step``) to finish."""
+        if not self.averager.allow_state_sharing:
+            return
+        src = [self.flat.fp32] + list(self.opt.state_tensors())
+        cuda = self.flat.fp32.is_cuda
+        with self._snapshot_lock:
+            if self._snapshot_bufs is None:
+                self._snapshot_bufs = [torch.empty_like(t) for t in src]
+            if cuda:
+                for ev in self._snapshot_readers:  # clones of the previous snapshot still in flight
+                    torch.cuda.current_stream().wait_event(ev)
+            self._snapshot_readers = []
+            for d, t in zip(self._snapshot_bufs, src):
+                d.copy_(t.detach(), non_blocking=True)
+            self._snapshot_ready = None
+            if cuda:
+                self._snapshot_ready = torch.cuda.Event()
+                self._snapshot_ready.record()
+            self._snapshot_meta = {"step": int(self.local_step), "opt_step": int(self.opt.step_count),
+                                   "lr_sched": self.scheduler.state_dict() if self.scheduler is not None else None}
+
     def _get_current_state(self):
-        with self.lock_step:
-            meta = {"step": int(self.local_step), "opt_step": int(self.opt.step_count),
-                    "lr_sched": self.scheduler.state_dict() if self.scheduler is not None else None}
-            tensors = [self.flat.fp32.detach().clone()] + [t.detach().clone() for t in self.opt.state_tensors()]
+        """The latest global step's state (``_take_snapshot``), cloned on the calling thread's own
+        stream; never waits for ``lock_step``."""
+        with self._snapshot_lock:
+            if self._snapshot_bufs is None:  # no snapshot yet (state sharing off): the live state
+                with self.lock_step:
+                    meta = {"step": int(self.local_step), "opt_step": int(self.opt.step_count),
+                            "lr_sched": self.scheduler.state_dict() if self.scheduler is not None else None}
+                    return meta, [self.flat.fp32.detach().clone()] + [t.detach().clone()
+                                                                      for t in self.opt.state_tensors()]
+            meta = dict(self._snapshot_meta)
+            if self._snapshot_ready is None:
+                return meta, [t.clone() for t in self._snapshot_bufs]
+            dev = self.flat.fp32.device
+            if self._serve_stream is None:
+                self._serve_stream = torch.cuda.Stream(dev)
+            with torch.cuda.stream(self._serve_stream):
+                self._serve_stream.wait_event(self._snapshot_ready)
+                tensors = [t.clone() for t in self._snapshot_bufs]
+                done = torch.cuda.Event()
+                done.record(self._serve_stream)
+            self._snapshot_readers.append(done)
+            # the caller continues on its own current stream (the RCCL / TCP sender): order it after
+            # the clones
+            torch.cuda.current_stream(dev).wait_event(done)
         return meta, tensors
 
     @torch.no_grad()
@@ -190,6 +248,7 @@ class CollaborativeOptimizer:
             self._reset_accumulators()
             self.update_scheduler()
             self.stats["state_loads"] += 1
+            self._take_snapshot()
             self.averager.publish_state_sharing(self.local_step)
         dl = self.averager.last_download or {}
         logger.warning(f"downloaded state from peers: step {self.local_step}, {dl.get('bytes', 0) / 2**20:.0f} MiB in "
@@ -275,6 +334,7 @@ class CollaborativeOptimizer:
             self._finish_param_round()
         if not (self.collaboration_state.ready_for_step or self._ready_exact()
                 or self._ready_within_slack(batch_size)):
+            self._maybe_prejoin(batch_size)
             return None
         self._resolve_finite(block=True)  # the global step's weight counts finite samples only
 
@@ -294,13 +354,15 @@ class CollaborativeOptimizer:
             torch.ops.dedloc.axpby(self.flat.grad, self.accumulator, 0.0, 1.0 / max(1, self.local_steps_accumulated))
             group = None
             t_avg = time.perf_counter()
-            if cs.num_peers > 1:
-                mean_samples = self.target_batch_size / cs.num_peers
+            prejoined, self._prejoin = self._prejoin, None
+            if cs.num_peers > 1 or prejoined is not None:
+                mean_samples = self.target_batch_size / max(1, cs.num_peers)
                 weight = self.local_samples_accumulated / mean_samples
                 group = self.averager.step(weight=weight, timeout=self.averaging_timeout,
                                            expected_group_size=cs.num_peers + self._num_aux(),
                                            gather={"step": int(self.local_step)},
-                                           tensors=[self.flat.grad] if self.delay_param_averaging else None)
+                                           tensors=[self.flat.grad] if self.delay_param_averaging else None,
+                                           prejoined=prejoined)
                 self.stats["averaging_rounds"] += 1
                 if group is None:
                     self.stats["averaging_failed"] += 1
@@ -322,10 +384,30 @@ class CollaborativeOptimizer:
             self.last_group = group
             self.stats["global_steps"] += 1
             self.should_report_progress.set()
+            self._take_snapshot()
         self.averager.publish_state_sharing(self.local_step)
         self.last_step_time = get_dht_time()
         logger.log(self.status_loglevel, f"optimizer step #{self.local_step} done")
         return group
+
+    def _maybe_prejoin(self, batch_size: int):
+        """Begin matchmaking now when the NEXT local step will start the global step (the
+        reference's ``batch_size_lead``: "begin looking for group in advance", albert/arguments.py:
+        67-70).  With one micro-step per global step (8 peers x 512 samples) the group then forms
+        while that micro-step computes instead of after it."""
+        if self._prejoin is not None or not self.prejoin_enabled or self.delay_param_averaging:
+            return
+        cs = self.collaboration_state
+        if cs.num_peers < 2 or cs.optimizer_step > self.local_step:
+            return
+        own_next = cs.samples_accumulated - cs.own_samples + self.local_samples_accumulated + batch_size
+        soon = own_next >= self.target_batch_size
+        sps = self.performance_ema.samples_per_second
+        if not soon and sps > 0:
+            soon = get_dht_time() + batch_size / sps * (1.0 + self.eta_slack) >= cs.eta_next_step
+        if soon:
+            self._prejoin = self.averager.prejoin(expected_group_size=cs.num_peers + self._num_aux(),
+                                                  gather={"step": int(self.local_step)})
 
     def _ready_exact(self) -> bool:
         """The collaboration's sample count with OUR part brought up to date: the fetched state counts
@@ -465,6 +547,7 @@ class CollaborativeOptimizer:
         with self.lock_step:
             ops.axpby(self.flat.fp32, self._param_delta, 1.0, 1.0)  # p += avg(snapshot) - snapshot
             self.flat.refresh_bf16()
+            self._take_snapshot()
         self.stats["param_rounds"] = self.stats.get("param_rounds", 0) + 1
 
     # ------------------------------------------------------------------ background threads

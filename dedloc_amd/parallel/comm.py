@@ -8,16 +8,22 @@ built by the members of one matchmade group, from scratch, through the control-p
 * **GPU groups: RCCL** (``csrc/comm/rccl_comm.cpp``).  The group's leader (the member with the
   smallest peer id) calls ``ncclGetUniqueId`` and publishes the 128 bytes under
   ``{prefix}_comm_{token}``; every member then runs a non-blocking ``ncclCommInitRankConfig`` and
-  the host polls readiness against the round's deadline.  Transfers are grouped
-  ``ncclSend``/``ncclRecv`` on the current HIP stream — all pairs at once, which drives every xGMI
-  link of a fully connected 8-GPU node concurrently — and a stalled round is cancelled with
-  ``ncclCommAbort``.
-* **Groups with a CPU member** (a CPU auxiliary peer, the CPU plumbing configuration): gloo.  The
-  leader hosts a ``TCPStore`` on an ephemeral port and publishes its address the same way; GPU
-  members stage their tensors through host memory for such a round.
+  polls readiness against the round's deadline.  Transfers are grouped ``ncclSend``/``ncclRecv``
+  on the caller's HIP stream — all pairs at once, which drives every xGMI link of a fully
+  connected 8-GPU node concurrently — and a stalled round is cancelled with ``ncclCommAbort``.
+* **All-CPU groups** (the CPU plumbing configuration): gloo.  The leader hosts a ``TCPStore`` on
+  an ephemeral port and publishes its address the same way.
+* **Mixed groups** (GPU trainers plus CPU auxiliary peers, the reference fleet's shape:
+  ``AWS_runner.ipynb:26-30``): ``HybridGroupComm`` — the GPU members keep RCCL among themselves and
+  only the pairs with a CPU member go over gloo (host-staged on the GPU side).  The averager's
+  load balancing gives a CPU member a part proportional to its bandwidth, so the GPU members stage
+  only that small share through host memory.
 
-**Reuse without disagreement** (ADVICE r2): a communicator is identified by a *token* — the id of
-the matchmaking round that created it — and bound to the sorted member set and backend it was
+Every RCCL call (and every gloo send/recv) runs on the process's data-plane owner thread
+(``comm_worker.CommWorker``): the classes below only build jobs and wait for them.
+
+**Reuse without disagreement**: a communicator is identified by a *token* — the id of the
+matchmaking round that created it — and bound to the sorted member set and backend it was
 created for.  Every peer announces the tokens it still holds in its matchmaking info; a round
 reuses a token only if EVERY member announced it, otherwise the members create a fresh one keyed
 by the new round's group id.  Each peer evicts (and aborts) communicators from its own bounded
@@ -31,6 +37,7 @@ from __future__ import annotations
 import datetime
 import logging
 import os
+import socket
 import threading
 import time
 from collections import OrderedDict
@@ -39,14 +46,13 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from . import comm_worker as cw
+from .comm_worker import CommError, CommWorker
+
 logger = logging.getLogger(__name__)
 
-NCCL_SUCCESS, NCCL_IN_PROGRESS = 0, 7
-_POLL_S = 1e-4
-
-
-class CommError(RuntimeError):
-    """A group operation failed or missed its deadline; the communicator has been aborted."""
+__all__ = ["CommError", "RcclGroupComm", "GlooGroupComm", "HybridGroupComm", "GroupCommunicators", "pairwise_rccl",
+           "rccl_available", "routable_host"]
 
 
 def rccl_available(device: torch.device) -> bool:
@@ -61,6 +67,10 @@ def _left(deadline: Optional[float]) -> float:
     return float("inf") if deadline is None else deadline - time.monotonic()
 
 
+def _caller_stream(device: torch.device):
+    return torch.cuda.current_stream(device) if device.type == "cuda" else None
+
+
 class RcclGroupComm:
     """One RCCL communicator (native handle) over ``nranks`` GPU peers."""
 
@@ -72,66 +82,38 @@ class RcclGroupComm:
 
     @staticmethod
     def new_unique_id() -> bytes:
-        return bytes(torch.ops.dedloc_comm.unique_id().numpy().tobytes())
+        return cw.unique_id()
 
     @classmethod
     def create(cls, uid: bytes, nranks: int, rank: int, device: torch.device, deadline: Optional[float]):
-        ops = torch.ops.dedloc_comm
-        t = torch.frombuffer(bytearray(uid), dtype=torch.uint8)
-        h = ops.comm_init(t, nranks, rank, device.index if device.index is not None else torch.cuda.current_device())
-        comm = cls(h, nranks, rank, device)
-        comm._wait_ready(deadline, "communicator bootstrap")
-        return comm
-
-    def _status(self) -> int:
-        return int(torch.ops.dedloc_comm.comm_status(self.handle))
-
-    def _fail(self, what: str, code: Optional[int] = None):
-        msg = f"RCCL {what} failed"
-        if code is not None:
-            msg += f": {torch.ops.dedloc_comm.error_string(code)} ({code})"
-        self.abort()
-        raise CommError(msg)
-
-    def _wait_ready(self, deadline: Optional[float], what: str):
-        while True:
-            st = self._status()
-            if st == NCCL_SUCCESS:
-                return
-            if st != NCCL_IN_PROGRESS:
-                self._fail(what, st)
-            if _left(deadline) <= 0:
-                self._fail(what + " (deadline)")
-            time.sleep(_POLL_S)
+        dev_index = device.index if device.index is not None else (
+            torch.cuda.current_device() if device.type == "cuda" else 0)
+        h = CommWorker.get().run(lambda: cw.init_job(uid, nranks, rank, dev_index, deadline))
+        return cls(h, nranks, rank, device)
 
     def p2p(self, sends: Sequence[torch.Tensor], send_peers: Sequence[int], recvs: Sequence[torch.Tensor],
             recv_peers: Sequence[int], deadline: Optional[float], tag: int = 0):
-        """All sends and receives as one RCCL group on the current stream; returns when they have
-        completed on the device, or aborts the communicator and raises at ``deadline``."""
+        """All sends and receives as one RCCL group on the caller's current stream (of this
+        communicator's device); returns when they have completed on the device, or aborts the
+        communicator and raises at ``deadline``."""
         if not self.alive:
             raise CommError("communicator was aborted")
-        rc = int(torch.ops.dedloc_comm.group_p2p(self.handle, list(sends), [int(p) for p in send_peers],
-                                                 list(recvs), [int(p) for p in recv_peers]))
-        if rc not in (NCCL_SUCCESS, NCCL_IN_PROGRESS):
-            self._fail("group send/recv", rc)
-        self._wait_ready(deadline, "group send/recv enqueue")
-        ev = torch.cuda.Event()
-        ev.record()
-        n = 0
-        while not ev.query():
-            n += 1
-            if n % 64 == 0:
-                st = self._status()
-                if st not in (NCCL_SUCCESS, NCCL_IN_PROGRESS):
-                    self._fail("group send/recv", st)
-            if _left(deadline) <= 0:
-                self._fail("group send/recv (deadline)")
-            time.sleep(_POLL_S)
+        stream = _caller_stream(self.device)
+        try:
+            CommWorker.get().run(lambda: cw.p2p_job(self.handle, self.device, stream, sends, send_peers, recvs,
+                                                    recv_peers, deadline))
+        except CommError:
+            self.alive = False  # the job aborted the communicator
+            raise
+
+    def p2p_job(self, sends, send_peers, recvs, recv_peers, deadline, stream):
+        """The same transfer as a job (for a caller already composing jobs: HybridGroupComm)."""
+        return cw.p2p_job(self.handle, self.device, stream, sends, send_peers, recvs, recv_peers, deadline)
 
     def abort(self):
         if self.alive:
             self.alive = False
-            torch.ops.dedloc_comm.comm_abort(self.handle)
+            CommWorker.get().run(lambda: cw.abort_job(self.handle))
 
 
 # gloo has no abort: a group whose operation timed out is parked here instead of being destroyed
@@ -140,7 +122,7 @@ _GLOO_GRAVEYARD: List[object] = []
 
 
 class GlooGroupComm:
-    """A gloo process group over ``nranks`` peers (CPU peers, or any group with one)."""
+    """A gloo process group over ``nranks`` peers (all-CPU groups, and the CPU side of mixed ones)."""
 
     backend = "gloo"
 
@@ -154,40 +136,123 @@ class GlooGroupComm:
         pg = dist.ProcessGroupGloo(store, rank, nranks, datetime.timedelta(seconds=max(1.0, timeout_s)))
         return cls(pg, nranks, rank, keep_store)
 
-    def p2p(self, sends, send_peers, recvs, recv_peers, deadline: Optional[float], tag: int = 0):
-        if not self.alive:
-            raise CommError("communicator was aborted")
+    @staticmethod
+    def stage(sends, recvs):
+        """Host copies of device tensors (synchronous on the caller's stream, after its producers)."""
         host_sends = [s.detach().cpu() if s.is_cuda else s.detach().contiguous() for s in sends]
         host_recvs = [torch.empty(r.shape, dtype=r.dtype) if r.is_cuda else r for r in recvs]
-        works = []
-        try:
-            for t, p in zip(host_recvs, recv_peers):
-                if t.numel():
-                    works.append(self.pg.recv([t], int(p), tag))
-            for t, p in zip(host_sends, send_peers):
-                if t.numel():
-                    works.append(self.pg.send([t], int(p), tag))
-            for w in works:
-                left = _left(deadline)
-                if left <= 0:
-                    raise CommError("gloo group send/recv (deadline)")
-                ok = w.wait(datetime.timedelta(seconds=min(left, 3600.0)))
-                if ok is False:
-                    raise CommError("gloo group send/recv (deadline)")
-        except CommError:
-            self.abort()
-            raise
-        except RuntimeError as e:
-            self.abort()
-            raise CommError(f"gloo group send/recv failed: {e}") from e
+        return host_sends, host_recvs
+
+    @staticmethod
+    def unstage(recvs, host_recvs):
         for r, h in zip(recvs, host_recvs):
             if r is not h:
                 r.copy_(h)
+
+    def p2p_job(self, host_sends, send_peers, host_recvs, recv_peers, deadline, tag):
+        return cw.gloo_p2p_job(self.pg, host_sends, send_peers, host_recvs, recv_peers, deadline, tag)
+
+    def p2p(self, sends, send_peers, recvs, recv_peers, deadline: Optional[float], tag: int = 0):
+        if not self.alive:
+            raise CommError("communicator was aborted")
+        host_sends, host_recvs = self.stage(sends, recvs)
+        try:
+            CommWorker.get().run(lambda: self.p2p_job(host_sends, send_peers, host_recvs, recv_peers, deadline, tag))
+        except CommError:
+            self.abort()
+            raise
+        self.unstage(recvs, host_recvs)
 
     def abort(self):
         if self.alive:
             self.alive = False
             _GLOO_GRAVEYARD.append(self.pg)
+
+
+def _both(a, b):
+    """Step two jobs until both are done (the RCCL and gloo halves of a mixed group's transfer)."""
+    done_a = done_b = False
+    err = None
+    while not (done_a and done_b):
+        for which in (0, 1):
+            if (done_a, done_b)[which]:
+                continue
+            try:
+                next(a if which == 0 else b)
+            except StopIteration:
+                if which == 0:
+                    done_a = True
+                else:
+                    done_b = True
+            except CommError as e:
+                err = err or e
+                if which == 0:
+                    done_a = True
+                else:
+                    done_b = True
+        if not (done_a and done_b):
+            yield
+    if err is not None:
+        raise err
+
+
+class HybridGroupComm:
+    """A mixed group: RCCL among its GPU members, gloo for every pair with a CPU member.
+
+    Peers are numbered like every group communicator (sorted peer ids of the whole group);
+    ``rccl_rank`` maps a member's group rank to its rank in the GPU members' RCCL communicator
+    (None for a CPU member)."""
+
+    backend = "rccl+gloo"
+
+    def __init__(self, rccl: Optional[RcclGroupComm], gloo: GlooGroupComm, rccl_rank: List[Optional[int]],
+                 rank: int, device: torch.device):
+        self.rccl, self.gloo, self.rccl_rank = rccl, gloo, rccl_rank
+        self.nranks, self.rank, self.device = len(rccl_rank), rank, device
+        self.alive = True
+
+    def _split(self, tensors, peers):
+        fast, slow = ([], []), ([], [])
+        for t, p in zip(tensors, peers):
+            if self.rccl is not None and self.rccl_rank[int(p)] is not None:
+                fast[0].append(t)
+                fast[1].append(self.rccl_rank[int(p)])
+            else:
+                slow[0].append(t)
+                slow[1].append(int(p))
+        return fast, slow
+
+    def p2p(self, sends, send_peers, recvs, recv_peers, deadline: Optional[float], tag: int = 0):
+        if not self.alive:
+            raise CommError("communicator was aborted")
+        (fs, fsp), (ss, ssp) = self._split(sends, send_peers)
+        (fr, frp), (sr, srp) = self._split(recvs, recv_peers)
+        host_sends, host_recvs = GlooGroupComm.stage(ss, sr)
+        stream = _caller_stream(self.device)
+        jobs = []
+        if fs or fr:
+            jobs.append(lambda: self.rccl.p2p_job(fs, fsp, fr, frp, deadline, stream))
+        if host_sends or host_recvs:
+            jobs.append(lambda: self.gloo.p2p_job(host_sends, ssp, host_recvs, srp, deadline, tag))
+        try:
+            if len(jobs) == 2:
+                CommWorker.get().run(lambda: _both(jobs[0](), jobs[1]()))
+            elif jobs:
+                CommWorker.get().run(jobs[0])
+        except CommError:
+            self.abort()
+            raise
+        GlooGroupComm.unstage(sr, host_recvs)
+
+    def abort(self):
+        if self.alive:
+            self.alive = False
+            if self.rccl is not None:
+                try:
+                    self.rccl.abort()
+                except Exception as e:  # noqa: BLE001
+                    logger.debug(f"abort of the RCCL half failed: {e}")
+            self.gloo.abort()
 
 
 class _Entry:
@@ -197,6 +262,26 @@ class _Entry:
         self.comm, self.key, self.members = comm, key, members
 
 
+def routable_host(listen_host: str) -> str:
+    """The address other machines can reach this peer's servers at: the listen address itself when
+    it is specific, else the host's outbound interface (no packet is sent: a UDP socket is only
+    connected to learn the route), else loopback."""
+    if listen_host not in ("", "0.0.0.0", "::", "[::]"):
+        return listen_host
+    env = os.environ.get("DEDLOC_ANNOUNCE_HOST")
+    if env:
+        return env
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+            s.connect(("10.255.255.255", 1))
+            ip = s.getsockname()[0]
+            if ip and not ip.startswith("0."):
+                return ip
+    except OSError:
+        pass
+    return "127.0.0.1"
+
+
 class GroupCommunicators:
     """Per-peer cache of group communicators, bootstrapped through the DHT (see module docstring).
 
@@ -204,6 +289,14 @@ class GroupCommunicators:
     id (the matchmaking result); it returns ``(comm, comm_rank_of)`` where ``comm_rank_of`` maps a
     member's peer id to its rank in the communicator (the rank order is the sorted peer ids, fixed
     for the communicator's lifetime, independent of each round's join order)."""
+
+    # After this many consecutive RCCL communicators failed to come up BECAUSE OF THIS PEER (its own
+    # RCCL stack reported an error: a broken install or transport on this host — not a deadline,
+    # which another member's death or preemption can cause), the peer announces gloo: every later
+    # group it joins runs over host-staged gloo.  The fallback is retried after
+    # RCCL_RETRY_AFTER_S seconds.  DEDLOC_DATA_PLANE=gloo forces gloo from the start.
+    RCCL_FALLBACK_AFTER = int(os.environ.get("DEDLOC_RCCL_FALLBACK_AFTER", "3"))
+    RCCL_RETRY_AFTER_S = 300.0
 
     def __init__(self, dht, prefix: str, peer_id: bytes, device: torch.device, timeout_s: float = 60.0,
                  max_cached: int = 8, host: str = "127.0.0.1"):
@@ -216,21 +309,18 @@ class GroupCommunicators:
         self._lock = threading.RLock()
         self.created = 0
         self.aborted = 0
-        self.rccl_create_failures = 0  # consecutive RCCL communicators that never came up
+        self.rccl_create_failures = 0  # consecutive RCCL communicators this peer could not bring up
+        self._fallback_since: Optional[float] = None
 
     # ------------------------------------------------------------------ matchmaking info
-    # After this many consecutive RCCL communicators failed to come up (a broken RCCL install or
-    # transport on this host), the peer announces gloo: every later group it joins runs over
-    # host-staged gloo — slower, but the collaboration keeps averaging instead of losing every
-    # round to the bootstrap deadline.  DEDLOC_DATA_PLANE=gloo forces that from the start.
-    RCCL_FALLBACK_AFTER = 3
-
     @property
     def backend(self) -> str:
         if os.environ.get("DEDLOC_DATA_PLANE", "").lower() == "gloo":
             return "gloo"
         if self.rccl_create_failures >= self.RCCL_FALLBACK_AFTER:
-            return "gloo"
+            if time.monotonic() - (self._fallback_since or 0.0) < self.RCCL_RETRY_AFTER_S:
+                return "gloo"
+            self.rccl_create_failures = self.RCCL_FALLBACK_AFTER - 1  # one more try
         return "rccl" if rccl_available(self.device) else "gloo"
 
     def announce(self) -> Dict:
@@ -238,11 +328,18 @@ class GroupCommunicators:
         with self._lock:
             return {"backend": self.backend, "comms": list(self._cache.keys())}
 
+    @staticmethod
+    def group_backend(members: Sequence[Tuple[bytes, Dict]]) -> str:
+        n_rccl = sum(1 for _, info in members if info.get("backend") == "rccl")
+        if n_rccl == len(members):
+            return "rccl"
+        return "hybrid" if n_rccl >= 2 else "gloo"
+
     # ------------------------------------------------------------------ communicator for a group
     def get(self, members: Sequence[Tuple[bytes, Dict]], group_id: bytes, deadline: Optional[float] = None):
         pids = sorted(bytes(pid) for pid, _ in members)
         assert self.peer_id in pids, "only members build a group communicator"
-        backend = "rccl" if all(info.get("backend") == "rccl" for _, info in members) else "gloo"
+        backend = self.group_backend(members)
         key = (tuple(pids), backend)
         rank_of = {pid: i for i, pid in enumerate(pids)}
         with self._lock:
@@ -261,7 +358,12 @@ class GroupCommunicators:
             tok = bytes(group_id).hex()
             if deadline is None:
                 deadline = time.monotonic() + self.timeout_s
-            comm = self._create(tok, backend, len(pids), rank_of[self.peer_id], deadline)
+            if backend == "hybrid":
+                info_of = {bytes(pid): info for pid, info in members}
+                gpu = [p for p in pids if info_of[p].get("backend") == "rccl"]
+                comm = self._create_hybrid(tok, pids, gpu, deadline)
+            else:
+                comm = self._create(tok, backend, len(pids), rank_of[self.peer_id], deadline)
             self._cache[tok] = _Entry(comm, key, pids)
             self.created += 1
             return comm, rank_of
@@ -285,29 +387,32 @@ class GroupCommunicators:
             time.sleep(delay)
             delay = min(0.05, delay * 1.5)
 
-    def _create(self, tok: str, backend: str, n: int, rank: int, deadline: float):
-        leader = rank == 0
-        if backend == "rccl":
-            if leader:
-                uid = RcclGroupComm.new_unique_id()
-                self._publish(tok, {"uid": uid})
-            else:
-                uid = bytes(self._await(tok, deadline)["uid"])
-            try:  # a healthy bootstrap takes seconds: a broken one should not hold the whole round
-                boot = time.monotonic() + float(os.environ.get("DEDLOC_RCCL_BOOTSTRAP_S", "30"))
-                boot = boot if deadline is None else min(deadline, boot)
-                comm = RcclGroupComm.create(uid, n, rank, self.device, boot)
-            except Exception:  # CommError (deadline) or an RCCL init error raised by the op
+    def _create_rccl(self, tok: str, n: int, rank: int, deadline: float) -> RcclGroupComm:
+        if rank == 0:
+            uid = RcclGroupComm.new_unique_id()
+            self._publish(tok, {"uid": uid})
+        else:
+            uid = bytes(self._await(tok, deadline)["uid"])
+        try:  # a healthy bootstrap takes seconds: a broken one should not hold the whole round
+            boot = time.monotonic() + float(os.environ.get("DEDLOC_RCCL_BOOTSTRAP_S", "30"))
+            boot = boot if deadline is None else min(deadline, boot)
+            comm = RcclGroupComm.create(uid, n, rank, self.device, boot)
+        except CommError as e:
+            if e.local:  # this peer's RCCL failed; a deadline may be another member's doing
                 self.rccl_create_failures += 1
                 if self.rccl_create_failures == self.RCCL_FALLBACK_AFTER:
-                    logger.warning(f"{self.rccl_create_failures} RCCL group communicators in a row did not come "
-                                   f"up; this peer now averages over host-staged gloo groups")
-                raise
-            self.rccl_create_failures = 0
-            return comm
+                    self._fallback_since = time.monotonic()
+                    logger.warning(f"{self.rccl_create_failures} RCCL group communicators in a row failed on this "
+                                   f"peer; it averages over host-staged gloo for the next "
+                                   f"{self.RCCL_RETRY_AFTER_S:.0f} s")
+            raise
+        self.rccl_create_failures = 0
+        return comm
+
+    def _create_gloo(self, tok: str, n: int, rank: int, deadline: float) -> GlooGroupComm:
         timeout = max(1.0, _left(deadline))
         store_td = datetime.timedelta(seconds=timeout)
-        if leader:
+        if rank == 0:
             server = dist.TCPStore(self.host, 0, n, True, store_td, wait_for_workers=False)
             self._publish(tok, {"host": self.host, "port": int(server.port)})
             store = server
@@ -320,6 +425,25 @@ class GroupCommunicators:
                                         keep_store=server)
         except RuntimeError as e:
             raise CommError(f"gloo group {tok[:12]} did not come up: {e}") from e
+
+    def _create(self, tok: str, backend: str, n: int, rank: int, deadline: float):
+        if backend == "rccl":
+            return self._create_rccl(tok, n, rank, deadline)
+        return self._create_gloo(tok, n, rank, deadline)
+
+    def _create_hybrid(self, tok: str, pids: List[bytes], gpu: List[bytes], deadline: float) -> HybridGroupComm:
+        rank = pids.index(self.peer_id)
+        rccl_rank = [gpu.index(p) if p in gpu else None for p in pids]
+        rccl = None
+        if self.peer_id in gpu:
+            rccl = self._create_rccl(tok + "r", len(gpu), gpu.index(self.peer_id), deadline)
+        try:
+            gloo = self._create_gloo(tok + "g", len(pids), rank, deadline)
+        except CommError:
+            if rccl is not None:
+                rccl.abort()
+            raise
+        return HybridGroupComm(rccl, gloo, rccl_rank, rank, self.device)
 
     # ------------------------------------------------------------------ failure handling
     def invalidate(self, comm) -> None:

@@ -249,8 +249,11 @@ def test_comm_reuse_requires_every_member_to_hold_it():
 
 
 def test_group_comms_fall_back_to_gloo_after_rccl_bootstrap_failures(monkeypatch):
-    """A peer whose RCCL communicators keep failing to come up announces gloo (host-staged groups)
-    from then on; DEDLOC_DATA_PLANE=gloo forces that; a successful bootstrap resets the count."""
+    """A peer whose OWN RCCL stack keeps failing (init error codes) announces gloo (host-staged
+    groups) for a while; DEDLOC_DATA_PLANE=gloo forces that; a successful bootstrap resets the
+    count.  A bootstrap that only misses its deadline — another member died or was preempted
+    between matchmaking and setup — never counts (under churn healthy peers were moved
+    to gloo for good)."""
     import torch
 
     from dedloc_amd.parallel import comm as C
@@ -261,19 +264,27 @@ def test_group_comms_fall_back_to_gloo_after_rccl_bootstrap_failures(monkeypatch
     monkeypatch.setenv("DEDLOC_DATA_PLANE", "gloo")
     assert g.backend == "gloo"
     monkeypatch.delenv("DEDLOC_DATA_PLANE")
-
-    def boom(*a, **k):
-        raise C.CommError("bootstrap deadline")
-
-    monkeypatch.setattr(C.RcclGroupComm, "create", classmethod(lambda cls, *a, **k: boom()))
     monkeypatch.setattr(g, "_await", lambda tok, deadline: {"uid": b"\0" * 128})
+
+    def failing(local):
+        def boom(cls, *a, **k):
+            raise C.CommError("bootstrap failed", local=local)
+        return classmethod(boom)
+
+    monkeypatch.setattr(C.RcclGroupComm, "create", failing(False))  # a missing member: deadline
+    for i in range(2 * C.GroupCommunicators.RCCL_FALLBACK_AFTER):
+        with pytest.raises(C.CommError):
+            g._create("late%d" % i, "rccl", 2, 1, deadline=None)
+    assert g.rccl_create_failures == 0 and g.backend == "rccl"
+
+    monkeypatch.setattr(C.RcclGroupComm, "create", failing(True))  # this peer's RCCL: error code
     for i in range(C.GroupCommunicators.RCCL_FALLBACK_AFTER):
         assert g.backend == "rccl"
-        try:
+        with pytest.raises(C.CommError):
             g._create("tok%d" % i, "rccl", 2, 1, deadline=None)
-        except C.CommError:
-            pass
     assert g.backend == "gloo"
+    g._fallback_since -= C.GroupCommunicators.RCCL_RETRY_AFTER_S + 1  # the retry period has passed
+    assert g.backend == "rccl"
     monkeypatch.setattr(C.RcclGroupComm, "create", classmethod(lambda cls, *a, **k: object()))
     g._create("ok", "rccl", 2, 1, deadline=None)
     assert g.rccl_create_failures == 0 and g.backend == "rccl"

@@ -1,0 +1,255 @@
+"""The RCCL data-plane logic on CPU, against a fake ``torch.ops.dedloc_comm``.
+
+Multi-rank RCCL cannot run on a one-GPU box, so the host-side protocol around it is pinned here:
+the comm worker's jobs (parallel/comm_worker.py), the butterfly all-reduce over ``RcclGroupComm``,
+the RCCL state-download path, and the mixed RCCL + gloo group.  The fake matches sends to receives
+per (communicator, sender, receiver) pair in order, as RCCL does, and can be told to report
+``ncclInProgress`` for a number of polls (non-blocking enqueue), to raise an asynchronous error on
+one member, or to never see a member's operations (a dead peer).
+
+Parity note: the fake checks the protocol (who sends what to whom, polling, abort on deadline and
+on error), not RCCL itself; a real multi-GPU run is the only check of the latter.
+"""
+import threading
+import time
+from collections import defaultdict, deque
+
+import pytest
+import torch
+
+import dedloc_amd.ops  # noqa: F401  (dedloc:: CPU kernels: pack / reduce_delta / unpack)
+from dedloc_amd.averaging.allreduce import GroupSpec, butterfly_allreduce
+from dedloc_amd.parallel import comm as C
+from dedloc_amd.parallel import comm_worker as W
+
+SUCCESS, IN_PROGRESS, SYSTEM_ERROR = 0, 7, 2
+
+
+class FakeRccl:
+    """A process-local stand-in for the native operators of csrc/comm/rccl_comm.cpp."""
+
+    def __init__(self, init_polls=2, enqueue_polls=2):
+        self.lock = threading.Lock()
+        self.next = 1
+        self.comms = {}           # handle -> dict(uid, n, rank, polls, pending recvs, error)
+        self.joined = defaultdict(set)
+        self.mail = defaultdict(deque)  # (uid, src, dst) -> tensors in send order
+        self.init_polls, self.enqueue_polls = init_polls, enqueue_polls
+        self.aborted = set()
+        self.mute = set()         # (uid, rank): this member's operations never arrive (dead peer)
+        self.calls = defaultdict(int)
+        self.threads = set()
+
+    def _note(self, name):
+        self.calls[name] += 1
+        self.threads.add(threading.current_thread().name)
+
+    def unique_id(self):
+        self._note("unique_id")
+        return torch.randint(0, 256, (128,), dtype=torch.uint8)
+
+    def comm_init(self, uid, n, rank, dev):
+        self._note("comm_init")
+        key = bytes(uid.numpy().tobytes())
+        with self.lock:
+            h = self.next
+            self.next += 1
+            self.comms[h] = {"uid": key, "n": n, "rank": rank, "polls": self.init_polls, "recvs": [], "error": 0}
+            self.joined[key].add(rank)
+        return h
+
+    def comm_status(self, h):
+        self._note("comm_status")
+        with self.lock:
+            c = self.comms[h]
+            if c["error"]:
+                return c["error"]
+            if len(self.joined[c["uid"]]) < c["n"]:
+                return IN_PROGRESS
+            if c["polls"] > 0:
+                c["polls"] -= 1
+                return IN_PROGRESS
+            still = []
+            for t, src in c["recvs"]:
+                box = self.mail[(c["uid"], src, c["rank"])]
+                if box:
+                    t.copy_(box.popleft())
+                else:
+                    still.append((t, src))
+            c["recvs"] = still
+            return SUCCESS if not still else IN_PROGRESS
+
+    def group_p2p(self, h, sends, send_peers, recvs, recv_peers):
+        self._note("group_p2p")
+        with self.lock:
+            c = self.comms[h]
+            if (c["uid"], c["rank"]) not in self.mute:
+                for t, p in zip(sends, send_peers):
+                    if t.numel():
+                        self.mail[(c["uid"], c["rank"], p)].append(t.detach().clone())
+            c["recvs"] += [(t, p) for t, p in zip(recvs, recv_peers) if t.numel()]
+            c["polls"] = self.enqueue_polls
+        return IN_PROGRESS
+
+    def comm_abort(self, h):
+        self._note("comm_abort")
+        with self.lock:
+            self.aborted.add(h)
+
+    def error_string(self, code):
+        return f"fake error {code}"
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    f = FakeRccl()
+    monkeypatch.setattr(W, "_ops", lambda: f)
+    monkeypatch.setattr(C, "rccl_available", lambda dev: True)
+    return f
+
+
+def _run_ranks(n, fn):
+    out, errs = {}, {}
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+
+    ts = [threading.Thread(target=body, args=(r,), name=f"rank{r}") for r in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    return out, errs
+
+
+def test_butterfly_over_rccl_nonuniform_parts_and_weights(fake):
+    """Three members, LP-style unequal parts (one member owns none), unequal weights, FLOAT16 wire:
+    every member ends with the weighted fp32 mean (to fp16 accuracy), and every RCCL call was made
+    on the comm worker thread."""
+    n, V = 3, 1000
+    uid = W.unique_id()
+    xs = [torch.randn(V, generator=torch.Generator().manual_seed(r)) for r in range(n)]
+    weights = [1.0, 2.5, 0.5]
+    parts = [600, 0, 400]
+    expected = sum(w * x for w, x in zip(weights, xs)) / sum(weights)
+
+    def rank(r):
+        comm = C.RcclGroupComm.create(uid, n, r, torch.device("cpu"), time.monotonic() + 20)
+        x = xs[r].clone()
+        spec = GroupSpec(ranks=list(range(n)), part_sizes=parts, weights=[weights[r] if k == r else 0.0 for k in range(n)],
+                         contributes=[True] * n, my_index=r)
+        butterfly_allreduce([x], spec, "FLOAT16", comm=comm, timeout=20)
+        comm.abort()
+        return x
+
+    out, errs = _run_ranks(n, rank)
+    assert not errs, errs
+    for r in range(n):
+        torch.testing.assert_close(out[r], expected, rtol=2e-3, atol=2e-3)
+    assert fake.threads == {"comm-worker"}, fake.threads  # the single RCCL owner
+    assert fake.calls["group_p2p"] == 2 * n and fake.calls["comm_abort"] == n
+
+
+def test_async_error_while_polling_aborts_and_raises(fake):
+    """An asynchronous RCCL error reported while a transfer is polled: the job aborts the
+    communicator and the caller gets a CommError flagged as this peer's own (local) failure."""
+    uid = W.unique_id()
+
+    def rank(r):
+        comm = C.RcclGroupComm.create(uid, 2, r, torch.device("cpu"), time.monotonic() + 20)
+        if r == 0:
+            fake.comms[comm.handle]["error"] = SYSTEM_ERROR
+        buf = torch.zeros(8)
+        comm.p2p([torch.ones(8)], [1 - r], [buf], [1 - r], time.monotonic() + 3)
+        return comm
+
+    out, errs = _run_ranks(2, rank)
+    assert isinstance(errs.get(0), C.CommError) and errs[0].local, errs
+    assert "fake error" in str(errs[0])
+    assert any(fake.comms[h]["rank"] == 0 for h in fake.aborted)
+
+
+def test_dead_member_is_aborted_at_the_deadline(fake):
+    """A member that never sends (dead peer): the live member's transfer is aborted at the round's
+    deadline — not later, and flagged as not this peer's fault (no RCCL fallback counting)."""
+    uid = W.unique_id()
+    fake.mute.add((uid, 1))
+
+    def rank(r):
+        comm = C.RcclGroupComm.create(uid, 2, r, torch.device("cpu"), time.monotonic() + 20)
+        if r == 1:
+            return None  # posts nothing, ever
+        t0 = time.monotonic()
+        try:
+            comm.p2p([torch.ones(8)], [1], [torch.zeros(8)], [1], time.monotonic() + 1.0)
+        finally:
+            fake_elapsed.append(time.monotonic() - t0)
+        return comm
+
+    fake_elapsed = []
+    out, errs = _run_ranks(2, rank)
+    assert isinstance(errs.get(0), C.CommError) and not errs[0].local, errs
+    assert 0.9 < fake_elapsed[0] < 2.0, fake_elapsed
+    assert len(fake.aborted) == 1
+
+
+def test_state_download_over_rccl_path(fake):
+    """The state server's 'R' mode (a donor sends its snapshot over a one-off 2-rank communicator
+    the requester bootstrapped): header over TCP, tensors through the comm worker."""
+    from dedloc_amd.averaging.averager import StateServer, download_state
+
+    state = [torch.randn(300), torch.arange(10, dtype=torch.float32)]
+    srv = StateServer(lambda: ({"step": 7}, [t.clone() for t in state]), "127.0.0.1:0", device=torch.device("cpu"))
+    try:
+        meta, tensors = download_state(srv.endpoint, timeout=20, device=torch.device("cpu"), allow_rccl=True)
+        t0 = time.monotonic()
+        while srv.served["R"] < 1 and time.monotonic() - t0 < 10:  # the server counts after its send
+            time.sleep(0.01)
+    finally:
+        srv.shutdown()
+    assert meta["_mode"] == "R" and meta["step"] == 7 and srv.served["R"] == 1
+    for a, b in zip(tensors, state):
+        torch.testing.assert_close(a, b)
+    assert fake.threads == {"comm-worker"}
+
+
+@pytest.mark.timeout(120)
+def test_mixed_group_keeps_gpu_members_on_rccl(fake):
+    """Two RCCL-capable members + one CPU (gloo) member: the group communicator is hybrid — the
+    GPU pair's transfers go through RCCL, only the pairs with the CPU member over gloo — and the
+    average is exact."""
+    from dedloc_amd.dht import DHT
+
+    root = DHT(listen_on="127.0.0.1:*")
+    dhts = [DHT(initial_peers=[root.endpoint], listen=False) for _ in range(3)]
+    names = [b"gpu-a", b"gpu-b", b"cpu-c"]
+    members = [(b"gpu-a", {"backend": "rccl", "comms": []}), (b"gpu-b", {"backend": "rccl", "comms": []}),
+               (b"cpu-c", {"backend": "gloo", "comms": []})]
+    xs = [torch.full((96,), float(r + 1)) for r in range(3)]
+    try:
+        def rank(r):
+            g = C.GroupCommunicators(dhts[r], "mixed", names[r], torch.device("cpu"), timeout_s=30)
+            comm, rank_of = g.get(members, b"round-0")
+            assert comm.backend == "rccl+gloo"
+            pids = [m for m, _ in members]
+            spec = GroupSpec(ranks=[rank_of[p] for p in pids], part_sizes=[40, 40, 16],
+                             weights=[1.0 if k == r else 0.0 for k in range(3)], contributes=[True] * 3, my_index=r)
+            x = xs[r].clone()
+            butterfly_allreduce([x], spec, "NONE", comm=comm, timeout=20)
+            g.close()
+            return x, comm.rccl is not None
+
+        out, errs = _run_ranks(3, rank)
+        assert not errs, errs
+        for r in range(3):
+            torch.testing.assert_close(out[r][0], torch.full((96,), 2.0))
+        assert [out[r][1] for r in range(3)] == [True, True, False]
+        # RCCL carried the GPU pair's traffic: exactly one 2-rank communicator was built
+        assert fake.calls["comm_init"] == 2
+    finally:
+        for d in dhts:
+            d.shutdown()
+        root.shutdown()

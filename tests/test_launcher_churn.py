@@ -54,3 +54,23 @@ def test_launcher_kill_and_respawn_with_cpu_aux(tmp_path):
     assert "downloaded state" in gen1, gen1[-3000:]
     aux = (logs / "aux0.log").read_text()
     assert "Traceback" not in aux, aux[-3000:]
+
+
+@pytest.mark.timeout(120)
+def test_launcher_gives_up_on_a_trainer_that_always_fails_fast(tmp_path):
+    """with --respawn a trainer that always crashes at start (here: a flag run_trainer
+    does not know) is restarted with a doubling delay and, after --max_fast_failures consecutive
+    fast failures, given up ('gave_up' event) — the launcher then ends instead of restarting it
+    forever."""
+    logs = tmp_path / "logs"
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "dedloc_amd.cli.launch_collaboration", "--n_trainers", "1", "--cpu",
+           "--no_coordinator", "--respawn", "--respawn_delay", "0.2", "--min_run_s", "60", "--max_fast_failures", "3",
+           "--log_dir", str(logs), "--", "--no_such_flag"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=100)
+    events = [json.loads(l) for l in (logs / "launcher_events.jsonl").read_text().splitlines()]
+    kinds = [e["kind"] for e in events]
+    assert kinds.count("respawn") == 2 and kinds[-2:] == ["gave_up", "stop"], kinds
+    delays = [e["respawn_in"] for e in events if e["kind"] == "died"]
+    assert delays == [0.4, 0.8], delays  # the delay doubles with each fast failure
+    assert r.returncode != 0

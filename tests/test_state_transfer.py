@@ -1,7 +1,9 @@
 """Peer state download (reference ``albert/run_trainer.py:124-128``,
 ``run_first_peer.py:119-121``) at the reference's size: params + LAMB m, v of ALBERT-large
-(3 x 17.8M fp32 = 214 MB).  The donor keeps training while it serves: ``step()`` may wait only for
-the on-device snapshot, never for the transfer itself."""
+(3 x 17.8M fp32 = 214 MB).  The donor keeps training while it serves: it copies its state into a
+snapshot at the end of every global step, and a request is served from that snapshot — the
+server never waits for the donor's step lock (held across averaging rounds and LAMB), and a step
+never waits for a transfer."""
 import threading
 import time
 
@@ -45,7 +47,7 @@ def test_albert_large_state_download_does_not_block_donor_steps():
         snap = []
         serve = co.averager.state_server.get_state
 
-        def timed_snapshot():  # what the server does under the donor's step lock
+        def timed_snapshot():  # the server's clone of the donor's last snapshot
             a = time.perf_counter()
             out = serve()
             snap.append(time.perf_counter() - a)
@@ -74,11 +76,80 @@ def test_albert_large_state_download_does_not_block_donor_steps():
         print(f"state download: {nbytes / 2**20:.0f} MiB in {transfer:.3f}s ({nbytes / transfer / 2**30:.2f} GiB/s); "
               f"snapshot (incl. waiting for the step lock) {snap[0]:.3f}s; donor steps during it: {len(during)}, "
               f"max {max(during):.3f}s, typical {typical:.3f}s")
-        assert len(during) >= 2, "the donor must keep stepping while it serves its state"
-        # the donor's step lock is held for the snapshot only (a clone), then released for the
-        # transfer: a step can be delayed by at most one snapshot, never by the transfer
+        assert len(during) >= 1, "the donor must keep stepping while it serves its state"
+        # serving clones the last snapshot without the step lock: it does not wait for the step in
+        # progress (one step here is ~1 s of CPU LAMB), and a step is never delayed by the transfer
         assert len(snap) == 1
+        assert snap[0] < 0.5 * typical, (snap[0], typical)
         assert max(during) < typical + snap[0] + 0.2, (max(during), typical, snap[0], transfer)
+    finally:
+        co.shutdown()
+        dht.shutdown()
+
+
+def _joiner(endpoint, q):
+    import time as _t
+
+    from dedloc_amd.averaging.averager import download_state
+
+    t0 = _t.perf_counter()
+    meta, tensors = download_state(endpoint, timeout=30)
+    q.put({"seconds": _t.perf_counter() - t0, "step": meta["step"], "n": len(tensors),
+           "p0": float(tensors[0][0])})
+
+
+@pytest.mark.multiproc
+@pytest.mark.timeout(120)
+def test_joiner_downloads_from_donor_in_the_middle_of_an_averaging_round():
+    """A peer joining while the donor is inside an averaging round (which holds the donor's step
+    lock for matchmaking + all-reduce + LAMB, up to averaging_timeout) gets the donor's last global
+    step state at once — here a round stalled for 8 s, and the download finishes within 2 s."""
+    import multiprocessing as mp
+
+    from dedloc_amd.dht import DHT, get_dht_time
+    from dedloc_amd.optim.collaborative import CollaborationState, CollaborativeOptimizer
+    from dedloc_amd.optim.lamb import FusedLamb
+    from dedloc_amd.utils.flat import FlatParams
+
+    torch.manual_seed(0)
+    flat = FlatParams([("w", torch.nn.Parameter(torch.randn(1 << 16))), ("b", torch.nn.Parameter(torch.zeros(64)))],
+                      with_bf16=False)
+    opt = FusedLamb(flat, lr=1e-3)
+    dht = DHT(listen_on="127.0.0.1:*")
+    co = CollaborativeOptimizer(opt, dht=dht, prefix="midround", target_batch_size=1, batch_size_per_step=1,
+                                listen_on="127.0.0.1:*", start=False)
+    try:
+        flat.grad.normal_()
+        co.step()  # global step 1, alone: the snapshot now holds step 1
+        assert co.local_step == 1
+        p_step1 = float(flat.fp32[0])
+        in_round = threading.Event()
+
+        def stalled_round(**kw):  # a round whose members are slow: holds lock_step for 8 s
+            in_round.set()
+            time.sleep(8.0)
+            return None
+
+        co.averager.step = stalled_round
+        co.fetch_collaboration_state = lambda: CollaborationState(1, 2, 1, num_peers=2, num_clients=0,
+                                                                  eta_next_step=get_dht_time(),
+                                                                  next_fetch_time=get_dht_time() + 60)
+        flat.grad.normal_()
+        th = threading.Thread(target=co.step)
+        th.start()
+        assert in_round.wait(10)
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        p = ctx.Process(target=_joiner, args=(co.averager.state_server.endpoint, q))
+        t0 = time.perf_counter()
+        p.start()
+        res = q.get(timeout=60)
+        p.join(30)
+        assert th.is_alive(), "the round must still be in flight when the download completes"
+        assert res["seconds"] < 2.0, res
+        assert res["step"] == 1 and res["n"] == 3 and res["p0"] == p_step1
+        print(f"download mid-round: {res['seconds']:.3f}s (process start included: {time.perf_counter() - t0:.2f}s)")
+        th.join(30)
     finally:
         co.shutdown()
         dht.shutdown()
