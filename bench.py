@@ -50,6 +50,10 @@ METRIC = "samples/sec (whole node) ALBERT-large MLM pretrain at 1/2/4/8 peers"
 # materialises the full [B*S, 30000] MLM logits; BASELINE.md "Measured MI355X results",
 # profiles/bench_eager_mb128.log).  vs_baseline = value / (this x N).
 EAGER_BASELINE_SPS_PER_GPU = 272.02
+# The SwAV counterpart (--model swav --impl eager: training/swav_eager.py, stock nn modules with one
+# trunk pass per crop, vissl-formula loss, apex-LARC SGD in torch ops, same collaborative engine),
+# samples/s per GPU at N=1, b=64; None until measured on MI355X.
+EAGER_SWAV_SPS_PER_GPU = None
 
 
 def parse():
@@ -73,7 +77,8 @@ def parse():
                     help="samples per collaborative step (default: 4096 ALBERT, 32768 SwAV — the reference values)")
     ap.add_argument("--compression", default="FLOAT16")
     ap.add_argument("--impl", default="dedloc", choices=["dedloc", "eager"],
-                    help="eager = HF AlbertForPreTraining + per-tensor torch LAMB (the measured baseline)")
+                    help="eager = the reference's compute on stock PyTorch (ALBERT: HF AlbertForPreTraining + "
+                         "per-tensor torch LAMB; SwAV: training/swav_eager.py) — the measured baselines")
     ap.add_argument("--cpu_test", default=None, metavar="CONFIG_DIR",
                     help="plumbing test only: run on CPU/gloo with the tiny ALBERT config in CONFIG_DIR (with "
                          "--model swav the value is ignored: full ResNet-50, use a tiny --micro_batch) — exercises "
@@ -196,16 +201,18 @@ def _swav_peer(args, rank, dev, root_ep):
           f'config.OPTIMIZER.dht_initial_peers=["{root_ep}"]', f"config.CHECKPOINT.DIR=/tmp/dedloc_swav_bench_{os.getpid()}",
           "config.CHECKPOINT.AUTO_RESUME=false", "config.CHECKPOINT.CHECKPOINT_ITER_FREQUENCY=0"]
     cfg = load_config("swav_1node_resnet_submit", ov)
-    peer = SwavPeer(cfg, dev, rank=rank)
+    peer = SwavPeer(cfg, dev, rank=rank, impl=args.impl)
 
     def describe(value, world):
+        base = EAGER_SWAV_SPS_PER_GPU
         return {"metric": "samples/sec (whole node) SwAV ResNet-50 at 1/2/4/8 peers", "value": round(value, 2),
-                "unit": "samples/s", "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "unit": "samples/s", "higher_is_better": True, "scaling": "strong",
+                "vs_baseline": round(value / (base * world), 3) if base else None,
                 "dtype": "bf16", "data": "synthetic (ImageNet-224-sized image pool, 2x224 + 6x96 multi-crop on the "
                                          "GPU; random-init weights)",
                 "config": {"model": "swav-resnet50", "global_batch": args.target_batch_size, "batch_per_peer": b,
                            "crops": "2x224+6x96", "parallelism": f"collaborative-dp{world}",
-                           "compression": args.compression, "optimizer": "LARC-SGD",
+                           "compression": args.compression, "optimizer": "LARC-SGD", "impl": args.impl,
                            "target_group_size": int(cfg.OPTIMIZER.target_group_size)}}
     return peer, b, describe
 

@@ -40,7 +40,10 @@ VARIANTS = {"gemm8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "0"},
             "g8rb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "0"},
             # per-lane DMA source bases computed once + peeled K-loop tail
             "g8pre": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_PRESRC": "1"},
-            "g8nopre": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_PRESRC": "0"}}
+            "g8nopre": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_PRESRC": "0"},
+            # the defaults, and 256 x 128 tiles with two co-resident workgroups per CU (gemm8h)
+            "g8": {},
+            "g8h": {"DEDLOC_GEMM8_HALF": "1"}}
 
 
 def timeit(fn, iters=10):
@@ -55,7 +58,7 @@ def timeit(fn, iters=10):
 
 def set_policy(pol):
     for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT", "DEDLOC_GEMM8_GROUP", "DEDLOC_GEMM8_KEEPB0",
-              "DEDLOC_GEMM8_PRESRC"):
+              "DEDLOC_GEMM8_PRESRC", "DEDLOC_GEMM8_HALF"):
         os.environ.pop(k, None)
     os.environ.update(pol)
 

@@ -957,8 +957,265 @@ __global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm8h: 256 x 128 tiles on 4 waves, TWO co-resident workgroups per CU (bf16 store epilogues).
+//
+// A 256 x 256 workgroup owns the whole CU (8 waves x 256 VGPRs = the register file; 128 KiB LDS),
+// so its output stores — 128 KiB per tile, issued at ~14 B/clk/CU, ~9K cycles — run with the
+// matrix pipes idle, ~20% of a K = 1024 GEMM (profiles/README.md round 3).  Here a workgroup is half
+// of that: 4 waves (2 x 2) each still own 128 x 64 outputs (the same per-wave MFMA/LDS-read work and
+// fragment layout as gemm8), 256 VGPRs, and 80 KiB of LDS, so two workgroups share every CU and
+// one's epilogue runs beside the other's main loop.
+//
+// LDS (80 KiB): a ring of 3 A half-tile slots (128 rows x 64 k, 16 KiB) and 4 B half-tile slots
+// (64 columns x 64 k, 8 KiB); half-tiles as in gemm8 (A half h = tile rows with bit 6 == h, B half
+// h = tile columns with bit 5 == h).  Per K-tile the waves run the quadrant phases (0,0) (0,1)
+// (1,1) (1,0), ONE barrier per phase (after its MFMAs); each phase issues one half-tile of the
+// next K-tile into the slot whose last reader was a phase that ended at an earlier barrier:
+//   ph0: A0(t+1) -> slot of A1(t-1)   ph1: B0(t+1) -> slot of B0(t-1)
+//   ph2: A1(t+1) -> slot of A0(t)     ph3: B1(t+1) -> slot of B1(t-1)
+// Counted waits (glds per thread: A half 4, B half 2): end of ph3 vmcnt(6) retires A0/B0(t+1)
+// (A1/B1(t+1) stay in flight), end of ph0 vmcnt(4) retires A1/B1(t+1) (A0(t+2) stays in flight);
+// the barrier after each wait publishes the other waves' DMAs before the next phase reads them.
+// K-inner operands only (forward GEMMs and the data gradients on transposed weight copies).
+// ---------------------------------------------------------------------------------------------
+constexpr int HBN = 128, HNT = 256;
+constexpr int HAH = 16384, HBH = 8192;
+constexpr int HA_SLOTS = 3, HB_SLOTS = 4;
+constexpr int HSMEM = HA_SLOTS * HAH + HB_SLOTS * HBH;  // 81920: two workgroups fill the 160 KiB
+
+// per-lane DMA source bases of one half-tile at k0 = 0: NP pieces of 1 KiB per wave
+template <bool ISB, int NP>
+__device__ __forceinline__ void hsrc_base(const bf16_t* __restrict__ g, long ld, int r0, int rows_valid, int half,
+                                          int w, int lane, const bf16_t* (&base)[NP]) {
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const int lrow = (j * 4 + w) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ kin_swz(lrow);
+    const int grow = min(r0 + half_to_tile<ISB>(lrow, half), rows_valid - 1);
+    base[j] = g + (long)grow * ld + c * 8;
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void hstage(const bf16_t* const (&base)[NP], long koff, uint8_t* slot, int w) {
+#pragma unroll
+  for (int j = 0; j < NP; ++j) dma16(base[j] + koff, slot + (j * 4 + w) * 1024);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(HNT, 2) void gemm8h_kernel(Args p) {
+  static_assert(EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU, "bf16 store epilogues");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[HSMEM];
+  uint8_t* const sA = smem;
+  uint8_t* const sB = smem + HA_SLOTS * HAH;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int tiles_n = p.N / HBN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int m0, n0;
+  {
+    const int G = p.group_m, band = G * tiles_n, first = (bid / band) * G;
+    const int gsz = min(tiles_m - first, G), r = bid % band;
+    m0 = (first + r % gsz) * BM;
+    n0 = (r / gsz) * HBN;
+  }
+  const int nk = p.K / BK;
+
+  floatx4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) acc[a][b][c][d] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const bf16_t* bA0[4];
+  const bf16_t* bA1[4];
+  const bf16_t* bB0[2];
+  const bf16_t* bB1[2];
+  hsrc_base<false, 4>(p.A, p.lda, m0, p.M, 0, w, lane, bA0);
+  hsrc_base<false, 4>(p.A, p.lda, m0, p.M, 1, w, lane, bA1);
+  hsrc_base<true, 2>(p.B, p.ldb, n0, p.N, 0, w, lane, bB0);
+  hsrc_base<true, 2>(p.B, p.ldb, n0, p.N, 1, w, lane, bB1);
+  // half-tile h of K-tile t: A slot (2t + h) % 3, B slot (2t + h) % 4
+  auto slotA = [&](int t, int h) { return sA + ((2 * t + h) % HA_SLOTS) * HAH; };
+  auto slotB = [&](int t, int h) { return sB + ((2 * t + h) % HB_SLOTS) * HBH; };
+  auto koff = [&](int t) { return (long)t * BK; };
+
+  // prologue: all of K-tile 0 (A0 B0 B1 A1); the first phases need A0, B0, B1
+  hstage<4>(bA0, 0, slotA(0, 0), w);
+  hstage<2>(bB0, 0, slotB(0, 0), w);
+  hstage<2>(bB1, 0, slotB(0, 1), w);
+  hstage<4>(bA1, 0, slotA(0, 1), w);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  const int ra = wm * 64, cb = wn * 32;
+  bf16x8 af[4][2], bfr[2][2], bf0[2][2];
+  auto ktile = [&](int t, auto more) {
+    constexpr bool M1 = decltype(more)::value;  // K-tile t + 1 exists: stage it
+    const uint8_t* iA0 = slotA(t, 0);
+    const uint8_t* iA1 = slotA(t, 1);
+    const uint8_t* iB0 = slotB(t, 0);
+    const uint8_t* iB1 = slotB(t, 1);
+    const long kn = koff(t + 1);
+
+    // ---- phase 0: quadrant (0,0); stage A0(t+1)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bf0[ni][ks] = frag<false>(iB0, cb + ni * 16, ks, lane);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<false>(iA0, ra + mi * 16, ks, lane);
+    if constexpr (M1) hstage<4>(bA0, kn, slotA(t + 1, 0), w);
+    DL_MFMA_QUAD_B(0, 0, bf0);
+    if constexpr (M1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 1: quadrant (0,1); stage B0(t+1)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<false>(iB1, cb + ni * 16, ks, lane);
+    if constexpr (M1) hstage<2>(bB0, kn, slotB(t + 1, 0), w);
+    DL_MFMA_QUAD(0, 1);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 2: quadrant (1,1); stage A1(t+1) (A0(t)'s slot: its last reader, phase 1, is done)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<false>(iA1, ra + mi * 16, ks, lane);
+    if constexpr (M1) hstage<4>(bA1, kn, slotA(t + 1, 1), w);
+    DL_MFMA_QUAD(1, 1);
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 3: quadrant (1,0); stage B1(t+1); retire A0 / B0 of K-tile t+1
+    if constexpr (M1) hstage<2>(bB1, kn, slotB(t + 1, 1), w);
+    DL_MFMA_QUAD_B(1, 0, bf0);
+    if constexpr (M1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int t = 0; t < nk - 1; ++t) ktile(t, std::true_type{});
+  ktile(nk - 1, std::false_type{});
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every fragment read done: the epilogue reuses the ring
+
+  // ---------------------------------------------------------------- epilogue (as gemm8)
+  uint8_t* ep = smem + w * 16384;
+  const int crow = 4 * (lane >> 4), ccol = lane & 15;
+  float bias_v[2][2];
+#pragma unroll
+  for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      bias_v[qn][ni] = 0.f;
+      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
+        if (p.bias) bias_v[qn][ni] = p.bias[n0 + wn * 64 + qn * 32 + ni * 16 + ccol];
+    }
+  float colsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
+  const int rch = lane & 7, rr = lane >> 3;
+  const int gn = n0 + wn * 64 + rch * 8;
+  const bool has_r = EPI == EPI_DGELU || (EPI == EPI_STORE && p.R != nullptr);
+  auto rrow = [&](int qm, int pass) -> uint4 {
+    const int gm = min(m0 + wm * 128 + qm * 64 + pass * 8 + rr, p.M - 1);
+    return *reinterpret_cast<const uint4*>(p.R + (long)gm * p.ldr + gn);
+  };
+  uint4 rbuf[8];
+  if (has_r) {
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) rbuf[pass] = rrow(0, pass);
+  }
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm) {
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = mi * 16 + crow + i;
+            const int c = qn * 32 + ni * 16 + ccol;
+            const int q = (c >> 2) ^ (r & 1);
+            *reinterpret_cast<float*>(ep + r * 256 + q * 16 + (c & 3) * 4) = acc[qm][qn][mi][ni][i] + bias_v[qn][ni];
+          }
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      const int r = pass * 8 + rr;
+      const float4 lo = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch) ^ (r & 1)) << 4));
+      const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const int gm = m0 + wm * 128 + qm * 64 + r;
+      float rv[8];
+      if (has_r) {
+        unpack8_bf16(rbuf[pass], rv);
+        if (qm == 0) rbuf[pass] = rrow(1, pass);
+      }
+      if (gm < p.M) {
+        if constexpr (EPI == EPI_STORE) {
+          if (has_r) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] += rv[j];
+          }
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
+        } else if constexpr (EPI == EPI_GELU) {
+          float h[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
+          store8_bf16(p.H + (long)gm * p.ldh + gn, h, p.nt);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = gelu_tanh_sig(h[j]);
+          store8_bf16(p.C + (long)gm * p.ldc + gn, h, p.nt);
+        } else {  // EPI_DGELU
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(rv[j]));
+            colsum[j] += v[j];
+          }
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
+        }
+      }
+    }
+  }
+  if constexpr (EPI == EPI_DGELU) {
+    if (p.dbias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float s = colsum[j];
+        s += __shfl_xor(s, 8, 64);
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        colsum[j] = s;
+      }
+      if (lane < 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + wn * 64 + lane * 8 + j], colsum[j]);
+      }
+    }
+  }
+}
+
 #undef DL_MFMA_QUAD
 #undef DL_MFMA_QUAD_B
+
+// DEDLOC_GEMM8_HALF=1: K-inner bf16-epilogue GEMMs on gemm8h (two co-resident 256 x 128 workgroups
+// per CU) instead of one 256 x 256 workgroup; read per call (A/B in one process)
+bool half_tiles() {
+  const char* e = std::getenv("DEDLOC_GEMM8_HALF");
+  return e && e[0] == '1';
+}
 
 bool keep_b0() {  // read per call (A/B in one process); DEDLOC_GEMM8_KEEPB0=0: re-read B0 in phase 3
   const char* e = std::getenv("DEDLOC_GEMM8_KEEPB0");
@@ -988,6 +1245,12 @@ int launch8(const Args& a, int splits, hipStream_t st) {
     const int ctas = persistent_ctas();
     if (ctas > 0 && splits == 1 && tiles > ctas && a.K / BK >= 2) {
       gemm8p_kernel<AKO, BKO, EPI><<<dim3(ctas), NT, 0, st>>>(a);
+      return 0;
+    }
+  }
+  if constexpr (!AKO && !BKO && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU)) {
+    if (splits == 1 && half_tiles() && a.N % HBN == 0) {
+      gemm8h_kernel<EPI><<<dim3(((a.M + BM - 1) / BM) * (a.N / HBN)), HNT, 0, st>>>(a);
       return 0;
     }
   }

@@ -6,41 +6,37 @@ Reference: ``swav/vissl/vissl/models/trunks/re
 ``base_ssl_model.py:76-105`` (one trunk pass per crop with SINGLE_PASS_EVERY_CROP, features
 concatenated before the head).
 
-MI355X-first choices: channels-last bf16 activations under autocast (fp32 master weights live in the
-flat parameter buffer and receive their gradients in place), optional per-resolution batching of
-the crops (``single_pass_every_crop=False``: 2 trunk passes instead of 8), optional activation
-checkpointing per stage (off by default: 288 GB HBM makes the recompute pointless).
+MI355X-first choices: channels-last bf16 activations (fp32 master weights live in the flat parameter
+buffer and receive their gradients in place), optional per-resolution batching of the crops
+(``single_pass_every_crop=False``: 2 trunk passes instead of 8), optional activation checkpointing
+per stage (off by default: 288 GB HBM makes the recompute pointless).
 Parameter names match torchvision/vissl (``trunk.*``, ``heads.0.*``) for checkpoint interchange.
+
+One code path on every device: each op of the model is a ``torch.ops.dedloc`` operator — the HIP
+kernels on the GPU, the CPU implementations registered under the CPU dispatch key in
+``ops/_lib.py`` (the plumbing configuration) — exactly like the ALBERT model.  There is no stock
+module fallback: an input outside a kernel's contract (not channels-last bf16, an unsupported conv
+form) raises.  The BatchNorm statistics ride in the producing convolution's epilogue, the identity
+branch's gradient in conv1's data-gradient epilogue, and each BatchNorm+ReLU's backward preparation
+in the consuming 1x1 convolution's data gradient (measured in profiles/README.md, round 3).
 """
 from __future__ import annotations
 
-import os
 from typing import List, Sequence
 
 import torch
 import torch.nn as nn
 
 from .. import ops as _ops  # noqa: F401  (registers torch.ops.dedloc.*)
-import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 
-# BN+ReLU (no residual) backward reads only dy and x: the ReLU mask is recomputed from x
-# (DEDLOC_BN_XMASK=0: read y instead — A/B measurement switch)
-_BN_XMASK = os.environ.get("DEDLOC_BN_XMASK", "1") != "0"
-# BatchNorm forward statistics accumulated in the producing conv's epilogue (DEDLOC_CONV_STATS=0:
-# a separate statistics pass per BN — A/B measurement switch)
-_CONV_STATS = os.environ.get("DEDLOC_CONV_STATS", "1") != "0"
-# identity-branch gradient added in conv1's data-gradient epilogue (DEDLOC_RES_LINK=0: autograd's add)
-_RES_LINK = os.environ.get("DEDLOC_RES_LINK", "1") != "0"
-# BatchNorm+ReLU backward statistics accumulated in the consuming 1x1 conv's data-gradient epilogue
-# (DEDLOC_BN_BWD_EPI=0: the BN backward's own statistics pass)
-_BN_BWD_EPI = os.environ.get("DEDLOC_BN_BWD_EPI", "1") != "0"
-# the same for bn1 in the 3x3 conv2's data gradient (conv.hip epilogue, DEDLOC_BN_BWD_EPI_3X3=1).
-# Off by default: same-box A/B of the b=64 iteration 2142 / 2095 samples/s on vs 2136 / 2139 off
-# (profiles/r3_swav_bn_bwd_epi_3x3_ab.log) — the epilogue's extra X reads and statistics reduction
-# cost what the 32 removed statistics passes saved
-_BN_BWD_EPI_3X3 = os.environ.get("DEDLOC_BN_BWD_EPI_3X3", "0") == "1"
+def _require_nhwc_bf16(x: torch.Tensor, what: str) -> torch.Tensor:
+    """The trunk's activation contract: channels-last bf16 (what every producing kernel writes)."""
+    if x.dtype != torch.bfloat16 or not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError(f"{what}: expected a channels-last bf16 activation, got {x.dtype} with strides "
+                         f"{tuple(x.stride())} for shape {tuple(x.shape)}")
+    return x
 
 
 class _GradLink:
@@ -116,7 +112,7 @@ class _BNAct(torch.autograd.Function):
                                                           None if ctx.ws is None else ctx.ws[1],
                                                           gw if acc else None, gb if acc else None,
                                                           # BN+ReLU without a residual: ReLU mask from x, y unread
-                                                          beta if (_BN_XMASK and ctx.relu and not ctx.has_res) else None,
+                                                          beta if (ctx.relu and not ctx.has_res) else None,
                                                           ready)
         if acc:
             dgamma = dbeta = None
@@ -212,11 +208,11 @@ def _dgrad_weights(module, wb, stride, pad):
 
 
 class ConvNHWC(nn.Conv2d):
-    """``nn.Conv2d`` (same parameters / state-dict keys) that runs every GPU convolution on the
-    hand-written kernels (forward, dgrad, wgrad): the implicit-GEMM MFMA convolution (conv.hip) for
-    3x3 and strided convs, the tiled GEMM kernels (gemm8.hip / gemm.hip) for the 1x1 convs and the
-    stem's im2col matrix.  GPU inputs are brought to channels-last bf16 (autocast's compute dtype);
-    CPU inputs (the plumbing configuration) take the stock module.  There is no MIOpen path."""
+    """``nn.Conv2d`` (same parameters / state-dict keys) on the dedloc conv operators (forward,
+    dgrad, wgrad): on the GPU the implicit-GEMM MFMA convolution (conv.hip) for 3x3 and strided convs
+    and the tiled GEMM kernels (gemm8.hip / gemm.hip) for the 1x1 convs and the stem's im2col matrix;
+    on the CPU their registered CPU implementations.  The input is brought to channels-last bf16
+    (the trunk's entry takes the images as they come).  There is no MIOpen path."""
 
     _wb_cache = None    # bf16 weight shared across the trunk passes of one model forward
     _wb_share = False   # set by SwAVModel.forward for the duration of that forward
@@ -232,13 +228,11 @@ class ConvNHWC(nn.Conv2d):
         data-gradient epilogue adds (Bottleneck conv1).  ``bn_link``: the _BnBwdLink of the
         BatchNorm+ReLU that produced ``x`` (its backward preparation rides in this conv's data
         gradient)."""
-        if not x.is_cuda:
-            return super().forward(x)
         if not (self.bias is None and self.groups == 1 and self.dilation == (1, 1)
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and self.padding_mode == "zeros"):
             raise NotImplementedError("ConvNHWC: only the ResNet-50 conv forms (no bias, groups 1, square "
-                                      "stride/padding) have GPU kernels")
+                                      "stride/padding) have kernels")
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         if bn is not None and bn.takes_conv_stats():
             bn.stats_ready = True
@@ -250,10 +244,10 @@ class ConvNHWC(nn.Conv2d):
 class BNAct(nn.BatchNorm2d):
     """BatchNorm2d with the Bottleneck epilogue fused: ``act(BN(x) [+ res])``.
 
-    Same parameters / buffers / state-dict keys as ``nn.BatchNorm2d``.  In training on channels-last
-    bf16 GPU activations it runs csrc/kernels/batchnorm.hip (2 kernels forward, 2 backward, ReLU and
-    the residual add folded in — MIOpen needs 4 + 3 plus separate add/ReLU kernels); otherwise it is
-    the stock module followed by the add / ReLU.
+    Same parameters / buffers / state-dict keys as ``nn.BatchNorm2d``.  In training it runs the
+    fused BN operators (csrc/kernels/batchnorm.hip on the GPU: 2 kernels forward, 2 backward, ReLU
+    and the residual add folded in) on channels-last bf16 activations; in evaluation the running
+    statistics as one scale / shift (``_bn_eval``).
     """
 
     # False: return dgamma / dbeta through autograd (HIP-graph capture needs an autograd grad for
@@ -262,44 +256,48 @@ class BNAct(nn.BatchNorm2d):
     _gslot = None        # (dgamma, dbeta) targets of a concurrent second trunk pass (SwAVModel)
     _rs_override = None  # (running_mean, running_var) stand-ins of that pass (deferred update)
 
-    def __init__(self, num_features, relu: bool = False, fused: bool = True):
+    def __init__(self, num_features, relu: bool = False):
         super().__init__(num_features)
-        self.relu, self.fused = relu, fused
+        self.relu = relu
         self.stat_groups = 1  # >1: the batch holds that many crops, each normalised with its own stats
         self.pass_ws = None   # set by ResNet50Trunk.forward: (fwd sums, bwd sums) slices, pre-zeroed
         self.count_deferred = False  # num_batches_tracked is advanced by the trunk, one launch per pass
         self.stats_ready = False  # the producing conv accumulated this call's statistics into pass_ws[0]
 
     def takes_conv_stats(self) -> bool:
-        """True when this BN's next forward runs the fused kernels over a pre-zeroed pass workspace,
-        so the conv producing its input can accumulate the batch statistics in its epilogue."""
-        return self.fused and self.training and self.pass_ws is not None and _CONV_STATS
+        """True when this BN's next forward runs over a pre-zeroed pass workspace, so the conv
+        producing its input can accumulate the batch statistics in its epilogue."""
+        return self.training and self.pass_ws is not None
 
     def forward(self, x, res=None, link=None, bwd_link=None):
-        G = self.stat_groups if self.training else 1
-        if (self.fused and self.training and x.is_cuda and x.dtype == torch.bfloat16
-                and x.is_contiguous(memory_format=torch.channels_last)
-                and (res is None or (res.dtype == torch.bfloat16
-                                     and res.is_contiguous(memory_format=torch.channels_last)))):
-            if not self.count_deferred:
-                self.num_batches_tracked.add_(G)
-            ws, self.pass_ws = self.pass_ws, None
-            ready, self.stats_ready = self.stats_ready and ws is not None, False
-            rm, rv = self._rs_override or (self.running_mean, self.running_var)
-            return _BNAct.apply(x, self.weight, self.bias, res, rm, rv, self.relu,
-                                self.eps, self.momentum, G, ws, self, ready, link, bwd_link)
-        self.stats_ready = False
-        if G > 1:  # reference semantics without the fused kernel: one BN call per crop chunk
-            y = torch.cat([super(BNAct, self).forward(c) for c in x.chunk(G)])
-        else:
-            y = super().forward(x)
+        if not self.training:
+            self.stats_ready = False
+            return _bn_eval(self, x, res, self.relu)
+        _require_nhwc_bf16(x, "BNAct input")
         if res is not None:
-            y = y + res
-        return F.relu(y) if self.relu else y
+            _require_nhwc_bf16(res, "BNAct residual")
+        G = self.stat_groups
+        if not self.count_deferred:
+            self.num_batches_tracked.add_(G)
+        ws, self.pass_ws = self.pass_ws, None
+        ready, self.stats_ready = self.stats_ready and ws is not None, False
+        rm, rv = self._rs_override or (self.running_mean, self.running_var)
+        return _BNAct.apply(x, self.weight, self.bias, res, rm, rv, self.relu,
+                            self.eps, self.momentum, G, ws, self, ready, link, bwd_link)
 
 
-def _native_nhwc(x) -> bool:
-    return x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)
+def _bn_eval(m, x, res, relu: bool):
+    """Inference BatchNorm with the running statistics: y = x * scale + shift (+ res) (ReLU), as one
+    broadcast expression in the input's layout (not on the training path)."""
+    scale = m.weight.float() * torch.rsqrt(m.running_var.float() + m.eps)
+    shift = m.bias.float() - m.running_mean.float() * scale
+    shp = (1, -1) + (1,) * (x.dim() - 2)
+    y = x.float() * scale.view(shp) + shift.view(shp)
+    if res is not None:
+        y = y + res.float()
+    if relu:
+        y = y.clamp_min(0)
+    return y.to(x.dtype)
 
 
 class _MaxPool(torch.autograd.Function):
@@ -317,14 +315,14 @@ class _MaxPool(torch.autograd.Function):
 
 
 class MaxPool3x3s2(nn.MaxPool2d):
-    """The stem's MaxPool2d(3, stride 2, padding 1); on channels-last bf16 GPU activations the
-    pool.hip kernels (the backward routes each gradient to its window's recorded maximum)."""
+    """The stem's MaxPool2d(3, stride 2, padding 1) on channels-last bf16 activations (pool.hip on
+    the GPU; the backward routes each gradient to its window's recorded maximum)."""
 
     def __init__(self):
         super().__init__(3, stride=2, padding=1)
 
     def forward(self, x):
-        return _MaxPool.apply(x) if _native_nhwc(x) else super().forward(x)
+        return _MaxPool.apply(_require_nhwc_bf16(x, "max-pool input"))
 
 
 class _AvgPool(torch.autograd.Function):
@@ -339,10 +337,8 @@ class _AvgPool(torch.autograd.Function):
 
 
 def global_avgpool(x):
-    """AdaptiveAvgPool2d(1) + flatten -> [N, C] (pool.hip on channels-last bf16 GPU activations)."""
-    if _native_nhwc(x):
-        return _AvgPool.apply(x)
-    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+    """AdaptiveAvgPool2d(1) + flatten -> [N, C] of channels-last bf16 activations (pool.hip)."""
+    return _AvgPool.apply(_require_nhwc_bf16(x, "average-pool input"))
 
 
 class Bottleneck(nn.Module):
@@ -363,18 +359,19 @@ class Bottleneck(nn.Module):
         # the previous block's bn3 backward preparation can ride in conv1's data gradient only when
         # that gradient is the whole gradient of x: identity block, identity gradient linked in
         in_link = getattr(x, "_dedloc_bn_link", None)
-        fused_bwd = _BN_BWD_EPI and x.is_cuda and x.requires_grad and torch.is_grad_enabled()
+        fused_bwd = x.requires_grad and torch.is_grad_enabled()
         if self.downsample is None:
             idt = x
-            if _RES_LINK and x.is_cuda and x.requires_grad and torch.is_grad_enabled():
+            if fused_bwd:
                 link = _GradLink()
         else:
             conv, bn = self.downsample[0], self.downsample[1]
             idt = bn(conv(x, bn))
-        l1 = _BnBwdLink() if fused_bwd and _BN_BWD_EPI_3X3 else None
-        out = self.bn1(self.conv1(x, self.bn1, link, in_link if link is not None else None), bwd_link=l1)
+        # bn1's backward preparation stays in the BN backward: in the 3x3 conv2's data-gradient
+        # epilogue the extra X reads cost what its statistics pass saves (profiles/README.md r3)
+        out = self.bn1(self.conv1(x, self.bn1, link, in_link if link is not None else None))
         l2 = _BnBwdLink() if fused_bwd else None
-        out = self.bn2(self.conv2(out, self.bn2, bn_link=l1), bwd_link=l2)
+        out = self.bn2(self.conv2(out, self.bn2), bwd_link=l2)
         l3 = _BnBwdLink() if fused_bwd else None
         y = self.bn3(self.conv3(out, self.bn3, bn_link=l2), idt, link, bwd_link=l3)
         if l3 is not None:
@@ -423,8 +420,7 @@ class ResNet50Trunk(nn.Module):
         num_batches_tracked counters (instead of two memsets and one add launch per BatchNorm; each
         is a ~5 us kernel at b=64).  Returns the per-BatchNorm workspace slices for ``forward``'s
         ``prepared`` (None: the per-call path)."""
-        if (not self.pass_workspace or not self.training or self.checkpoint_stages or not x.is_cuda
-                or x.dtype != torch.bfloat16 or not x.is_contiguous(memory_format=torch.channels_last)):
+        if not self.pass_workspace or not self.training or self.checkpoint_stages:
             return None
         bns = self._bn_modules()
         G = bns[0].stat_groups
@@ -503,15 +499,13 @@ class _HeadLinearFn(torch.autograd.Function):
 
 
 class HeadLinear(nn.Linear):
-    """``nn.Linear`` (same parameters / keys) on the dedloc GEMM kernels for GPU inputs."""
+    """``nn.Linear`` (same parameters / keys) on the dedloc GEMM operators (bf16, fp32 accumulation)."""
 
     inplace_grad = True
     _wb_cache = None  # bf16 weight view set by SwAVModel.forward (the flat buffer's bf16 mirror)
 
     def forward(self, x):
-        if x.is_cuda:
-            return _HeadLinearFn.apply(x.to(torch.bfloat16).contiguous(), self.weight, self.bias, self)
-        return super().forward(x)
+        return _HeadLinearFn.apply(x.to(torch.bfloat16).contiguous(), self.weight, self.bias, self)
 
 
 class HeadBN1dReLU(nn.BatchNorm1d):
@@ -522,13 +516,15 @@ class HeadBN1dReLU(nn.BatchNorm1d):
     stat_groups = 1
 
     def forward(self, x):
-        if self.training and x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous():
-            N, C = x.shape
-            self.num_batches_tracked.add_(1)
-            y = _BNAct.apply(x.view(N, C, 1, 1), self.weight, self.bias, None, self.running_mean, self.running_var,
-                             True, self.eps, self.momentum, 1, None, self)
-            return y.view(N, C)
-        return F.relu(super().forward(x))
+        if not self.training:
+            return _bn_eval(self, x, None, True)
+        if x.dtype != torch.bfloat16 or x.dim() != 2 or not x.is_contiguous():
+            raise ValueError(f"HeadBN1dReLU: expected a contiguous [N, C] bf16 input, got {x.dtype} {tuple(x.shape)}")
+        N, C = x.shape
+        self.num_batches_tracked.add_(1)
+        y = _BNAct.apply(x.view(N, C, 1, 1), self.weight, self.bias, None, self.running_mean, self.running_var,
+                         True, self.eps, self.momentum, 1, None, self)
+        return y.view(N, C)
 
 
 class _L2Norm(torch.autograd.Function):
@@ -545,10 +541,10 @@ class _L2Norm(torch.autograd.Function):
 
 
 def l2_normalize(x, eps: float = 1e-12):
-    """F.normalize(x, p=2, dim=1) (pool.hip on GPU rows of up to 1024 values)."""
-    if x.is_cuda and x.dim() == 2 and x.shape[1] <= 1024:
-        return _L2Norm.apply(x.to(torch.bfloat16).contiguous(), eps)
-    return F.normalize(x, dim=1, p=2, eps=eps)
+    """F.normalize(x, p=2, dim=1) of [N, D] rows, D <= 1024 (pool.hip on the GPU)."""
+    if x.dim() != 2 or x.shape[1] > 1024:
+        raise ValueError(f"l2_normalize: rows of at most 1024 values, got {tuple(x.shape)}")
+    return _L2Norm.apply(x.to(torch.bfloat16).contiguous(), eps)
 
 
 class SwAVPrototypesHead(nn.Module):
@@ -627,7 +623,8 @@ class SwAVModel(nn.Module):
 
     def _concurrent_ok(self, groups) -> bool:
         x = groups[0][0]
-        return (self.concurrent_passes and len(groups) == 2 and self._flat is not None and x.is_cuda
+        return (self.concurrent_passes and len(groups) == 2 and self._flat is not None
+                and x.device.type == "cuda"  # a second HIP stream
                 and self.training and torch.is_grad_enabled() and ResNet50Trunk.pass_workspace
                 and not self.trunk.checkpoint_stages and BNAct.inplace_grad and ConvNHWC.inplace_wgrad
                 and all(m.momentum is not None for m in self.trunk._bn_modules())
@@ -740,11 +737,7 @@ class SwAVModel(nn.Module):
     @torch.no_grad()
     def normalize_prototypes(self):
         """NormalizePrototypesHook (swav_hooks.py:63-92): L2-normalise every prototype row."""
-        w = self.heads[0].prototypes0.weight.data
-        if w.is_cuda:
-            torch.ops.dedloc.row_normalize_(w)
-        else:
-            w.div_(w.norm(dim=1, keepdim=True).clamp_min(1e-12))
+        torch.ops.dedloc.row_normalize_(self.heads[0].prototypes0.weight.data)
 
     def prototype_param_names(self):
         return [n for n, _ in self.named_parameters() if "prototypes" in n]

@@ -94,11 +94,9 @@ class SwAVLoss(nn.Module):
         return loss
 
     def _queue_scores(self, i, prototypes):
-        """Scores of queue i against the prototypes, [L, K] fp32: on the GPU the own GEMM kernels
-        (bf16 operands like the batch's prototype scores, fp32 accumulation and output)."""
+        """Scores of queue i against the prototypes, [L, K] fp32, on the GEMM operators (bf16 operands
+        like the batch's prototype scores, fp32 accumulation and output)."""
         q = self.queue[i]
-        if not q.is_cuda:
-            return q @ prototypes.detach().float().t()
         out = torch.zeros(q.shape[0], prototypes.shape[0], dtype=torch.float32, device=q.device)
         torch.ops.dedloc.gemm_acc_f32(q.to(torch.bfloat16), prototypes.detach().to(torch.bfloat16), out, False, True)
         return out

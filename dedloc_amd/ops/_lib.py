@@ -624,9 +624,35 @@ def _bn_bwd_prep_cpu(g, x, y, mean, rstd, gamma, beta, sums, groups):
     return g
 
 
+@_impl("im2col_stem")
+def _im2col_stem_cpu(x, R, S, stride, pad):
+    # the GPU builds the stem's column matrix once per pass for the forward and the weight gradient;
+    # the CPU implementations convolve the image directly, so the "column matrix" they hand through
+    # is (a copy of) the image itself (conv2d_wgrad(cols=...) below reads it back)
+    return x.clone()
+
+
+@_impl("conv2d_dgrad_weights")
+def _conv2d_dgrad_weights_cpu(w, stride, pad):
+    # per parity class (a, b) of a stride-s conv, the contributing taps, transposed to [C][R'][S'][K]
+    # (the same tensors as the GPU op; the CPU data gradient does not need them)
+    wk = w.permute(0, 2, 3, 1)
+    R, S = wk.shape[1], wk.shape[2]
+    out = []
+    for a in range(stride):
+        for b in range(stride):
+            r0, s0 = (a + pad) % stride, (b + pad) % stride
+            if r0 < R and s0 < S:
+                out.append(wk[:, r0::stride, s0::stride, :].permute(3, 1, 2, 0).contiguous())
+            else:
+                out.append(torch.empty(0, dtype=w.dtype))
+    return out
+
+
 @_impl("conv2d_wgrad")
 def _conv2d_wgrad_cpu(dy, x, dw, stride, pad, cols=None):
-    dw.add_(torch.nn.grad.conv2d_weight(x.float(), dw.shape, dy.float(), stride=stride, padding=pad))
+    src = cols if cols is not None and cols.dim() == 4 else x  # the stem: im2col_stem handed the image
+    dw.add_(torch.nn.grad.conv2d_weight(src.float(), dw.shape, dy.float(), stride=stride, padding=pad))
 
 
 @_impl("bn_bwd")

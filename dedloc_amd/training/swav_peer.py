@@ -14,6 +14,10 @@ Per local iteration (reference ``vissl/trainer/train_steps/standard_train_step.p
 Deliberate differences: bf16 autocast instead of apex O1 fp16 + loss scaling (V15); activation
 checkpointing off by default (P11); optimizer state is shared through the DHT state server and saved
 in local checkpoints (the reference's ``get_classy_state`` returns None, D17).
+
+``impl="eager"`` swaps the model, loss and optimizer for the stock-PyTorch stack of
+``training/swav_eager.py`` (the measured SwAV baseline); data, hooks and the collaborative engine
+stay the same.
 """
 from __future__ import annotations
 
@@ -58,39 +62,58 @@ def _port_endpoint(port) -> str:
 
 
 class SwavPeer:
-    def __init__(self, cfg, device, dht: Optional[DHT] = None, rank: int = 0):
-        self.cfg = cfg
+    def __init__(self, cfg, device, dht: Optional[DHT] = None, rank: int = 0, impl: str = "dedloc"):
+        if impl not in ("dedloc", "eager"):
+            raise ValueError(f"impl must be 'dedloc' or 'eager', got {impl!r}")
+        self.cfg, self.impl = cfg, impl
         self.device = torch.device(device)
         torch.manual_seed(int(cfg.get("SEED_VALUE", 0)))
         mcfg, lcfg, ocfg = cfg.MODEL, cfg.LOSS.swav_loss, cfg.OPTIMIZER
         dcfg = cfg.DATA.TRAIN
         self.batch_size = int(dcfg.BATCHSIZE_PER_REPLICA)
-        self.model = SwAVModel(num_prototypes=int(mcfg.HEAD.num_clusters),
-                               single_pass_every_crop=bool(mcfg.SINGLE_PASS_EVERY_CROP),
-                               checkpoint_stages=bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING),
-                               conv_impl=mcfg.get("CONV_IMPL") or None)
-        self.model.to(self.device).train()
+        if impl == "eager":
+            from .swav_eager import EagerSwAVModel
+
+            self.model = EagerSwAVModel(num_prototypes=int(mcfg.HEAD.num_clusters),
+                                        single_pass_every_crop=bool(mcfg.SINGLE_PASS_EVERY_CROP))
+            self.model.to(self.device, memory_format=torch.channels_last)
+        else:
+            self.model = SwAVModel(num_prototypes=int(mcfg.HEAD.num_clusters),
+                                   single_pass_every_crop=bool(mcfg.SINGLE_PASS_EVERY_CROP),
+                                   checkpoint_stages=bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING),
+                                   conv_impl=mcfg.get("CONV_IMPL") or None)
+            self.model.to(self.device)
+        self.model.train()
         hooks = cfg.get("HOOKS") or {}
         self.check_nan = bool(hooks.get("CHECK_NAN", True))
         self.log_frequency = max(1, int(cfg.get("LOG_FREQUENCY", 10)))
         # vissl PerfTimer/LogPerfTimeMetricsHook (V20): HIP-event phase timers, reported per global step
         self.perf = PerfStats(self.device, enabled=bool(hooks.get("PERF_STATS", True)))
         self.flat = FlatParams(self.model.named_parameters(), device=self.device,
-                               with_bf16=self.device.type == "cuda", autograd=True,
+                               with_bf16=self.device.type == "cuda" and impl == "dedloc", autograd=True,
                                channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
-        self.model.bind_flat(self.flat)  # GEMM / conv weights read from the flat buffer's bf16 mirror
-        # the two crop resolutions' trunk passes on two streams (SwAVModel.concurrent_passes; this
-        # trainer calls after_backward after every backward)
-        self.model.concurrent_passes = bool(cfg.MODEL.get("CONCURRENT_PASSES", True))
+        if impl == "dedloc":
+            self.model.bind_flat(self.flat)  # GEMM / conv weights read from the flat buffer's bf16 mirror
+            # the two crop resolutions' trunk passes on two streams (SwAVModel.concurrent_passes; this
+            # trainer calls after_backward after every backward)
+            self.model.concurrent_passes = bool(cfg.MODEL.get("CONCURRENT_PASSES", True))
         self.model.normalize_prototypes()
         larc = ocfg.larc_config
         assert ocfg.use_larc, "we can't use collab sgd without larc (sgd_collaborative.py:138)"
-        self.opt = FusedLarcSGD(self.flat, lr=float(ocfg.lr), momentum=float(ocfg.momentum),
-                                weight_decay=float(ocfg.weight_decay), nesterov=bool(ocfg.nesterov),
-                                trust_coefficient=float(larc.trust_coefficient), clip=bool(larc.clip),
-                                eps=float(larc.eps),
-                                no_decay=_no_decay_names(self.model, bool(ocfg.regularize_bn),
-                                                         bool(ocfg.regularize_bias)))
+        no_decay = _no_decay_names(self.model, bool(ocfg.regularize_bn), bool(ocfg.regularize_bias))
+        if impl == "eager":
+            from .swav_eager import EagerLarcSGD
+
+            assert not bool(ocfg.nesterov), "nesterov LARC-SGD is not used by the reference"
+            self.opt = EagerLarcSGD(self.flat, lr=float(ocfg.lr), momentum=float(ocfg.momentum),
+                                    weight_decay=float(ocfg.weight_decay),
+                                    trust_coefficient=float(larc.trust_coefficient), clip=bool(larc.clip),
+                                    eps=float(larc.eps), no_decay=no_decay)
+        else:
+            self.opt = FusedLarcSGD(self.flat, lr=float(ocfg.lr), momentum=float(ocfg.momentum),
+                                    weight_decay=float(ocfg.weight_decay), nesterov=bool(ocfg.nesterov),
+                                    trust_coefficient=float(larc.trust_coefficient), clip=bool(larc.clip),
+                                    eps=float(larc.eps), no_decay=no_decay)
         self.scheduler = LinearWarmupCosineAnnealingLR(self.opt, warmup_epochs=int(ocfg.warmup_epochs),
                                                        max_epochs=int(ocfg.max_epochs),
                                                        warmup_start_lr=float(ocfg.warmup_start_lr),
@@ -110,7 +133,10 @@ class SwavPeer:
             metadata_expiration=float(ocfg.get("metadata_expiration", 30)),
             averaging_timeout=float(ocfg.get("averaging_timeout", 30)), device=self.device)
         q = lcfg.queue
-        self.loss_fn = SwAVLoss(num_crops=sum(dcfg.MULTICROP.num_crops), crops_for_assign=lcfg.crops_for_assign,
+        loss_cls = SwAVLoss
+        if impl == "eager":
+            from .swav_eager import EagerSwAVLoss as loss_cls
+        self.loss_fn = loss_cls(num_crops=sum(dcfg.MULTICROP.num_crops), crops_for_assign=lcfg.crops_for_assign,
                                 temperature=float(lcfg.temperature), epsilon=float(lcfg.epsilon),
                                 num_iters=int(lcfg.num_iters), num_prototypes=int(mcfg.HEAD.num_clusters),
                                 embedding_dim=int(mcfg.HEAD.dims[-1]), queue_length=int(q.queue_length),
@@ -131,7 +157,7 @@ class SwavPeer:
             self.data = StreamPrefetcher(self.data, self.device)  # next batch's crops under this step's compute
         self.frozen = [(name, int(iters)) for name, iters in (mcfg.get("TEMP_FROZEN_PARAMS_ITER_MAP") or [])]
         self.use_graph = bool(mcfg.get("CUDA_GRAPH", False)) and self.device.type == "cuda" and \
-            not bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING)
+            not bool(mcfg.ACTIVATION_CHECKPOINTING.USE_ACTIVATION_CHECKPOINTING) and impl == "dedloc"
         self.graph_warmup = int(mcfg.get("CUDA_GRAPH_WARMUP", 3))  # eager iterations before the capture
         self._graphed = None
         self.iteration = 0
@@ -222,7 +248,8 @@ class SwavPeer:
                 proto = self.model.heads[0].prototypes0.weight
                 loss = self.loss_fn(emb.float(), scores, proto, training_iterations=int(self.collab_opt.local_step))
                 loss.backward()
-                self.model.after_backward()
+                if self.impl == "dedloc":
+                    self.model.after_backward()
         for name, iters in self.frozen:  # FreezeParametersHook (state_update_hooks.py:235-280)
             if self.iteration < iters:
                 name = name[len("module."):] if name.startswith("module.") else name

@@ -780,3 +780,38 @@ def test_gemm8_persistent_deferred_stores_bitwise(cuda, monkeypatch, M, N, K):
                 assert torch.equal(o, e), (ctas, nt, i, (o.float() - e.float()).abs().max().item())
     ref = x.float() @ w.float().t() + b
     assert rel(base[0], ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 1024), (3000, 3072, 256), (1000, 256, 128), (512, 512, 64),
+                                   (777, 1024, 4096)])
+def test_gemm8_half_tiles_bitwise(cuda, monkeypatch, M, N, K):
+    """gemm8h (DEDLOC_GEMM8_HALF=1: 256 x 128 tiles on 4 waves, two co-resident workgroups per CU,
+    3 + 4 half-tile LDS ring with one barrier per phase) accumulates every output in the same order
+    as gemm8: bitwise equal for every bf16 epilogue (bias, residual, bias + GELU, GELU' + bias
+    gradient, plain), with M tails and K-tile counts 1 .. 64, and within bf16 rounding of fp32."""
+    torch.manual_seed(29)
+    x = (torch.rand(M, K, device=cuda) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device=cuda) * 2 - 1) * 0.1).bfloat16()
+    b = torch.randn(N, device=cuda)
+    r = torch.randn(M, N, device=cuda).bfloat16()
+    f = torch.randn(M, N, device=cuda).bfloat16()
+    dy = (torch.rand(M, K, device=cuda) * 2 - 1).bfloat16()
+
+    def run():
+        db = torch.zeros(N, device=cuda)
+        return [OPS.gemm(x, w, b, None, False, True, 0), OPS.gemm(x, w, b, r, False, True, 0),
+                *OPS.gemm_gelu(x, w, b), OPS.gemm(x, w, None, None, False, True, 0),
+                OPS.gemm_dgelu(dy, w, f, db, True), db, OPS.gemm(dy, w, None, r, False, True, 0)]
+
+    monkeypatch.setenv("DEDLOC_GEMM8_HALF", "0")
+    base = run()
+    monkeypatch.setenv("DEDLOC_GEMM8_HALF", "1")
+    out = run()
+    torch.cuda.synchronize()
+    for i, (o, e) in enumerate(zip(out, base)):
+        if e.dtype == torch.float32:  # dbias: atomics in a different order
+            torch.testing.assert_close(o, e, rtol=1e-5, atol=1e-4)
+        else:
+            assert torch.equal(o, e), (i, (o.float() - e.float()).abs().max().item())
+    assert rel(out[0], x.float() @ w.float().t() + b) < 1e-2
+    assert rel(out[-1], dy.float() @ w.float().t() + r.float()) < 1e-2

@@ -67,7 +67,8 @@ def test_swav_loss_and_grad_vs_vissl(use_queue):
     loss = crit(emb, scores, protos, training_iterations=7)
     (g,) = torch.autograd.grad(loss, scores)
     s2 = scores.detach().clone().requires_grad_(True)
-    qs = [queue_before[i] @ protos.t() for i in range(2)] if use_queue else None
+    # queue scores: bf16 operands, fp32 accumulation (the precision of every prototype-score GEMM)
+    qs = [queue_before[i].bfloat16().float() @ protos.bfloat16().float().t() for i in range(2)] if use_queue else None
     ref = vissl_loss(s2, bs, nc, (0, 1), 0.05, 3, 0.1, qs)
     (gref,) = torch.autograd.grad(ref, s2)
     assert abs(loss.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
@@ -235,6 +236,29 @@ def test_swav_peer_cpu_steps_and_checkpoint(tmp_path):
         dht.shutdown()
 
 
+def test_swav_peer_eager_stack_cpu_steps(tmp_path):
+    """SwavPeer(impl="eager") — stock nn modules, vissl-formula loss, apex LARC in torch ops (the
+    measured SwAV baseline of bench.py --impl eager) — runs collaborative iterations, and loads the
+    dedloc model's parameters by state-dict key."""
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.models.resnet_swav import SwAVModel
+    from dedloc_amd.training.swav_peer import SwavPeer
+
+    cfg = _tiny_cfg([f"config.CHECKPOINT.DIR={tmp_path}"])
+    dht = DHT(start=True)
+    peer = SwavPeer(cfg, "cpu", dht=dht, impl="eager")
+    try:
+        assert not any(type(m).__module__.startswith("dedloc_amd.models") for m in peer.model.modules())
+        peer.model.load_state_dict(SwAVModel(num_prototypes=int(cfg.MODEL.HEAD.num_clusters)).state_dict())
+        losses = [float(peer.train_step()) for _ in range(2)]
+        assert all(math.isfinite(x) for x in losses)
+        w = peer.model.heads[0].prototypes0.weight
+        assert torch.allclose(w.norm(dim=1), torch.ones(w.shape[0]), atol=1e-5)
+    finally:
+        peer.shutdown()
+        dht.shutdown()
+
+
 # ----------------------------------------------------------------------------- GPU tier
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,bs,K", [(64, 64, 3000), (64 + 3840, 64, 3000), (100, 37, 777)])
@@ -244,7 +268,7 @@ def test_sinkhorn_gpu_vs_fp32_reference(cuda, n, bs, K):
     p = torch.nn.functional.normalize(torch.randn(K, 128, device=cuda), dim=1)
     s = (e @ p.t()).contiguous()
     q = torch.ops.dedloc.sinkhorn(s, bs, 0.03, 3)
-    ref = torch.ops.dedloc.sinkhorn(s.cpu(), bs, 0.03, 3)
+    ref = vissl_sinkhorn(s.cpu(), 0.03, 3)[-bs:]  # vissl's formula (fp64 Sinkhorn), the op emits the last bs rows
     assert q.shape == (bs, K)
     assert torch.allclose(q.cpu(), ref, atol=1e-6, rtol=2e-3), (q.cpu() - ref).abs().max()
 
@@ -272,6 +296,31 @@ def test_row_normalize_gpu(cuda):
     ref = torch.nn.functional.normalize(w, dim=1)
     torch.ops.dedloc.row_normalize_(w)
     assert torch.allclose(w, ref, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_swav_loss_gpu_matches_vissl_formula(cuda):
+    """The GPU SwAV loss (Sinkhorn and cross-entropy kernels, queue scores on the GEMM kernels)
+    against vissl's formulas in plain fp32 PyTorch (vissl_loss above), loss and score gradient."""
+    torch.manual_seed(2)
+    bs, nc, K, D, L = 16, 8, 3000, 128, 64
+    protos = torch.nn.functional.normalize(torch.randn(K, D), dim=1)
+    emb = torch.nn.functional.normalize(torch.randn(nc * bs, D), dim=1)
+    scores = emb @ protos.t()
+    crit = SwAVLoss(num_crops=nc, crops_for_assign=(0, 1), num_prototypes=K, embedding_dim=D, queue_length=L,
+                    queue_start_iter=0, batch_size=bs).to(cuda)
+    queue_before = crit.queue.cpu().clone()
+    s_gpu = scores.to(cuda).requires_grad_(True)
+    loss = crit(emb.to(cuda), s_gpu, protos.to(cuda), 5)
+    loss.backward()
+    s_ref = scores.clone().requires_grad_(True)
+    qs = [queue_before[i].bfloat16().float() @ protos.bfloat16().float().t() for i in range(2)]
+    ref = vissl_loss(s_ref, bs, nc, (0, 1), 0.03, 3, 0.1, qs)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-3 * abs(ref.item())
+    g, gr = s_gpu.grad.cpu(), s_ref.grad
+    assert ((g - gr).norm() / gr.norm()).item() < 1e-3
+    assert (g - gr).abs().max().item() < 1e-2 * gr.abs().max().item()
 
 
 @pytest.mark.gpu

@@ -128,13 +128,14 @@ def test_bottleneck_conv_stats_match_separate_pass(cuda, monkeypatch):
         bns = [mod for mod in m.modules() if isinstance(mod, rs.BNAct)]
         x = torch.randn(4, cin, 16, 16, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
         outs = []
-        for flag in (True, False):
-            monkeypatch.setattr(rs, "_CONV_STATS", flag)
+        for with_ws in (True, False):  # pass workspace: statistics from the conv epilogues; none: bn_fwd's pass
             ws = torch.zeros(sum(4 * 2 * b.num_features for b in bns), device=cuda)
             off = 0
             for b in bns:  # the trunk's per-pass workspace, as ResNet50Trunk._prepare_bn_pass lays it out
                 n = 2 * 2 * b.num_features
-                b.stat_groups, b.pass_ws, b.count_deferred = 2, (ws[off:off + n], ws[off + n:off + 2 * n]), True
+                b.stat_groups = 2
+                b.pass_ws = (ws[off:off + n], ws[off + n:off + 2 * n]) if with_ws else None
+                b.count_deferred = with_ws
                 off += 2 * n
             with torch.no_grad():
                 outs.append(m(x).float())
@@ -164,8 +165,9 @@ def test_conv_dgrad_residual_epilogue(cuda, cin, cout):
     (64, 64, 3, 2, 4, False, False, False)])   # class rows per group 128: not fused -> prep pass
 def test_conv_dgrad_bn_matches_reference(cuda, cin, cout, k, stride, N, ymask, res, expect_fused):
     """conv2d_dgrad_bn (BN+ReLU backward preparation in the data-gradient epilogue; where it reports
-    not fused, the plain gradient followed by the separate bn_bwd_prep pass) against the op's fp32
-    CPU reference: the ReLU-masked gradient and the two backward sums."""
+    not fused, the plain gradient followed by the separate bn_bwd_prep pass) against plain fp32
+    PyTorch: the data gradient (+ residual) masked by the BN+ReLU's live outputs, and the BN
+    backward's two per-group column sums."""
     torch.manual_seed(7)
     CLF = torch.channels_last
     G, H = 2, 16
@@ -183,12 +185,20 @@ def test_conv_dgrad_bn_matches_reference(cuda, cin, cout, k, stride, N, ymask, r
     assert fused == expect_fused
     if not fused:
         g = torch.ops.dedloc.bn_bwd_prep(g, x, y, mean, rstd, gamma, beta, sums, G)
-    cpu = lambda t: None if t is None else t.cpu()  # noqa: E731
-    sums_ref = torch.zeros(G * 2 * cin)
-    g_ref, _ = torch.ops.dedloc.conv2d_dgrad_bn(dy.cpu(), w.cpu(), stride, k // 2, H, H, cpu(r), x.cpu(), cpu(y),
-                                                mean.cpu(), rstd.cpu(), gamma.cpu(), beta.cpu(), sums_ref, G)
-    torch.testing.assert_close(g.float().cpu(), g_ref.float(), rtol=2e-2, atol=3e-2)
-    torch.testing.assert_close(sums.cpu(), sums_ref, rtol=2e-2, atol=2.0)
+    # fp32 PyTorch reference
+    d = torch.nn.grad.conv2d_input((N, cin, H, H), w.float(), dy.float(), stride=stride, padding=k // 2)
+    if r is not None:
+        d = d + r.float()
+    shp = (G, N // G, cin, H, H)
+    xf, mu, rs_ = x.float().reshape(shp), mean.view(G, 1, cin, 1, 1), rstd.view(G, 1, cin, 1, 1)
+    if y is not None:
+        live = y.float().reshape(shp) > 0
+    else:
+        live = (xf - mu) * rs_ * gamma.view(1, 1, cin, 1, 1) + beta.view(1, 1, cin, 1, 1) > 0
+    gr = torch.where(live, d.reshape(shp), torch.zeros(()))
+    sums_ref = torch.stack([gr.sum((1, 3, 4)), (gr * (xf - mu) * rs_).sum((1, 3, 4))], 1).reshape(-1)
+    torch.testing.assert_close(g.float(), gr.reshape(N, cin, H, H), rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(sums, sums_ref, rtol=2e-2, atol=2.0)
 
 
 def test_swav_queue_scores_on_own_gemm(cuda):
