@@ -716,13 +716,33 @@ at::Tensor sinkhorn(const at::Tensor& scores, int64_t bs, double eps, int64_t it
   expect(scores, at::kFloat, "scores");
   const int64_t n = scores.size(0), K = scores.size(1);
   TORCH_CHECK(bs <= n, "bs > rows");
-  auto P = at::empty_like(scores);
   auto Q = at::empty({bs, K}, scores.options());
-  auto ws = at::empty({2 * K + 1}, scores.options());
-  check(dl_sinkhorn(f32(scores), f32(P), f32(Q), f32(ws), (int)n, (int)K, (int)bs, (float)eps, (int)iters,
+  auto ws = at::empty({(int64_t)dl_sinkhorn_ws((int)n, (int)K)}, scores.options());
+  check(dl_sinkhorn(f32(scores), f32(Q), f32(ws), (int)n, (int)K, (int)bs, (float)eps, (int)iters,
                     cur_stream(scores)),
         "sinkhorn");
   return Q;
+}
+
+// every (assignment crop, other crop) pair of the SwAV loss in one launch: scores [num_crops * bs, K]
+// (bf16 / fp32), q [n_assign, bs, K] fp32, crops = the assignments' crop ids; ds [num_crops * bs, K]
+// fp32 is written, loss [1] accumulated
+void swav_ce_multi(const at::Tensor& scores, const at::Tensor& q, at::IntArrayRef crops, at::Tensor dscores,
+                   at::Tensor loss, double temperature, double scale) {
+  TORCH_CHECK(scores.is_cuda() && scores.is_contiguous() && scores.dim() == 2, "scores: contiguous [rows, K] GPU");
+  TORCH_CHECK(scores.scalar_type() == at::kFloat || scores.scalar_type() == at::kBFloat16, "scores dtype");
+  expect(q, at::kFloat, "q");
+  expect(dscores, at::kFloat, "dscores");
+  expect(loss, at::kFloat, "loss");
+  const int64_t K = scores.size(1), na = (int64_t)crops.size();
+  TORCH_CHECK(na >= 1 && na <= 4 && q.dim() == 3 && q.size(0) == na && q.size(2) == K, "q: [n_assign <= 4, bs, K]");
+  const int64_t bs = q.size(1);
+  TORCH_CHECK(scores.size(0) % bs == 0 && dscores.numel() == scores.numel(), "scores / dscores shape");
+  std::vector<int> cr(crops.begin(), crops.end());
+  check(dl_swav_ce_multi(scores.data_ptr(), scores.scalar_type() == at::kBFloat16, f32(q), cr.data(), (int)na,
+                         f32(dscores), f32(loss), (int)(scores.size(0) / bs), (int)bs, (int)K, (float)temperature,
+                         (float)scale, cur_stream(scores)),
+        "swav_ce_multi");
 }
 
 void swav_ce(const at::Tensor& scores, const at::Tensor& q, at::Tensor dscores, at::Tensor loss, double temperature,
@@ -1323,6 +1343,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("bn_bwd", &bn_bwd);
   m.impl("sinkhorn", &sinkhorn);
   m.impl("swav_ce", &swav_ce);
+  m.impl("swav_ce_multi", &swav_ce_multi);
   m.impl("row_normalize_", &row_normalize_);
   m.impl("maxpool_fwd", &maxpool_fwd);
   m.impl("maxpool_bwd", &maxpool_bwd);

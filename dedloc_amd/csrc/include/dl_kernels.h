@@ -86,10 +86,14 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
              float* stats = nullptr, long stat_rows = 0, const DlBnBwdEpi* bn = nullptr);
 
 // swav.hip
-int dl_sinkhorn(const float* scores, float* P, float* Q, float* ws, int n, int K, int bs, float eps, int iters,
+int dl_sinkhorn_ws(int n, int K);
+int dl_sinkhorn(const float* scores, float* Q, float* ws, int n, int K, int bs, float eps, int iters,
                 hipStream_t st);
 int dl_swav_ce(const void* scores, int scores_bf16, const float* q, float* dscores, float* loss, int rows, int K,
                float temperature, float scale, hipStream_t st);
+int dl_swav_ce_multi(const void* scores, int scores_bf16, const float* q, const int* crops, int n_assign,
+                     float* dscores, float* loss, int num_crops, int bs, int K, float temperature, float scale,
+                     hipStream_t st);
 int dl_row_normalize(float* w, int rows, int d, hipStream_t st);
 // SwAV multi-crop augmentation (augment.hip): pool [P, 3, Hp, Wp] fp32, params [nb, 20] fp32,
 // ws >= 2 * nb*3*S*S + nb floats, out [nb, S, S, 3] bf16 (channels-last [nb, 3, S, S])

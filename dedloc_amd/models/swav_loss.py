@@ -4,8 +4,9 @@ Reference: ``swav/vissl/vissl/losses/swav_loss.py:24-380`` (SwAVLoss/SwAVCriteri
 the DeDLOC modification (``:84-91``, D18): the queue switches on at a *global collaborative* step
 (``queue_start_iter`` compared with ``collaboration_state.optimizer_step``), not a local iteration.
 
-Device path: Sinkhorn-Knopp and the fused log-softmax x assignment cross-entropy (fwd + bwd in one
-pass) are HIP kernels (csrc/kernels/swav.hip); the queue is a ring buffer (no shifting copies).
+Device path: Sinkhorn-Knopp (column-owning workgroups, two scale vectors instead of a rewritten
+matrix) and the fused log-softmax x assignment cross-entropy of every crop pair (fwd + bwd in one
+launch) are HIP kernels (csrc/kernels/swav.hip); the queue is a ring buffer (no shifting copies).
 """
 from __future__ import annotations
 
@@ -22,22 +23,18 @@ logger = logging.getLogger(__name__)
 
 
 class _SwAVCE(torch.autograd.Function):
-    """sum over (assignment crop i, other crop v) of -mean_b <q_i, log_softmax(s_v / T)>."""
+    """sum over (assignment crop i, other crop v) of -mean_b <q_i, log_softmax(s_v / T)>, every pair in
+    one launch (swav_ce_multi: each crop's score row and its log-sum-exp are read once)."""
 
     @staticmethod
     def forward(ctx, scores, assignments, crops_for_assign, num_crops, bs, temperature):
-        ops = torch.ops.dedloc
         s = scores.contiguous()
-        ds = torch.zeros(s.shape, dtype=torch.float32, device=s.device)
+        ds = torch.empty(s.shape, dtype=torch.float32, device=s.device)
         loss = torch.zeros(1, dtype=torch.float32, device=s.device)
         n_pairs = (num_crops - 1) * len(crops_for_assign)
-        for i, crop_id in enumerate(crops_for_assign):
-            q = assignments[i]
-            for v in range(num_crops):
-                if v == crop_id:
-                    continue
-                ops.swav_ce(s[bs * v: bs * (v + 1)].contiguous(), q, ds[bs * v: bs * (v + 1)], loss, temperature,
-                            1.0 / (bs * n_pairs))
+        q = torch.stack(assignments) if len(assignments) > 1 else assignments[0].unsqueeze(0)
+        torch.ops.dedloc.swav_ce_multi(s, q.contiguous(), list(crops_for_assign), ds, loss, temperature,
+                                       1.0 / (bs * n_pairs))
         ctx.save_for_backward(ds)
         ctx.dtype = scores.dtype
         return loss.squeeze(0)

@@ -50,6 +50,8 @@ _SCHEMAS = [
     "gemm_gelu(Tensor x, Tensor w, Tensor bias, bool trans_w=False) -> (Tensor, Tensor)",
     "sinkhorn(Tensor scores, int bs, float eps, int iters) -> Tensor",
     "swav_ce(Tensor scores, Tensor q, Tensor(a!) dscores, Tensor(b!) loss, float temperature, float scale) -> ()",
+    "swav_ce_multi(Tensor scores, Tensor q, int[] crops, Tensor(a!) dscores, Tensor(b!) loss, float temperature, "
+    "float scale) -> ()",
     "row_normalize_(Tensor(a!) w) -> ()",
     "maxpool_fwd(Tensor x) -> (Tensor, Tensor)",
     "maxpool_bwd(Tensor dy, Tensor arg, int H, int W) -> Tensor",
@@ -490,6 +492,26 @@ def _swav_ce_cpu(scores, q, dscores, loss, temperature, scale):
     qs = q.sum(-1, keepdim=True)
     loss.add_(-(q * logp).sum() * scale)
     dscores.add_((torch.softmax(x, -1) * qs - q) / temperature * scale)
+
+
+@_impl("swav_ce_multi")
+def _swav_ce_multi_cpu(scores, q, crops, dscores, loss, temperature, scale):
+    n_assign, bs, K = q.shape
+    nc = scores.shape[0] // bs
+    x = scores.float().view(nc, bs, K) / temperature
+    lsm = torch.log_softmax(x, dim=-1)
+    sm = lsm.exp()
+    ds = torch.zeros(nc, bs, K)
+    tot = torch.zeros(())
+    for i, cid in enumerate(crops):
+        for v in range(nc):
+            if v == cid:
+                continue
+            qi = q[i]
+            tot = tot - (qi * lsm[v]).sum()
+            ds[v] += sm[v] * qi.sum(-1, keepdim=True) - qi
+    loss.add_(tot * scale)
+    dscores.copy_((ds * (scale / temperature)).view_as(dscores))
 
 
 @_impl("row_normalize_")

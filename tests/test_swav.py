@@ -291,6 +291,31 @@ def test_swav_ce_gpu_vs_fp32_reference(cuda, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_swav_ce_multi_gpu_vs_fp32_reference(cuda, dtype):
+    """Every (assignment crop, other crop) pair in one launch, against plain fp32 PyTorch: the loss
+    sum_i sum_{v != crop_i} -mean_b <q_i, log_softmax(s_v / T)> / n_pairs and its score gradient."""
+    torch.manual_seed(0)
+    bs, nc, K, T = 32, 8, 3000, 0.1
+    s = (torch.randn(nc * bs, K, device=cuda) * 0.5).to(dtype)
+    q = torch.softmax(torch.randn(2, bs, K, device=cuda) * 3, -1)
+    ds = torch.full((nc * bs, K), 7.0, device=cuda)  # written, not accumulated
+    loss = torch.zeros(1, device=cuda)
+    n_pairs = 2 * (nc - 1)
+    torch.ops.dedloc.swav_ce_multi(s, q, [0, 1], ds, loss, T, 1.0 / (bs * n_pairs))
+    sr = s.float().cpu().requires_grad_(True)
+    lref = 0
+    for i, cid in enumerate((0, 1)):
+        for v in range(nc):
+            if v != cid:
+                lref = lref - (q[i].cpu() * torch.log_softmax(sr[v * bs:(v + 1) * bs] / T, -1)).sum(1).mean()
+    lref = lref / n_pairs
+    (g,) = torch.autograd.grad(lref, sr)
+    assert abs(loss.item() - lref.item()) < 1e-4 * abs(lref.item())
+    assert torch.allclose(ds.cpu(), g, atol=1e-7, rtol=1e-3)
+
+
+@pytest.mark.gpu
 def test_row_normalize_gpu(cuda):
     w = torch.randn(3000, 128, device=cuda)
     ref = torch.nn.functional.normalize(w, dim=1)
