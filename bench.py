@@ -51,9 +51,10 @@ METRIC = "samples/sec (whole node) ALBERT-large MLM pretrain at 1/2/4/8 peers"
 # profiles/bench_eager_mb128.log).  vs_baseline = value / (this x N).
 EAGER_BASELINE_SPS_PER_GPU = 272.02
 # The SwAV counterpart (--model swav --impl eager: training/swav_eager.py, stock nn modules with one
-# trunk pass per crop, vissl-formula loss, apex-LARC SGD in torch ops, same collaborative engine),
-# samples/s per GPU at N=1, b=64; None until measured on MI355X.
-EAGER_SWAV_SPS_PER_GPU = None
+# trunk pass per crop, vissl-formula loss, apex-LARC SGD in torch ops, same collaborative engine and
+# GPU multi-crop data), samples/s per GPU at N=1, b=64, measured on MI355X
+# (profiles/r4_bench_swav_eager_n1.log).
+EAGER_SWAV_SPS_PER_GPU = 619.19
 
 
 def parse():

@@ -21,14 +21,10 @@ from bench.model_step import synthetic  # noqa: E402
 def set_variant(ab, v):
     if ab == "residual":
         albert._RESIDUAL_IN_GEMM = v == "B"
-    elif ab == "wgradstream":  # weight-gradient GEMMs on a side stream (B)
-        albert._WGRAD_STREAM = v == "B"
     elif ab == "sharedwgrad":  # shared-layer weight-gradient slabs summed once per micro-step (B)
         albert._SHARED_WGRAD = v == "B"
     elif ab == "dgradwt":  # dgrad GEMMs against transposed weight copies (B) vs the plain weights (A)
         albert._DGRAD_WT = v == "B"
-    elif ab == "ew":
-        os.environ["DEDLOC_EW"] = "1" if v == "A" else "2"
     else:
         raise ValueError(ab)
 

@@ -12,7 +12,6 @@ O = torch.ops.dedloc
 
 
 def main():
-    os.environ["DEDLOC_GEMM"] = "mfma"
     T, N, K = 32768, 4096, 1024
     x = (torch.rand(T, K, device="cuda") * 2 - 1).bfloat16()
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()

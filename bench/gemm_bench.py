@@ -1,15 +1,10 @@
-"""ALBERT-large layer GEMMs: the hand-written MFMA kernel variants (same random bf16 data, one
-process, interleaved rounds — cdna_hip_programming.md §5.4 rules 24/25).
+"""ALBERT-large layer GEMMs on the hand-written MFMA kernels (gemm8.hip: one 256 x 256 tile per
+workgroup, LDS-DMA 8-phase pipeline), per shape at T tokens, random bf16 data
+(cdna_hip_programming.md §5.4 rules 24/25).  VARIANTS maps names to environment settings for A/B
+builds of future variants; the shipped dispatch is "g8".  Fused epilogues are timed as the op the
+model calls (gemm_gelu: bias + GELU; gemm_dgelu: GELU' + bias-gradient column sums).
 
-Variants per GEMM (the dispatch knobs are read per call, so one process times them all):
-  gemm8  : csrc/kernels/gemm8.hip, one tile per workgroup (LDS-DMA 8-phase pipeline)
-  g8p    : gemm8's persistent form, deferred output stores             DEDLOC_GEMM8_PERSIST=256
-  g8pnt  : g8p with non-temporal output stores                         + DEDLOC_GEMM8_NT=1
-  gemm1  : csrc/kernels/gemm.hip (register-staged)                     DEDLOC_GEMM=mfma1
-Fused epilogues are timed as the op the model calls (gemm_gelu: bias + GELU; gemm_dgelu: GELU'
-+ bias-gradient column sums).
-
-usage: T=131072 VARIANTS=gemm8,g8p,g8pnt [KINDS=fwd,dgrad_wT] python bench/gemm_bench.py [--check]
+usage: T=262144 [DGRAD_T=1] [KINDS=fwd,dgrad_wT] python bench/gemm_bench.py [--check]
 """
 import os as _os
 import sys as _sys
@@ -25,25 +20,7 @@ import torch
 import dedloc_amd.ops  # noqa: F401
 
 O = torch.ops.dedloc
-VARIANTS = {"gemm8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "0"},
-            "g8p": {"DEDLOC_GEMM8_PERSIST": "256", "DEDLOC_GEMM8_NT": "0"},
-            "g8pnt": {"DEDLOC_GEMM8_PERSIST": "256", "DEDLOC_GEMM8_NT": "1"},
-            "g8nt": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1"},
-            "gemm1": {"DEDLOC_GEMM": "mfma1"},
-            # tile order: bands of G row blocks walked column by column (gemm8.hip tile_of)
-            "g8g2": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "2"},
-            "g8g4": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "4"},
-            "g8g8": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "8"},
-            "g8g16": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_GROUP": "16"},
-            # B0 fragments kept in registers for phase 3 (default) vs read again from LDS
-            "g8kb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "1"},
-            "g8rb": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_KEEPB0": "0"},
-            # per-lane DMA source bases computed once + peeled K-loop tail
-            "g8pre": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_PRESRC": "1"},
-            "g8nopre": {"DEDLOC_GEMM8_PERSIST": "0", "DEDLOC_GEMM8_NT": "1", "DEDLOC_GEMM8_PRESRC": "0"},
-            # the defaults, and 256 x 128 tiles with two co-resident workgroups per CU (gemm8h)
-            "g8": {},
-            "g8h": {"DEDLOC_GEMM8_HALF": "1"}}
+VARIANTS = {"g8": {}}  # the shipped dispatch (the A/B knobs of rounds 2-3 were removed with their losing forms)
 
 
 def timeit(fn, iters=10):
@@ -57,9 +34,6 @@ def timeit(fn, iters=10):
 
 
 def set_policy(pol):
-    for k in ("DEDLOC_GEMM", "DEDLOC_GEMM8_PERSIST", "DEDLOC_GEMM8_NT", "DEDLOC_GEMM8_GROUP", "DEDLOC_GEMM8_KEEPB0",
-              "DEDLOC_GEMM8_PRESRC", "DEDLOC_GEMM8_HALF"):
-        os.environ.pop(k, None)
     os.environ.update(pol)
 
 
@@ -78,7 +52,7 @@ def rel(a, b):
 def main():
     T = int(os.environ.get("T", 32768))
     check = "--check" in sys.argv
-    variants = os.environ.get("VARIANTS", "gemm8,g8p").split(",")
+    variants = os.environ.get("VARIANTS", "g8").split(",")
     dev = torch.device("cuda")
     H, I = 1024, 4096
     torch.manual_seed(0)

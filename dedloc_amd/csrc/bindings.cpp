@@ -77,10 +77,7 @@ at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& s, const at::Te
   expect(dgamma, at::kFloat, "dgamma");
   expect(dbeta, at::kFloat, "dbeta");
   const int64_t D = dy.size(-1), rows = dy.numel() / D;
-  static const int64_t max_parts = [] {  // DEDLOC_LN_PARTS: measurement override of the grid cap
-    const char* e = std::getenv("DEDLOC_LN_PARTS");
-    return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(512);
-  }();
+  constexpr int64_t max_parts = 512;  // grid cap of the LayerNorm backward's partial sums
   const int nparts = (int)std::min<int64_t>(max_parts, std::max<int64_t>(1, rows / 32));
   auto ds = at::empty_like(dy);
   if (!accumulate) {
@@ -393,11 +390,7 @@ std::tuple<at::Tensor, at::Tensor> attn_softmax_bwd(const at::Tensor& s, const a
 // There is no vendor-library or ATen path: a shape no kernel takes is an error, not a fallback.
 // The fp32-accumulating weight-gradient form writes straight into the fp32 gradient buffer, so the
 // shared ALBERT layer's 24 weight-gradient contributions never round through bf16.
-// DEDLOC_GEMM=mfma1 skips gemm8 (A/B measurements of the two tiled kernels).
-bool use_gemm8() {
-  const char* e = std::getenv("DEDLOC_GEMM");
-  return !(e && !std::strcmp(e, "mfma1"));
-}
+constexpr bool use_gemm8() { return true; }
 
 struct Mat {  // (rows, k) operand view: K-inner means element (r, k) at p[r*ld + k]
   const at::Tensor& t;
@@ -532,11 +525,6 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
 // smaller S on ties (fewer slab bytes to sum).
 int wgrad_splits8(const Mat& A, const Mat& B) {
   const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
-  if (const char* e = std::getenv("DEDLOC_WGRAD_SPLITS")) {
-    int S = std::max(1, std::atoi(e));
-    while (S > 1 && A.k % (S * 64)) S /= 2;
-    return S;
-  }
   // any S dividing the K-tile count (SwAV's 14x14 maps: 25088 tokens = 392 K-tiles = 2^3 7^2, so
   // S = 56 puts 224 workgroups on the chip where powers of two stop at 32), each slice at least 4
   // K-tiles (8 while S > 32)
@@ -974,25 +962,16 @@ inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t
 // stride-1 unpadded convs over NHWC tensors (x[N*H*W, C] x W[K, C]^T; dgrad dY[N*H*W, K] x W
 // with the KRSC weight as a K-outer operand) and the stem's column-matrix GEMM; their
 // weight gradients use gemm8's split-K slabs where both channel counts are multiples of 256 and the
-// implicit-GEMM conv.hip wgrad otherwise.  DEDLOC_CONV_GEMM=hip routes the 1x1 convs through
-// conv.hip too (kernel tests).
-bool conv_gemm() {
-  const char* e = std::getenv("DEDLOC_CONV_GEMM");
-  return !(e && e[0] == 'h');
-}
+// implicit-GEMM conv.hip wgrad otherwise.
+constexpr bool conv_gemm() { return true; }
 inline bool is_pointwise(int64_t R, int64_t S, int64_t stride, int64_t pad) {
   return R == 1 && S == 1 && stride == 1 && pad == 0;
 }
 // 1x1 convs whose GEMM output has at most this many columns (forward: output channels; data
 // gradient: input channels) run on conv.hip's implicit-GEMM kernel (256x64 / 128x128 tiles, 2-deep
-// register prefetch) instead of gemm_small (DEDLOC_CONV_NARROW_1X1 = 0 / 64 / 128)
-inline int64_t narrow_1x1_max() {
-  static const int64_t v = [] {
-    const char* e = std::getenv("DEDLOC_CONV_NARROW_1X1");
-    return e ? (int64_t)std::atol(e) : (int64_t)128;
-  }();
-  return v;
-}
+// register prefetch) instead of gemm_small: 128 won the round-3 A/B over 0 / 64 / 256 / 512
+// (SwAV b=64: 2087 / 2128 / 2205 / 2197 / 2190 samples/s, profiles/README.md)
+constexpr int64_t narrow_1x1_max() { return 128; }
 inline at::Tensor rows2d(const at::Tensor& t) {  // channels-last [N, C, H, W] -> [N*H*W, C] view
   return t.permute({0, 2, 3, 1}).reshape({-1, t.size(1)});
 }
@@ -1079,14 +1058,10 @@ at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t str
   auto wp = at::zeros({K, sc.Kp}, w.options());
   wp.narrow(1, 0, R * sc.SCp).view({K, R, sc.SCp}).narrow(2, 0, S * C).copy_(wk.reshape({K, R, S * C}));
   // the column-matrix GEMM as a 1x1 conv over the [N*P*Q, 1, 1, Kp] "image" on conv.hip (its
-  // 256x64 tiles for the 64 stem channels, with the statistics epilogue); the tiled GEMM kernels
-  // otherwise (DEDLOC_STEM_GEMM=1)
-  static const bool stem_gemm = [] {
-    const char* e = std::getenv("DEDLOC_STEM_GEMM");
-    return e && e[0] == '1';
-  }();
+  // 256x64 tiles for the 64 stem channels, with the statistics epilogue; +2% over the tiled GEMM
+  // kernels in round 3), the tiled GEMM kernels for a column width conv.hip does not take
   const int64_t Mc = col.size(0);
-  if (!stem_gemm && sc.Kp % 64 == 0) {
+  if (sc.Kp % 64 == 0) {
     const DlConvGeom gc = geom(cbf(col), Mc, 1, 1, sc.Kp, 1, 1, 1, 1, 1, 1, 0, 1, 0, 1);
     if (stats && dl_conv_fwd(gc, cbf(wp), sc.Kp, (int)K, bf(y), 1, 1, 1, 1, 0, 0, K, cur_stream(x), stats,
                              stat_rows) == 0)
@@ -1251,14 +1226,6 @@ std::tuple<at::Tensor, bool> conv2d_dgrad_bn(const at::Tensor& dy, const at::Ten
                                 nullptr, 0, 0, 0, nullptr, rp, C, nullptr, 0, nullptr, 1, st, f32(sums), stat_rows,
                                 &bn) == 0)
       return {dx, true};
-    static const bool small_ok = [] {
-      const char* e = std::getenv("DEDLOC_BN_BWD_SMALL");
-      return e && e[0] == '1';
-    }();
-    if (small_ok && C <= 192 && dl_gemm_small_splits(M, (int)C, (int)A.k) == 1 &&
-        dl_gemm_small(0, cbf(dyr), A.srow(), A.sk(), cbf(wkc), B.srow(), B.sk(), M, (int)C, (int)A.k, bf(dx), C,
-                      nullptr, 0, 0, nullptr, rp, C, 1, nullptr, st, f32(sums), stat_rows, &bn) == 0)
-      return {dx, true};
   }
   // 3x3 / strided data gradients (Bottleneck conv2 <- bn1) and the 1x1 ones gemm8 does not take
   // (at most 128 input channels: conv3 <- bn2 in the first stages): conv.hip's epilogue
@@ -1304,15 +1271,9 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
     gemm_acc_f32(rows2d(dy), rows2d(x), acc.view({K, C}), true, false);
   } else if (C % 8 == 0 && C >= 8 && C % 64 == 0) {
     const DlConvGeom gm = geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1);
-    // DEDLOC_CONV_WGRAD_SLAB=1: split partials as fp32 slabs summed in one pass instead of fp32
-    // atomics (SwAV b=64, interleaved on one box: slabs 2168 / 2141, atomics 2226 / 2104 samples/s —
-    // no consistent gain, atomics stay the default)
-    const char* slab_env = std::getenv("DEDLOC_CONV_WGRAD_SLAB");  // read per call: tests A/B both forms
-    const bool slabs = slab_env && slab_env[0] == '1';
-    const size_t nws = slabs ? dl_conv_wgrad_ws_floats(gm, (int)K, (int)(R * S * C)) : 0;
-    at::Tensor ws = nws ? at::empty({(int64_t)nws}, dw.options()) : at::Tensor();
-    rc = dl_conv_wgrad(gm, cbf(dy), K, (int)K, f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy),
-                       nws ? f32(ws) : nullptr, nws);
+    // split partials accumulate with fp32 atomics (the slab-and-sum form measured no consistent
+    // gain in round 3 and was removed)
+    rc = dl_conv_wgrad(gm, cbf(dy), K, (int)K, f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy));
     check(rc, "conv2d_wgrad");
   } else {
     // stem: wgrad over the padded column matrix into a [K, R, SCp] slab, then the real columns

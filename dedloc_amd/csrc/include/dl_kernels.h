@@ -127,12 +127,10 @@ struct DlConvGeom {
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
                 int oh0, int ow0, long ldo, hipStream_t st, float* stats = nullptr, long stat_rows = 0,
                 const DlBnBwdEpi* bn = nullptr);  // bn (needs stats): BN-backward preparation epilogue
-// dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols)
-// ws (optional, >= dl_conv_wgrad_ws_floats floats): per-split slabs summed into a dense dw instead
-// of fp32 atomics
+// dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols; the pixel
+// reduction is split over workgroups that add their partial tiles with fp32 atomics)
 int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,
-                  hipStream_t st, float* ws = nullptr, size_t ws_floats = 0);
-size_t dl_conv_wgrad_ws_floats(const DlConvGeom& g, int Cout, int Ncols);
+                  hipStream_t st);
 // stem im2col: col[m][r*SCp + s*C + c] (filter rows padded to SCp columns), zero columns up to Kp
 int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int P, int Q, int SCp,
               int Kp, bf16_t* col, hipStream_t st);

@@ -927,47 +927,9 @@ __global__ __launch_bounds__(256, KS == 2 ? 1 : 2) void attn_bwd_dkdv_kernel(
   }
 }
 
-// DEDLOC_ATTN_RING=1/0 selects the LDS-DMA ring / the register-staged pipeline.  Default: the ring
-// for the 2-sub-block forward (it frees the 16 staging VGPRs that sub-block needs), registers for the
-// backward (measured equal at B=256 and 2-5% faster with padding: those loops are latency-bound).
-bool attn_ring(bool dflt) {
-  const char* e = std::getenv("DEDLOC_ATTN_RING");
-  return e ? e[0] == '1' : dflt;
-}
-
-// DEDLOC_ATTN_QS = query sub-blocks of 32 rows per wave in the forward (1 or 2; default 2)
-int attn_fwd_qs() {
-  const char* e = std::getenv("DEDLOC_ATTN_QS");
-  return (e && e[0] == '1') ? 1 : 2;
-}
-
-// DEDLOC_ATTN_NW = waves per forward block (4 or 8; default 4 — 8 measured 5% slower)
-int attn_fwd_nw() {
-  const char* e = std::getenv("DEDLOC_ATTN_NW");
-  return (e && e[0] == '8') ? 8 : 4;
-}
-
-// DEDLOC_ATTN_DQ_QS = query sub-blocks per wave in the dQ backward kernel (1 or 2; default 2)
-int attn_dq_qs() {
-  const char* e = std::getenv("DEDLOC_ATTN_DQ_QS");
-  return (e && e[0] == '1') ? 1 : 2;
-}
-
-// DEDLOC_ATTN_DKDV_KS = key sub-blocks per wave in the dK/dV kernel (1 or 2; default 1: the
-// one-wave-per-SIMD KS=2 form measured 8% slower, profiles/README.md)
-int attn_dkdv_ks() {
-  const char* e = std::getenv("DEDLOC_ATTN_DKDV_KS");
-  return (e && e[0] == '2') ? 2 : 1;
-}
-
-// DEDLOC_ATTN_XCD=0 restores the hardware block order (A/B measurement)
-int attn_xcd() {
-  static const int v = [] {
-    const char* e = std::getenv("DEDLOC_ATTN_XCD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v;
-}
+// Block order remapped so that the query blocks of one (batch, head) share an XCD's L2 (their K/V
+// tiles are read by every one of them).
+constexpr int kAttnXcd = 1;
 
 }  // namespace
 
@@ -975,24 +937,10 @@ int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
                 int B, int H, int S, int D, float scale, hipStream_t st) {
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
-  const int qs = attn_fwd_qs();
-  if (attn_fwd_nw() == 8 && qs == 2) {
-    dim3 grid8((S + 511) / 512, H, B);
-    attn_fwd_kernel<true, 2, 8><<<grid8, 512, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
-    return 0;
-  }
-  dim3 grid((S + 128 * qs - 1) / (128 * qs), H, B);
-  if (attn_ring(qs == 2)) {
-    if (qs == 2)
-      attn_fwd_kernel<true, 2><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
-    else
-      attn_fwd_kernel<true, 1><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
-  } else {
-    if (qs == 2)
-      attn_fwd_kernel<false, 2><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
-    else
-      attn_fwd_kernel<false, 1><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, attn_xcd());
-  }
+  // 4 waves x 2 query sub-blocks of 32 rows per wave, K/V staged by the LDS-DMA ring (it frees the
+  // 16 staging VGPRs the second sub-block needs); 8-wave blocks measured 5% slower (round 2)
+  dim3 grid((S + 255) / 256, H, B);
+  attn_fwd_kernel<true, 2><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, kAttnXcd);
   return 0;
 }
 
@@ -1001,32 +949,13 @@ int dl_attn_bwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
                 int S, int D, float scale, hipStream_t st) {
   if (D != HD || S % 64 != 0 || ld % 8 != 0 || ldo % 8 != 0) return -1;
   const float sl2 = scale * 1.4426950408889634f;
-  dim3 grid((S + 127) / 128, H, B);
-  const int qs = attn_dq_qs();
-  dim3 grid_dq((S + 128 * qs - 1) / (128 * qs), H, B);
-  const bool ring_dq = attn_ring(qs == 2);
-  if (qs == 2 && ring_dq)
-    attn_bwd_dq_kernel<true, 2><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
-                                                         dbias, B, H, S, sl2, scale, attn_xcd());
-  else if (qs == 2)
-    attn_bwd_dq_kernel<false, 2><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
-                                                          dbias, B, H, S, sl2, scale, attn_xcd());
-  else if (ring_dq)
-    attn_bwd_dq_kernel<true, 1><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
-                                                         dbias, B, H, S, sl2, scale, attn_xcd());
-  else
-    attn_bwd_dq_kernel<false, 1><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
-                                                          dbias, B, H, S, sl2, scale, attn_xcd());
-  const int ks = attn_dkdv_ks();
-  dim3 grid_kv((S + 128 * ks - 1) / (128 * ks), H, B);
-  if (ks == 2)
-    attn_bwd_dkdv_kernel<true, 2><<<grid_kv, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H,
-                                                           S, sl2, scale, attn_xcd());
-  else if (attn_ring(false))
-    attn_bwd_dkdv_kernel<true, 1><<<grid_kv, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H,
-                                                           S, sl2, scale, attn_xcd());
-  else
-    attn_bwd_dkdv_kernel<false, 1><<<grid_kv, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H,
-                                                            S, sl2, scale, attn_xcd());
+  // dQ: 2 query sub-blocks per wave with the LDS-DMA ring; dK/dV: one key sub-block per wave with
+  // register staging (the one-wave-per-SIMD 2-sub-block form measured 8% slower, profiles/README.md)
+  dim3 grid_dq((S + 255) / 256, H, B);
+  attn_bwd_dq_kernel<true, 2><<<grid_dq, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, dout, ldo, lse, delta, dqkv,
+                                                       dbias, B, H, S, sl2, scale, kAttnXcd);
+  dim3 grid_kv((S + 127) / 128, H, B);
+  attn_bwd_dkdv_kernel<false, 1><<<grid_kv, 256, 0, st>>>(qkv, ld, mbias, kvinfo, dout, ldo, lse, delta, dqkv, B, H,
+                                                          S, sl2, scale, kAttnXcd);
   return 0;
 }

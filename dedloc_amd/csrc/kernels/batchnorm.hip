@@ -367,20 +367,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
   }
 }
 
-inline int bn_unroll() {
-  static const int u = [] {
-    const char* e = std::getenv("DEDLOC_BN_UNROLL");
-    return e && std::atoi(e) == 4 ? 4 : 2;
-  }();
-  return u;
-}
-
-// launch KERNEL<2> or KERNEL<4> by the unroll knob
-#define DL_BN_LAUNCH(KERNEL, GRID, ...)                                     \
-  do {                                                                      \
-    if (bn_unroll() == 2) KERNEL<2><<<GRID, kThreads, 0, st>>>(__VA_ARGS__); \
-    else KERNEL<4><<<GRID, kThreads, 0, st>>>(__VA_ARGS__);                  \
-  } while (0)
+// streaming kernels with 2 rows in flight per thread (4 measured slower in round 3: 2186 / 2191 vs
+// 2212 / 2203 samples/s)
+#define DL_BN_LAUNCH(KERNEL, GRID, ...) KERNEL<2><<<GRID, kThreads, 0, st>>>(__VA_ARGS__)
 
 inline bool bn_shape_ok(int C) {
   if (C % 8 || C > 2048) return false;

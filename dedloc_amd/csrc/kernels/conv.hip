@@ -410,7 +410,6 @@ struct WgradArgs {
   int m_per_split;
   float rIJ, rJ;
   unsigned img_bytes, dy_bytes;
-  float* slab;  // split > 1: per-split fp32 partials [split][Cout][Ncols] (plain stores) instead of atomics
 };
 
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
@@ -512,12 +511,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
   // acc[mi][ni][i] = dW[channel m0+wm*64+mi*16+4*(lane>>4)+i][col n0+wn*64+ni*16+(lane&15)]
   const bool split = gridDim.z > 1;
   float* out = p.dw;
-  long ld = p.lddw;
-  if (split && p.slab != nullptr) {  // this split's own slab: plain stores, summed by a second pass
-    out = p.slab + (long)blockIdx.z * p.Cout * p.Ncols;
-    ld = p.Ncols;
-  }
-  const bool atomics = split && p.slab == nullptr;
+  const long ld = p.lddw;
+  const bool atomics = split;
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
 #pragma unroll
@@ -594,12 +589,9 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
   if (M == 0 || N == 0) return 0;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * ldw;
   if (img_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
-  // outputs of at most 64 channels: 256 x 64 tiles (DEDLOC_CONV_NARROW=0: always 128 x 128)
-  static const bool narrow_ok = [] {
-    const char* e = std::getenv("DEDLOC_CONV_NARROW");
-    return !(e && e[0] == '0');
-  }();
-  const bool narrow = narrow_ok && N <= 64 && (!stats || stat_rows % 256 == 0);
+  // outputs of at most 64 channels: 256 x 64 tiles (the 128-wide channel tile would be half empty;
+  // SwAV b=64 2015 / 2037 -> 2058 / 2055 samples/s in round 3)
+  const bool narrow = N <= 64 && (!stats || stat_rows % 256 == 0);
   const int TMv = narrow ? 256 : BM, TNv = narrow ? 64 : BN;
   const int tiles = (int)((M + TMv - 1) / TMv) * ((N + TNv - 1) / TNv);
   // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
@@ -623,27 +615,19 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
 // Split count of dl_conv_wgrad: the (long) pixel reduction is split so that ~`target` workgroups
 // exist (default 256: one per CU; SwAV b=64 iteration 1990-1997 samples/s at 1024, 2051-2061 at 256,
 // 2041 at 512, with atomic adds), each split a multiple of the 64-deep k-step and at least 8 k-steps
-// long (DEDLOC_CONV_WGRAD_WGS: A/B measurements)
+// long
 static long wgrad_splits(const DlConvGeom& g, int Cout, int Ncols) {
   const long M = (long)g.Nimg * g.I * g.J;
   const int tiles = ((Cout + BM - 1) / BM) * ((Ncols + BN - 1) / BN);
-  static const long target = [] {
-    const char* e = std::getenv("DEDLOC_CONV_WGRAD_WGS");
-    return e ? std::max(1L, std::atol(e)) : 256L;
-  }();
+  constexpr long target = 256;
   const long ksteps = (M + BK - 1) / BK;
   long splits = std::max(1L, std::min<long>((target + tiles - 1) / tiles, ksteps / 8));
   const long steps_per = (ksteps + splits - 1) / splits;
   return (ksteps + steps_per - 1) / steps_per;
 }
 
-size_t dl_conv_wgrad_ws_floats(const DlConvGeom& g, int Cout, int Ncols) {
-  const long s = wgrad_splits(g, Cout, Ncols);
-  return s > 1 ? (size_t)s * Cout * Ncols : 0;
-}
-
 int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,
-                  hipStream_t st, float* ws, size_t ws_floats) {
+                  hipStream_t st) {
   const int Brows = g.TR * g.TS * g.C;
   if (g.C % 8 || Cout % 8 || Cout < 8 || ldy % 8 || Brows < 8 || Ncols > Brows) return -1;
   const long M = (long)g.Nimg * g.I * g.J;
@@ -655,22 +639,14 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
   const long steps_per = (ksteps + splits - 1) / splits;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, dy_bytes = 2L * M * ldy;
   if (img_bytes >= (1L << 31) || dy_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
-  // slab mode (a workspace of splits x Cout x Ncols floats and a dense dw): each split stores its
-  // partial tile and one pass adds the slabs into dw — atomics are issue-bound (256 wave-instructions
-  // per 128x128 tile and split), the slab stores and the summing pass are plain streams
-  float* slab = (splits > 1 && ws != nullptr && ws_floats >= (size_t)splits * Cout * Ncols && lddw == Ncols &&
-                 Ncols % 4 == 0 && ((uintptr_t)dw & 15) == 0)
-                    ? ws
-                    : nullptr;
   WgradArgs a{g, dy, ldy, Cout, dw, lddw, Ncols, Brows, (int)M, (int)(steps_per * BK),
-              1.f / (float)(g.I * g.J), 1.f / (float)g.J, (unsigned)img_bytes, (unsigned)dy_bytes, slab};
+              1.f / (float)(g.I * g.J), 1.f / (float)g.J, (unsigned)img_bytes, (unsigned)dy_bytes};
   static bool attr = false;
   if (!attr) {
     set_lds(conv_wgrad_kernel);
     attr = true;
   }
   conv_wgrad_kernel<<<dim3(tiles, 1, (unsigned)splits), NT, LDS_BYTES, st>>>(a);
-  if (slab) return dl_sum_slabs(dw, slab, (int)splits, (size_t)Cout * Ncols, st);
   return 0;
 }
 

@@ -16,21 +16,10 @@ inline int grid_for(size_t nvec, int block) {
   return (int)(g < (size_t)kMaxGrid ? (g == 0 ? 1 : g) : kMaxGrid);
 }
 
-__global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ y, size_t nvec) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
-    float v[8];
-    load_bf16<8>(h + i * 8, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh(v[j]);
-    store_bf16<8>(y + i * 8, v);
-  }
-}
-
-// v2 (default): no grid stride — each thread owns VPT vectors of a 1024-vector block chunk and
-// issues all their loads before any math (LayerNorm's access shape, which streams at ~6.3 TB/s),
-// branch-free hardware bf16 conversion: 498 -> 389 us at T=131072 x 4096 (4.3 -> 5.5 TB/s,
-// bench/ew_bench.py), sigmoid-form GELU (one exp2 + one rcp).  DEDLOC_EW=1 selects the grid-strided v1 (A/B).  The same
-// change to the GELU-backward column-sum kernel (8 rows in flight) measured no gain (640 vs 649 us).
+// No grid stride: each thread owns VPT vectors of a 1024-vector block chunk and issues all their
+// loads before any math (LayerNorm's access shape, which streams at ~6.3 TB/s), branch-free
+// hardware bf16 conversion: 498 -> 389 us at T=131072 x 4096 against the grid-strided form (4.3 ->
+// 5.5 TB/s, bench/ew_bench.py), sigmoid-form GELU (one exp2 + one rcp).
 constexpr int VPT = 4;
 __global__ __launch_bounds__(256) void gelu_fwd_v2_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ y,
                                                           size_t nvec) {
@@ -54,10 +43,6 @@ __global__ __launch_bounds__(256) void gelu_fwd_v2_kernel(const bf16_t* __restri
   }
 }
 
-bool ew_v1() {
-  const char* e = std::getenv("DEDLOC_EW");
-  return e && e[0] == '1';
-}
 
 __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
                                                        bf16_t* __restrict__ dh, size_t nvec) {
@@ -71,67 +56,6 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// Column sums over a [rows, N] bf16 matrix, optionally fused with gelu_new backward
-// (GELU: dh = dy * gelu'(h) is written out and summed).  Block = 4 waves x (64 lanes x 8 columns):
-// 512 columns x rpb rows; wave w takes rows w, w+4, ... with 4 rows of 16-byte loads in flight per
-// lane.  The 4 wave partials meet in LDS and leave as lane-contiguous fp32 atomics (256 B per wave
-// instruction, Guideline 12) — one atomic per column per block.
-template <bool GELU, int RU = 4>
-__global__ __launch_bounds__(256) void colsum_tile_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ h,
-                                                          bf16_t* __restrict__ dh, float* __restrict__ out, int rows,
-                                                          int N, int rpb) {
-  __shared__ float red[4][512];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int cb = blockIdx.x * 512;
-  const int c0 = cb + lane * 8;
-  const bool active = c0 < N;
-  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (active) {
-    int r = r0 + w;
-    for (; r + 4 * (RU - 1) < r1; r += 4 * RU) {
-      uint4 xr[RU], hr[RU];
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        xr[u] = *reinterpret_cast<const uint4*>(x + (size_t)(r + 4 * u) * N + c0);
-        if (GELU) hr[u] = *reinterpret_cast<const uint4*>(h + (size_t)(r + 4 * u) * N + c0);
-      }
-#pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        float g[8];
-        load_bf16<8>(reinterpret_cast<const bf16_t*>(&xr[u]), g);
-        if (GELU) {
-          float v[8];
-          load_bf16<8>(reinterpret_cast<const bf16_t*>(&hr[u]), v);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
-          store_bf16<8>(dh + (size_t)(r + 4 * u) * N + c0, g);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += g[j];
-      }
-    }
-    for (; r < r1; r += 4) {
-      float g[8];
-      load_bf16<8>(x + (size_t)r * N + c0, g);
-      if (GELU) {
-        float v[8];
-        load_bf16<8>(h + (size_t)r * N + c0, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad(v[j])));
-        store_bf16<8>(dh + (size_t)r * N + c0, g);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += g[j];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = acc[j];
-  __syncthreads();
-  for (int c = threadIdx.x; c < 512; c += 256) {
-    if (cb + c < N) atomicAdd(&out[cb + c], red[0][c] + red[1][c] + red[2][c] + red[3][c]);
-  }
-}
 
 // v2 of the fused GELU backward + bias-gradient column sums: straight-line per wave (no row loop):
 // each of the 8 waves of a block issues the loads of its 8 rows x 8 columns-per-lane at once, then
@@ -276,10 +200,6 @@ __global__ __launch_bounds__(256) void add_bf16_to_f32_kernel(const bf16_t* __re
 
 int dl_gelu_fwd(const bf16_t* h, bf16_t* y, size_t n, hipStream_t st) {
   if (n % 8) return -1;
-  if (ew_v1()) {
-    gelu_fwd_kernel<<<grid_for(n / 8, 256), 256, 0, st>>>(h, y, n / 8);
-    return 0;
-  }
   const size_t nvec = n / 8;
   gelu_fwd_v2_kernel<<<(unsigned)((nvec + 256 * VPT - 1) / (256 * VPT)), 256, 0, st>>>(h, y, nvec);
   return 0;
@@ -293,12 +213,6 @@ int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStre
 
 int dl_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* h, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st) {
   if (N % 8) return -1;
-  if (ew_v1()) {
-    const int rpb = 256;
-    dim3 grid((N + 511) / 512, (rows + rpb - 1) / rpb);
-    colsum_tile_kernel<true, 4><<<grid, 256, 0, st>>>(dy, h, dh, dbias, rows, N, rpb);
-    return 0;
-  }
   dim3 grid((N + 511) / 512, (rows + 63) / 64);
   colsum_rows_kernel<true><<<grid, 512, 0, st>>>(dy, h, dh, dbias, rows, N);
   return 0;
@@ -319,12 +233,6 @@ int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hi
   // `part` is the fp32 [N] destination: every block adds its row-chunk sums atomically
   if (N % 8) {
     colsum_bf16_scalar_kernel<<<dim3((N + 255) / 256, nparts), 256, 0, st>>>(x, part, rows, N, rpb);
-    return 0;
-  }
-  if (ew_v1()) {
-    const int rpb2 = 256;
-    dim3 grid((N + 511) / 512, (rows + rpb2 - 1) / rpb2);
-    colsum_tile_kernel<false, 4><<<grid, 256, 0, st>>>(x, nullptr, nullptr, part, rows, N, rpb2);
     return 0;
   }
   dim3 grid((N + 511) / 512, (rows + 63) / 64);

@@ -227,11 +227,11 @@ __device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int G
   } while (0)
 #define DL_MFMA_QUAD(QM, QN) DL_MFMA_QUAD_B(QM, QN, bfr)
 
-// KEEPB0: the B0 fragments read in phase 0 stay in registers for phase 3 (16 more VGPRs) instead of
-// being read again — 24 instead of 28 KiB of LDS reads per wave and K-tile, and phase 3 issues no
-// LDS reads at all
+// The B0 fragments read in phase 0 stay in registers for phase 3 (16 more VGPRs) instead of being
+// read again — 24 instead of 28 KiB of LDS reads per wave and K-tile, and phase 3 issues no LDS
+// reads at all.
 // PRESRC: DMA source addresses from per-lane bases computed once (src_base / stage_pre)
-template <bool AKO, bool BKO, int EPI, bool KEEPB0, bool PRESRC>
+template <bool AKO, bool BKO, int EPI, bool PRESRC>
 __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
   const int lane = threadIdx.x & 63;
@@ -331,10 +331,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        if constexpr (KEEPB0) bf0[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-        else bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-      }
+      for (int ni = 0; ni < 2; ++ni) bf0[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -342,8 +339,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA0, ra + mi * 16, ks, lane);
     if constexpr (M1) DL_STAGE(t + 1, 2);
     __builtin_amdgcn_s_barrier();
-    if constexpr (KEEPB0) DL_MFMA_QUAD_B(0, 0, bf0);
-    else DL_MFMA_QUAD(0, 0);
+    DL_MFMA_QUAD_B(0, 0, bf0);
     __builtin_amdgcn_s_barrier();
 
     // ---- phase 1: quadrant (0,1); prefetch B0 of tile t+1
@@ -367,12 +363,6 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     __builtin_amdgcn_s_barrier();
 
     // ---- phase 3: quadrant (1,0); prefetch B1 of tile t+2; retire tile t+1
-    if constexpr (!KEEPB0) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-    }
     if constexpr (M2) {
       DL_STAGE(t + 2, 1);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -380,8 +370,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
-    if constexpr (KEEPB0) DL_MFMA_QUAD_B(1, 0, bf0);
-    else DL_MFMA_QUAD(1, 0);
+    DL_MFMA_QUAD_B(1, 0, bf0);
     __builtin_amdgcn_s_barrier();
     };
   if constexpr (PRESRC) {
@@ -401,10 +390,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        if constexpr (KEEPB0) bf0[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-        else bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-      }
+      for (int ni = 0; ni < 2; ++ni) bf0[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -412,8 +398,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA0, ra + mi * 16, ks, lane);
     if (more1) DL_STAGE(t + 1, 2);
     __builtin_amdgcn_s_barrier();
-    if constexpr (KEEPB0) DL_MFMA_QUAD_B(0, 0, bf0);
-    else DL_MFMA_QUAD(0, 0);
+    DL_MFMA_QUAD_B(0, 0, bf0);
     __builtin_amdgcn_s_barrier();
 
     // ---- phase 1: quadrant (0,1); prefetch B0 of tile t+1
@@ -437,12 +422,6 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     __builtin_amdgcn_s_barrier();
 
     // ---- phase 3: quadrant (1,0); prefetch B1 of tile t+2; retire tile t+1
-    if constexpr (!KEEPB0) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-    }
     if (more2) {
       DL_STAGE(t + 2, 1);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -450,8 +429,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
-    if constexpr (KEEPB0) DL_MFMA_QUAD_B(1, 0, bf0);
-    else DL_MFMA_QUAD(1, 0);
+    DL_MFMA_QUAD_B(1, 0, bf0);
     __builtin_amdgcn_s_barrier();
       }
   }
@@ -666,598 +644,20 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Persistent form with deferred output stores (bf16 epilogues).  A CU can issue only ~14 B/clk of
-// 16-byte stores, so a 256x256 bf16 tile (128 KiB) needs ~9K cycles to leave the CU; in the
-// one-tile-per-workgroup form those stores sit between two main loops (16% of the QKV GEMM).
-// Here one workgroup per CU walks its tiles, and tile i's output leaves during tile i+1:
-//   * the epilogue packs the tile into registers (acc is dead by then): 12 of its 16 x 16 B per
-//     lane are stored right after tile i+1's prologue loads are issued (queued behind them, so the
-//     prologue wait never waits for them);
-//   * the last 4 x 16 B per lane go to the 32 KiB of LDS the pipeline leaves free (128 + 32 = 160
-//     KiB) and leave one per phase of tile i+1's first K-tile, whose counted wait then allows
-//     vmcnt(6) instead of vmcnt(4) (two stores + two half-tiles issued after the awaited loads);
-//   * stores are raw buffer stores against a per-tile resource whose range ends at the last valid
-//     row: rows past M are dropped by the hardware range check, so every store instruction is
-//     issued (exact vmcnt accounting) and there is no divergent branch.
-// ---------------------------------------------------------------------------------------------
-constexpr int SPARE = 32768;
-
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, unsigned off, const uint4& v, bool nt) {
-  const u32x4 w = {v.x, v.y, v.z, v.w};
-  if (nt)
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 2);  // slc: streaming
-  else
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(bf16_t* base, long ld, int m0, int M) {
-  const long rows = min(BM, M - m0);
-  return __builtin_amdgcn_make_buffer_rsrc(base + (long)m0 * ld, 0, (int)(rows * ld * 2), 0x00020000);
-}
-
-template <bool AKO, bool BKO, int EPI>
-__global__ __launch_bounds__(NT, 2) void gemm8p_kernel(Args p) {
-  static_assert(EPI != EPI_F32, "the persistent form covers the bf16 epilogues");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM + SPARE];
-  const int lane0 = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w >> 2, wn = w & 3;
-  const int tiles_n = p.N / BN;
-  const int tiles_m = (p.M + BM - 1) / BM;
-  const int total = tiles_m * tiles_n;
-  const int nk = p.K / BK;
-  uint8_t* spare = smem + SMEM + w * 4096;  // this wave's deferred passes 4..7 (16 B per lane each)
-  const bool nt = p.nt != 0;
-
-  // the previous tile's output: qm = 0 half (imm) and the deferred qm = 1 half (dreg + spare)
-  int dm0 = -1;
-  __amdgpu_buffer_rsrc_t drs = tile_rsrc(p.C, p.ldc, 0, p.M);
-  uint4 imm[12];
-  // byte offset (in the deferred tile's resource) of pass j of row half qm for this lane
-  int lane = lane0;
-  auto out_off = [&](int dn0, int qm, int j) -> unsigned {
-    const int rch = lane & 7, rr = lane >> 3;
-    return (unsigned)((((long)(wm * 128 + qm * 64 + j * 8 + rr)) * p.ldc + dn0 + colperm<BKO>(wn * 64 + rch * 8)) * 2);
-  };
-  int dn0 = 0;
-
-  floatx4 acc[2][2][4][2];
-  bf16x8 af[4][2], bfr[2][2];
-  const int ra = wm * 64, cb = wn * 32;
-
-  for (int tix = blockIdx.x; tix < total; tix += gridDim.x) {
-    // the lane id through an opaque move, once per tile: every lane-dependent address below is
-    // then recomputed per tile instead of being hoisted out of the tile loop into ~40 registers
-    // that would stay live through the main loop (the persistent form's register limit)
-    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
-    const int rch = lane & 7, rr = lane >> 3;
-    const int bid = xcd_remap(tix, total);
-    int m0, n0;
-    tile_of(bid, tiles_m, tiles_n, p.group_m, m0, n0);
-#define DL_STAGEP(T, KSLOT)                                                                         \
-  do {                                                                                              \
-    uint8_t* slot_ = smem + ((T) & 1) * BUF + (KSLOT) * HALF;                                       \
-    const int k0_ = (T) * BK;                                                                       \
-    if ((KSLOT) == 0) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 0, slot_, w, lane);          \
-    else if ((KSLOT) == 1) stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 1, slot_, w, lane);      \
-    else if ((KSLOT) == 2) stage_half<AKO, false>(p.A, p.lda, m0, p.M, k0_, 1, slot_, w, lane);     \
-    else stage_half<BKO, true>(p.B, p.ldb, n0, p.N, k0_, 0, slot_, w, lane);                        \
-  } while (0)
-
-    // prologue: tile 0 and half of tile 1, then the previous tile's first row half behind them
-    DL_STAGEP(0, 0); DL_STAGEP(0, 1); DL_STAGEP(0, 2); DL_STAGEP(0, 3);
-    if (nk > 1) { DL_STAGEP(1, 0); DL_STAGEP(1, 1); }
-    const bool def = dm0 >= 0;
-    if (def) {
-#pragma unroll
-      for (int j = 0; j < 12; ++j) bstore(drs, out_off(dn0, j >> 3, j & 7), imm[j], nt);
-      if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    } else {
-      if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    if (wm == 1) __builtin_amdgcn_s_barrier();
-    // accumulators zeroed only now: the previous tile's 48 output registers are free again
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-          for (int d = 0; d < 2; ++d) acc[a][b][c][d] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    // one K-tile; CARRY: this K-tile issues the previous tile's 4 deferred stores (one per phase,
-    // from the spare LDS) — a compile-time flag, so the steady-state loop carries no store code
-    auto ktile = [&](int t, auto carry) {
-      constexpr bool CARRY = decltype(carry)::value;
-      const uint8_t* buf = smem + (t & 1) * BUF;
-      const uint8_t* iA0 = buf;
-      const uint8_t* iB1 = buf + HALF;
-      const uint8_t* iA1 = buf + 2 * HALF;
-      const uint8_t* iB0 = buf + 3 * HALF;
-      const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
-      auto carry_store = [&](int ph) {
-        if constexpr (CARRY)
-          bstore(drs, out_off(dn0, 1, 4 + ph), *reinterpret_cast<const uint4*>(spare + ph * 1024 + lane * 16), nt);
-      };
-
-      // ---- phase 0
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA0, ra + mi * 16, ks, lane);
-      carry_store(0);
-      if (more1) DL_STAGEP(t + 1, 2);
-      __builtin_amdgcn_s_barrier();
-      DL_MFMA_QUAD(0, 0);
-      __builtin_amdgcn_s_barrier();
-
-      // ---- phase 1
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB1, cb + ni * 16, ks, lane);
-      carry_store(1);
-      if (more1) DL_STAGEP(t + 1, 3);
-      __builtin_amdgcn_s_barrier();
-      DL_MFMA_QUAD(0, 1);
-      __builtin_amdgcn_s_barrier();
-
-      // ---- phase 2
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<AKO>(iA1, ra + mi * 16, ks, lane);
-      carry_store(2);
-      if (more2) DL_STAGEP(t + 2, 0);
-      __builtin_amdgcn_s_barrier();
-      DL_MFMA_QUAD(1, 1);
-      __builtin_amdgcn_s_barrier();
-
-      // ---- phase 3
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<BKO>(iB0, cb + ni * 16, ks, lane);
-      carry_store(3);
-      if (more2) {
-        DL_STAGEP(t + 2, 1);
-        // awaited: the half-tiles issued up to phase 1; after them: [store] 2 glds [store] 2 glds
-        if constexpr (CARRY) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      DL_MFMA_QUAD(1, 0);
-      __builtin_amdgcn_s_barrier();
-    };
-    int t0 = 0;
-    if (def) {
-      ktile(0, std::true_type{});
-      t0 = 1;
-    }
-    for (int t = t0; t < nk; ++t) ktile(t, std::false_type{});
-#undef DL_STAGEP
-    if (wm == 0) __builtin_amdgcn_s_barrier();
-    // every wave's deferred stores of the previous tile have left (the spare LDS is rewritten
-    // below) and every fragment read is done (the epilogue reuses the pipeline's LDS)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-
-    // ---------------------------------------------------------------- epilogue -> registers
-    uint8_t* ep = smem + w * 16384;
-    const int crow = 4 * (lane >> 4), ccol = lane & 15;
-    float bias_v[2][2];
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        bias_v[qn][ni] = 0.f;
-        if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
-          if (p.bias) bias_v[qn][ni] = p.bias[n0 + colperm<BKO>(wn * 64 + qn * 32 + ni * 16 + ccol)];
-      }
-    float colsum[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
-    const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.C, p.ldc, m0, p.M);
-#pragma unroll
-    for (int qm = 0; qm < 2; ++qm) {
-#pragma unroll
-      for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int r = mi * 16 + crow + i;
-              const int c = qn * 32 + ni * 16 + ccol;
-              const int q = (c >> 2) ^ (r & 1);
-              *reinterpret_cast<float*>(ep + r * 256 + q * 16 + (c & 3) * 4) = acc[qm][qn][mi][ni][i] + bias_v[qn][ni];
-            }
-#pragma unroll
-      for (int pass = 0; pass < 8; ++pass) {
-        const int r = pass * 8 + rr;
-        const float4 lo = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch) ^ (r & 1)) << 4));
-        const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
-        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        const int gm = m0 + wm * 128 + qm * 64 + r;
-        const int gmc = min(gm, p.M - 1);  // rows past M: computed, then dropped by the range check
-        const int gn = n0 + colperm<BKO>(wn * 64 + rch * 8);
-        if constexpr (EPI == EPI_STORE) {
-          if (p.R) {
-            float rv[8];
-            load_bf16<8>(p.R + (long)gmc * p.ldr + gn, rv);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += rv[j];
-          }
-        } else if constexpr (EPI == EPI_GELU) {
-          float h[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
-          bstore(tile_rsrc(p.H, p.ldh, m0, p.M),
-                 (unsigned)((((long)(wm * 128 + qm * 64 + r)) * p.ldh + gn) * 2), pack8_bf16(h), nt);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = gelu_tanh_sig(h[j]);
-        } else {  // EPI_DGELU
-          float f[8];
-          load_bf16<8>(p.R + (long)gmc * p.ldr + gn, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(f[j]));
-            if (gm < p.M) colsum[j] += v[j];
-          }
-        }
-        const uint4 packed = pack8_bf16(v);
-        if (qm == 0 || pass < 4) imm[qm * 8 + pass] = packed;
-        else *reinterpret_cast<uint4*>(spare + (pass - 4) * 1024 + lane * 16) = packed;
-      }
-    }
-    if constexpr (EPI == EPI_DGELU) {
-      if (p.dbias) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float s = colsum[j];
-          s += __shfl_xor(s, 8, 64);
-          s += __shfl_xor(s, 16, 64);
-          s += __shfl_xor(s, 32, 64);
-          colsum[j] = s;
-        }
-        if (lane < 8) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + colperm<BKO>(wn * 64 + lane * 8) + j], colsum[j]);
-        }
-      }
-    }
-    dm0 = m0;
-    dn0 = n0;
-    drs = crs;
-    // the next prologue's LDS-DMA overwrites the epilogue staging: all waves' reads done first
-    // (and the outstanding epilogue loads / GELU stores / atomics retired, for exact counting)
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  // the last tile: flush both row halves
-  if (dm0 >= 0) {
-#pragma unroll
-    for (int j = 0; j < 12; ++j) bstore(drs, out_off(dn0, j >> 3, j & 7), imm[j], nt);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bstore(drs, out_off(dn0, 1, 4 + j), *reinterpret_cast<const uint4*>(spare + j * 1024 + lane * 16), nt);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// gemm8h: 256 x 128 tiles on 4 waves, TWO co-resident workgroups per CU (bf16 store epilogues).
-//
-// A 256 x 256 workgroup owns the whole CU (8 waves x 256 VGPRs = the register file; 128 KiB LDS),
-// so its output stores — 128 KiB per tile, issued at ~14 B/clk/CU, ~9K cycles — run with the
-// matrix pipes idle, ~20% of a K = 1024 GEMM (profiles/README.md round 3).  Here a workgroup is half
-// of that: 4 waves (2 x 2) each still own 128 x 64 outputs (the same per-wave MFMA/LDS-read work and
-// fragment layout as gemm8), 256 VGPRs, and 80 KiB of LDS, so two workgroups share every CU and
-// one's epilogue runs beside the other's main loop.
-//
-// LDS (80 KiB): a ring of 3 A half-tile slots (128 rows x 64 k, 16 KiB) and 4 B half-tile slots
-// (64 columns x 64 k, 8 KiB); half-tiles as in gemm8 (A half h = tile rows with bit 6 == h, B half
-// h = tile columns with bit 5 == h).  Per K-tile the waves run the quadrant phases (0,0) (0,1)
-// (1,1) (1,0), ONE barrier per phase (after its MFMAs); each phase issues one half-tile of the
-// next K-tile into the slot whose last reader was a phase that ended at an earlier barrier:
-//   ph0: A0(t+1) -> slot of A1(t-1)   ph1: B0(t+1) -> slot of B0(t-1)
-//   ph2: A1(t+1) -> slot of A0(t)     ph3: B1(t+1) -> slot of B1(t-1)
-// Counted waits (glds per thread: A half 4, B half 2): end of ph3 vmcnt(6) retires A0/B0(t+1)
-// (A1/B1(t+1) stay in flight), end of ph0 vmcnt(4) retires A1/B1(t+1) (A0(t+2) stays in flight);
-// the barrier after each wait publishes the other waves' DMAs before the next phase reads them.
-// K-inner operands only (forward GEMMs and the data gradients on transposed weight copies).
-// ---------------------------------------------------------------------------------------------
-constexpr int HBN = 128, HNT = 256;
-constexpr int HAH = 16384, HBH = 8192;
-constexpr int HA_SLOTS = 3, HB_SLOTS = 4;
-constexpr int HSMEM = HA_SLOTS * HAH + HB_SLOTS * HBH;  // 81920: two workgroups fill the 160 KiB
-
-// per-lane DMA source bases of one half-tile at k0 = 0: NP pieces of 1 KiB per wave
-template <bool ISB, int NP>
-__device__ __forceinline__ void hsrc_base(const bf16_t* __restrict__ g, long ld, int r0, int rows_valid, int half,
-                                          int w, int lane, const bf16_t* (&base)[NP]) {
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    const int lrow = (j * 4 + w) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ kin_swz(lrow);
-    const int grow = min(r0 + half_to_tile<ISB>(lrow, half), rows_valid - 1);
-    base[j] = g + (long)grow * ld + c * 8;
-  }
-}
-
-template <int NP>
-__device__ __forceinline__ void hstage(const bf16_t* const (&base)[NP], long koff, uint8_t* slot, int w) {
-#pragma unroll
-  for (int j = 0; j < NP; ++j) dma16(base[j] + koff, slot + (j * 4 + w) * 1024);
-}
-
-template <int EPI>
-__global__ __launch_bounds__(HNT, 2) void gemm8h_kernel(Args p) {
-  static_assert(EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU, "bf16 store epilogues");
-  __shared__ __attribute__((aligned(16))) uint8_t smem[HSMEM];
-  uint8_t* const sA = smem;
-  uint8_t* const sB = smem + HA_SLOTS * HAH;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int tiles_n = p.N / HBN;
-  const int tiles_m = (p.M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  int m0, n0;
-  {
-    const int G = p.group_m, band = G * tiles_n, first = (bid / band) * G;
-    const int gsz = min(tiles_m - first, G), r = bid % band;
-    m0 = (first + r % gsz) * BM;
-    n0 = (r / gsz) * HBN;
-  }
-  const int nk = p.K / BK;
-
-  floatx4 acc[2][2][4][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) acc[a][b][c][d] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  const bf16_t* bA0[4];
-  const bf16_t* bA1[4];
-  const bf16_t* bB0[2];
-  const bf16_t* bB1[2];
-  hsrc_base<false, 4>(p.A, p.lda, m0, p.M, 0, w, lane, bA0);
-  hsrc_base<false, 4>(p.A, p.lda, m0, p.M, 1, w, lane, bA1);
-  hsrc_base<true, 2>(p.B, p.ldb, n0, p.N, 0, w, lane, bB0);
-  hsrc_base<true, 2>(p.B, p.ldb, n0, p.N, 1, w, lane, bB1);
-  // half-tile h of K-tile t: A slot (2t + h) % 3, B slot (2t + h) % 4
-  auto slotA = [&](int t, int h) { return sA + ((2 * t + h) % HA_SLOTS) * HAH; };
-  auto slotB = [&](int t, int h) { return sB + ((2 * t + h) % HB_SLOTS) * HBH; };
-  auto koff = [&](int t) { return (long)t * BK; };
-
-  // prologue: all of K-tile 0 (A0 B0 B1 A1); the first phases need A0, B0, B1
-  hstage<4>(bA0, 0, slotA(0, 0), w);
-  hstage<2>(bB0, 0, slotB(0, 0), w);
-  hstage<2>(bB1, 0, slotB(0, 1), w);
-  hstage<4>(bA1, 0, slotA(0, 1), w);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  const int ra = wm * 64, cb = wn * 32;
-  bf16x8 af[4][2], bfr[2][2], bf0[2][2];
-  auto ktile = [&](int t, auto more) {
-    constexpr bool M1 = decltype(more)::value;  // K-tile t + 1 exists: stage it
-    const uint8_t* iA0 = slotA(t, 0);
-    const uint8_t* iA1 = slotA(t, 1);
-    const uint8_t* iB0 = slotB(t, 0);
-    const uint8_t* iB1 = slotB(t, 1);
-    const long kn = koff(t + 1);
-
-    // ---- phase 0: quadrant (0,0); stage A0(t+1)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) bf0[ni][ks] = frag<false>(iB0, cb + ni * 16, ks, lane);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<false>(iA0, ra + mi * 16, ks, lane);
-    if constexpr (M1) hstage<4>(bA0, kn, slotA(t + 1, 0), w);
-    DL_MFMA_QUAD_B(0, 0, bf0);
-    if constexpr (M1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-
-    // ---- phase 1: quadrant (0,1); stage B0(t+1)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) bfr[ni][ks] = frag<false>(iB1, cb + ni * 16, ks, lane);
-    if constexpr (M1) hstage<2>(bB0, kn, slotB(t + 1, 0), w);
-    DL_MFMA_QUAD(0, 1);
-    __builtin_amdgcn_s_barrier();
-
-    // ---- phase 2: quadrant (1,1); stage A1(t+1) (A0(t)'s slot: its last reader, phase 1, is done)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) af[mi][ks] = frag<false>(iA1, ra + mi * 16, ks, lane);
-    if constexpr (M1) hstage<4>(bA1, kn, slotA(t + 1, 1), w);
-    DL_MFMA_QUAD(1, 1);
-    __builtin_amdgcn_s_barrier();
-
-    // ---- phase 3: quadrant (1,0); stage B1(t+1); retire A0 / B0 of K-tile t+1
-    if constexpr (M1) hstage<2>(bB1, kn, slotB(t + 1, 1), w);
-    DL_MFMA_QUAD_B(1, 0, bf0);
-    if constexpr (M1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  for (int t = 0; t < nk - 1; ++t) ktile(t, std::true_type{});
-  ktile(nk - 1, std::false_type{});
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every fragment read done: the epilogue reuses the ring
-
-  // ---------------------------------------------------------------- epilogue (as gemm8)
-  uint8_t* ep = smem + w * 16384;
-  const int crow = 4 * (lane >> 4), ccol = lane & 15;
-  float bias_v[2][2];
-#pragma unroll
-  for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      bias_v[qn][ni] = 0.f;
-      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU)
-        if (p.bias) bias_v[qn][ni] = p.bias[n0 + wn * 64 + qn * 32 + ni * 16 + ccol];
-    }
-  float colsum[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) colsum[j] = 0.f;
-  const int rch = lane & 7, rr = lane >> 3;
-  const int gn = n0 + wn * 64 + rch * 8;
-  const bool has_r = EPI == EPI_DGELU || (EPI == EPI_STORE && p.R != nullptr);
-  auto rrow = [&](int qm, int pass) -> uint4 {
-    const int gm = min(m0 + wm * 128 + qm * 64 + pass * 8 + rr, p.M - 1);
-    return *reinterpret_cast<const uint4*>(p.R + (long)gm * p.ldr + gn);
-  };
-  uint4 rbuf[8];
-  if (has_r) {
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) rbuf[pass] = rrow(0, pass);
-  }
-#pragma unroll
-  for (int qm = 0; qm < 2; ++qm) {
-#pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = mi * 16 + crow + i;
-            const int c = qn * 32 + ni * 16 + ccol;
-            const int q = (c >> 2) ^ (r & 1);
-            *reinterpret_cast<float*>(ep + r * 256 + q * 16 + (c & 3) * 4) = acc[qm][qn][mi][ni][i] + bias_v[qn][ni];
-          }
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int r = pass * 8 + rr;
-      const float4 lo = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch) ^ (r & 1)) << 4));
-      const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      const int gm = m0 + wm * 128 + qm * 64 + r;
-      float rv[8];
-      if (has_r) {
-        unpack8_bf16(rbuf[pass], rv);
-        if (qm == 0) rbuf[pass] = rrow(1, pass);
-      }
-      if (gm < p.M) {
-        if constexpr (EPI == EPI_STORE) {
-          if (has_r) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += rv[j];
-          }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
-        } else if constexpr (EPI == EPI_GELU) {
-          float h[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
-          store8_bf16(p.H + (long)gm * p.ldh + gn, h, p.nt);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = gelu_tanh_sig(h[j]);
-          store8_bf16(p.C + (long)gm * p.ldc + gn, h, p.nt);
-        } else {  // EPI_DGELU
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(rv[j]));
-            colsum[j] += v[j];
-          }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
-        }
-      }
-    }
-  }
-  if constexpr (EPI == EPI_DGELU) {
-    if (p.dbias) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float s = colsum[j];
-        s += __shfl_xor(s, 8, 64);
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        colsum[j] = s;
-      }
-      if (lane < 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) atomicAdd(&p.dbias[n0 + wn * 64 + lane * 8 + j], colsum[j]);
-      }
-    }
-  }
-}
-
 #undef DL_MFMA_QUAD
 #undef DL_MFMA_QUAD_B
 
-// DEDLOC_GEMM8_HALF=1: K-inner bf16-epilogue GEMMs on gemm8h (two co-resident 256 x 128 workgroups
-// per CU) instead of one 256 x 256 workgroup; read per call (A/B in one process)
-bool half_tiles() {
-  const char* e = std::getenv("DEDLOC_GEMM8_HALF");
-  return e && e[0] == '1';
-}
-
-bool keep_b0() {  // read per call (A/B in one process); DEDLOC_GEMM8_KEEPB0=0: re-read B0 in phase 3
-  const char* e = std::getenv("DEDLOC_GEMM8_KEEPB0");
-  return !(e && e[0] == '0');
-}
-
-// read per call; DEDLOC_GEMM8_PRESRC=0: the per-K-tile source address math and run-time prefetch
-// conditions.  Default on: at T = 262144 the weight gradients run 5-7% and the forward / data-gradient
-// forms 1-3% faster, the B=512 micro-step 924.3 / 926.1 -> 946.6 / 944.7 samples/s same box
-// (profiles/r3_gemm8_presrc_*); the bias+GELU form measured 2% slower and keeps the old loop
-bool pre_src() {
-  const char* e = std::getenv("DEDLOC_GEMM8_PRESRC");
-  return !(e && e[0] == '0');
-}
-
-int persistent_ctas() {  // read per call: tests and benchmarks A/B the two forms in one process
-  const char* e = std::getenv("DEDLOC_GEMM8_PERSIST");
-  return e ? std::atoi(e) : 0;
-}
-
+// B0 fragments kept in registers for phase 3 (+1-4% per GEMM, +1.8% on the power-capped step) and
+// DMA source bases computed once with the K-loop tail peeled (weight gradients +5-7%, forward / data
+// gradients +1-3%; the bias+GELU form measured 2% slower with it and keeps the per-K-tile address
+// math) — round 3, profiles/r3_gemm8_keep_b0_*, r3_gemm8_presrc_*.  The losing forms (B0 re-read,
+// persistent deferred-store tiles, 256 x 128 co-resident tiles: profiles/README.md) are gone.
 template <bool AKO, bool BKO, int EPI>
 int launch8(const Args& a, int splits, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
-  if constexpr (EPI != EPI_F32 && EPI != EPI_STATS && EPI != EPI_BNBWD) {
-    // DEDLOC_GEMM8_PERSIST=n: the persistent deferred-store form on min(tiles, n) workgroups
-    // (n = 256: one per CU of an MI355X)
-    const int ctas = persistent_ctas();
-    if (ctas > 0 && splits == 1 && tiles > ctas && a.K / BK >= 2) {
-      gemm8p_kernel<AKO, BKO, EPI><<<dim3(ctas), NT, 0, st>>>(a);
-      return 0;
-    }
-  }
-  if constexpr (!AKO && !BKO && (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_DGELU)) {
-    if (splits == 1 && half_tiles() && a.N % HBN == 0) {
-      gemm8h_kernel<EPI><<<dim3(((a.M + BM - 1) / BM) * (a.N / HBN)), HNT, 0, st>>>(a);
-      return 0;
-    }
-  }
   const dim3 grid(tiles * splits);
-  if (!keep_b0()) gemm8_kernel<AKO, BKO, EPI, false, false><<<grid, NT, 0, st>>>(a);
-  else if (EPI != EPI_GELU && pre_src()) gemm8_kernel<AKO, BKO, EPI, true, true><<<grid, NT, 0, st>>>(a);
-  else gemm8_kernel<AKO, BKO, EPI, true, false><<<grid, NT, 0, st>>>(a);
+  if constexpr (EPI == EPI_GELU) gemm8_kernel<AKO, BKO, EPI, false><<<grid, NT, 0, st>>>(a);
+  else gemm8_kernel<AKO, BKO, EPI, true><<<grid, NT, 0, st>>>(a);
   return 0;
 }
 
@@ -1291,15 +691,12 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
                              (!bn->Y && (!bn->gamma || !bn->beta))))
       return -1;
   }
-  // non-temporal bf16 output stores by default (+4..17% on the store-bound epilogues, gemm_bench);
-  // DEDLOC_GEMM8_NT=0 for A/B runs
-  const char* nte = std::getenv("DEDLOC_GEMM8_NT");
-  const int nt = nte ? std::atoi(nte) : 1;
-  // tile order (tile_of): DEDLOC_GEMM8_GROUP row blocks per band.  Default 4: against row-major
-  // (1) at T = 262144 the QKV forward 1507 -> 1468 us, FFN-up + GELU 2409 -> 2324 us, FFN-down data
-  // gradient 2027 -> 1970 us, the rest within +-1.5% (profiles/r3_gemm8_tile_order_T262144.jsonl)
-  const char* ge = std::getenv("DEDLOC_GEMM8_GROUP");
-  const int group_m = ge ? std::max(1, std::atoi(ge)) : 4;
+  // non-temporal bf16 output stores (+4..17% on the store-bound epilogues, gemm_bench)
+  constexpr int nt = 1;
+  // tile order (tile_of): bands of 4 row blocks.  Against row-major at T = 262144 the QKV forward
+  // 1507 -> 1468 us, FFN-up + GELU 2409 -> 2324 us, FFN-down data gradient 2027 -> 1970 us, the rest
+  // within +-1.5% (profiles/r3_gemm8_tile_order_T262144.jsonl)
+  constexpr int group_m = 4;
   Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt,
          stats, stat_rows, DlBnBwdEpi{}, group_m};
   if (epi == EPI_BNBWD) a.bn = *bn;  // by value: the kernel reads it from its argument buffer

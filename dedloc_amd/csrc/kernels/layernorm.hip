@@ -274,25 +274,12 @@ void launch_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const floa
 template <int D>
 void launch_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
                 bf16_t* ds, float* dg_part, float* db_part, float* dsum, int rows, int nparts, hipStream_t st) {
-  // waves per block (DEDLOC_LN_WPB, measurement override): 8 measured equal to 4 — the two-row
-  // form's 202 VGPRs cap the kernel at 2 waves per SIMD either way
-  static const int wpb = [] {
-    const char* e = std::getenv("DEDLOC_LN_WPB");
-    return e ? std::max(1, std::min(8, std::atoi(e))) : 4;
-  }();
+  // 4 waves per block (8 measured equal: the two-row form's 202 VGPRs cap the kernel at 2 waves per
+  // SIMD either way) and 2 rows in flight per wave (the round-2 A/B winner over 1 and 4)
+  constexpr int wpb = 4;
   const int rpb = (rows + nparts - 1) / nparts;
-  size_t lds = (size_t)wpb * D * sizeof(float);
-  // DEDLOC_LN_ROWS=1|2|4: rows in flight per wave (A/B measurement); default 2
-  static const int R = [] {
-    const char* e = std::getenv("DEDLOC_LN_ROWS");
-    return e ? std::atoi(e) : 2;
-  }();
-  if (R == 4)
-    ln_bwd_kernel<D, 4><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
-  else if (R == 1)
-    ln_bwd_kernel<D, 1><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
-  else
-    ln_bwd_kernel<D, 2><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
+  const size_t lds = (size_t)wpb * D * sizeof(float);
+  ln_bwd_kernel<D, 2><<<nparts, 64 * wpb, lds, st>>>(dy, s, gamma, mean, rstd, ds, dg_part, db_part, dsum, rows, rpb);
 }
 
 }  // namespace

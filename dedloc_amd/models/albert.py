@@ -135,32 +135,18 @@ def _layer_prefix(g: int, i: int) -> str:
     return f"albert.encoder.albert_layer_groups.{g}.albert_layers.{i}."
 
 
-# DEDLOC_RESIDUAL=ln keeps the residual add inside the LayerNorm kernel (A/B measurement)
-_RESIDUAL_IN_GEMM = os.environ.get("DEDLOC_RESIDUAL", "gemm") != "ln"
+# The residual sums ride in the output-projection / FFN-down GEMM epilogues (C = h, beta = 1): the
+# LayerNorms then read one tensor and write one — 2 of 4 LN HBM passes removed (round 2).
+# (Module constants, not environment knobs: tests and bench/ab_step.py flip them in-process.)
+_RESIDUAL_IN_GEMM = True
 # The backward's data-gradient GEMMs (dX = dY W) run against transposed weight copies made once per
 # encoder call (the 24 layers share them): gemm8 with both operands K-inner beats the K-outer-B form
-# by 5-10% on these shapes (profiles/gemm8_asm_dma_layouts_T131072.log).  DEDLOC_DGRAD_WT=0: plain
-# weights.
-_DGRAD_WT = os.environ.get("DEDLOC_DGRAD_WT", "1") != "0"
+# by 5-10% on these shapes (profiles/gemm8_asm_dma_layouts_T131072.log).
+_DGRAD_WT = True
 # Weight gradients of the shared layer keep their token-split fp32 slabs across the layer
 # applications and add them into the flat gradient once, at the last backward call
-# (gemm_acc_f32_shared).  DEDLOC_SHARED_WGRAD=0: one slab sum per call.
-_SHARED_WGRAD = os.environ.get("DEDLOC_SHARED_WGRAD", "1") != "0"
-# Weight-gradient GEMMs are off the backward's critical path (nothing reads them before the
-# optimizer).  DEDLOC_WGRAD_STREAM=1 pairs each with a memory-bound kernel of the main stream:
-# the wgrad is forked onto a side HIP stream right before the main stream's GELU-backward /
-# LayerNorm-backward kernel and joined before the next data-gradient GEMM, so two GEMMs never
-# co-run (they contend; a free-running side stream measured 10% slower) while MFMA-bound and
-# HBM-bound work overlap.
-_WGRAD_STREAM = os.environ.get("DEDLOC_WGRAD_STREAM", "0") == "1"
-_SIDE_STREAMS: Dict = {}
-
-
-def _side_stream(device):
-    st = _SIDE_STREAMS.get(device)
-    if st is None:
-        st = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
-    return st
+# (gemm_acc_f32_shared).
+_SHARED_WGRAD = True
 
 
 class _AlbertLayerFn(torch.autograd.Function):
@@ -204,8 +190,6 @@ class _AlbertLayerFn(torch.autograd.Function):
         lv = ctx.lv
         dy = dy.contiguous()
         H = ctx.H
-        if "wg_stream" in lv:
-            return _AlbertLayerFn._backward_overlapped(ctx, dy.contiguous())
         # LN backward also accumulates colsum(ds) = the bias grad of the Linear that fed it
         ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True, lv["gb2"])
         _wgrad(O, ds2, g, lv, "gw2")
@@ -226,63 +210,12 @@ class _AlbertLayerFn(torch.autograd.Function):
         dh = _dgrad(O, dqkv, lv, "wqkv", ds1)
         return dh, None, None, None, None, None
 
-    @staticmethod
-    def _backward_overlapped(ctx, dy):
-        """The same backward with every weight-gradient GEMM forked onto the side stream beside a
-        memory-bound main-stream kernel and joined before the main stream's next GEMM:
-        W2 || GELU-backward, W1 || LayerNorm-1 backward, Wo + Wqkv || the next backward call's
-        LayerNorm-2 backward (the first backward call of a weight set joins at its end)."""
-        O = ops.OPS
-        h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2 = ctx.saved_tensors
-        lv = ctx.lv
-        ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True, lv["gb2"])
-        _join_wgrads(lv)  # the previous backward call's Wo / Wqkv GEMMs ran beside that LayerNorm
-        dg = (O.gemm(ds2, lv["w2t"], None, None, False, True, 0) if "w2t" in lv
-              else O.gemm(ds2, lv["w2"], None, None, False, False, 0))
-        _wgrad(O, ds2, g, lv, "gw2")
-        df = O.gelu_bwd(dg, f, lv["gb1"])  # gelu'(f) * dg + ffn bias grad
-        del dg
-        _join_wgrads(lv)
-        dh1 = _dgrad(O, df, lv, "w1", ds2)
-        _wgrad(O, df, h1, lv, "gw1")
-        del df
-        ds1 = O.layernorm_bwd(dh1, s1, lv["ln1g"], m1, r1, lv["gln1g"], lv["gln1b"], True, lv["gbo"])
-        _join_wgrads(lv)
-        datt = _dgrad(O, ds1, lv, "wo", None)
-        H = ctx.H
-        dqkv = ops.attn_bwd(qkv, ctx.mask[0], att, datt, lse, H, ctx.S, 1.0 / math.sqrt(qkv.shape[1] // (3 * H)),
-                          ctx.mask[1], lv["gbqkv"])
-        dh = _dgrad(O, dqkv, lv, "wqkv", ds1)
-        _wgrad(O, ds1, att, lv, "gwo")
-        _wgrad(O, dqkv, h, lv, "gwqkv")
-        if lv.get("wg_last"):  # last backward call for these weights: nothing follows to pair with
-            _join_wgrads(lv)
-        return dh, None, None, None, None, None
-
 
 def _wgrad(O, dy, x, lv, name):
     """lv[name] += dY^T X; with the layer's position among the applications of its weights
     (``wg_first`` / ``wg_last``, set by encode) the slab sum is deferred to the last backward call.
-    With ``wg_stream`` the GEMM is forked onto that side stream after everything the main stream
-    has queued so far (joined by _join_wgrads before the main stream's next GEMM)."""
-    side = lv.get("wg_stream")
-    if side is None:
-        _wgrad_now(O, dy, x, lv, name)
-        return
-    side.wait_stream(torch.cuda.current_stream(dy.device))
-    with torch.cuda.stream(side):
-        _wgrad_now(O, dy, x, lv, name)
-    dy.record_stream(side)  # the caching allocator must not hand these to the main stream early
-    x.record_stream(side)
-
-
-def _join_wgrads(lv):
-    side = lv.get("wg_stream")
-    if side is not None:
-        torch.cuda.current_stream(side.device).wait_stream(side)
-
-
-def _wgrad_now(O, dy, x, lv, name):
+    (Forking these GEMMs onto a side stream beside the memory-bound kernels measured 10% slower
+    free-running and no gain paired; removed in round 4.)"""
     if "wg_first" in lv:
         O.gemm_acc_f32_shared(dy, x, lv[name], True, False, lv["wg_first"], lv["wg_last"])
     else:
@@ -518,8 +451,6 @@ class AlbertPreTrainedModel(nn.Module):
                     # backward runs the layers in reverse: the last application is the first to
                     # write the weight's gradient slabs, the first application sums them in
                     lv = dict(lv, wg_first=layer == uses[-1], wg_last=layer == uses[0])
-                    if _WGRAD_STREAM and h.is_cuda:
-                        lv["wg_stream"] = _side_stream(h.device)
                 h = self._albert_layer(h, lv, mask, Sp)
         return h, Sp
 

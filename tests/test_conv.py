@@ -28,14 +28,15 @@ SHAPES = [
 ]
 
 
-# 1x1 stride-1 convs and the stem's column GEMM route to hipBLASLt by default (bindings.cpp conv_lt)
+# 1x1 stride-1 convs and the stem's column GEMM take the tiled GEMM kernels (gemm8 / gemm.hip /
+# gemm_small) where their output is wider than 128 columns, conv.hip otherwise
 LT_SHAPES = [s for s in SHAPES if s[1] == 3 or (s[4] == 1 and s[5] == 1)]
 
 
 @pytest.fixture
-def hip_kernels(monkeypatch):
-    """Force conv.hip for every shape (the library route would otherwise take the GEMM-shaped ones)."""
-    monkeypatch.setenv("DEDLOC_CONV_GEMM", "hip")
+def hip_kernels():
+    """The default dispatch (every conv on the hand-written kernels: conv.hip or the GEMM tiles)."""
+    yield
 
 
 def _rel(a, b):
@@ -142,10 +143,9 @@ def test_conv_wgrad_large_reduction_split_k(cuda, hip_kernels):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", LT_SHAPES + [(4, 3, 224, 64, 7, 2, 3)], ids=lambda s: "x".join(map(str, s)))
-def test_conv_library_gemm_route_gpu(cuda, shape, monkeypatch):
-    """Default routing: pointwise convs and the stem GEMM through hipBLASLt (fwd, dgrad, fp32 wgrad
+def test_conv_gemm_route_gpu(cuda, shape):
+    """Pointwise convs and the stem's column GEMM on the tiled GEMM kernels (fwd, dgrad, fp32 wgrad
     accumulated with token-split slabs)."""
-    monkeypatch.delenv("DEDLOC_CONV_GEMM", raising=False)
     N, Cin, H, Cout, k, stride, pad = shape
     x, w, dy = _data(cuda, *shape, seed=4)
     yr, dxr, dwr = _reference(x, w, dy, stride, pad)
@@ -328,25 +328,3 @@ def test_chained_bottlenecks_grads_match_fp32(cuda, cin, planes, stride):
     for n, _ in m.named_parameters():
         ours, theirs = _rel(flat.view(flat.grad, n), rp[n].grad), _rel(sp[n].grad, rp[n].grad)
         assert ours < bound(theirs), (n, ours, theirs)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(8, 64, 28, 64, 3, 1, 1), (4, 128, 28, 256, 3, 2, 1), (8, 64, 28, 256, 1, 1, 0)])
-def test_conv_wgrad_slab_mode_matches_atomics(cuda, monkeypatch, shape):
-    """The split weight gradient's slab form (per-split fp32 partials + a summing pass) equals the
-    atomic-add form up to fp32 summation order, accumulating into the existing gradient."""
-    N, Cin, H, Cout, k, stride, pad = shape
-    torch.manual_seed(4)
-    x = torch.randn(N, Cin, H, H, device=cuda).bfloat16().contiguous(memory_format=CL)
-    P = (H + 2 * pad - k) // stride + 1
-    dy = torch.randn(N, Cout, P, P, device=cuda).bfloat16().contiguous(memory_format=CL)
-    outs = []
-    for slab in ("0", "1"):
-        monkeypatch.setenv("DEDLOC_CONV_WGRAD_SLAB", slab)
-        monkeypatch.setenv("DEDLOC_CONV_GEMM", "hip")
-        dw = torch.ones(Cout, Cin, k, k, device=cuda).contiguous(memory_format=CL)
-        torch.ops.dedloc.conv2d_wgrad(dy, x, dw, stride, pad)
-        outs.append(dw)
-    torch.testing.assert_close(outs[1], outs[0], rtol=1e-4, atol=1e-3)
-    ref = torch.nn.grad.conv2d_weight(x.float(), (Cout, Cin, k, k), dy.float(), stride=stride, padding=pad) + 1
-    assert _rel(outs[1], ref) < 1e-2

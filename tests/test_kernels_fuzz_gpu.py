@@ -208,15 +208,12 @@ def test_sinkhorn_and_swav_ce_fuzz(cuda, O, bs, extra, K, seed):
 @FUZZ
 @given(N=st.integers(1, 3), Cin=st.sampled_from([64, 128, 192, 256]), Cout=st.sampled_from([64, 128, 192, 256]),
        H=st.integers(3, 20), geo=st.sampled_from([(1, 1, 0), (1, 2, 0), (3, 1, 1), (3, 2, 1)]),
-       route=st.sampled_from(["hip", "default"]), seed=st.integers(0, 2**16))
-def test_conv_fuzz(cuda, O, monkeypatch, N, Cin, Cout, H, geo, route, seed):
-    """NHWC convolution forward / data gradient / fp32 weight gradient (conv.hip implicit GEMM, or
-    the default per-shape routing through hipBLASLt for pointwise convs) at arbitrary spatial sizes."""
+       seed=st.integers(0, 2**16))
+def test_conv_fuzz(cuda, O, N, Cin, Cout, H, geo, seed):
+    """NHWC convolution forward / data gradient / fp32 weight gradient (the per-shape routing:
+    conv.hip implicit GEMM, the tiled GEMM kernels for wide pointwise convs) at arbitrary spatial
+    sizes."""
     k, stride, pad = geo
-    if route == "hip":
-        monkeypatch.setenv("DEDLOC_CONV_GEMM", "hip")
-    else:
-        monkeypatch.delenv("DEDLOC_CONV_GEMM", raising=False)
     cl = torch.channels_last
     g = torch.Generator(device="cpu").manual_seed(seed)
     x = torch.randn(N, Cin, H, H, generator=g).bfloat16().to(cuda).contiguous(memory_format=cl)
