@@ -1180,8 +1180,8 @@ at::Tensor conv2d_dgrad(const at::Tensor& dy_in, const at::Tensor& w, int64_t st
 // backward (which then skips its statistics pass, bn_bwd(stats_ready)): returns g = dX (+ residual)
 // masked by the ReLU — mask from y > 0 when y is given (the BN had a residual branch), else from
 // the forward's pre-activation over x (the BN input) — and adds sums[grp][c] += g, sums[grp][C + c]
-// += g * (x - mean) * rstd, in the GEMM epilogue of a 1x1 stride-1 data gradient (gemm8 EPI 5;
-// gemm_small's per-element epilogue with DEDLOC_BN_BWD_SMALL=1) or in conv.hip's epilogue on every
+// += g * (x - mean) * rstd, in the GEMM epilogue of a 1x1 stride-1 data gradient (gemm8 EPI 5)
+// or in conv.hip's epilogue on every
 // parity class of the others (no residual; whole 256-row tiles per statistics group).  Returns
 // (dx, fused): where the epilogue cannot take it, dx is the plain data gradient (+ residual), unmasked, and fused is false —
 // the BN backward then runs its own statistics pass (a separate preparation pass here would cost

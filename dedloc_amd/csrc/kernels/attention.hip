@@ -400,7 +400,7 @@ __device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int
 
 // Block = NW waves x QS x 32 query rows of one (batch, head).  NW = 8 (ring only): one 512-query
 // block per head at S = 512, so K / V are staged once per head, and each SIMD's two waves belong
-// to one block (DEDLOC_ATTN_NW=8).
+// to one block.
 template <bool RING, int QS, int NW = 4>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                           const float* __restrict__ mbias,

@@ -29,8 +29,8 @@ namespace {
 
 constexpr int kThreads = 256;
 // 16-byte vectors (rows) in flight per thread in the streaming passes (apply, backward statistics,
-// dx): template parameter BN_U, DEDLOC_BN_UNROLL = 2 (default) or 4.  4 needs 116-190 VGPRs and
-// halves the resident waves: SwAV iteration 2186-2191 vs 2202-2212 samples/s with 2 (same box)
+// dx): template parameter BN_U = 2.  4 needed 116-190 VGPRs and halved the resident waves: SwAV
+// iteration 2186-2191 vs 2202-2212 samples/s with 2 (same box; the 4 form was removed in round 4)
 
 __device__ __forceinline__ void ld8(const bf16_t* p, float (&v)[8]) { load_bf16<8>(p, v); }
 

@@ -220,6 +220,8 @@ class ConvNHWC(nn.Conv2d):
     # False: return the weight gradient through autograd instead of adding it into the bound .grad
     # (HIP-graph capture via make_graphed_callables needs every parameter to receive an autograd grad)
     inplace_wgrad = True
+    # False: the consuming BatchNorm runs its own statistics pass (tests compare the two orders)
+    epilogue_stats = True
 
     def forward(self, x, bn=None, link=None, bn_link=None):
         """``bn``: the BNAct that consumes this output.  When it will take its fused path with a
@@ -234,7 +236,7 @@ class ConvNHWC(nn.Conv2d):
             raise NotImplementedError("ConvNHWC: only the ResNet-50 conv forms (no bias, groups 1, square "
                                       "stride/padding) have kernels")
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        if bn is not None and bn.takes_conv_stats():
+        if bn is not None and self.epilogue_stats and bn.takes_conv_stats():
             bn.stats_ready = True
             return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, bn.pass_ws[0],
                                    bn.stat_groups, link, bn_link)
