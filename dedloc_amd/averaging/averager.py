@@ -333,7 +333,8 @@ class DecentralizedAverager:
         V = sum(t.numel() for t in tensors)
         bws = [i["bandwidth"] for i in infos]
         if GroupCommunicators.group_backend(members) == "hybrid":
-            bws = [(self.XGMI_MBPS if b > 0 else 0.0) if i.get("backend") == "rccl" else b for b, i in zip(bws, infos)]
+            on_rccl = set(GroupCommunicators.rccl_members(members))
+            bws = [(self.XGMI_MBPS if b > 0 else 0.0) if p in on_rccl else b for b, p in zip(bws, pids)]
         parts = load_balance_peers(V, bws, min_size=0)
         if not any(not i["aux"] for i in infos):
             return None

@@ -388,7 +388,21 @@ class CollaborativeOptimizer:
         self.averager.publish_state_sharing(self.local_step)
         self.last_step_time = get_dht_time()
         logger.log(self.status_loglevel, f"optimizer step #{self.local_step} done")
+        self._prejoin_next(batch_size, cs.num_peers)
         return group
+
+    def _prejoin_next(self, batch_size: int, num_peers: int):
+        """Right after a global step: when one micro-step of every peer completes the next global
+        batch (num_peers x batch_size >= target, e.g. 8 peers x 512 samples at 4096), the next global
+        step begins right after this peer's next micro-step — _maybe_prejoin, which runs only between
+        micro-steps, never sees that moment — so matchmaking for it starts now and runs while the
+        micro-step computes."""
+        if self._prejoin is not None or not self.prejoin_enabled or self.delay_param_averaging or num_peers < 2:
+            return
+        if num_peers * batch_size < self.target_batch_size:
+            return
+        self._prejoin = self.averager.prejoin(expected_group_size=num_peers + self._num_aux(),
+                                              gather={"step": int(self.local_step)})
 
     def _maybe_prejoin(self, batch_size: int):
         """Begin matchmaking now when the NEXT local step will start the global step (the

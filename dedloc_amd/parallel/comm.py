@@ -310,6 +310,7 @@ class GroupCommunicators:
         self.created = 0
         self.aborted = 0
         self.rccl_create_failures = 0  # consecutive RCCL communicators this peer could not bring up
+        self._gpu_id: Optional[str] = None
         self._fallback_since: Optional[float] = None
 
     # ------------------------------------------------------------------ matchmaking info
@@ -323,14 +324,43 @@ class GroupCommunicators:
             self.rccl_create_failures = self.RCCL_FALLBACK_AFTER - 1  # one more try
         return "rccl" if rccl_available(self.device) else "gloo"
 
+    @property
+    def gpu_id(self) -> Optional[str]:
+        """Host + device identity: RCCL takes one rank per device, so peers that share a GPU (a
+        protocol emulation on a small box) cannot be ranks of one communicator."""
+        if self._gpu_id is None and self.device.type == "cuda":
+            props = torch.cuda.get_device_properties(self.device)
+            uid = getattr(props, "uuid", None)
+            self._gpu_id = f"{socket.gethostname()}/{uid if uid is not None else self.device.index}"
+        return self._gpu_id
+
     def announce(self) -> Dict:
         """The fields this peer adds to its matchmaking info."""
         with self._lock:
-            return {"backend": self.backend, "comms": list(self._cache.keys())}
+            backend = self.backend
+            return {"backend": backend, "comms": list(self._cache.keys()),
+                    "gpu": self.gpu_id if backend == "rccl" else None}
 
     @staticmethod
-    def group_backend(members: Sequence[Tuple[bytes, Dict]]) -> str:
-        n_rccl = sum(1 for _, info in members if info.get("backend") == "rccl")
+    def rccl_members(members: Sequence[Tuple[bytes, Dict]]) -> List[bytes]:
+        """Sorted peer ids of the members that take an RCCL rank: every member announcing rccl,
+        except that of several members on one device only the first (in peer-id order) does — the
+        others join the group's gloo side like CPU members."""
+        seen, out = set(), []
+        for pid, info in sorted(members, key=lambda m: bytes(m[0])):
+            if info.get("backend") != "rccl":
+                continue
+            gpu = info.get("gpu")
+            if gpu is not None:
+                if gpu in seen:
+                    continue
+                seen.add(gpu)
+            out.append(bytes(pid))
+        return out
+
+    @classmethod
+    def group_backend(cls, members: Sequence[Tuple[bytes, Dict]]) -> str:
+        n_rccl = len(cls.rccl_members(members))
         if n_rccl == len(members):
             return "rccl"
         return "hybrid" if n_rccl >= 2 else "gloo"
@@ -359,9 +389,7 @@ class GroupCommunicators:
             if deadline is None:
                 deadline = time.monotonic() + self.timeout_s
             if backend == "hybrid":
-                info_of = {bytes(pid): info for pid, info in members}
-                gpu = [p for p in pids if info_of[p].get("backend") == "rccl"]
-                comm = self._create_hybrid(tok, pids, gpu, deadline)
+                comm = self._create_hybrid(tok, pids, self.rccl_members(members), deadline)
             else:
                 comm = self._create(tok, backend, len(pids), rank_of[self.peer_id], deadline)
             self._cache[tok] = _Entry(comm, key, pids)

@@ -253,3 +253,20 @@ def test_mixed_group_keeps_gpu_members_on_rccl(fake):
         for d in dhts:
             d.shutdown()
         root.shutdown()
+
+
+def test_peers_sharing_a_gpu_take_one_rccl_rank():
+    """RCCL takes one rank per device: of several members announcing the same GPU only the first (in
+    peer-id order) is an RCCL member, the rest join the group's gloo side — so 8 peers emulated on one
+    GPU average over gloo instead of failing communicator set-up every round, and 2 GPUs with 4
+    peers each form a hybrid group with one RCCL rank per GPU."""
+    G = C.GroupCommunicators
+    one_gpu = [(bytes([65 + i]), {"backend": "rccl", "gpu": "host/gpu0"}) for i in range(8)]
+    assert G.rccl_members(one_gpu) == [b"A"] and G.group_backend(one_gpu) == "gloo"
+    two_gpus = [(bytes([65 + i]), {"backend": "rccl", "gpu": f"host/gpu{i % 2}"}) for i in range(8)]
+    assert G.rccl_members(two_gpus) == [b"A", b"B"] and G.group_backend(two_gpus) == "hybrid"
+    distinct = [(bytes([65 + i]), {"backend": "rccl", "gpu": f"host/gpu{i}"}) for i in range(4)]
+    assert G.group_backend(distinct) == "rccl"
+    # members that announce no device identity (older peers) keep the previous rule
+    legacy = [(b"x", {"backend": "rccl"}), (b"y", {"backend": "rccl"}), (b"z", {"backend": "gloo"})]
+    assert G.rccl_members(legacy) == [b"x", b"y"] and G.group_backend(legacy) == "hybrid"
