@@ -57,7 +57,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     inc = ["-I", os.path.join(CSRC, "include")]
-    hip_flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-munsafe-fp-atomics"]
+    hip_flags = ["--offload-arch=" + ARCH, *HIP_FLAGS]
     jobs = jobs or min(8, os.cpu_count() or 4)
 
     jobs_list = []
@@ -103,17 +103,56 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         list(ex.map(lambda c: _run(c, verbose), jobs_list))
 
     if _newer(SO_PATH, objs):
-        cmd = ["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", SO_PATH]
-        for p in tlib:
-            cmd += ["-L", p, f"-Wl,-rpath,{p}"]
-        # -lrccl resolves in torch's lib dir first: the same librccl.so.1 torch loads (one RCCL per process)
-        cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl", "-L", f"{ROCM}/lib",
-                f"-Wl,-rpath,{ROCM}/lib"]
-        _run(cmd, verbose)
+        _link(objs, SO_PATH, tlib, verbose)
     if rt_objs and _newer(DHT_SO_PATH, rt_objs):
         _run(["g++", "-shared", "-fPIC", *rt_objs, "-o", DHT_SO_PATH, "-lpthread"], verbose)
+    _OBJS[:] = objs
     return SO_PATH
 
 
+_OBJS: list = []  # the kernel library's objects, in link order (filled by build)
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-munsafe-fp-atomics"]
+
+
+def _link(objs, out, tlib, verbose):
+    cmd = ["hipcc", "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", out]
+    for p in tlib:
+        cmd += ["-L", p, f"-Wl,-rpath,{p}"]
+    # -lrccl resolves in torch's lib dir first: the same librccl.so.1 torch loads (one RCCL per process)
+    cmd += ["-lc10", "-ltorch", "-ltorch_cpu", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl", "-L", f"{ROCM}/lib",
+            f"-Wl,-rpath,{ROCM}/lib"]
+    _run(cmd, verbose)
+
+
+def build_variant(name: str, rev: str, kernels, verbose: bool = False) -> str:
+    """Measurement helper for same-box A/B runs: the kernel library with the given ``csrc/kernels``
+    files taken from git revision ``rev`` (everything else as built now), linked into
+    ``ab/_C_<name>.so``; a process loads it instead of ``_C.so`` with DEDLOC_NATIVE_LIB=<that path>."""
+    build(verbose)
+    vdir = os.path.join(os.path.dirname(BUILD), "variant_" + name)
+    os.makedirs(vdir, exist_ok=True)
+    repo = os.path.dirname(ROOT)
+    swap = {}
+    for k in kernels:
+        src = os.path.join(vdir, os.path.basename(k))
+        text = subprocess.run(["git", "-C", repo, "show", f"{rev}:dedloc_amd/csrc/kernels/{os.path.basename(k)}"],
+                              check=True, capture_output=True, text=True).stdout
+        with open(src, "w") as f:
+            f.write(text)
+        obj = src.replace(".hip", ".o")
+        _run(["hipcc", "--offload-arch=" + ARCH, *HIP_FLAGS, "-I", os.path.join(CSRC, "include"), "-c", src, "-o", obj],
+             verbose)
+        swap[os.path.basename(obj)] = obj
+    out_dir = os.path.join(repo, "ab")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"_C_{name}.so")
+    objs = [swap.get(os.path.basename(o), o) for o in _OBJS]
+    _link(objs, out, _torch_paths()[1], verbose)
+    return out
+
+
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    if len(sys.argv) > 3 and sys.argv[1] == "variant":  # python -m dedloc_amd._build variant NAME REV kernel.hip ...
+        print(build_variant(sys.argv[2], sys.argv[3], sys.argv[4:], verbose="-v" in sys.argv))
+    else:
+        print(build(verbose="-v" in sys.argv))

@@ -948,6 +948,38 @@ inline StemCols stem_cols(int64_t R, int64_t S, int64_t C, bool lt) {
   const int64_t SCp = (S * C + 7) / 8 * 8;  // hipBLASLt needs 16-byte rows only; conv.hip a multiple of BK
   return {SCp, lt ? R * SCp : (R * SCp + 63) / 64 * 64};
 }
+// The 7x7 stride-2 pad-3 stem over 3 channels (even H, W) runs as a 4x4 stride-1 conv over the
+// space-to-depth image xs [N, H/2, W/2, 16] (dl_stem_s2d): tap (tr, ts) and xs channel
+// (2a + b) * 3 + c carry the original tap r = 2 tr + a - 1, s = 2 ts + b - 1 (r or s of -1 or 7:
+// a zero weight).  The "cols" tensor of im2col_stem is then xs as a [N*H/2*W/2, 16] matrix.
+inline bool stem_s2d_ok(int64_t C, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t H, int64_t W) {
+  return C == 3 && R == 7 && S == 7 && stride == 2 && pad == 3 && H % 2 == 0 && W % 2 == 0;
+}
+// column of the [K, 256] s2d weight for each (r, s, c) of the KRSC weight's 147 columns
+at::Tensor stem_s2d_index(const at::Device& dev) {
+  static std::mutex mu;
+  static std::unordered_map<int, at::Tensor> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(dev.index());
+  if (it != cache.end()) return it->second;
+  std::vector<int64_t> idx(147);
+  for (int r = 0; r < 7; ++r)
+    for (int s = 0; s < 7; ++s)
+      for (int c = 0; c < 3; ++c) {
+        const int tr = (r + 1) / 2, a = (r + 1) % 2, ts = (s + 1) / 2, b = (s + 1) % 2;
+        idx[(r * 7 + s) * 3 + c] = (tr * 4 + ts) * 16 + (2 * a + b) * 3 + c;
+      }
+  at::Tensor t = at::tensor(idx, at::TensorOptions().dtype(at::kLong)).to(dev);
+  cache.emplace(dev.index(), t);
+  return t;
+}
+inline at::Tensor stem_s2d(const at::Tensor& x) {
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  auto xs = at::empty({N * (H / 2) * (W / 2), 16}, x.options());
+  check(dl_stem_s2d(cbf(x), (int)N, (int)H, (int)W, bf(xs), cur_stream(x)), "stem_s2d");
+  return xs;
+}
+
 inline at::Tensor stem_im2col(const at::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t P,
                               int64_t Q, const StemCols& sc) {
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -1011,6 +1043,7 @@ at::Tensor conv2d_fwd_stats(const at::Tensor& x, const at::Tensor& w, int64_t st
 // the stem's column matrix [N*P*Q, Kp] (see stem_cols) for conv2d_fwd / conv2d_wgrad(cols=...)
 at::Tensor im2col_stem(const at::Tensor& x, int64_t R, int64_t S, int64_t stride, int64_t pad) {
   expect_nhwc(x, "x");
+  if (stem_s2d_ok(x.size(1), R, S, stride, pad, x.size(2), x.size(3))) return stem_s2d(x);
   const int64_t P = conv_out(x.size(2), R, stride, pad), Q = conv_out(x.size(3), S, stride, pad);
   return stem_im2col(x, R, S, stride, pad, P, Q, stem_cols(R, S, x.size(1), false));
 }
@@ -1051,7 +1084,28 @@ at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t str
     if (stats) check(dl_bn_stats(cbf(y), stats, stat_rows, (int)K, (int)groups, cur_stream(x)), "bn_stats");
     return y;
   }
-  // stem (3 input channels): im2col into a column matrix padded to a multiple of 64 columns, then
+  if (stem_s2d_ok(C, R, S, stride, pad, H, W)) {
+    at::Tensor xs;
+    if (cols.has_value()) {
+      TORCH_CHECK(cols->scalar_type() == at::kBFloat16 && cols->is_contiguous() && cols->dim() == 2 &&
+                      cols->size(0) == N * P * Q && cols->size(1) == 16,
+                  "cols must be the stem's im2col_stem (space-to-depth) matrix for this input");
+      xs = *cols;
+    } else {
+      xs = stem_s2d(x);
+    }
+    auto w2 = at::zeros({K, 256}, w.options());
+    w2.index_copy_(1, stem_s2d_index(w.device()), wk.reshape({K, 147}));
+    const DlConvGeom gs = geom(cbf(xs), N, H / 2, W / 2, 16, P, Q, 1, 1, 4, 4, -2, 1, -2, 1);
+    if (stats && dl_conv_fwd(gs, cbf(w2), 256, (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x), stats,
+                             stat_rows) == 0)
+      return y;
+    check(dl_conv_fwd(gs, cbf(w2), 256, (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x)),
+          "conv2d_fwd(stem)");
+    if (stats) check(dl_bn_stats(cbf(y), stats, stat_rows, (int)K, (int)groups, cur_stream(x)), "bn_stats");
+    return y;
+  }
+  // other small-channel convs: im2col into a column matrix padded to a multiple of 64 columns, then
   // one GEMM against the equally padded weight rows
   const StemCols sc = stem_cols(R, S, C, false);
   const at::Tensor col = stem_cols_checked(cols, x, R, S, stride, pad, P, Q, sc);
@@ -1275,8 +1329,25 @@ void conv2d_wgrad(const at::Tensor& dy_in, const at::Tensor& x, at::Tensor dw, i
     // gain in round 3 and was removed)
     rc = dl_conv_wgrad(gm, cbf(dy), K, (int)K, f32(acc), R * S * C, (int)(R * S * C), cur_stream(dy));
     check(rc, "conv2d_wgrad");
+  } else if (stem_s2d_ok(C, R, S, stride, pad, H, W)) {
+    // stem: 4x4 wgrad over the space-to-depth image into [K, 256], folded back onto the 7x7 taps
+    at::Tensor xs;
+    if (cols.has_value()) {
+      TORCH_CHECK(cols->scalar_type() == at::kBFloat16 && cols->is_contiguous() && cols->dim() == 2 &&
+                      cols->size(0) == N * P * Q && cols->size(1) == 16,
+                  "cols must be the stem's im2col_stem (space-to-depth) matrix for this input");
+      xs = *cols;
+    } else {
+      xs = stem_s2d(x);
+    }
+    auto slab = at::zeros({K, 256}, dw.options());
+    rc = dl_conv_wgrad(geom(cbf(xs), N, H / 2, W / 2, 16, P, Q, 1, 1, 4, 4, -2, 1, -2, 1), cbf(dy), K, (int)K,
+                       f32(slab), 256, 256, cur_stream(dy));
+    check(rc, "conv2d_wgrad(stem)");
+    acc.view({K, R * S * C}).add_(slab.index_select(1, stem_s2d_index(dw.device())));
   } else {
-    // stem: wgrad over the padded column matrix into a [K, R, SCp] slab, then the real columns
+    // other small-channel convs: wgrad over the padded column matrix into a [K, R, SCp] slab, then
+    // the real columns
     const StemCols sc = stem_cols(R, S, C, false);
     const int64_t M = N * P * Q;
     const at::Tensor col = stem_cols_checked(cols, x, R, S, stride, pad, P, Q, sc);

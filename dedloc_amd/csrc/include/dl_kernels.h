@@ -132,6 +132,8 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
 int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,
                   hipStream_t st);
 // stem im2col: col[m][r*SCp + s*C + c] (filter rows padded to SCp columns), zero columns up to Kp
+// space-to-depth of the 3-channel stem input: x NHWC [N, H, W, 3] -> [N, H/2, W/2, 16] (H, W even)
+int dl_stem_s2d(const bf16_t* x, int N, int H, int W, bf16_t* xs, hipStream_t st);
 int dl_im2col(const bf16_t* x, int N, int H, int W, int C, int R, int S, int stride, int pad, int P, int Q, int SCp,
               int Kp, bf16_t* col, hipStream_t st);
 

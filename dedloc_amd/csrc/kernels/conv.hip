@@ -152,7 +152,9 @@ __device__ __forceinline__ void st_kin_n(const StageN<U>& s, uint8_t* img) {
   }
 }
 
-template <int TM_, int TN_>
+// SUB: C < 64 (a divisor of 64, multiple of 8): a 64-deep k-step spans 64 / C taps, so each thread
+// decodes the tap of its own 8-channel chunk (the space-to-depth stem: C = 16, 4 x 4 taps)
+template <int TM_, int TN_, bool SUB = false>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   constexpr int WN = TN_ / 64, UA = TM_ / 32, UB = TN_ / 32;
   constexpr int CPR = TN_ / 8;            // 16-byte chunks per staged output row
@@ -208,14 +210,22 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     s = min(s, nsteps - 1);
     const int tile = tile0 + s / nk, k0 = (s % nk) * BK;
     if (tile != dec_tile) decode(tile);
-    const int t = k0 / g.C, c0 = k0 - t * g.C;
+    int t, cc;  // tap and channel offset of this thread's chunk
+    if constexpr (SUB) {
+      const int kk = k0 + cofs;
+      t = kk / g.C;
+      cc = kk - t * g.C;
+    } else {
+      t = k0 / g.C;
+      cc = k0 - t * g.C + cofs;
+    }
     const int tr = t / g.TS, ts = t - tr * g.TS;
     const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
 #pragma unroll
     for (int u = 0; u < UA; ++u) {
       const int h = hb[u] + dh, w = wb[u] + dw;
       const bool ok = (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const unsigned off = 2u * ((unsigned)((nb[u] + h) * g.W + w) * (unsigned)g.C + (unsigned)(c0 + cofs));
+      const unsigned off = 2u * ((unsigned)((nb[u] + h) * g.W + w) * (unsigned)g.C + (unsigned)cc);
       sa.v[u] = bload(rimg, ok ? off : OOB);
     }
 #pragma unroll
@@ -571,6 +581,34 @@ __global__ __launch_bounds__(256) void im2col_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// Space-to-depth of the stem's input: x NHWC [N, H, W, 3] -> xs [N, H/2, W/2, 16], channel
+// (2a + b) * 3 + c = x[2i + a, 2j + b, c], channels 12-15 zero.  The 7x7 stride-2 pad-3 stem conv
+// over x is then a 4x4 stride-1 conv over xs (taps i - 2 .. i + 1, weights remapped by the caller):
+// one implicit GEMM with K = 256 on conv.hip instead of an im2col matrix of 1.6 G bf16 elements.
+__global__ __launch_bounds__(256) void stem_s2d_kernel(const bf16_t* __restrict__ x, int N, int H, int W,
+                                                       bf16_t* __restrict__ xs) {
+  const int H2 = H >> 1, W2 = W >> 1;
+  const long total = (long)N * H2 * W2;
+  for (long o = blockIdx.x * 256L + threadIdx.x; o < total; o += (long)gridDim.x * 256) {
+    const int j = (int)(o % W2);
+    const long r = o / W2;
+    const int i = (int)(r % H2), n = (int)(r / H2);
+    uint32_t w32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const bf16_t* row = x + (((long)n * H + 2 * i + a) * W + 2 * j) * 3;  // 2 pixels x 3 channels
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        const int ch = a * 6 + e;  // (2a + b) * 3 + c with b = e / 3, c = e % 3
+        w32[ch >> 1] |= (uint32_t)row[e] << (16 * (ch & 1));
+      }
+    }
+    uint4* dst = reinterpret_cast<uint4*>(xs + o * 16);
+    dst[0] = uint4{w32[0], w32[1], w32[2], w32[3]};
+    dst[1] = uint4{w32[4], w32[5], w32[6], w32[7]};
+  }
+}
+
 template <typename Kern>
 void set_lds(Kern k) {
   DL_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
@@ -580,7 +618,9 @@ void set_lds(Kern k) {
 
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
                 int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows, const DlBnBwdEpi* bn) {
-  if (g.C % BK || N % 4 || ldw % 8 || ldo % 4 || g.I < 0 || g.J < 0) return -1;
+  const bool sub = g.C < BK;  // C in {8, 16, 32}: several taps per k-step (SUB kernels)
+  if ((sub ? (BK % g.C || g.C % 8) : g.C % BK) || N % 4 || ldw % 8 || ldo % 4 || g.I < 0 || g.J < 0) return -1;
+  if (sub && (bn || (g.TR * g.TS * g.C) % BK)) return -1;
   if (bn && (!stats || !bn->X || bn->ldx % 8 || (!bn->Y && (!bn->gamma || !bn->beta)))) return -1;
   const long M = (long)g.Nimg * g.I * g.J;
   // statistics: every 128-row tile inside one group, whole 8-channel chunks
@@ -605,10 +645,20 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
     DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
     attr = true;
   }
-  if (narrow) conv_fwd_kernel<256, 64><<<dim3((tiles + tpw - 1) / tpw), NT, lds, st>>>(a);
-  else conv_fwd_kernel<BM, BN><<<dim3((tiles + tpw - 1) / tpw), NT, lds, st>>>(a);
+  const dim3 grid((tiles + tpw - 1) / tpw);
+  if (sub) {
+    if (narrow) conv_fwd_kernel<256, 64, true><<<grid, NT, lds, st>>>(a);
+    else conv_fwd_kernel<BM, BN, true><<<grid, NT, lds, st>>>(a);
+  } else {
+    if (narrow) conv_fwd_kernel<256, 64><<<grid, NT, lds, st>>>(a);
+    else conv_fwd_kernel<BM, BN><<<grid, NT, lds, st>>>(a);
+  }
   return 0;
 }
 
@@ -647,6 +697,15 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
     attr = true;
   }
   conv_wgrad_kernel<<<dim3(tiles, 1, (unsigned)splits), NT, LDS_BYTES, st>>>(a);
+  return 0;
+}
+
+int dl_stem_s2d(const bf16_t* x, int N, int H, int W, bf16_t* xs, hipStream_t st) {
+  if (H % 2 || W % 2 || N < 0) return -1;
+  const long total = (long)N * (H / 2) * (W / 2);
+  if (total == 0) return 0;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 256L * 64);
+  stem_s2d_kernel<<<blocks, 256, 0, st>>>(x, N, H, W, xs);
   return 0;
 }
 

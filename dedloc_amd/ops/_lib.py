@@ -102,7 +102,9 @@ def load_native(required: bool | None = None) -> bool:
     if required is None:
         required = torch.cuda.is_available()
     pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    path = os.path.join(pkg, "_C.so")
+    # DEDLOC_NATIVE_LIB: an alternative build of the same library (same-box A/B measurements,
+    # _build.build_variant); the default is the in-tree _C.so
+    path = os.environ.get("DEDLOC_NATIVE_LIB") or os.path.join(pkg, "_C.so")
     try:
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} not built (run python -m dedloc_amd._build)")

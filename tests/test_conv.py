@@ -14,7 +14,8 @@ CL = torch.channels_last
 
 # (N, Cin, H, Cout, k, stride, pad)
 SHAPES = [
-    (2, 3, 32, 64, 7, 2, 3),        # stem (im2col)
+    (2, 3, 32, 64, 7, 2, 3),        # stem (space-to-depth 4x4 conv)
+    (2, 3, 33, 64, 7, 2, 3),        # stem, odd size (im2col column GEMM)
     (2, 64, 14, 64, 1, 1, 0),       # layer1 reduce
     (2, 64, 14, 64, 3, 1, 1),       # layer1 3x3
     (2, 64, 14, 256, 1, 1, 0),      # expand / downsample (stride 1)
@@ -139,6 +140,29 @@ def test_conv_wgrad_large_reduction_split_k(cuda, hip_kernels):
     dw = torch.zeros(64, 3, 7, 7, device=cuda).contiguous(memory_format=CL)
     torch.ops.dedloc.conv2d_wgrad(dy, x, dw, 2, 3)
     assert _rel(dw, dwr) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H", [96, 224])
+def test_stem_space_to_depth_cols_stats_and_wgrad(cuda, H):
+    """The 7x7/2 3-channel stem as a 4x4 conv over the space-to-depth image: im2col_stem returns that
+    image ([N*H/2*W/2, 16]), which the forward (with the BatchNorm-statistics epilogue, 3 groups) and
+    the weight gradient take in place of the input — against fp32 PyTorch."""
+    N = 3
+    x, w, dy = _data(cuda, N, 3, H, 64, 7, 2, 3, seed=7)
+    yr, _, dwr = _reference(x, w, dy, 2, 3)
+    cols = torch.ops.dedloc.im2col_stem(x, 7, 7, 2, 3)
+    assert cols.shape == (N * (H // 2) ** 2, 16) and cols.dtype == torch.bfloat16
+    sums = torch.zeros(2 * N * 64, device=cuda)
+    y = torch.ops.dedloc.conv2d_fwd_stats(x, w, 2, 3, sums, N, cols)
+    assert _rel(y, yr) < 1e-2, _rel(y, yr)
+    yf = y.float().permute(0, 2, 3, 1).reshape(N, -1, 64)
+    ref_sums = torch.cat([yf.sum(1), (yf * yf).sum(1)], dim=1).reshape(-1)
+    assert _rel(sums, ref_sums) < 1e-4, _rel(sums, ref_sums)
+    xs = torch.empty((), dtype=torch.bfloat16, device=cuda).expand(x.shape)  # only the shape is read
+    dw = torch.zeros(64, 3, 7, 7, device=cuda).contiguous(memory_format=CL)
+    torch.ops.dedloc.conv2d_wgrad(dy, xs, dw, 2, 3, cols)
+    assert _rel(dw, dwr) < 1e-3, _rel(dw, dwr)
 
 
 @pytest.mark.gpu
