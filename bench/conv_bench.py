@@ -16,27 +16,28 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import dedloc_amd.ops  # noqa: E402,F401
-from dedloc_amd.models.resnet_swav import ConvNHWC, ResNet50Trunk  # noqa: E402
 
 CL = torch.channels_last
 
 
 def collect_shapes(batch224, batch96):
-    trunk = ResNet50Trunk().to("meta")
+    """Every conv of the SwAV ResNet-50 trunk (torchvision v1.5 layout: stride on the 3x3) as
+    (batch, Cin, H_in, Cout, k, stride, pad) with its count, for both crop resolutions."""
     shapes = Counter()
-    hooks = []
-    for m in trunk.modules():
-        if isinstance(m, ConvNHWC):
-            def pre(mod, inp):
-                x = inp[0]
-                shapes[(x.shape[0], mod.in_channels, x.shape[2], mod.out_channels, mod.kernel_size[0],
-                        mod.stride[0], mod.padding[0])] += 1
-            hooks.append(m.register_forward_pre_hook(pre))
-    with torch.no_grad():
-        for n, s in ((batch224, 224), (batch96, 96)):
-            trunk(torch.zeros(n, 3, s, s, device="meta"))
-    for h in hooks:
-        h.remove()
+    for n, s in ((batch224, 224), (batch96, 96)):
+        shapes[(n, 3, s, 64, 7, 2, 3)] += 1
+        h = ((s + 6 - 7) // 2 + 1 + 2 - 3) // 2 + 1  # stem, then the 3x3/2 max-pool
+        cin = 64
+        for planes, blocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+            for bi in range(blocks):
+                st = stride if bi == 0 else 1
+                h2 = (h + 2 - 3) // st + 1
+                shapes[(n, cin, h, planes, 1, 1, 0)] += 1
+                shapes[(n, planes, h, planes, 3, st, 1)] += 1
+                shapes[(n, planes, h2, planes * 4, 1, 1, 0)] += 1
+                if bi == 0:
+                    shapes[(n, cin, h, planes * 4, 1, st, 0)] += 1
+                cin, h = planes * 4, h2
     return shapes
 
 

@@ -65,8 +65,9 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     for src in hip_srcs:
         obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
         objs.append(obj)
-        if _newer(obj, [src] + headers):
-            jobs_list.append(["hipcc", *hip_flags, *inc, "-c", src, "-o", obj])
+        if _newer(obj, [src] + headers + [__file__]):
+            jobs_list.append(["hipcc", *hip_flags, *FILE_FLAGS.get(os.path.basename(src), []), *inc, "-c", src,
+                              "-o", obj])
 
     tinc, tlib, abi = _torch_paths()
     # translation units that include torch: the operator bindings and the RCCL data plane (csrc/comm)
@@ -112,6 +113,10 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
 
 _OBJS: list = []  # the kernel library's objects, in link order (filled by build)
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-munsafe-fp-atomics"]
+# per-file flags: the attention kernels' softmax f32 arithmetic stays scalar — -O3's SLP vectoriser
+# packs adjacent f32 adds / multiplies / FMAs into v_pk_*_f32, which cost more than two scalar ops
+# when they sit between MFMAs (MI355X_MICROARCH.md, per-instruction cycle constants)
+FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
 
 
 def _link(objs, out, tlib, verbose):
@@ -124,7 +129,7 @@ def _link(objs, out, tlib, verbose):
     _run(cmd, verbose)
 
 
-def build_variant(name: str, rev: str, kernels, verbose: bool = False) -> str:
+def build_variant(name: str, rev: str, kernels, verbose: bool = False, flags=None) -> str:
     """Measurement helper for same-box A/B runs: the kernel library with the given ``csrc/kernels``
     files taken from git revision ``rev`` (everything else as built now), linked into
     ``ab/_C_<name>.so``; a process loads it instead of ``_C.so`` with DEDLOC_NATIVE_LIB=<that path>."""
@@ -140,8 +145,9 @@ def build_variant(name: str, rev: str, kernels, verbose: bool = False) -> str:
         with open(src, "w") as f:
             f.write(text)
         obj = src.replace(".hip", ".o")
-        _run(["hipcc", "--offload-arch=" + ARCH, *HIP_FLAGS, "-I", os.path.join(CSRC, "include"), "-c", src, "-o", obj],
-             verbose)
+        extra = FILE_FLAGS.get(os.path.basename(k), []) if flags is None else list(flags)
+        _run(["hipcc", "--offload-arch=" + ARCH, *HIP_FLAGS, *extra, "-I", os.path.join(CSRC, "include"), "-c", src,
+              "-o", obj], verbose)
         swap[os.path.basename(obj)] = obj
     out_dir = os.path.join(repo, "ab")
     os.makedirs(out_dir, exist_ok=True)
@@ -153,6 +159,10 @@ def build_variant(name: str, rev: str, kernels, verbose: bool = False) -> str:
 
 if __name__ == "__main__":
     if len(sys.argv) > 3 and sys.argv[1] == "variant":  # python -m dedloc_amd._build variant NAME REV kernel.hip ...
-        print(build_variant(sys.argv[2], sys.argv[3], sys.argv[4:], verbose="-v" in sys.argv))
+        # [--flags="-fno-x -fy"]: compile the swapped files with these extra flags instead of FILE_FLAGS
+        fl = [a for a in sys.argv[4:] if a.startswith("--flags=")]
+        ks = [a for a in sys.argv[4:] if not a.startswith("--") and a != "-v"]
+        print(build_variant(sys.argv[2], sys.argv[3], ks, verbose="-v" in sys.argv,
+                            flags=fl[0][len("--flags="):].split() if fl else None))
     else:
         print(build(verbose="-v" in sys.argv))

@@ -581,6 +581,152 @@ __global__ __launch_bounds__(256) void im2col_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// Weight gradient for Cout <= 64 (the stem and the first stage's convs): the 128 x 128 tile above
+// would compute 64 duplicate output rows.  Here a workgroup owns 64 output channels x 256 gathered
+// columns, its four waves side by side along the columns (64 x 64 each, the same MFMA work per wave
+// and k-step as the wide kernel).  The dY image holds 64-column k-rows (128 B) with its own swizzle:
+// 32-byte segment s of k-row r at s ^ f(r), f(r) = ((r >> 1) & 1) | (((r >> 3) & 1) << 1), so the
+// eight k-rows of one ds_read_b64_tr_b16 lane group (r, r+1, r+2, r+3, r+8 ... r+11; segment fixed)
+// fall on eight distinct 32-byte bank groups.  The gathered operand is two standard 128-column
+// images.  LDS: 2 stages x (8 + 32) KiB = 80 KiB, two workgroups per CU.
+constexpr int NW_AIMG = 64 * 128;           // dY image: 64 k-rows x 64 channels
+constexpr int NW_STAGE = NW_AIMG + 2 * TILE;  // + two 128-column gathered images
+constexpr int NW_LDS = 2 * NW_STAGE;
+
+__device__ __forceinline__ int kout64_off(int krow, int c) {  // c: 16-byte chunk 0..7 of the k-row
+  const int f = ((krow >> 1) & 1) | (((krow >> 3) & 1) << 1);
+  return krow * 128 + (((((c >> 1) ^ f) << 1) | (c & 1)) << 4);
+}
+__device__ __forceinline__ bf16x8 load_frag64(const uint8_t* img, int r0, int ksub, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int krow = 32 * ksub + 8 * g + (i >> 2);
+  const int col = r0 + 4 * (i & 3);
+  const int o1 = kout64_off(krow, col >> 3) + ((col & 7) << 1);
+  const int o2 = kout64_off(krow + 4, col >> 3) + ((col & 7) << 1);
+  const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + o1));
+  const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + o2));
+  const s8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+struct NarrowStage {
+  uint4 a[2];  // dY: chunk (tid & 7) of k-rows (tid >> 3) + 32u
+  uint4 b[8];  // gathered: chunk (tid & 31) of k-rows (tid >> 5) + 8u
+};
+
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_narrow_kernel(WgradArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const DlConvGeom& g = p.g;
+  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
+  const int tiles_n = (p.Ncols + 255) / 256;
+  const int bid = xcd_remap(blockIdx.x, tiles_n);
+  const int n0 = bid * 256;
+  const int kbeg = blockIdx.z * p.m_per_split;
+  const int kend = min(p.M, kbeg + p.m_per_split);
+  if (kbeg >= kend) return;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int IJ = g.I * g.J;
+
+  const int achunk = tid & 7, akrow = tid >> 3;
+  const int acol = min(achunk * 8, p.Cout - 8);
+  const int bchunk = tid & 31, bkrow = tid >> 5;
+  const int kk = min(n0 + bchunk * 8, p.Brows - 8);
+  const int t = kk / g.C, c = kk - t * g.C;
+  const int tr = t / g.TS, ts = t - tr * g.TS;
+  const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
+
+  const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
+  const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, p.dy_bytes);
+  auto load = [&](NarrowStage& s, int k0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int m = kbeg + k0 + akrow + 32 * u;
+      const unsigned off = 2u * ((unsigned)m * (unsigned)p.ldy + (unsigned)acol);
+      s.a[u] = bload(rdy, m < kend ? off : OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = kbeg + k0 + bkrow + 8 * u;
+      const int n = fdiv(m, IJ, p.rIJ), r = m - n * IJ;
+      const int i = fdiv(r, g.J, p.rJ), j = r - i * g.J;
+      const int h = i * g.sh + dh, w = j * g.sw + dw;
+      const bool ok = m < kend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const unsigned off = 2u * ((unsigned)((n * g.H + h) * g.W + w) * (unsigned)g.C + (unsigned)c);
+      s.b[u] = bload(rimg, ok ? off : OOB);
+    }
+  };
+  auto store = [&](const NarrowStage& s, uint8_t* st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(st + kout64_off(akrow + 32 * u, achunk)) = s.a[u];
+    uint8_t* bimg = st + NW_AIMG + (bchunk >> 4) * TILE;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4*>(bimg + kout_off(bkrow + 8 * u, bchunk & 15)) = s.b[u];
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const uint8_t* st) {
+    const uint8_t* Bi = st + NW_AIMG + (wn >> 1) * TILE;
+    const int cb = (wn & 1) * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bfr[ni] = load_frag<true>(Bi, cb + ni * 16, ks, lane);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const bf16x8 af = load_frag64(st, mi * 16, ks, lane);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(af, bfr[ni], acc[mi][ni]);
+      }
+    }
+  };
+
+  // 2-deep register prefetch, as the wide kernel
+  uint8_t* buf0 = smem;
+  uint8_t* buf1 = smem + NW_STAGE;
+  NarrowStage x, y;
+  const int last = (nk - 1) * BK;
+  load(x, 0);
+  load(y, min(BK, last));
+  store(x, buf0);
+  load(x, min(2 * BK, last));
+  __syncthreads();
+  for (int s = 0; s < nk; s += 2) {
+    compute(buf0);
+    store(y, buf1);
+    load(y, min((s + 3) * BK, last));
+    __syncthreads();
+    if (s + 1 < nk) compute(buf1);
+    store(x, buf0);
+    load(x, min((s + 4) * BK, last));
+    __syncthreads();
+  }
+
+  // acc[mi][ni][i] = dW[channel mi*16+4*(lane>>4)+i][col n0+wn*64+ni*16+(lane&15)]
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = mi * 16 + 4 * (lane >> 4) + i;
+      if (ch >= p.Cout) continue;
+      float* drow = p.dw + (long)ch * p.lddw;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + wn * 64 + ni * 16 + (lane & 15);
+        if (col >= p.Ncols) continue;
+        if (split) atomicAdd(drow + col, acc[mi][ni][i]);
+        else drow[col] += acc[mi][ni][i];
+      }
+    }
+  }
+}
+
 // Space-to-depth of the stem's input: x NHWC [N, H, W, 3] -> xs [N, H/2, W/2, 16], channel
 // (2a + b) * 3 + c = x[2i + a, 2j + b, c], channels 12-15 zero.  The 7x7 stride-2 pad-3 stem conv
 // over x is then a 4x4 stride-1 conv over xs (taps i - 2 .. i + 1, weights remapped by the caller):
@@ -666,9 +812,8 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
 // exist (default 256: one per CU; SwAV b=64 iteration 1990-1997 samples/s at 1024, 2051-2061 at 256,
 // 2041 at 512, with atomic adds), each split a multiple of the 64-deep k-step and at least 8 k-steps
 // long
-static long wgrad_splits(const DlConvGeom& g, int Cout, int Ncols) {
+static long wgrad_splits(const DlConvGeom& g, int tiles) {
   const long M = (long)g.Nimg * g.I * g.J;
-  const int tiles = ((Cout + BM - 1) / BM) * ((Ncols + BN - 1) / BN);
   constexpr long target = 256;
   const long ksteps = (M + BK - 1) / BK;
   long splits = std::max(1L, std::min<long>((target + tiles - 1) / tiles, ksteps / 8));
@@ -683,9 +828,10 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
   const long M = (long)g.Nimg * g.I * g.J;
   if (M >= (1L << 24)) return -1;  // fdiv exactness bound
   if (M == 0 || Ncols == 0) return 0;
-  const int tiles = ((Cout + BM - 1) / BM) * ((Ncols + BN - 1) / BN);
+  const bool narrow = Cout <= 64;  // conv_wgrad_narrow_kernel: 64 x 256 tiles
+  const int tiles = narrow ? (Ncols + 255) / 256 : ((Cout + BM - 1) / BM) * ((Ncols + BN - 1) / BN);
   const long ksteps = (M + BK - 1) / BK;
-  const long splits = wgrad_splits(g, Cout, Ncols);
+  const long splits = wgrad_splits(g, tiles);
   const long steps_per = (ksteps + splits - 1) / splits;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, dy_bytes = 2L * M * ldy;
   if (img_bytes >= (1L << 31) || dy_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
@@ -694,9 +840,12 @@ int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, flo
   static bool attr = false;
   if (!attr) {
     set_lds(conv_wgrad_kernel);
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_wgrad_narrow_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, NW_LDS));
     attr = true;
   }
-  conv_wgrad_kernel<<<dim3(tiles, 1, (unsigned)splits), NT, LDS_BYTES, st>>>(a);
+  if (narrow) conv_wgrad_narrow_kernel<<<dim3(tiles, 1, (unsigned)splits), NT, NW_LDS, st>>>(a);
+  else conv_wgrad_kernel<<<dim3(tiles, 1, (unsigned)splits), NT, LDS_BYTES, st>>>(a);
   return 0;
 }
 
