@@ -83,6 +83,34 @@ __device__ __forceinline__ void gload(const bf16_t* __restrict__ p, long srow, l
   }
 }
 
+// K-outer image of a 128-row operand (U = 2 chunks per thread): [32 k][128 rows], 256-byte k-rows,
+// 16-byte chunk c of k-row k at c ^ kswz(k) (conflict-free for the ds_read_b64_tr_b16 lane groups,
+// the layout of gemm8.hip's K-outer half-tiles).  A row-walked (L_RIN) operand lands here with one
+// 16-byte write per chunk instead of eight 2-byte writes into a K-inner image.
+__device__ __forceinline__ int kswz(int k) { return ((k & 3) << 2) | ((k >> 2) & 3); }
+__device__ __forceinline__ void lds_put_kout(bf16_t* img, const uint4 (&v)[2]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int idx = threadIdx.x + NTH * u;
+    const int c = idx & 15, k = idx >> 4;
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(img) + k * 256 + ((c ^ kswz(k)) << 4)) = v[u];
+  }
+}
+typedef short s4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4_t lds_s4;
+// MFMA operand fragment (rows r0 + (lane & 15), k = 8 (lane >> 4) + j) from the K-outer image
+__device__ __forceinline__ bf16x8 frag_kout(const bf16_t* img, int r0, int lane) {
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(img);
+  const int g = lane >> 4, i = lane & 15;
+  const int kr = 8 * g + (i >> 2);
+  const int col = r0 + 4 * (i & 3);
+  const int o1 = kr * 256 + (((col >> 3) ^ kswz(kr)) << 4) + ((col & 7) << 1);
+  const int o2 = (kr + 4) * 256 + (((col >> 3) ^ kswz(kr + 4)) << 4) + ((col & 7) << 1);
+  const s4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(b + o1));
+  const s4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(b + o2));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 template <int L, int U>
 __device__ __forceinline__ void lds_put(bf16_t* img, const uint4 (&v)[U]) {
 #pragma unroll
@@ -123,12 +151,16 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // row-walked operands of 128-row tiles go through the K-outer image (lds_put_kout / frag_kout)
+  constexpr bool AKO = LA == L_RIN, BKO = LB == L_RIN && TN == 128;
   uint4 ra[2], rb[UB];
   gload<LA, VA, 2>(Ap, p.sam, p.sak, m0, p.M, kbeg, kend, ra);
   gload<LB, VB, UB>(Bp, p.sbn, p.sbk, n0, p.N, kbeg, kend, rb);
   for (int k0 = kbeg; k0 < kend; k0 += TK) {
-    lds_put<LA, 2>(sa, ra);
-    lds_put<LB, UB>(sb, rb);
+    if constexpr (AKO) lds_put_kout(sa, ra);
+    else lds_put<LA, 2>(sa, ra);
+    if constexpr (BKO) lds_put_kout(sb, reinterpret_cast<const uint4(&)[2]>(rb));
+    else lds_put<LB, UB>(sb, rb);
     __syncthreads();
     if (k0 + TK < kend) {  // next K-step's loads are in flight during this one's MFMAs
       gload<LA, VA, 2>(Ap, p.sam, p.sak, m0, p.M, k0 + TK, kend, ra);
@@ -136,11 +168,15 @@ __global__ __launch_bounds__(NTH) void gemm_small_kernel(SmallArgs p) {
     }
     bf16x8 af[4], bfr[NJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      af[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * 64 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (AKO) af[i] = frag_kout(sa, wm * 64 + i * 16, lane);
+      else af[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * 64 + i * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
+    }
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (wn * (TN / 2) + j * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
+    for (int j = 0; j < NJ; ++j) {
+      if constexpr (BKO) bfr[j] = frag_kout(sb, wn * (TN / 2) + j * 16, lane);
+      else bfr[j] = *reinterpret_cast<const bf16x8*>(sb + (wn * (TN / 2) + j * 16 + (lane & 15)) * ROW + 8 * (lane >> 4));
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
