@@ -439,10 +439,20 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
 
   const int chunk = tid & 15, krow0 = tid >> 4;
   const int acol = min(m0 + chunk * 8, p.Cout - 8);
-  const int kk = min(n0 + chunk * 8, p.Brows - 8);
-  const int t = kk / g.C, c = kk - t * g.C;
-  const int tr = t / g.TS, ts = t - tr * g.TS;
-  const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
+  // gathered operand: thread = one pixel row (tid >> 2) x chunks (tid & 3) + 4u, so the pixel
+  // decode (two divisions) runs once per thread and k-step instead of once per chunk; the chunks'
+  // tap offsets and channels are fixed per workgroup
+  const int brow = tid >> 2;
+  int bdh[4], bdw[4], bc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int kk = min(n0 + ((tid & 3) + 4 * u) * 8, p.Brows - 8);
+    const int t = kk / g.C;
+    bc[u] = kk - t * g.C;
+    const int tr = t / g.TS, ts = t - tr * g.TS;
+    bdh[u] = g.dh0 + tr * g.dhs;
+    bdw[u] = g.dw0 + ts * g.dws;
+  }
 
   const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, p.dy_bytes);
@@ -455,16 +465,23 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
     }
   };
   auto load_b = [&](Stage& s, int k0) {
+    const int m = kbeg + k0 + brow;
+    const int n = fdiv(m, IJ, p.rIJ), r = m - n * IJ;
+    const int i = fdiv(r, g.J, p.rJ), j = r - i * g.J;
+    const int h0 = i * g.sh, w0 = j * g.sw, nh = n * g.H;
+    const bool mok = m < kend;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int m = kbeg + k0 + krow0 + 16 * u;
-      const int n = fdiv(m, IJ, p.rIJ), r = m - n * IJ;
-      const int i = fdiv(r, g.J, p.rJ), j = r - i * g.J;
-      const int h = i * g.sh + dh, w = j * g.sw + dw;
-      const bool ok = m < kend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const unsigned off = 2u * ((unsigned)((n * g.H + h) * g.W + w) * (unsigned)g.C + (unsigned)c);
+      const int h = h0 + bdh[u], w = w0 + bdw[u];
+      const bool ok = mok && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const unsigned off = 2u * ((unsigned)((nh + h) * g.W + w) * (unsigned)g.C + (unsigned)bc[u]);
       s.v[u] = bload(rimg, ok ? off : OOB);
     }
+  };
+  auto st_b = [&](const Stage& s, uint8_t* img) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<uint4*>(img + kout_off(brow, (tid & 3) + 4 * u)) = s.v[u];
   };
 
   floatx4 acc[4][4];
@@ -499,20 +516,20 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
   load_a(ya, min(BK, last));
   load_b(yb, min(BK, last));
   st_kout(xa, buf0);
-  st_kout(xb, buf0 + TILE);
+  st_b(xb, buf0 + TILE);
   load_a(xa, min(2 * BK, last));
   load_b(xb, min(2 * BK, last));
   __syncthreads();
   for (int s = 0; s < nk; s += 2) {
     compute(buf0);
     st_kout(ya, buf1);
-    st_kout(yb, buf1 + TILE);
+    st_b(yb, buf1 + TILE);
     load_a(ya, min((s + 3) * BK, last));
     load_b(yb, min((s + 3) * BK, last));
     __syncthreads();
     if (s + 1 < nk) compute(buf1);
     st_kout(xa, buf0);
-    st_kout(xb, buf0 + TILE);
+    st_b(xb, buf0 + TILE);
     load_a(xa, min((s + 4) * BK, last));
     load_b(xb, min((s + 4) * BK, last));
     __syncthreads();
@@ -611,7 +628,7 @@ __device__ __forceinline__ bf16x8 load_frag64(const uint8_t* img, int r0, int ks
 
 struct NarrowStage {
   uint4 a[2];  // dY: chunk (tid & 7) of k-rows (tid >> 3) + 32u
-  uint4 b[8];  // gathered: chunk (tid & 31) of k-rows (tid >> 5) + 8u
+  uint4 b[8];  // gathered: chunks (tid & 3) + 4u of k-row (tid >> 2)
 };
 
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_narrow_kernel(WgradArgs p) {
@@ -629,11 +646,18 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_narrow_kernel(WgradArgs p) {
 
   const int achunk = tid & 7, akrow = tid >> 3;
   const int acol = min(achunk * 8, p.Cout - 8);
-  const int bchunk = tid & 31, bkrow = tid >> 5;
-  const int kk = min(n0 + bchunk * 8, p.Brows - 8);
-  const int t = kk / g.C, c = kk - t * g.C;
-  const int tr = t / g.TS, ts = t - tr * g.TS;
-  const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
+  // gathered operand: thread = one pixel row (tid >> 2) x chunks (tid & 3) + 4u (see the wide kernel)
+  const int brow = tid >> 2;
+  int bdh[8], bdw[8], bc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int kk = min(n0 + ((tid & 3) + 4 * u) * 8, p.Brows - 8);
+    const int t = kk / g.C;
+    bc[u] = kk - t * g.C;
+    const int tr = t / g.TS, ts = t - tr * g.TS;
+    bdh[u] = g.dh0 + tr * g.dhs;
+    bdw[u] = g.dw0 + ts * g.dws;
+  }
 
   const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
   const __amdgpu_buffer_rsrc_t rdy = make_rsrc(p.dy, p.dy_bytes);
@@ -644,23 +668,27 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_narrow_kernel(WgradArgs p) {
       const unsigned off = 2u * ((unsigned)m * (unsigned)p.ldy + (unsigned)acol);
       s.a[u] = bload(rdy, m < kend ? off : OOB);
     }
+    const int m = kbeg + k0 + brow;
+    const int n = fdiv(m, IJ, p.rIJ), r = m - n * IJ;
+    const int i = fdiv(r, g.J, p.rJ), j = r - i * g.J;
+    const int h0 = i * g.sh, w0 = j * g.sw, nh = n * g.H;
+    const bool mok = m < kend;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int m = kbeg + k0 + bkrow + 8 * u;
-      const int n = fdiv(m, IJ, p.rIJ), r = m - n * IJ;
-      const int i = fdiv(r, g.J, p.rJ), j = r - i * g.J;
-      const int h = i * g.sh + dh, w = j * g.sw + dw;
-      const bool ok = m < kend && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
-      const unsigned off = 2u * ((unsigned)((n * g.H + h) * g.W + w) * (unsigned)g.C + (unsigned)c);
+      const int h = h0 + bdh[u], w = w0 + bdw[u];
+      const bool ok = mok && (unsigned)h < (unsigned)g.H && (unsigned)w < (unsigned)g.W;
+      const unsigned off = 2u * ((unsigned)((nh + h) * g.W + w) * (unsigned)g.C + (unsigned)bc[u]);
       s.b[u] = bload(rimg, ok ? off : OOB);
     }
   };
   auto store = [&](const NarrowStage& s, uint8_t* st) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(st + kout64_off(akrow + 32 * u, achunk)) = s.a[u];
-    uint8_t* bimg = st + NW_AIMG + (bchunk >> 4) * TILE;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) *reinterpret_cast<uint4*>(bimg + kout_off(bkrow + 8 * u, bchunk & 15)) = s.b[u];
+    for (int u = 0; u < 8; ++u) {
+      const int ch = (tid & 3) + 4 * u;  // chunk 0..31 of the 256 columns: image ch >> 4
+      *reinterpret_cast<uint4*>(st + NW_AIMG + (ch >> 4) * TILE + kout_off(brow, ch & 15)) = s.b[u];
+    }
   };
 
   floatx4 acc[4][4];
