@@ -140,14 +140,24 @@ def build_variant(name: str, rev: str, kernels, verbose: bool = False, flags=Non
     swap = {}
     for k in kernels:
         src = os.path.join(vdir, os.path.basename(k))
-        text = subprocess.run(["git", "-C", repo, "show", f"{rev}:dedloc_amd/csrc/kernels/{os.path.basename(k)}"],
+        where = "" if k.endswith(".cpp") else "kernels/"  # bindings.cpp lives in csrc/ itself
+        text = subprocess.run(["git", "-C", repo, "show", f"{rev}:dedloc_amd/csrc/{where}{os.path.basename(k)}"],
                               check=True, capture_output=True, text=True).stdout
         with open(src, "w") as f:
             f.write(text)
-        obj = src.replace(".hip", ".o")
-        extra = FILE_FLAGS.get(os.path.basename(k), []) if flags is None else list(flags)
-        _run(["hipcc", "--offload-arch=" + ARCH, *HIP_FLAGS, *extra, "-I", os.path.join(CSRC, "include"), "-c", src,
-              "-o", obj], verbose)
+        if k.endswith(".cpp"):
+            obj = src.replace(".cpp", ".o")
+            tinc, _, abi = _torch_paths()
+            cmd = ["g++", "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__",
+                   "-DUSE_ROCM", "-I", f"{ROCM}/include", "-I", os.path.join(CSRC, "include")]
+            for ip in tinc:
+                cmd += ["-I", ip]
+            _run(cmd + ["-I", sysconfig.get_paths()["include"], "-c", src, "-o", obj], verbose)
+        else:
+            obj = src.replace(".hip", ".o")
+            extra = FILE_FLAGS.get(os.path.basename(k), []) if flags is None else list(flags)
+            _run(["hipcc", "--offload-arch=" + ARCH, *HIP_FLAGS, *extra, "-I", os.path.join(CSRC, "include"), "-c",
+                  src, "-o", obj], verbose)
         swap[os.path.basename(obj)] = obj
     out_dir = os.path.join(repo, "ab")
     os.makedirs(out_dir, exist_ok=True)
