@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void mc_color_kernel(float* __restrict__ x, in
 __device__ __forceinline__ int reflect(int j, int n) { return j < 0 ? -j : (j >= n ? 2 * (n - 1) - j : j); }
 
 // Gaussian taps for one image: w[k] = exp(-k^2 / 2 sigma^2) normalised over [-rad, rad]; sigma <= 0
-// is the identity kernel (the p=0.5 "no blur" draw)
+// is the identity kernel (the p=0.5 "no blur" draw; the blur kernels copy those images directly)
 __device__ __forceinline__ void blur_taps(float sigma, int rad, float* w) {
   if (sigma <= 0.f) {
     for (int k = 0; k <= 2 * rad; ++k) w[k] = k == rad ? 1.f : 0.f;
@@ -110,7 +110,8 @@ __global__ __launch_bounds__(256) void mc_hblur_kernel(const float* __restrict__
                                                         const float* __restrict__ prm, int rad) {
   __shared__ float w[2 * MAX_RAD + 1];
   const int i = blockIdx.y;
-  if (threadIdx.x == 0) blur_taps(prm[(size_t)i * NP + 19], rad, w);
+  const bool blur = prm[(size_t)i * NP + 19] > 0.f;  // uniform per block: the p=0.5 "no blur" draw copies
+  if (blur && threadIdx.x == 0) blur_taps(prm[(size_t)i * NP + 19], rad, w);
   __syncthreads();
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= S * S) return;
@@ -120,7 +121,11 @@ __global__ __launch_bounds__(256) void mc_hblur_kernel(const float* __restrict__
   for (int c = 0; c < 3; ++c) {
     const float* row = x + ((size_t)i * 3 + c) * HW + (size_t)yy * S;
     float acc = 0.f;
-    for (int k = -rad; k <= rad; ++k) acc += w[k + rad] * row[reflect(xx + k, S)];
+    if (blur) {
+      for (int k = -rad; k <= rad; ++k) acc += w[k + rad] * row[reflect(xx + k, S)];
+    } else {
+      acc = row[xx];
+    }
     y[((size_t)i * 3 + c) * HW + p] = acc;
   }
 }
@@ -131,7 +136,8 @@ __global__ __launch_bounds__(256) void mc_vblur_norm_kernel(const float* __restr
                                                              float is2) {
   __shared__ float w[2 * MAX_RAD + 1];
   const int i = blockIdx.y;
-  if (threadIdx.x == 0) blur_taps(prm[(size_t)i * NP + 19], rad, w);
+  const bool blur = prm[(size_t)i * NP + 19] > 0.f;
+  if (blur && threadIdx.x == 0) blur_taps(prm[(size_t)i * NP + 19], rad, w);
   __syncthreads();
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= S * S) return;
@@ -143,7 +149,11 @@ __global__ __launch_bounds__(256) void mc_vblur_norm_kernel(const float* __restr
   for (int c = 0; c < 3; ++c) {
     const float* col = x + ((size_t)i * 3 + c) * HW + xx;
     float acc = 0.f;
-    for (int k = -rad; k <= rad; ++k) acc += w[k + rad] * col[(size_t)reflect(yy + k, S) * S];
+    if (blur) {
+      for (int k = -rad; k <= rad; ++k) acc += w[k + rad] * col[(size_t)reflect(yy + k, S) * S];
+    } else {
+      acc = col[(size_t)yy * S];
+    }
     o[c] = f2bf((acc - mean[c]) * istd[c]);
   }
 }
