@@ -190,6 +190,14 @@ void grad_norm_clip(at::Tensor g, double max_norm, at::Tensor part, at::Tensor o
         "grad_norm_clip");
 }
 
+void scale_by_(at::Tensor x, const at::Tensor& s) {
+  expect(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.is_contiguous(), "scale_by_: x must be contiguous");
+  TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kFloat && s.numel() == 1, "scale_by_: s must be one fp32 GPU scalar");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "scale_by_ needs a 16-byte aligned tensor");
+  check(dl_scale_by(bf(x), x.numel(), f32(s.contiguous()), cur_stream(x)), "scale_by_");
+}
+
 void axpby(at::Tensor y, const at::Tensor& x, double a, double b, const c10::optional<at::Tensor>& flag) {
   expect(y, at::kFloat, "y");
   expect(x, at::kFloat, "x");
@@ -1396,6 +1404,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("larc_sgd_step", &larc_sgd_step);
   m.impl("grad_norm_clip", &grad_norm_clip);
   m.impl("axpby", &axpby);
+  m.impl("scale_by_", &scale_by_);
   m.impl("pack", &pack);
   m.impl("reduce_parts", &reduce_parts);
   m.impl("unpack", &unpack);

@@ -37,6 +37,8 @@ int dl_larc_sgd_step(float* p, const float* g, float* buf, const int* chunk_tens
                      hipStream_t st);
 int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, hipStream_t st);
 int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, hipStream_t st);
+// x *= s[0] in place (bf16; a device scalar, no pass at all when it is exactly 1)
+int dl_scale_by(bf16_t* x, size_t n, const float* s, hipStream_t st);
 int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st);
 
 // comm.hip

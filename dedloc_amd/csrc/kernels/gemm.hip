@@ -175,6 +175,45 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_kernel(GemmArgs p) {
 
   // ---- epilogue: lane holds C[row 4*(lane>>4) + i][col lane&15] of each 16x16 tile
   const int rq = 4 * (lane >> 4), cl = lane & 15;
+  if constexpr (EPI == EPI_STORE) {
+    if (p.R == nullptr && p.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(p.C) & 15) == 0) {
+      // bf16 tile staged through the (now free) 128 KiB of LDS and written as 16-byte row chunks:
+      // the per-element stores (4 rows x 32 bytes per wave instruction) made the ALBERT decoder's
+      // 39424 x 30000 logits GEMM (K = 128) store-bound at ~1.3 TB/s.  Row r's 16-byte chunk c sits
+      // at chunk c ^ (r & 31) of its 512-byte LDS row.
+      uint8_t* st = smem;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = wn * 64 + ni * 16 + cl;
+        const float bv = (p.bias && n0 + col < p.N) ? p.bias[n0 + col] : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = wm * 128 + mi * 16 + rq + i;
+            const int off = row * 512 + ((((col >> 3) ^ (row & 31)) << 4) | ((col & 7) << 1));
+            *reinterpret_cast<bf16_t*>(st + off) = f2bf(acc[mi][ni][i] + bv);
+          }
+      }
+      __syncthreads();
+      const int ch = threadIdx.x & 31;
+#pragma unroll 4
+      for (int pass = 0; pass < 16; ++pass) {
+        const int row = pass * 16 + (threadIdx.x >> 5);
+        const int m = m0 + row, n = n0 + ch * 8;
+        if (m >= p.M || n >= p.N) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(st + row * 512 + ((ch ^ (row & 31)) << 4));
+        bf16_t* dst = p.C + (long)m * p.ldc + n;
+        if (n + 8 <= p.N) {
+          *reinterpret_cast<uint4*>(dst) = v;
+        } else {
+          const bf16_t* e = reinterpret_cast<const bf16_t*>(&v);
+          for (int j = 0; j < p.N - n; ++j) dst[j] = e[j];
+        }
+      }
+      return;
+    }
+  }
   float colsum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) {

@@ -178,6 +178,24 @@ __global__ __launch_bounds__(kBlock) void axpby_kernel(float* __restrict__ y, co
     y[i] = (a != 0.f ? a * y[i] : 0.f) + (b != 0.f ? b * x[i] : 0.f);
 }
 
+// x *= *s (bf16, in place) — skipped entirely when the device scalar is exactly 1 (the gradient of a
+// loss that is backpropagated with the default ones seed: the cross-entropy's saved d(loss)/d(logits)
+// needs no 2.4 GB read-modify-write pass then)
+__global__ __launch_bounds__(kBlock) void scale_by_kernel(bf16_t* __restrict__ x, size_t n, const float* __restrict__ s) {
+  const float f = s[0];
+  if (f == 1.f) return;
+  const size_t nvec = n / 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float v[8];
+    load_bf16<8>(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= f;
+    store_bf16<8>(x + i * 8, v);
+  }
+  for (size_t i = nvec * 8 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    x[i] = f2bf(bf2f(x[i]) * f);
+}
+
 // out += sum_j slabs[j * n : (j + 1) * n]   (split-K partial reduction, fp32, float4 lanes)
 __global__ __launch_bounds__(kBlock) void sum_slabs_kernel(float* __restrict__ out, const float* __restrict__ slabs,
                                                            int s, size_t n) {
@@ -235,6 +253,12 @@ int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int npart
 
 int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st) {
   sum_slabs_kernel<<<grid_for(n), kBlock, 0, st>>>(out, slabs, s, n);
+  return 0;
+}
+
+int dl_scale_by(bf16_t* x, size_t n, const float* s, hipStream_t st) {
+  if (n == 0) return 0;
+  scale_by_kernel<<<grid_for(n / 8 + 1), kBlock, 0, st>>>(x, n, s);
   return 0;
 }
 

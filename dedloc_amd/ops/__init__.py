@@ -250,7 +250,11 @@ class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         (dlogits,) = ctx.saved_tensors
-        # the kernel already produced d(mean loss)/dlogits; scale in place by the upstream grad
+        # the kernel already produced d(mean loss)/dlogits; scale in place by the upstream grad (a
+        # no-op on the device when it is 1, the usual loss.backward() seed: no host sync, no pass)
+        if dlogits.dtype == torch.bfloat16 and dlogits.is_contiguous():
+            OPS.scale_by_(dlogits, dloss.reshape(1).float())
+            return dlogits, None, None
         return dlogits.mul_(dloss.to(dlogits.dtype)), None, None
 
 

@@ -30,6 +30,7 @@ _SCHEMAS = [
     "larc_sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(c!) norms, float lr, float momentum, float trust_coef, float eps, bool clip, bool first_step, float grad_scale) -> ()",
     "grad_norm_clip(Tensor(a!) g, float max_norm, Tensor(b!) part, Tensor(c!) out) -> ()",
     "axpby(Tensor(a!) y, Tensor x, float a, float b, Tensor? flag=None) -> ()",
+    "scale_by_(Tensor(a!) x, Tensor s) -> ()",
     "pack(Tensor src, Tensor(a!) dst, float weight) -> ()",
     "reduce_parts(Tensor parts, int nparts, Tensor(a!) out, float inv_total) -> ()",
     "unpack(Tensor src, Tensor(a!) dst, Tensor? snap, bool add=False) -> ()",
@@ -274,6 +275,11 @@ def _clip_cpu(g, max_norm, part, out):
         coef = max_norm / (norm.item() + 1e-6)
         if coef < 1:
             g.mul_(coef)
+
+
+@_impl("scale_by_")
+def _scale_by_cpu(x, s):
+    x.mul_(s.to(x.dtype))
 
 
 @_impl("axpby")

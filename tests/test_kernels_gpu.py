@@ -676,3 +676,15 @@ def test_albert_pretraining_converges_on_gpu(cuda):
         losses.append(float(out["loss"].detach()))
     assert all(math.isfinite(v) for v in losses)
     assert losses[-1] < 0.5 * losses[0], (losses[0], losses[-1])
+
+
+def test_scale_by_device_scalar(cuda):
+    """scale_by_: in-place bf16 scale by a device scalar (the cross-entropy backward's upstream
+    gradient), a no-op when the scalar is exactly 1; odd length exercises the tail."""
+    torch.manual_seed(31)
+    x = torch.randn(1001, device=cuda).bfloat16()
+    ref = x.clone()
+    OPS.scale_by_(x, torch.ones(1, device=cuda))
+    assert torch.equal(x, ref)
+    OPS.scale_by_(x, torch.full((1,), 0.5, device=cuda))
+    assert torch.equal(x, (ref.float() * 0.5).bfloat16())
