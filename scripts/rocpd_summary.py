@@ -21,6 +21,29 @@ def short(name: str) -> str:
     return re.sub(r"\(.*$", "", name)[:110]
 
 
+def timeline(spans, t0, t1):
+    """Union of the kernel intervals (GPU busy with >= 1 kernel), time with >= 2 kernels in flight,
+    and the kernel time and busy union of each stream."""
+    ev = sorted([(s, 1) for s, _, _ in spans] + [(min(e, t1), -1) for _, e, _ in spans])
+    depth, last, busy, overlap = 0, t0, 0.0, 0.0
+    for t, d in ev:
+        if depth >= 1:
+            busy += t - last
+        if depth >= 2:
+            overlap += t - last
+        depth += d
+        last = t
+    span = t1 - t0
+    print(f"timeline: busy (>=1 kernel) {busy / 1e6:.2f} ms = {100 * busy / span:.1f}% of {span / 1e6:.2f} ms; "
+          f">=2 kernels {overlap / 1e6:.2f} ms; idle {(span - busy) / 1e6:.2f} ms")
+    per = defaultdict(list)
+    for s, e, st in spans:
+        per[st].append((s, e))
+    for st, iv in sorted(per.items(), key=lambda kv: -sum(e - s for s, e in kv[1])):
+        tot = sum(e - s for s, e in iv)
+        print(f"  stream {st}: {len(iv)} kernels, {tot / 1e6:.2f} ms kernel time")
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
@@ -29,10 +52,12 @@ def main(argv=None):
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--from_ms", type=float, default=None, help="window start, ms after the first dispatch")
     ap.add_argument("--to_ms", type=float, default=None, help="window end, ms after the first dispatch")
+    ap.add_argument("--timeline", action="store_true",
+                    help="also print the window's union busy time, overlap and per-stream kernel time")
     a = ap.parse_args(argv)
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x, vgpr_count, accum_vgpr_count, "
-                     "lds_size from kernels order by start").fetchall()
+                     "lds_size, stream_id from kernels order by start").fetchall()
     if not rows:
         print("no kernels")
         return 1
@@ -44,7 +69,7 @@ def main(argv=None):
     rows = [r for r in rows if r[1] < t_end]
     agg = defaultdict(lambda: [0, 0.0, None])
     busy = 0.0
-    for name, s, e, gx, gy, gz, wx, vg, ag, lds in rows:
+    for name, s, e, gx, gy, gz, wx, vg, ag, lds, _ in rows:
         if s < t0:
             continue
         k = short(name)
@@ -61,6 +86,8 @@ def main(argv=None):
     for k, (n, tot, meta) in out[:a.top]:
         wgs, wx, vg, ag, lds = meta
         print(f"{tot / 1e3:9.2f} {100 * tot / busy:6.2f} {n:6d} {tot / n:9.1f}  {wgs:7d} {wx:4d} {vg:4d} {ag:4d} {lds:6d}  {k}")
+    if a.timeline:
+        timeline([(r[1], r[2], r[10]) for r in rows if r[1] >= t0], t0, t_end)
     if a.csv:
         with open(a.csv, "w", newline="") as f:
             w = csv.writer(f)
