@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--queue", action="store_true", help="queue active (3840 rows in Sinkhorn)")
     ap.add_argument("--graph", action="store_true", help="capture trunk+head fwd/bwd as HIP graphs")
     ap.add_argument("--sequential", action="store_true", help="the two resolution passes on one stream")
+    ap.add_argument("--splits", default=None, help="concurrent passes per resolution, e.g. 2,1 (whole crops each)")
     ap.add_argument("--no_prefetch", action="store_true", help="generate each batch in line (no side-stream prefetch)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -36,6 +37,8 @@ def main():
           "config.OPTIMIZER.target_batch_size=100000000", f"config.MODEL.SINGLE_PASS_EVERY_CROP={not args.grouped}",
           f"config.LOSS.swav_loss.queue.start_iter={0 if args.queue else 10**9}", "config.CHECKPOINT.DIR=/tmp/swav_bench", f"config.MODEL.CUDA_GRAPH={args.graph}",
           f"config.MODEL.CONCURRENT_PASSES={not args.sequential}", f"config.DATA.TRAIN.PREFETCH={not args.no_prefetch}"]
+    if args.splits:
+        ov.append(f"config.MODEL.CONCURRENT_SPLITS=[{args.splits}]")
     cfg = load_config("swav_1node_resnet_submit", ov)
     dht = DHT(start=True)
     peer = SwavPeer(cfg, dev, dht=dht)
@@ -63,7 +66,7 @@ def main():
         print(json.dumps({"metric": "swav_rn50_local_samples_per_sec_per_gpu", "value": args.batch / dt,
                           "ms_per_iter": dt * 1e3, "data_ms": data_ms, "larc_sgd_step_ms": opt_ms,
                           "batch": args.batch, "crops": "2x224+6x96", "grouped": args.grouped, "queue": args.queue, "hip_graph": args.graph,
-                          "concurrent_passes": not args.sequential, "prefetch": not args.no_prefetch,
+                          "concurrent_passes": not args.sequential, "splits": args.splits, "prefetch": not args.no_prefetch,
                           "peak_mem_gb": torch.cuda.max_memory_allocated() / 2**30}))
     finally:
         peer.shutdown()

@@ -592,6 +592,7 @@ class SwAVModel(nn.Module):
     # gradient by after_backward) and its running-statistics updates into zeroed stand-ins (merged
     # after the join: the update is affine, rm <- (1-m)^G rm + D, so the crop order is kept).
     concurrent_passes = False
+    pass_splits = (1, 1)  # concurrent passes per resolution group (_pass_plan)
 
     def bind_flat(self, flat):
         """Take the GEMM / conv weights of every forward from ``flat``'s bf16 mirror: one cast
@@ -601,88 +602,112 @@ class SwAVModel(nn.Module):
                           if isinstance(m, (ConvNHWC, HeadLinear))]
         self._conc = None
 
-    def _conc_state(self):
+    def _conc_state(self, sides: int):
+        """Per side pass: a HIP stream, a flat-gradient-shaped buffer for its weight / BN-parameter
+        gradients and zeroed running-statistics stand-ins (created once per number of side passes)."""
         c = getattr(self, "_conc", None)
-        if c is None:
+        if c is None or len(c["passes"]) != sides:
             flat = self._flat
-            gb = torch.zeros_like(flat.grad)
-            slots = []
-            for n, m in self.trunk.named_modules():
-                if isinstance(m, ConvNHWC):
-                    slots.append((m, flat.view(gb, f"trunk.{n}.weight")))
-                elif isinstance(m, BNAct):
-                    slots.append((m, (flat.view(gb, f"trunk.{n}.weight"), flat.view(gb, f"trunk.{n}.bias"))))
             bns = self.trunk._bn_modules()
-            rs = torch.zeros(2 * sum(m.num_features for m in bns), dtype=torch.float32, device=gb.device)
-            views, off = [], 0
-            for m in bns:
-                C = m.num_features
-                views.append((rs[off:off + C], rs[off + C:off + 2 * C]))
-                off += 2 * C
-            c = self._conc = {"grad_b": gb, "slots": slots, "rs": rs, "rs_views": views,
-                              "stream": torch.cuda.Stream(gb.device), "pending": False}
+            passes = []
+            for _ in range(sides):
+                gb = torch.zeros_like(flat.grad)
+                slots = []
+                for n, m in self.trunk.named_modules():
+                    if isinstance(m, ConvNHWC):
+                        slots.append((m, flat.view(gb, f"trunk.{n}.weight")))
+                    elif isinstance(m, BNAct):
+                        slots.append((m, (flat.view(gb, f"trunk.{n}.weight"), flat.view(gb, f"trunk.{n}.bias"))))
+                rs = torch.zeros(2 * sum(m.num_features for m in bns), dtype=torch.float32, device=gb.device)
+                views, off = [], 0
+                for m in bns:
+                    C = m.num_features
+                    views.append((rs[off:off + C], rs[off + C:off + 2 * C]))
+                    off += 2 * C
+                passes.append({"grad_b": gb, "slots": slots, "rs": rs, "rs_views": views,
+                               "stream": torch.cuda.Stream(gb.device)})
+            c = self._conc = {"passes": passes, "pending": False}
         return c
 
-    def _concurrent_ok(self, groups) -> bool:
-        x = groups[0][0]
-        return (self.concurrent_passes and len(groups) == 2 and self._flat is not None
-                and x.device.type == "cuda"  # a second HIP stream
+    def _pass_plan(self, groups):
+        """The trunk passes of one forward: each resolution group, or — ``pass_splits[i]`` > 1 and one
+        statistics group per crop — that group cut into ``pass_splits[i]`` passes of whole crops
+        (per-crop BatchNorm statistics make the cut exact)."""
+        out = []
+        for i, (x, g) in enumerate(groups):
+            s = self.pass_splits[i] if i < len(self.pass_splits) else 1
+            if s > 1 and g > 1 and g % s == 0:
+                n = x.shape[0] // s
+                out += [(x[j * n:(j + 1) * n], g // s) for j in range(s)]
+            else:
+                out.append((x, g))
+        return out
+
+    def _concurrent_ok(self, passes) -> bool:
+        x = passes[0][0]
+        return (self.concurrent_passes and len(passes) >= 2 and self._flat is not None
+                and x.device.type == "cuda"  # side HIP streams
                 and self.training and torch.is_grad_enabled() and ResNet50Trunk.pass_workspace
                 and not self.trunk.checkpoint_stages and BNAct.inplace_grad and ConvNHWC.inplace_wgrad
                 and all(m.momentum is not None for m in self.trunk._bn_modules())
                 and all(g.is_contiguous(memory_format=torch.channels_last) and g.dtype == torch.bfloat16
-                        for g, _ in groups))
+                        for g, _ in passes))
 
-    def _trunk_concurrent(self, groups):
-        c = self._conc_state()
-        cur, side = torch.cuda.current_stream(), c["stream"]
+    def _trunk_concurrent(self, passes):
+        c = self._conc_state(len(passes) - 1)
+        cur = torch.cuda.current_stream()
         convs = [m for m in self.trunk.modules() if isinstance(m, ConvNHWC)]
-        for m in convs:  # shared by both passes' backward: made here, before the fork
+        for m in convs:  # shared by every pass's backward: made here, before the fork
             _dgrad_weights(m, m._wb_cache, m.stride[0], m.padding[0])
-        (xa, ga), (xb, gb) = groups
-        self.set_bn_stat_groups(ga)
-        prep_a = self.trunk.alloc_bn_pass(xa)
-        self.set_bn_stat_groups(gb)
-        prep_b = self.trunk.alloc_bn_pass(xb)
-        side.wait_stream(cur)
-        self.set_bn_stat_groups(ga)
-        fa = self.trunk(xa, prep_a)
+        preps = []
+        for x, g in passes:
+            self.set_bn_stat_groups(g)
+            preps.append(self.trunk.alloc_bn_pass(x))
+        for sp in c["passes"]:
+            sp["stream"].wait_stream(cur)
+        self.set_bn_stat_groups(passes[0][1])
+        feats = [self.trunk(passes[0][0], preps[0])]
         bns = self.trunk._bn_modules()
-        self.set_bn_stat_groups(gb)
-        for m, g in c["slots"]:
-            m._gslot = g
-        for m, r in zip(bns, c["rs_views"]):
-            m._rs_override = r
-        try:
-            with torch.cuda.stream(side):
-                fb = self.trunk(xb, prep_b)
-        finally:
-            for m, _ in c["slots"]:
-                m._gslot = None
-            for m in bns:
-                m._rs_override = None
-        cur.wait_stream(side)
-        fb.record_stream(cur)
-        with torch.no_grad():  # the second pass's running-statistics updates, in crop order
-            torch._foreach_mul_([m.running_mean for m in bns], [(1.0 - m.momentum) ** gb for m in bns])
-            torch._foreach_add_([m.running_mean for m in bns], [v[0] for v in c["rs_views"]])
-            torch._foreach_mul_([m.running_var for m in bns], [(1.0 - m.momentum) ** gb for m in bns])
-            torch._foreach_add_([m.running_var for m in bns], [v[1] for v in c["rs_views"]])
-            c["rs"].zero_()
+        for (x, g), prep, sp in zip(passes[1:], preps[1:], c["passes"]):
+            self.set_bn_stat_groups(g)
+            for m, gs in sp["slots"]:
+                m._gslot = gs
+            for m, r in zip(bns, sp["rs_views"]):
+                m._rs_override = r
+            try:
+                with torch.cuda.stream(sp["stream"]):
+                    feats.append(self.trunk(x, prep))
+            finally:
+                for m, _ in sp["slots"]:
+                    m._gslot = None
+                for m in bns:
+                    m._rs_override = None
+        for f, sp in zip(feats[1:], c["passes"]):
+            cur.wait_stream(sp["stream"])
+            f.record_stream(cur)
+        with torch.no_grad():  # the side passes' running-statistics updates, in crop order
+            for (_, g), sp in zip(passes[1:], c["passes"]):
+                torch._foreach_mul_([m.running_mean for m in bns], [(1.0 - m.momentum) ** g for m in bns])
+                torch._foreach_add_([m.running_mean for m in bns], [v[0] for v in sp["rs_views"]])
+                torch._foreach_mul_([m.running_var for m in bns], [(1.0 - m.momentum) ** g for m in bns])
+                torch._foreach_add_([m.running_var for m in bns], [v[1] for v in sp["rs_views"]])
+                sp["rs"].zero_()
         c["pending"] = True
-        return [fa, fb]
+        return feats
 
     def after_backward(self):
-        """Add the concurrent second pass's gradients into the flat gradient (after every backward
-        of a forward that ran the passes concurrently; a no-op otherwise)."""
+        """Add the concurrent side passes' gradients into the flat gradient (after every backward of
+        a forward that ran the passes concurrently; a no-op otherwise)."""
         c = getattr(self, "_conc", None)
         if c is not None and c["pending"]:
-            # the second pass's backward ran on the side stream and ends there (its gradients are
-            # written in place, nothing flows back): join it before reading its gradients (this also
-            # joins the side stream's work into a HIP-graph capture of the backward)
-            torch.cuda.current_stream().wait_stream(c["stream"])
-            self._flat.grad.add_(c["grad_b"])
-            c["grad_b"].zero_()
+            # a side pass's backward runs on its stream and ends there (its gradients are written in
+            # place, nothing flows back): join it before reading its gradients (this also joins the
+            # side streams' work into a HIP-graph capture of the backward)
+            cur = torch.cuda.current_stream()
+            for sp in c["passes"]:
+                cur.wait_stream(sp["stream"])
+                self._flat.grad.add_(sp["grad_b"])
+                sp["grad_b"].zero_()
             c["pending"] = False
 
     def set_bn_stat_groups(self, g: int):
@@ -726,8 +751,9 @@ class SwAVModel(nn.Module):
             groups.append((torch.cat(crops[i:j]) if j - i > 1 else crops[i],
                            j - i if self.single_pass_every_crop else 1))
             i = j
-        if self._concurrent_ok(groups):
-            feats = self._trunk_concurrent(groups)
+        passes = self._pass_plan(groups) if self.concurrent_passes else groups
+        if self._concurrent_ok(passes):
+            feats = self._trunk_concurrent(passes)
         else:
             feats = []
             for x, g in groups:

@@ -94,9 +94,11 @@ class SwavPeer:
                                channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
         if impl == "dedloc":
             self.model.bind_flat(self.flat)  # GEMM / conv weights read from the flat buffer's bf16 mirror
-            # the two crop resolutions' trunk passes on two streams (SwAVModel.concurrent_passes; this
+            # the crop groups' trunk passes on several streams (SwAVModel.concurrent_passes: one per
+            # resolution, CONCURRENT_SPLITS cuts a resolution into passes of whole crops; this
             # trainer calls after_backward after every backward)
             self.model.concurrent_passes = bool(cfg.MODEL.get("CONCURRENT_PASSES", True))
+            self.model.pass_splits = tuple(int(v) for v in cfg.MODEL.get("CONCURRENT_SPLITS", (1, 1)))
         self.model.normalize_prototypes()
         larc = ocfg.larc_config
         assert ocfg.use_larc, "we can't use collab sgd without larc (sgd_collaborative.py:138)"

@@ -670,12 +670,14 @@ def test_trunk_bn_pass_workspace_and_inplace_grads(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_concurrent_trunk_passes_match_sequential(cuda):
-    """SwAVModel.concurrent_passes (the two crop resolutions' trunk passes on two streams, the second
-    pass's parameter gradients in a buffer of its own added by after_backward, its running-statistics
-    updates merged after the join) gives the sequential path's gradients, running statistics and
-    counters.  The sequential path run twice gives the run-to-run spread (fp32 atomics in the BN
-    statistics) the comparison allows for."""
+@pytest.mark.parametrize("splits", [(1, 1), (2, 1), (2, 2)])
+def test_concurrent_trunk_passes_match_sequential(cuda, splits):
+    """SwAVModel.concurrent_passes (the crop groups' trunk passes on several streams — one per
+    resolution, or with pass_splits a resolution cut into passes of whole crops — each side pass's
+    parameter gradients in a buffer of its own added by after_backward, its running-statistics
+    updates merged after the join in crop order) gives the sequential path's gradients, running
+    statistics and counters.  The sequential path run twice gives the run-to-run spread (fp32
+    atomics in the BN statistics) the comparison allows for."""
     from dedloc_amd.models.resnet_swav import SwAVModel
     from dedloc_amd.utils.flat import FlatParams
 
@@ -687,6 +689,7 @@ def test_concurrent_trunk_passes_match_sequential(cuda):
         flat = FlatParams(model.named_parameters(), device=cuda, with_bf16=True, autograd=True, channels_last=True)
         model.bind_flat(flat)
         model.concurrent_passes = concurrent
+        model.pass_splits = splits
         g = torch.Generator(device="cpu").manual_seed(1)
         for _ in range(2):  # two iterations: the stand-ins / second-pass gradients are re-zeroed
             crops = [torch.randn(8, 3, 64, 64, generator=g).to(cuda).bfloat16().contiguous(memory_format=CLF)
@@ -698,14 +701,15 @@ def test_concurrent_trunk_passes_match_sequential(cuda):
             (scores.float().pow(2).mean() + emb.float().pow(2).mean()).backward()
             model.after_backward()
         torch.cuda.synchronize()
-        ran = getattr(model, "_conc", None) is not None
+        conc = getattr(model, "_conc", None)
+        ran = 0 if conc is None else len(conc["passes"]) + 1
         bufs = torch.cat([b.float().flatten() for _, b in model.named_buffers()])
         return flat.grad.clone(), bufs, ran
 
     g0, b0, r0 = run(False)
     ga, ba, _ = run(False)
     g1, b1, r1 = run(True)
-    assert not r0 and r1
+    assert r0 == 0 and r1 == 2 + (splits[0] - 1) + (splits[1] - 1)
 
     def rel(a, b):
         return ((a - b).norm() / b.norm()).item()
