@@ -531,12 +531,15 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at
 // the chip idle for the second half of the kernel, 48 x 16 = 768 = 3 full waves does not.  Among
 // the splits with at least 1024 reduction rows per slice, the best wave efficiency wins, the
 // smaller S on ties (fewer slab bytes to sum).
+#ifndef DL_WGRAD_CUS
+#define DL_WGRAD_CUS 256  // CUs one weight gradient is split to fill (a measurement build may override)
+#endif
 int wgrad_splits8(const Mat& A, const Mat& B) {
   const int64_t tiles = ((A.rows + 255) / 256) * ((B.rows + 255) / 256);
   // any S dividing the K-tile count (SwAV's 14x14 maps: 25088 tokens = 392 K-tiles = 2^3 7^2, so
   // S = 56 puts 224 workgroups on the chip where powers of two stop at 32), each slice at least 4
   // K-tiles (8 while S > 32)
-  constexpr int64_t kCUs = 256;
+  constexpr int64_t kCUs = DL_WGRAD_CUS;
   const int64_t ktiles = A.k / 64;
   if (A.k % 64) return 1;
   int best = 1;

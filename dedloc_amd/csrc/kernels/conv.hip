@@ -840,9 +840,12 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
 // exist (default 256: one per CU; SwAV b=64 iteration 1990-1997 samples/s at 1024, 2051-2061 at 256,
 // 2041 at 512, with atomic adds), each split a multiple of the 64-deep k-step and at least 8 k-steps
 // long
+#ifndef DL_CONV_WGRAD_TARGET
+#define DL_CONV_WGRAD_TARGET 256  // (a measurement build may override)
+#endif
 static long wgrad_splits(const DlConvGeom& g, int tiles) {
   const long M = (long)g.Nimg * g.I * g.J;
-  constexpr long target = 256;
+  constexpr long target = DL_CONV_WGRAD_TARGET;
   const long ksteps = (M + BK - 1) / BK;
   long splits = std::max(1L, std::min<long>((target + tiles - 1) / tiles, ksteps / 8));
   const long steps_per = (ksteps + splits - 1) / splits;
