@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture trunk+head fwd/bwd as HIP graphs")
     ap.add_argument("--sequential", action="store_true", help="the two resolution passes on one stream")
     ap.add_argument("--splits", default=None, help="concurrent passes per resolution, e.g. 2,1 (whole crops each)")
+    ap.add_argument("--model_attr", action="append", default=[],
+                    help="NAME=INT: set a SwAVModel class attribute for an A/B (e.g. dgrad_weights_stream=0)")
     ap.add_argument("--no_prefetch", action="store_true", help="generate each batch in line (no side-stream prefetch)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -40,6 +42,12 @@ def main():
     if args.splits:
         ov.append(f"config.MODEL.CONCURRENT_SPLITS=[{args.splits}]")
     cfg = load_config("swav_1node_resnet_submit", ov)
+    from dedloc_amd.models.resnet_swav import SwAVModel
+
+    for kv in args.model_attr:
+        k, v = kv.split("=")
+        assert hasattr(SwAVModel, k), k
+        setattr(SwAVModel, k, type(getattr(SwAVModel, k))(int(v)))
     dht = DHT(start=True)
     peer = SwavPeer(cfg, dev, dht=dht)
     try:

@@ -593,6 +593,7 @@ class SwAVModel(nn.Module):
     # after the join: the update is affine, rm <- (1-m)^G rm + D, so the crop order is kept).
     concurrent_passes = False
     pass_splits = (1, 1)  # concurrent passes per resolution group (_pass_plan)
+    dgrad_weights_stream = True  # the data-gradient weights on a stream of their own (_trunk_concurrent)
 
     def bind_flat(self, flat):
         """Take the GEMM / conv weights of every forward from ``flat``'s bf16 mirror: one cast
@@ -626,7 +627,7 @@ class SwAVModel(nn.Module):
                     off += 2 * C
                 passes.append({"grad_b": gb, "slots": slots, "rs": rs, "rs_views": views,
                                "stream": torch.cuda.Stream(gb.device)})
-            c = self._conc = {"passes": passes, "pending": False}
+            c = self._conc = {"passes": passes, "pending": False, "wprep": torch.cuda.Stream(flat.grad.device)}
         return c
 
     def _pass_plan(self, groups):
@@ -657,8 +658,20 @@ class SwAVModel(nn.Module):
         c = self._conc_state(len(passes) - 1)
         cur = torch.cuda.current_stream()
         convs = [m for m in self.trunk.modules() if isinstance(m, ConvNHWC)]
-        for m in convs:  # shared by every pass's backward: made here, before the fork
-            _dgrad_weights(m, m._wb_cache, m.stride[0], m.padding[0])
+        # the data-gradient weights (shared by every pass's backward, ~40 small copy kernels) on a
+        # stream of their own, under the forward passes; each pass's stream waits for them behind its
+        # forward
+        wprep = c["wprep"] if self.dgrad_weights_stream else cur
+        wprep.wait_stream(cur)
+        with torch.cuda.stream(wprep):
+            for m in convs:
+                _dgrad_weights(m, m._wb_cache, m.stride[0], m.padding[0])
+        users = [cur] + [sp["stream"] for sp in c["passes"]]
+        for m in convs:
+            for t in (getattr(m, "_wd_cache", None) or (None, ()))[1] or ():
+                if t.numel():
+                    for st in users:
+                        t.record_stream(st)
         preps = []
         for x, g in passes:
             self.set_bn_stat_groups(g)
@@ -667,6 +680,7 @@ class SwAVModel(nn.Module):
             sp["stream"].wait_stream(cur)
         self.set_bn_stat_groups(passes[0][1])
         feats = [self.trunk(passes[0][0], preps[0])]
+        cur.wait_stream(wprep)  # (behind pass 0's forward) its backward reads the data-gradient weights
         bns = self.trunk._bn_modules()
         for (x, g), prep, sp in zip(passes[1:], preps[1:], c["passes"]):
             self.set_bn_stat_groups(g)
@@ -677,6 +691,7 @@ class SwAVModel(nn.Module):
             try:
                 with torch.cuda.stream(sp["stream"]):
                     feats.append(self.trunk(x, prep))
+                sp["stream"].wait_stream(wprep)
             finally:
                 for m, _ in sp["slots"]:
                     m._gslot = None
