@@ -198,6 +198,20 @@ void scale_by_(at::Tensor x, const at::Tensor& s) {
   check(dl_scale_by(bf(x), x.numel(), f32(s.contiguous()), cur_stream(x)), "scale_by_");
 }
 
+// out += sum over the rows of slabs [S, out.numel()] (fp32), then slabs = 0: the concurrent SwAV
+// passes' side gradient buffers folded into the flat gradient in one pass
+void add_slabs_zero_(at::Tensor out, at::Tensor slabs) {
+  expect(out, at::kFloat, "out");
+  expect(slabs, at::kFloat, "slabs");
+  TORCH_CHECK(out.is_contiguous() && slabs.is_contiguous() && slabs.dim() == 2 && slabs.size(1) == out.numel(),
+              "add_slabs_zero_: slabs must be a contiguous [S, out.numel()] buffer");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(slabs.data_ptr()) % 16 == 0 && out.numel() % 4 == 0,
+              "add_slabs_zero_ needs 16-byte aligned buffers and rows");
+  check(dl_add_slabs_zero(f32(out), f32(slabs), (int)slabs.size(0), (size_t)out.numel(), cur_stream(out)),
+        "add_slabs_zero_");
+}
+
 void axpby(at::Tensor y, const at::Tensor& x, double a, double b, const c10::optional<at::Tensor>& flag) {
   expect(y, at::kFloat, "y");
   expect(x, at::kFloat, "x");
@@ -1407,6 +1421,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("larc_sgd_step", &larc_sgd_step);
   m.impl("grad_norm_clip", &grad_norm_clip);
   m.impl("axpby", &axpby);
+  m.impl("add_slabs_zero_", &add_slabs_zero_);
   m.impl("scale_by_", &scale_by_);
   m.impl("pack", &pack);
   m.impl("reduce_parts", &reduce_parts);

@@ -40,6 +40,7 @@ int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* 
 // x *= s[0] in place (bf16; a device scalar, no pass at all when it is exactly 1)
 int dl_scale_by(bf16_t* x, size_t n, const float* s, hipStream_t st);
 int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st);
+int dl_add_slabs_zero(float* out, float* slabs, int s, size_t n, hipStream_t st);
 
 // comm.hip
 int dl_pack(const float* src, void* dst, int dst_dt, size_t n, float weight, hipStream_t st);

@@ -196,14 +196,18 @@ __global__ __launch_bounds__(kBlock) void scale_by_kernel(bf16_t* __restrict__ x
     x[i] = f2bf(bf2f(x[i]) * f);
 }
 
-// out += sum_j slabs[j * n : (j + 1) * n]   (split-K partial reduction, fp32, float4 lanes)
-__global__ __launch_bounds__(kBlock) void sum_slabs_kernel(float* __restrict__ out, const float* __restrict__ slabs,
+// out += sum_j slabs[j * n : (j + 1) * n]   (split-K partial reduction, fp32, float4 lanes); ZERO:
+// each slab element is cleared once read (gradient buffers that are accumulated into again)
+template <bool ZERO>
+__global__ __launch_bounds__(kBlock) void sum_slabs_kernel(float* __restrict__ out, float* __restrict__ slabs,
                                                            int s, size_t n) {
   const size_t nvec = n / 4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     float4 acc = reinterpret_cast<float4*>(out)[i];
     for (int j = 0; j < s; ++j) {
-      const float4 v = reinterpret_cast<const float4*>(slabs + (size_t)j * n)[i];
+      float4* sp = reinterpret_cast<float4*>(slabs + (size_t)j * n) + i;
+      const float4 v = *sp;
+      if (ZERO) *sp = float4{0.f, 0.f, 0.f, 0.f};
       acc.x += v.x;
       acc.y += v.y;
       acc.z += v.z;
@@ -212,7 +216,10 @@ __global__ __launch_bounds__(kBlock) void sum_slabs_kernel(float* __restrict__ o
     reinterpret_cast<float4*>(out)[i] = acc;
   }
   for (size_t i = nvec * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    for (int j = 0; j < s; ++j) out[i] += slabs[(size_t)j * n + i];
+    for (int j = 0; j < s; ++j) {
+      out[i] += slabs[(size_t)j * n + i];
+      if (ZERO) slabs[(size_t)j * n + i] = 0.f;
+    }
 }
 
 inline int grid_for(size_t n) {
@@ -252,7 +259,12 @@ int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int npart
 }
 
 int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st) {
-  sum_slabs_kernel<<<grid_for(n), kBlock, 0, st>>>(out, slabs, s, n);
+  sum_slabs_kernel<false><<<grid_for(n), kBlock, 0, st>>>(out, const_cast<float*>(slabs), s, n);
+  return 0;
+}
+
+int dl_add_slabs_zero(float* out, float* slabs, int s, size_t n, hipStream_t st) {
+  sum_slabs_kernel<true><<<grid_for(n), kBlock, 0, st>>>(out, slabs, s, n);
   return 0;
 }
 

@@ -31,6 +31,23 @@ from .. import ops as _ops  # noqa: F401  (registers torch.ops.dedloc.*)
 from torch.utils.checkpoint import checkpoint
 
 
+def join_batch(ts: Sequence[torch.Tensor]) -> torch.Tensor:
+    """``torch.cat(ts)`` along the batch dimension, as a zero-copy view when the tensors already lie
+    back to back in one storage with equal shapes and strides and a dense batch stride (the multi-crop
+    pipeline's ``x.split(b)`` outputs, the graphed iteration's static inputs)."""
+    if len(ts) == 1:
+        return ts[0]
+    t0 = ts[0]
+    step = t0.shape[0] * t0.stride(0) * t0.element_size()
+    dense = t0.dim() >= 1 and t0.stride(0) == max(1, t0[0].numel()) and (
+        t0.is_contiguous() or t0.is_contiguous(memory_format=torch.channels_last))
+    if dense and all(t.shape == t0.shape and t.stride() == t0.stride() and t.dtype == t0.dtype
+                     and t.device == t0.device and t.untyped_storage().data_ptr() == t0.untyped_storage().data_ptr()
+                     and t.data_ptr() == t0.data_ptr() + i * step for i, t in enumerate(ts)):
+        return t0.as_strided((t0.shape[0] * len(ts),) + tuple(t0.shape[1:]), t0.stride())
+    return torch.cat(ts)
+
+
 def _require_nhwc_bf16(x: torch.Tensor, what: str) -> torch.Tensor:
     """The trunk's activation contract: channels-last bf16 (what every producing kernel writes)."""
     if x.dtype != torch.bfloat16 or not x.is_contiguous(memory_format=torch.channels_last):
@@ -416,12 +433,12 @@ class ResNet50Trunk(nn.Module):
         layers += [Bottleneck(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
-    def alloc_bn_pass(self, x):
+    def alloc_bn_pass(self, x, count: bool = True):
         """One zeroed workspace for every BatchNorm's forward and backward statistics sums of the
         pass over ``x`` (with the BatchNorms' current stat_groups), and one multi-tensor add for their
         num_batches_tracked counters (instead of two memsets and one add launch per BatchNorm; each
         is a ~5 us kernel at b=64).  Returns the per-BatchNorm workspace slices for ``forward``'s
-        ``prepared`` (None: the per-call path)."""
+        ``prepared`` (None: the per-call path).  ``count=False``: the caller adds the counters."""
         if not self.pass_workspace or not self.training or self.checkpoint_stages:
             return None
         bns = self._bn_modules()
@@ -432,7 +449,8 @@ class ResNet50Trunk(nn.Module):
         for n in sizes:
             out.append((ws[off:off + n], ws[off + n:off + 2 * n]))
             off += 2 * n
-        torch._foreach_add_([m.num_batches_tracked for m in bns], G)
+        if count:
+            torch._foreach_add_([m.num_batches_tracked for m in bns], G)
         return out
 
     def _prepare_bn_pass(self, x, prepared=None):
@@ -611,8 +629,11 @@ class SwAVModel(nn.Module):
             flat = self._flat
             bns = self.trunk._bn_modules()
             passes = []
-            for _ in range(sides):
-                gb = torch.zeros_like(flat.grad)
+            # every side pass's gradient buffer as one row of a [sides, n] buffer (after_backward
+            # folds all of them into the flat gradient and clears them in one pass)
+            gb_all = torch.zeros((sides, flat.grad.numel()), dtype=flat.grad.dtype, device=flat.grad.device)
+            for si in range(sides):
+                gb = gb_all[si].view_as(flat.grad)
                 slots = []
                 for n, m in self.trunk.named_modules():
                     if isinstance(m, ConvNHWC):
@@ -627,7 +648,8 @@ class SwAVModel(nn.Module):
                     off += 2 * C
                 passes.append({"grad_b": gb, "slots": slots, "rs": rs, "rs_views": views,
                                "stream": torch.cuda.Stream(gb.device)})
-            c = self._conc = {"passes": passes, "pending": False, "wprep": torch.cuda.Stream(flat.grad.device)}
+            c = self._conc = {"passes": passes, "pending": False, "grad_all": gb_all,
+                              "wprep": torch.cuda.Stream(flat.grad.device)}
         return c
 
     def _pass_plan(self, groups):
@@ -672,12 +694,18 @@ class SwAVModel(nn.Module):
                 if t.numel():
                     for st in users:
                         t.record_stream(st)
-        preps = []
-        for x, g in passes:
-            self.set_bn_stat_groups(g)
-            preps.append(self.trunk.alloc_bn_pass(x))
         for sp in c["passes"]:
             sp["stream"].wait_stream(cur)
+        # each pass's zeroed BN workspace on its own stream; every pass's counter increments in one
+        # add on the weight stream (training never reads the counters: momentum is set)
+        preps = []
+        for (x, g), st in zip(passes, users):
+            self.set_bn_stat_groups(g)
+            with torch.cuda.stream(st):
+                preps.append(self.trunk.alloc_bn_pass(x, count=False))
+        with torch.cuda.stream(wprep):
+            torch._foreach_add_([m.num_batches_tracked for m in self.trunk._bn_modules()],
+                                sum(g for _, g in passes))
         self.set_bn_stat_groups(passes[0][1])
         feats = [self.trunk(passes[0][0], preps[0])]
         cur.wait_stream(wprep)  # (behind pass 0's forward) its backward reads the data-gradient weights
@@ -721,8 +749,7 @@ class SwAVModel(nn.Module):
             cur = torch.cuda.current_stream()
             for sp in c["passes"]:
                 cur.wait_stream(sp["stream"])
-                self._flat.grad.add_(sp["grad_b"])
-                sp["grad_b"].zero_()
+            torch.ops.dedloc.add_slabs_zero_(self._flat.grad, c["grad_all"])
             c["pending"] = False
 
     def set_bn_stat_groups(self, g: int):
@@ -763,7 +790,7 @@ class SwAVModel(nn.Module):
             j = i
             while j < len(crops) and crops[j].shape[-1] == crops[i].shape[-1]:
                 j += 1
-            groups.append((torch.cat(crops[i:j]) if j - i > 1 else crops[i],
+            groups.append((join_batch(crops[i:j]),
                            j - i if self.single_pass_every_crop else 1))
             i = j
         passes = self._pass_plan(groups) if self.concurrent_passes else groups

@@ -30,6 +30,7 @@ _SCHEMAS = [
     "larc_sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(c!) norms, float lr, float momentum, float trust_coef, float eps, bool clip, bool first_step, float grad_scale) -> ()",
     "grad_norm_clip(Tensor(a!) g, float max_norm, Tensor(b!) part, Tensor(c!) out) -> ()",
     "axpby(Tensor(a!) y, Tensor x, float a, float b, Tensor? flag=None) -> ()",
+    "add_slabs_zero_(Tensor(a!) out, Tensor(b!) slabs) -> ()",
     "scale_by_(Tensor(a!) x, Tensor s) -> ()",
     "pack(Tensor src, Tensor(a!) dst, float weight) -> ()",
     "reduce_parts(Tensor parts, int nparts, Tensor(a!) out, float inv_total) -> ()",
@@ -280,6 +281,12 @@ def _clip_cpu(g, max_norm, part, out):
 @_impl("scale_by_")
 def _scale_by_cpu(x, s):
     x.mul_(s.to(x.dtype))
+
+
+@_impl("add_slabs_zero_")
+def _add_slabs_zero_cpu(out, slabs):
+    out.add_(slabs.sum(0).view_as(out))
+    slabs.zero_()
 
 
 @_impl("axpby")

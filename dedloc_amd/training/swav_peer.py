@@ -33,7 +33,7 @@ import torch
 from ..data.multicrop import MultiCropAugment, StreamPrefetcher, SyntheticMultiCropStream
 from ..dht import DHT, get_dht_time
 from ..metrics import LocalMetrics, make_validators
-from ..models.resnet_swav import SwAVModel
+from ..models.resnet_swav import SwAVModel, join_batch
 from ..models.swav_loss import SwAVLoss
 from ..optim.collaborative import CollaborativeOptimizer
 from ..optim.lamb import FusedLarcSGD, LinearWarmupCosineAnnealingLR
@@ -183,7 +183,12 @@ class SwavPeer:
         backward graph's static seed.  Warm-up iterations run on a side stream first (first-call
         allocations, kernel attributes), after which gradients and BN statistics are restored."""
         model = self.model
-        static = [c.detach().clone() for c in crops]
+        # static inputs laid out like the pipeline's crops: one buffer per resolution, the crops its
+        # batch slices (the model then joins them without a copy, and each replay refills them with
+        # one copy per resolution)
+        static = []
+        for grp in self._resolution_groups(crops):
+            static.extend(join_batch(grp).detach().clone().split(grp[0].shape[0]))
         grads = self.flat.grad.clone()
         bufs = {k: v.clone() for k, v in model.named_buffers()}
 
@@ -214,11 +219,23 @@ class SwavPeer:
         self.flat.rebind_grads()
         return {"fwd": g_fwd, "bwd": g_bwd, "in": static, "emb": emb, "scores": scores, "seed": seed}
 
+    @staticmethod
+    def _resolution_groups(crops):
+        out = []
+        for c in crops:
+            if out and out[-1][0].shape == c.shape:
+                out[-1].append(c)
+            else:
+                out.append([c])
+        return out
+
     def _graph_iteration(self, crops):
         """One forward + loss + backward through the captured graphs (see _build_graph)."""
         gr = self._graphed
-        for s, c in zip(gr["in"], crops):
-            s.copy_(c)
+        i = 0
+        for grp in self._resolution_groups(crops):
+            join_batch(gr["in"][i:i + len(grp)]).copy_(join_batch(grp))
+            i += len(grp)
         with self.perf.phase("fwd"):
             gr["fwd"].replay()
         with self.perf.phase("loss_bwd"):

@@ -688,3 +688,16 @@ def test_scale_by_device_scalar(cuda):
     assert torch.equal(x, ref)
     OPS.scale_by_(x, torch.full((1,), 0.5, device=cuda))
     assert torch.equal(x, (ref.float() * 0.5).bfloat16())
+
+
+@pytest.mark.parametrize("n", [4096, 1000004])
+def test_add_slabs_zero(cuda, n):
+    """add_slabs_zero_: out += sum of the [S, n] slab rows (fp32, float4 lanes + tail), then the slabs
+    read zero — the concurrent SwAV passes' side gradients folded into the flat gradient."""
+    torch.manual_seed(32)
+    out = torch.randn(n, device=cuda)
+    slabs = torch.randn(3, n, device=cuda)
+    ref = out.double() + slabs.double().sum(0)
+    OPS.add_slabs_zero_(out, slabs)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-6, atol=1e-5)
+    assert not slabs.any()

@@ -717,3 +717,22 @@ def test_concurrent_trunk_passes_match_sequential(cuda, splits):
     assert torch.isfinite(g1).all()
     assert rel(g1, g0) < max(3 * rel(ga, g0), 2e-3), (rel(g1, g0), rel(ga, g0))
     assert rel(b1, b0) < max(3 * rel(ba, b0), 1e-4), (rel(b1, b0), rel(ba, b0))
+
+
+def test_join_batch_views_adjacent_crops_and_copies_otherwise():
+    """join_batch: the multi-crop pipeline's split outputs (back to back in one channels-last buffer)
+    join without a copy; anything else falls back to torch.cat with the same values."""
+    from dedloc_amd.models.resnet_swav import join_batch
+
+    base = torch.randn(12, 3, 8, 8).contiguous(memory_format=torch.channels_last)
+    parts = base.split(4)
+    j = join_batch(parts)
+    assert j.data_ptr() == base.data_ptr() and torch.equal(j, base)
+    assert j.is_contiguous(memory_format=torch.channels_last)
+    assert join_batch(parts[1:]).data_ptr() == parts[1].data_ptr()
+    shuffled = [parts[2], parts[0]]
+    k = join_batch(shuffled)
+    assert k.data_ptr() != parts[2].data_ptr() and torch.equal(k, torch.cat(shuffled))
+    sep = [torch.randn(4, 3, 8, 8), torch.randn(4, 3, 8, 8)]
+    assert torch.equal(join_batch(sep), torch.cat(sep))
+    assert join_batch(parts[:1]) is parts[0]
