@@ -787,7 +787,7 @@ at::Tensor multicrop(const at::Tensor& pool, const at::Tensor& params, int64_t s
   const int64_t nb = params.size(0), S = size;
   auto out = at::empty({nb, 3, S, S}, pool.options().dtype(at::kBFloat16), at::MemoryFormat::ChannelsLast);
   if (nb == 0) return out;
-  auto ws = at::empty({2 * nb * 3 * S * S + nb}, pool.options());
+  auto ws = at::empty({nb * 3 * S * S + nb}, pool.options());
   const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   const float sd[3] = {(float)std[0], (float)std[1], (float)std[2]};
   check(dl_multicrop(f32(pool), (int)pool.size(0), (int)pool.size(2), (int)pool.size(3), f32(params), (int)nb, (int)S, (int)rad, m, sd,

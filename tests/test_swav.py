@@ -185,7 +185,8 @@ def test_multicrop_kernels_match_reference(cuda):
     pool = _smooth_images(6, 64, torch.Generator(device=cuda).manual_seed(0), cuda)
     aug = MultiCropAugment()
     gen = torch.Generator().manual_seed(3)
-    for size, scale in ((40, (0.14, 1.0)), (16, (0.05, 0.14))):
+    # 224 / 96: the bench's crop sizes (several row bands per image in the fused colour-blur kernel)
+    for size, scale in ((40, (0.14, 1.0)), (16, (0.05, 0.14)), (224, (0.14, 1.0)), (96, (0.05, 0.14))):
         params = aug.sample_params(torch.randint(0, 6, (24,), generator=gen), scale, gen)
         out = torch.ops.dedloc.multicrop(pool, params.to(cuda), size, aug.rad, list(aug.mean), list(aug.std))
         ref = augment_reference(pool.cpu(), params, size, aug.rad, aug.mean, aug.std)
