@@ -2,8 +2,8 @@
 
 ``cryptography`` is not available in this image, so RSA is implemented over Python integers:
 keygen with Miller-Rabin primes, e = 65537, EMSA-PKCS1-v1_5 with a SHA-256 DigestInfo.  Signing
-and verification are single modular exponentiations (microseconds at 1024 bits, sub-millisecond at
-2048); keygen runs once per process.
+uses the CRT form (two half-size exponentiations), verification one exponentiation with e = 65537;
+keygen runs once per process.
 """
 from __future__ import annotations
 
@@ -65,6 +65,10 @@ class RSAPrivateKey:
         self.n, self.e = p * q, e
         self.d = pow(e, -1, phi)
         self.k = (self.n.bit_length() + 7) // 8
+        # CRT form of the private exponent (PKCS#1 RSAPrivateKey's dP, dQ, qInv): a signature is two
+        # half-size exponentiations, ~3x faster than m^d mod n; the result is the same integer
+        self.p, self.q = p, q
+        self.dp, self.dq, self.qinv = self.d % (p - 1), self.d % (q - 1), pow(q, -1, p)
 
     @classmethod
     def process_wide(cls) -> "RSAPrivateKey":
@@ -78,7 +82,8 @@ class RSAPrivateKey:
 
     def sign(self, data: bytes) -> bytes:
         m = int.from_bytes(_emsa(data, self.k), "big")
-        return pow(m, self.d, self.n).to_bytes(self.k, "big")
+        s1, s2 = pow(m, self.dp, self.p), pow(m, self.dq, self.q)
+        return (s2 + self.q * ((s1 - s2) * self.qinv % self.p)).to_bytes(self.k, "big")
 
 
 class RSAPublicKey:

@@ -565,13 +565,24 @@ class CollaborativeOptimizer:
         self.stats["param_rounds"] = self.stats.get("param_rounds", 0) + 1
 
     # ------------------------------------------------------------------ background threads
+    # Progress records are signed (dht/crypto.py, big-integer RSA holding the GIL ~1.5 ms per record):
+    # stored after every micro-step they would take the trainer thread's GIL ~50 times a second at
+    # SwAV's 21 ms iterations.  One record per this interval at most still refreshes every peer's
+    # ETA far faster than a global step (seconds), and a micro-step slower than it reports each time.
+    min_report_interval = 0.1
+
     def _report_loop(self):
+        last = 0.0
         while not self._stop.is_set():
             self.should_report_progress.wait()
+            wait = last + self.min_report_interval - time.monotonic()
+            if wait > 0 and self._stop.wait(wait):
+                break
             self.should_report_progress.clear()
             if self._stop.is_set():
                 break
             if not self.auxiliary and not getattr(self, "_left", False):
+                last = time.monotonic()
                 self.report_training_progress()
 
     def report_training_progress(self):

@@ -73,6 +73,9 @@ def _peer(rank, world, dht_ep, out_q, cfg, mode="", compression="NONE", barrier=
                 os.kill(os.getpid(), 9)
             if mode == "kill":
                 steps = 8
+            if mode == "delay":
+                steps = 5  # a parameter round runs behind each global step: a few, so one lost to a
+                #            matchmaking timeout under a loaded host still leaves completed ones
             peer.train(max_steps=600, stop_after_global_steps=steps, max_seconds=60 if mode != "churn" else 90)
             peer.collab_opt._finish_param_round()
         res["local_step"] = peer.collab_opt.local_step
