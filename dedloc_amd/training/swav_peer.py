@@ -274,9 +274,8 @@ class SwavPeer:
                 name = name[len("module."):] if name.startswith("module.") else name
                 self.flat.view(self.flat.grad, name).zero_()
         self._loss_sum += loss.detach()
-        if self.check_nan and (self.iteration + 1) % self.log_frequency == 0 and \
-                not bool(torch.isfinite(self._loss_sum)):  # before the step: NaN grads never reach the averaging
-            self._nan_dump(float(self._loss_sum))
+        if self.check_nan and (self.iteration + 1) % self.log_frequency == 0:
+            self._check_nan_async()
         with self.perf.phase("collab_step"):
             self.collab_opt.step(batch_size=self.batch_size)
         self.opt.zero_grad()
@@ -310,11 +309,35 @@ class SwavPeer:
         self._loss_sum.zero_()
         self.mini_steps = 0
 
+    def _check_nan_async(self):
+        """Every LOG_FREQUENCY iterations: queue a device-to-pinned-host copy of the running loss's
+        finite flag behind this iteration, and act on the flags that have landed (the previous
+        check's, typically).  A blocking read here drained the GPU queue every LOG_FREQUENCY
+        iterations and left the device idle while the host refilled it; this way a non-finite loss
+        is still caught within ~2 LOG_FREQUENCY iterations and at every global-step report."""
+        pend = self.__dict__.setdefault("_nan_pending", [])
+        flag = torch.isfinite(self._loss_sum)
+        if flag.is_cuda:
+            host = torch.empty((), dtype=torch.bool, pin_memory=True)
+            host.copy_(flag, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            pend.append((host, ev))
+        else:
+            pend.append((flag, None))
+        while pend:
+            host, ev = pend[0]
+            if ev is not None and not ev.query():
+                break
+            pend.pop(0)
+            if not bool(host):
+                self._nan_dump(float(self._loss_sum))
+
     def _nan_dump(self, loss: float):
         """vissl CheckNanLossHook (``state_update_hooks.py:207-233``) / the SwAV loss's NaN dump: save
         the model, optimizer and loss state next to the checkpoints, then stop this peer.  Checked every
-        LOG_FREQUENCY iterations (one host sync per check, before the collaborative step) and at every
-        global-step report, where the loss is read anyway."""
+        LOG_FREQUENCY iterations without a host sync (``_check_nan_async``) and at every global-step
+        report, where the loss is read anyway."""
         d = Path(self.cfg.CHECKPOINT.DIR)
         d.mkdir(parents=True, exist_ok=True)
         path = d / f"nan_dump_iteration{self.iteration}.torch"
