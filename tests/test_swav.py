@@ -404,6 +404,38 @@ def test_swav_peer_gpu_step(cuda, tmp_path, graph):
 
 
 @pytest.mark.gpu
+def test_swav_peer_gpu_nan_check_is_async_and_stops(cuda, tmp_path):
+    """The GPU peer's NaN-loss check copies the device flag to pinned memory and reads it at the
+    next check (no host sync per check): finite iterations never stop, and a non-finite loss dumps
+    the state and raises within a few LOG_FREQUENCY periods."""
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.training.swav_peer import SwavPeer
+
+    cfg = load_config("swav_1node_resnet_submit", [
+        "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=8", "config.DATA.TRAIN.SYNTHETIC_POOL_SIZE=16",
+        "config.OPTIMIZER.target_batch_size=100000", "config.OPTIMIZER.batch_size_for_tracking=8",
+        f"config.CHECKPOINT.DIR={tmp_path}", "config.MODEL.CUDA_GRAPH=false", "config.LOG_FREQUENCY=2"])
+    dht = DHT(start=True)
+    peer = SwavPeer(cfg, cuda, dht=dht)
+    try:
+        for _ in range(6):
+            peer.train_step()
+        torch.cuda.synchronize()
+        assert not list(tmp_path.glob("nan_dump_iteration*.torch"))
+        with torch.no_grad():
+            peer.model.trunk.conv1.weight.fill_(float("nan"))
+            peer.flat.refresh_bf16()
+        with pytest.raises(FloatingPointError):
+            for _ in range(12):
+                peer.train_step()
+                torch.cuda.synchronize()  # the copies land; the next check reads them
+        assert len(list(tmp_path.glob("nan_dump_iteration*.torch"))) == 1
+    finally:
+        peer.shutdown()
+        dht.shutdown()
+
+
+@pytest.mark.gpu
 def test_swav_peer_graph_matches_eager(cuda, tmp_path):
     """The graph-replayed iteration computes what the eager one does: two peers from the same
     initialisation, fed the same crops, with the queue active, through collaborative LARC steps
@@ -737,3 +769,12 @@ def test_join_batch_views_adjacent_crops_and_copies_otherwise():
     sep = [torch.randn(4, 3, 8, 8), torch.randn(4, 3, 8, 8)]
     assert torch.equal(join_batch(sep), torch.cat(sep))
     assert join_batch(parts[:1]) is parts[0]
+
+
+def test_add_slabs_zero_cpu():
+    """add_slabs_zero_ (the side-pass gradient fold): CPU implementation."""
+    out = torch.randn(64)
+    slabs = torch.randn(3, 64)
+    ref = out + slabs.sum(0)
+    torch.ops.dedloc.add_slabs_zero_(out, slabs)
+    assert torch.allclose(out, ref) and not slabs.any()
