@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--graph", action="store_true", help="capture trunk+head fwd/bwd as HIP graphs")
     ap.add_argument("--sequential", action="store_true", help="the two resolution passes on one stream")
     ap.add_argument("--splits", default=None, help="concurrent passes per resolution, e.g. 2,1 (whole crops each)")
+    ap.add_argument("--cfg", action="append", default=[], help="extra config override, e.g. config.HOOKS.PERF_STATS=false")
     ap.add_argument("--model_attr", action="append", default=[],
                     help="NAME=INT: set a SwAVModel class attribute for an A/B (e.g. dgrad_weights_stream=0)")
     ap.add_argument("--no_prefetch", action="store_true", help="generate each batch in line (no side-stream prefetch)")
@@ -39,6 +40,7 @@ def main():
           "config.OPTIMIZER.target_batch_size=100000000", f"config.MODEL.SINGLE_PASS_EVERY_CROP={not args.grouped}",
           f"config.LOSS.swav_loss.queue.start_iter={0 if args.queue else 10**9}", "config.CHECKPOINT.DIR=/tmp/swav_bench", f"config.MODEL.CUDA_GRAPH={args.graph}",
           f"config.MODEL.CONCURRENT_PASSES={not args.sequential}", f"config.DATA.TRAIN.PREFETCH={not args.no_prefetch}"]
+    ov += args.cfg
     if args.splits:
         ov.append(f"config.MODEL.CONCURRENT_SPLITS=[{args.splits}]")
     cfg = load_config("swav_1node_resnet_submit", ov)

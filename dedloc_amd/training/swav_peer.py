@@ -88,7 +88,8 @@ class SwavPeer:
         self.check_nan = bool(hooks.get("CHECK_NAN", True))
         self.log_frequency = max(1, int(cfg.get("LOG_FREQUENCY", 10)))
         # vissl PerfTimer/LogPerfTimeMetricsHook (V20): HIP-event phase timers, reported per global step
-        self.perf = PerfStats(self.device, enabled=bool(hooks.get("PERF_STATS", True)))
+        self.perf = PerfStats(self.device, enabled=bool(hooks.get("PERF_STATS", True)),
+                              sample_every=int(cfg.get("LOG_FREQUENCY", 10)) if self.device.type == "cuda" else 1)
         self.flat = FlatParams(self.model.named_parameters(), device=self.device,
                                with_bf16=self.device.type == "cuda" and impl == "dedloc", autograd=True,
                                channels_last=bool(mcfg.get("CHANNELS_LAST", True)))
@@ -281,6 +282,7 @@ class SwavPeer:
         self.opt.zero_grad()
         self.model.normalize_prototypes()  # NormalizePrototypesHook.on_update (swav_hooks.py:63-92)
         self.iteration += 1
+        self.perf.next_iteration()
         self.mini_steps += 1
         self._on_step_end()
         return loss.detach()
