@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
       for (int j = 0; j < 8; ++j) {
         float o = fmaf(v[u][j], sc[c0 + j], sh[c0 + j]);
         if (res != nullptr) o += rr[u][j];
-        v[u][j] = relu ? fmaxf(o, 0.f) : o;
+        v[u][j] = relu && o < 0.f ? 0.f : o;  // NaN passes, as torch.relu
       }
       store_bf16<8>(y + (i + u * stride) * 8, v[u]);
     }
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(v[j], sc[c0 + j], sh[c0 + j]);
       if (res != nullptr) o += rr[j];
-      v[j] = relu ? fmaxf(o, 0.f) : o;
+      v[j] = relu && o < 0.f ? 0.f : o;
     }
     store_bf16<8>(y + i * 8, v);
   }

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
         load8(x + (((long)n * H + h) * W + w) * C + c8 * 8, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (v[j] > best[j]) {  // first maximum in window order wins (torch's tie rule)
+          if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) {  // first maximum in window order wins (torch's tie rule); the first NaN wins over numbers, as in torch
             best[j] = v[j];
             slot[j] = (uint8_t)(r * 3 + s);
           }

@@ -422,8 +422,8 @@ def test_swav_peer_gpu_nan_check_is_async_and_stops(cuda, tmp_path):
             peer.train_step()
         torch.cuda.synchronize()
         assert not list(tmp_path.glob("nan_dump_iteration*.torch"))
-        with torch.no_grad():  # (a trunk weight would not do: the fused BN+ReLU kernels map NaN to 0)
-            peer.model.heads[0].prototypes0.weight.fill_(float("nan"))
+        with torch.no_grad():  # a trunk weight: the NaN must survive the fused BN+ReLU and the max pool
+            peer.model.trunk.conv1.weight.fill_(float("nan"))
             peer.flat.refresh_bf16()
         with pytest.raises(FloatingPointError):
             for _ in range(12):

@@ -37,6 +37,24 @@ def test_maxpool_matches_torch(cuda, hw):
         torch.testing.assert_close(dx.float().sum((2, 3)), xr.grad.sum((2, 3)), rtol=2e-2, atol=2e-1)
 
 
+def test_nan_propagates_through_relu_and_maxpool_like_torch(cuda):
+    """torch.relu(NaN) and a max-pool window holding a NaN give NaN; the fused BN+ReLU and the max
+    pool kernels keep that (a NaN-loss check must see NaNs that arise in the trunk)."""
+    N, C, H, W = 2, 64, 8, 8
+    x = torch.randn(N, C, H, W, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    x[0, 3, 2, 5] = float("nan")
+    y, arg = torch.ops.dedloc.maxpool_fwd(x)
+    yr = F.max_pool2d(x.float(), 3, 2, 1)
+    assert torch.equal(torch.isnan(y.float()), torch.isnan(yr))
+    torch.testing.assert_close(torch.nan_to_num(y.float()), torch.nan_to_num(yr), rtol=0, atol=0)
+    g, b = torch.ones(C, device=cuda), torch.zeros(C, device=cuda)
+    x2 = torch.randn(N, C, H, W, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+    x2[1, 7, 0, 0] = float("nan")
+    out = torch.ops.dedloc.bn_fwd(x2, None, g, b, None, None, 1e-5, 0.1, True)[0]
+    ref = torch.relu(F.batch_norm(x2.float(), None, None, g, b, training=True, eps=1e-5))
+    assert torch.equal(torch.isnan(out.float()), torch.isnan(ref))  # channel 7: NaN statistics
+
+
 @pytest.mark.parametrize("shape", [(8, 2048, 7, 7), (5, 256, 3, 3), (2, 64, 56, 56)])
 def test_avgpool_matches_torch(cuda, shape):
     N, C, H, W = shape
