@@ -1029,6 +1029,14 @@ inline bool is_pointwise(int64_t R, int64_t S, int64_t stride, int64_t pad) {
 // register prefetch) instead of gemm_small: 128 won the round-3 A/B over 0 / 64 / 256 / 512
 // (SwAV b=64: 2087 / 2128 / 2205 / 2197 / 2190 samples/s, profiles/README.md)
 constexpr int64_t narrow_1x1_max() { return 128; }
+// 1x1 forward convs whose gemm8 grid (256 x 256 tiles) has fewer than this many workgroups run on
+// conv.hip's 128 x 128 tiles instead (4x the workgroups, lower latency): SwAV's layer-3/4 convs of the
+// 96-crop pass, which with the 224 crops split into passes of their own is the iteration's critical
+// path (a measurement build may override)
+#ifndef DL_FEW_TILE_1X1
+#define DL_FEW_TILE_1X1 128
+#endif
+inline bool few_tile_gemm(int64_t M, int64_t N) { return ((M + 255) / 256) * ((N + 255) / 256) < DL_FEW_TILE_1X1; }
 inline at::Tensor rows2d(const at::Tensor& t) {  // channels-last [N, C, H, W] -> [N*H*W, C] view
   return t.permute({0, 2, 3, 1}).reshape({-1, t.size(1)});
 }
@@ -1093,7 +1101,8 @@ at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t str
   auto y = at::empty({N, K, P, Q}, x.options(), at::MemoryFormat::ChannelsLast);
   const at::Tensor wk = krsc_view(w);
   const long stat_rows = N / groups * P * Q;  // output rows per statistics group
-  if (is_pointwise(R, S, stride, pad) && conv_gemm() && !(K <= narrow_1x1_max() && C % 64 == 0)) {
+  if (is_pointwise(R, S, stride, pad) && conv_gemm() && !(K <= narrow_1x1_max() && C % 64 == 0) &&
+      !(C % 64 == 0 && few_tile_gemm(N * P * Q, K))) {
     const at::Tensor xr = rows2d(x), wr = wk.view({K, C});
     if (stats) gemm_store_stats(a_view(xr, false), b_view(wr, true), xr, wr, bf(y), K, stats, stat_rows, cur_stream(x));
     else gemm_plain(xr, wr, bf(y), K, cur_stream(x));
