@@ -173,6 +173,17 @@ def test_rsa_sign_verify_roundtrip():
     assert not RSAPublicKey.from_bytes(other.public_key().to_bytes()).verify(b"hello", sig)
 
 
+def test_rsa_crt_signature_equals_plain_exponentiation():
+    """CRT signing (two half-size exponentiations, dht/crypto.py) yields the PKCS#1 v1.5 signature
+    m^d mod n byte for byte."""
+    from dedloc_amd.dht.crypto import _emsa
+
+    k = RSAPrivateKey(bits=1024)
+    for msg in (b"", b"x" * 200, bytes(range(256))):
+        m = int.from_bytes(_emsa(msg, k.k), "big")
+        assert k.sign(msg) == pow(m, k.d, k.n).to_bytes(k.k, "big")
+
+
 def test_signature_validator_owner_only():
     owner = RSASignatureValidator(RSAPrivateKey(bits=1024))
     intruder = RSASignatureValidator(RSAPrivateKey(bits=1024))
