@@ -778,3 +778,23 @@ def test_add_slabs_zero_cpu():
     ref = out + slabs.sum(0)
     torch.ops.dedloc.add_slabs_zero_(out, slabs)
     assert torch.allclose(out, ref) and not slabs.any()
+
+
+def test_pass_plan_cuts_groups_into_whole_crops():
+    """SwAVModel._pass_plan: a resolution group with one statistics group per crop is cut into
+    pass_splits[i] passes of whole crops (views, crop order kept); a group whose statistics span
+    the whole group, or whose crop count the split does not divide, stays one pass."""
+    from dedloc_amd.models.resnet_swav import SwAVModel
+
+    m = SwAVModel.__new__(SwAVModel)
+    m.pass_splits = (2, 1)
+    a, b = torch.randn(4, 3, 8, 8), torch.randn(12, 3, 4, 4)
+    plan = m._pass_plan([(a, 2), (b, 6)])
+    assert [(x.shape[0], g) for x, g in plan] == [(2, 1), (2, 1), (12, 6)]
+    assert plan[0][0].data_ptr() == a.data_ptr() and plan[1][0].data_ptr() == a[2:].data_ptr()
+    m.pass_splits = (2, 2)
+    assert [(x.shape[0], g) for x, g in m._pass_plan([(a, 2), (b, 6)])] == [(2, 1), (2, 1), (6, 3), (6, 3)]
+    m.pass_splits = (4, 4)  # 4 does not divide 2 crops / 6 crops
+    assert [(x.shape[0], g) for x, g in m._pass_plan([(a, 2), (b, 6)])] == [(4, 2), (12, 6)]
+    m.pass_splits = (2, 2)  # statistics over the whole group (g = 1): never cut
+    assert [(x.shape[0], g) for x, g in m._pass_plan([(a, 1), (b, 1)])] == [(4, 1), (12, 1)]
