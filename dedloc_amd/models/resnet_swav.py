@@ -728,7 +728,10 @@ class SwAVModel(nn.Module):
         for f, sp in zip(feats[1:], c["passes"]):
             cur.wait_stream(sp["stream"])
             f.record_stream(cur)
-        with torch.no_grad():  # the side passes' running-statistics updates, in crop order
+        # the side passes' running-statistics updates, in crop order, on the weight stream under the
+        # head's forward (nothing in training reads them; SwAVModel.forward joins the stream)
+        wprep.wait_stream(cur)
+        with torch.cuda.stream(wprep), torch.no_grad():
             for (_, g), sp in zip(passes[1:], c["passes"]):
                 torch._foreach_mul_([m.running_mean for m in bns], [(1.0 - m.momentum) ** g for m in bns])
                 torch._foreach_add_([m.running_mean for m in bns], [v[0] for v in sp["rs_views"]])
@@ -736,6 +739,7 @@ class SwAVModel(nn.Module):
                 torch._foreach_add_([m.running_var for m in bns], [v[1] for v in sp["rs_views"]])
                 sp["rs"].zero_()
         c["pending"] = True
+        c["join"] = wprep
         return feats
 
     def after_backward(self):
@@ -802,7 +806,12 @@ class SwAVModel(nn.Module):
                 self.set_bn_stat_groups(g)
                 feats.append(self.trunk(x))
         self.set_bn_stat_groups(1)
-        return self.heads[0](torch.cat(feats))
+        out = self.heads[0](torch.cat(feats))
+        c = getattr(self, "_conc", None)
+        if c is not None and c.get("join") is not None:  # the running-statistics merge (_trunk_concurrent)
+            torch.cuda.current_stream().wait_stream(c["join"])
+            c["join"] = None
+        return out
 
     @torch.no_grad()
     def normalize_prototypes(self):
