@@ -365,9 +365,15 @@ __device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
+#ifdef ATTN_PROBE_NO_EXP  // measurement build only (profiles/README.md): the exponentials' cost
+          const float pv = LEAN ? fmaf(s[u][j][i], c.sl2, nm) : s[u][j][i] + nm;
+#else
           const float pv = __builtin_amdgcn_exp2f(LEAN ? fmaf(s[u][j][i], c.sl2, nm) : s[u][j][i] + nm);
+#endif
           s[u][j][i] = pv;
+#ifndef ATTN_PROBE_NO_SUM  // measurement build only: the row sums' cost
           rsa[i & 7] += pv;
+#endif
         }
       float rs = ((rsa[0] + rsa[1]) + (rsa[2] + rsa[3])) + ((rsa[4] + rsa[5]) + (rsa[6] + rsa[7]));
       l[u] += half_sum(rs);
