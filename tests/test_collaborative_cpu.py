@@ -37,6 +37,7 @@ def _peer(rank, world, dht_ep, out_q, cfg, mode="", compression="NONE", barrier=
         aux = False
     if mode == "delay":
         cargs.delay_param_averaging = True
+        targs.throttle = 0.05  # paced micro-steps: on a loaded host neither peer runs its steps alone
     elif mode == "hetero":
         targs.peer_batch_sizes, targs.peer_slowdowns = "2,1,3", "1,2,1"
         cargs.peer_bandwidths = "200,50,100"
