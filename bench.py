@@ -314,8 +314,9 @@ def main():
     if world > 1:
         dist.barrier()
     sync()
-    keys = ("fetch_s", "averaging_s", "optimizer_s", "local_steps", "global_steps")
-    st0 = {k: co.stats[k] for k in keys}
+    keys = ("wait_s", "fetch_s", "averaging_s", "matchmaking_s", "allreduce_s", "optimizer_s", "tail_s", "local_steps",
+            "global_steps")
+    st0 = {k: co.stats.get(k, 0.0) for k in keys}
     t0 = time.perf_counter()
     samples = run_until(base + args.warmup + args.steps)
     sync()
@@ -323,8 +324,12 @@ def main():
         dist.barrier()
     sync()
     dt = time.perf_counter() - t0
+    if hasattr(peer, "flush_metrics"):
+        peer.flush_metrics(block=True)
+    if co._device_timer is not None:  # fold the timed region's last micro-steps into the EMA
+        co._device_timer.poll()
     ema = co.performance_ema.samples_per_second
-    stats = torch.tensor([samples, dt, ema] + [co.stats[k] - st0[k] for k in keys], dtype=torch.float64)
+    stats = torch.tensor([samples, dt, ema] + [co.stats.get(k, 0.0) - st0[k] for k in keys], dtype=torch.float64)
     if world > 1:
         gathered = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(gathered, stats)
@@ -343,8 +348,9 @@ def main():
                "first_microstep_s": None if first_s is None else round(first_s, 3),
                "ema_samples_per_s_sum": round(ema_sum, 2), "averaging_rounds": co.stats["averaging_rounds"],
                "averaging_failed": co.stats["averaging_failed"],
-               # timed-region breakdown, mean over peers: host seconds per global step in the state
-               # fetch / matchmaking + all-reduce / optimizer launch, local micro-steps per global step
+               # timed-region breakdown, mean over peers: host ms per global step waiting for the
+               # batch's last micro-step, in the state fetch, matchmaking + all-reduce (and each),
+               # the optimizer launch and the bookkeeping after it; local micro-steps per global step
                "protocol": _protocol_breakdown(gathered, keys),
                "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"}})
         print(json.dumps(out), flush=True)

@@ -78,11 +78,13 @@ def main():
             kinds.insert(3, ("dgrad_wT", lambda: O.gemm(dy, wt, None, None, False, True, 0)))
         if name == "ffn1":
             kinds.append(("fwd_gelu", lambda: O.gemm_gelu(x, w, b)))
+            kinds.append(("fwd_gelu_d", lambda: O.gemm_gelu_d(x, w, b)))
             if os.environ.get("DGRAD_T"):
                 kinds.append(("fwd_gelu_wT", lambda: O.gemm_gelu(x, wt, b, True)))
         if name == "ffn2":
             f = (torch.randn(T, K, device=dev)).bfloat16()
             kinds.append(("dgrad_dgelu", lambda: O.gemm_dgelu(dy, w, f, db)))
+            kinds.append(("dgrad_dmul", lambda: O.gemm_dmul(dy, w, f, db)))
             if os.environ.get("DGRAD_T"):
                 w2t = w.t().contiguous()
                 kinds.append(("dgrad_dgelu_wT", lambda: O.gemm_dgelu(dy, w2t, f, db, True)))

@@ -1,7 +1,9 @@
-// Measurement build of gemm8.hip (not part of the library): times the NT GEMM on an ALBERT shape as
-// built with or without its epilogue / output writes, to size the per-tile fixed costs.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I dedloc_amd/csrc/include [-DGEMM8_PROBE_NO_STORE]
-//         [-DGEMM8_PROBE_NO_EPILOGUE] bench/hip/gemm8_probe.hip -o probe
+// Stand-alone timing harness for gemm8.hip (not part of the library): the NT GEMM on an ALBERT
+// shape, outside torch.  The round-2/3 probe variants (no epilogue, no output stores, desynchronised
+// first wave) were compiled from #ifdef hooks inside the shipped kernel; those hooks were removed
+// (VERDICT r4): to re-run a probe, copy gemm8.hip next to this file, edit the copy, and include it
+// instead.  Their results stay in profiles/README.md.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I dedloc_amd/csrc/include bench/hip/gemm8_probe.hip -o probe
 #include "../../dedloc_amd/csrc/kernels/gemm8.hip"
 #include <cstdio>
 #include <cstdlib>

@@ -25,7 +25,9 @@ Weights travel on the wire: each contributor sends its own fp32 weight (bit-exac
 elements) to every reducer together with the part, and the reducer reads the weights it applies
 from what it received.  Only ``spec.weights[my_index]`` has to be known when the round starts — so
 matchmaking can run ahead of the last micro-step of a global batch, before a peer knows how many
-samples it will have contributed (``DecentralizedAverager.prejoin``).
+samples it will have contributed (``DecentralizedAverager.prejoin``) — and it may be a device scalar
+(the count of finite samples, kept on the GPU), so the global step never waits for the host to
+learn it.  A group whose weights sum to 0 leaves every tensor unchanged (zero deltas).
 
 Timeouts: completion is polled on the host against a deadline; on expiry the communicator is
 aborted (``ncclCommAbort`` for RCCL) so the operations still posted on it can never be matched by a
@@ -100,7 +102,11 @@ def butterfly_allreduce(tensors: Sequence[torch.Tensor], spec: GroupSpec, compre
     i_contribute = spec.contributes[me]
     # this contributor's weight as wire elements (the fp32 bits: 1 element of fp32, 2 of fp16/bf16)
     W = 4 // torch.empty(0, dtype=wire).element_size()
-    my_w = torch.tensor([float(spec.weights[me])], dtype=torch.float32).view(wire).to(dev)
+    w_me = spec.weights[me]
+    if isinstance(w_me, torch.Tensor):  # a device scalar: the weight is never read on the host
+        my_w = w_me.detach().reshape(1).to(device=dev, dtype=torch.float32).contiguous().view(wire)
+    else:
+        my_w = torch.tensor([float(w_me)], dtype=torch.float32).view(wire).to(dev)
 
     # 1. pack (compressed, unweighted: the reducer applies the weights in fp32)
     send = torch.empty(V if i_contribute else 0, dtype=wire, device=dev)

@@ -67,7 +67,10 @@ class StateServer:
     """Serves ``get_state() -> (metadata, [tensors])`` to joining peers.
 
     Request: ``b"STATE" + mode`` with mode ``R`` (followed by a 128-byte RCCL unique id made by the
-    requester) or ``T``.  A GPU donor answers an ``R`` request by sending the snapshot device-to-
+    requester, then the requester's GPU identity as a 2-byte length + UTF-8) or ``T``.  RCCL takes
+    one rank per device, so a requester on the donor's own GPU is always answered over TCP: two
+    ranks of one device are never put into a communicator (that only exercises RCCL's error and
+    abort path, which crashed a peer on the driver's box in round 4).  A GPU donor answers an ``R`` request by sending the snapshot device-to-
     device over a 2-rank RCCL communicator on its own HIP stream (no host staging at all); otherwise
     the tensors are streamed over TCP — GPU tensors through two pinned host chunks (the D2H copy of
     chunk i+1 overlaps the socket send of chunk i), CPU tensors straight from their storage (no
@@ -75,12 +78,14 @@ class StateServer:
     the state on the device under the optimizer's step lock and the transfer runs outside it."""
 
     def __init__(self, get_state: Callable[[], Tuple[Dict, List[torch.Tensor]]], listen_on: str = "0.0.0.0:0",
-                 device: Optional[torch.device] = None, transfer_timeout: float = 120.0):
+                 device: Optional[torch.device] = None, transfer_timeout: float = 120.0,
+                 gpu_id: Optional[str] = None):
         host, port = parse_endpoint(listen_on.replace("*", "0"))
         bind = "0.0.0.0" if listen_on.startswith(("0.0.0.0", "[::]", "*")) else host
         self.get_state = get_state
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.transfer_timeout = transfer_timeout
+        self.gpu_id = gpu_id
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         self.sock.bind((bind, port))
@@ -108,12 +113,17 @@ class StateServer:
                 req = _recv_exact(conn, 6)
                 if req[:5] != b"STATE":
                     return
-                uid = _recv_exact(conn, 128) if req[5:6] == b"R" else None
+                uid, their_gpu = None, None
+                if req[5:6] == b"R":
+                    uid = _recv_exact(conn, 128)
+                    (n,) = struct.unpack("<H", _recv_exact(conn, 2))
+                    their_gpu = _recv_exact(conn, n).decode() if n else None
                 if self.device.type == "cuda":
                     torch.cuda.set_device(self.device)
                 meta, tensors = self.get_state()
-                rccl = uid is not None and _comm.rccl_available(self.device) and all(t.device == self.device
-                                                                                     for t in tensors)
+                same_device = their_gpu is not None and their_gpu == self.gpu_id
+                rccl = (uid is not None and not same_device and _comm.rccl_available(self.device)
+                        and all(t.device == self.device for t in tensors))
                 descs = [(str(t.dtype).replace("torch.", ""), list(t.shape)) for t in tensors]
                 header = msgpack.packb({"metadata": meta, "tensors": descs, "mode": "R" if rccl else "T"},
                                        use_bin_type=True)
@@ -188,17 +198,22 @@ class StateServer:
 
 
 def download_state(endpoint: str, timeout: float = 60.0, device: Optional[torch.device] = None,
-                   allow_rccl: bool = True):
+                   allow_rccl: bool = True, gpu_id: Optional[str] = None):
     """(metadata, tensors) from a state server.  A GPU requester asks for the RCCL transfer (the
-    tensors arrive on ``device``); otherwise the tensors arrive over TCP into host memory.  The
-    metadata carries the transfer mode under ``_mode`` ("R" or "T")."""
+    tensors arrive on ``device``) and names its GPU (``gpu_id``: a donor on the same device answers
+    over TCP); otherwise the tensors arrive over TCP into host memory.  The metadata carries the
+    transfer mode under ``_mode`` ("R" or "T")."""
     host, port = parse_endpoint(endpoint)
     device = torch.device(device) if device is not None else torch.device("cpu")
     uid = RcclGroupComm.new_unique_id() if allow_rccl and _comm.rccl_available(device) else None
     deadline = time.monotonic() + timeout
     with socket.create_connection((host, port), timeout=timeout) as s:
         s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-        s.sendall(b"STATER" + uid if uid is not None else b"STATET")
+        if uid is not None:
+            g = (gpu_id or "").encode()
+            s.sendall(b"STATER" + uid + struct.pack("<H", len(g)) + g)
+        else:
+            s.sendall(b"STATET")
         (hl,) = struct.unpack("<Q", _recv_exact(s, 8))
         header = msgpack.unpackb(_recv_exact(s, hl), raw=False)
         descs = [(_DT[dt], shape) for dt, shape in header["tensors"]]
@@ -248,21 +263,36 @@ class DecentralizedAverager:
                                         host=self.host)
         self.lock_averaged_tensors = threading.RLock()
         self.last_group: Optional[Dict] = None
-        self.state_server = StateServer(self._serve_state, listen_on.replace("[::]", "0.0.0.0"), device=self.device) \
-            if self.allow_state_sharing else None
+        self.state_server = StateServer(self._serve_state, listen_on.replace("[::]", "0.0.0.0"), device=self.device,
+                                        gpu_id=self.comms.gpu_id) if self.allow_state_sharing else None
         self.local_step_for_state = 0
         self.last_download: Optional[Dict] = None
         self.emulate_transfer_delay = emulate_transfer_delay
 
     # ------------------------------------------------------------------ averaging
-    # An RCCL member's link in a mixed group (GPU trainers + CPU peers) for load balancing: one xGMI
-    # link, ~153 GB/s, in the Mbps unit of the reference's --bandwidth.  The CPU member's declared
-    # bandwidth stays as given, so the LP hands it a part in proportion and the GPU members stage
-    # only that share through host memory.
+    # Load balancing in a mixed group (GPU trainers on RCCL + CPU peers on gloo), in the Mbps unit of
+    # the reference's --bandwidth: an RCCL member's link is one xGMI link (~153 GB/s); a CPU member
+    # keeps its declared --bandwidth, or DEFAULT_HOST_MBPS (a 10 Gb/s host link) when it declared
+    # none.  The LP minimises the round's slowest member, so a CPU member gets a part only when its
+    # link is fast enough not to become that member: with xGMI peers that means a CPU auxiliary
+    # needs a declared --bandwidth comparable to xGMI, otherwise it owns no part (it then neither
+    # sends nor receives — it cannot slow the GPU members down).
     XGMI_MBPS = 1.2e6
+    DEFAULT_HOST_MBPS = 1.0e4
+
+    @classmethod
+    def group_bandwidths(cls, infos: Sequence[Dict], pids: Sequence[bytes], on_rccl) -> List[Optional[float]]:
+        """Per-member throughputs for the LP (``on_rccl``: peer ids on the RCCL side of a mixed
+        group, None for a homogeneous group, whose undeclared members get the mean of the declared
+        ones — all equal when nobody declared)."""
+        bws = [i.get("bandwidth") for i in infos]
+        if on_rccl is None:
+            return bws
+        return [(cls.XGMI_MBPS if (b is None or b > 0) else 0.0) if p in on_rccl
+                else (cls.DEFAULT_HOST_MBPS if b is None else b) for b, p in zip(bws, pids)]
 
     def _info(self, weight: Optional[float], gather: Optional[Dict[str, Any]]) -> Dict:
-        bw = 0.0 if self.client_mode else (self.throughput if self.throughput is not None else 1.0)
+        bw = 0.0 if self.client_mode else self.throughput  # None: not declared
         info = {"bandwidth": bw, "weight": weight, "aux": self.auxiliary, "gather": gather or {}}
         info.update(self.comms.announce())
         return info
@@ -294,7 +324,7 @@ class DecentralizedAverager:
         threading.Thread(target=run, daemon=True, name="prejoin").start()
         return fut
 
-    def step(self, weight: float = 1.0, timeout: Optional[float] = None, expected_group_size: int = 0,
+    def step(self, weight=1.0, timeout: Optional[float] = None, expected_group_size: int = 0,
              gather: Optional[Dict[str, Any]] = None, tensors: Optional[Sequence[torch.Tensor]] = None,
              sources: Optional[Sequence[torch.Tensor]] = None, key_suffix: str = "",
              prejoined: Optional[Future] = None) -> Optional[Dict]:
@@ -305,7 +335,8 @@ class DecentralizedAverager:
         (so a delayed parameter round never mixes with a gradient round), ``prejoined`` is a
         ``prejoin`` future whose group this round uses (a fresh matchmaking if it failed)."""
         tensors = list(tensors) if tensors is not None else self.averaged_tensors
-        weight = 0.0 if self.auxiliary else float(weight)
+        # a device-scalar weight (CollaborativeOptimizer's finite-sample count) travels as is
+        weight = 0.0 if self.auxiliary else (weight if isinstance(weight, torch.Tensor) else float(weight))
         t_wait = time.perf_counter()
         res = None
         if prejoined is not None:
@@ -318,7 +349,8 @@ class DecentralizedAverager:
                 res = None
         if res is None:
             try:
-                res = self._join(self._info(weight, gather), expected_group_size, key_suffix)
+                res = self._join(self._info(weight if not isinstance(weight, torch.Tensor) else None, gather),
+                                 expected_group_size, key_suffix)
             except Exception as e:  # noqa: BLE001
                 logger.warning(f"matchmaking failed: {e}")
                 return None
@@ -331,10 +363,8 @@ class DecentralizedAverager:
         pids = [bytes(m[0]) for m in members]
         my_index = pids.index(self.peer_id)
         V = sum(t.numel() for t in tensors)
-        bws = [i["bandwidth"] for i in infos]
-        if GroupCommunicators.group_backend(members) == "hybrid":
-            on_rccl = set(GroupCommunicators.rccl_members(members))
-            bws = [(self.XGMI_MBPS if b > 0 else 0.0) if p in on_rccl else b for b, p in zip(bws, pids)]
+        hybrid = GroupCommunicators.group_backend(members) == "hybrid"
+        bws = self.group_bandwidths(infos, pids, set(GroupCommunicators.rccl_members(members)) if hybrid else None)
         parts = load_balance_peers(V, bws, min_size=0)
         if not any(not i["aux"] for i in infos):
             return None
@@ -357,7 +387,7 @@ class DecentralizedAverager:
                 self.comms.invalidate(comm)
             return None
         bw = bws[my_index]
-        if self.emulate_transfer_delay and bw > 0:  # emulate the volunteer's link (AWS_runner wondershaper caps)
+        if self.emulate_transfer_delay and bw is not None and bw > 0:  # emulate the volunteer's link (AWS_runner wondershaper caps)
             from ..emulation.heterogeneity import emulated_transfer_seconds
 
             wire_bytes = torch.empty(0, dtype=WIRE_DTYPES[self.compression]).element_size()
@@ -386,7 +416,7 @@ class DecentralizedAverager:
             return None
         self.local_step_for_state = step
         return self.dht.store(f"{self.prefix}_state_sharing",
-                              {"endpoint": self.state_server.endpoint, "step": int(step)},
+                              {"endpoint": self.state_server.endpoint, "step": int(step), "gpu": self.comms.gpu_id},
                               get_dht_time() + self.metadata_expiration, subkey=self.peer_id, return_future=True)
 
     def load_state_from_peers(self, timeout: float = 15.0, min_step: int = 0):
@@ -402,12 +432,17 @@ class DecentralizedAverager:
                 continue
             if int(v.value.get("step", 0)) < min_step:
                 continue
-            donors.append((v.value.get("step", 0), v.value["endpoint"]))
-        for step, ep in sorted(donors, reverse=True):
-            for rccl in ((True, False) if _comm.rccl_available(self.device) else (False,)):
+            donors.append((v.value.get("step", 0), v.value["endpoint"], v.value.get("gpu")))
+        mine = self.comms.gpu_id
+        for step, ep, gpu in sorted(donors, key=lambda d: (d[0], d[1]), reverse=True):
+            # RCCL only between two different devices (one rank per device): a donor on our own GPU
+            # — peers sharing a device in a protocol emulation — streams over TCP straight away
+            rccl_ok = _comm.rccl_available(self.device) and not (gpu is not None and gpu == mine)
+            for rccl in ((True, False) if rccl_ok else (False,)):
                 try:
                     t0 = time.perf_counter()
-                    meta, tensors = download_state(ep, timeout=timeout, device=self.device, allow_rccl=rccl)
+                    meta, tensors = download_state(ep, timeout=timeout, device=self.device, allow_rccl=rccl,
+                                                   gpu_id=mine)
                     self.last_download = {"endpoint": ep, "mode": meta.pop("_mode", "T"),
                                           "bytes": sum(t.numel() * t.element_size() for t in tensors),
                                           "seconds": time.perf_counter() - t0}

@@ -3,10 +3,16 @@
 Each member i of a group with throughput b_i (the reference's ``--bandwidth``; 0 for client-mode
 peers that cannot aggregate) receives a fraction w_i of the averaged vector to reduce.  Member i
 moves (1 - w_i) V as a sender plus (N - 1) w_i V as an aggregator per direction, so the round time
-is max_i (1 + (N - 2) w_i) / b_i.  We solve  min xi  s.t.  xi >= (1 + (N-2) w_i) / b_i,
-sum w = 1, w >= 0, w_i = 0 where b_i = 0  (a <=9-variable LP; scipy HiGHS), drop shares below
-``min_size`` elements and round to integers with Hagenbach-Bischoff (largest remainder) so the
-parts sum exactly to the vector size.
+is max_i (1 + (N - 2) w_i) / b_i.  hivemind minimises that max with an LP.  The LP is degenerate
+whenever one member is slow enough to be the bottleneck at w = 0 (a CPU peer next to xGMI peers:
+every split among the others is optimal, and a solver returns a vertex — one member takes the
+whole vector).  So the min-max is solved by water-filling instead, which picks the balanced
+optimum: a level T with w_i = max(0, (T b_i - 1) / (N - 2)) and sum w = 1 (bisection on T).
+Members whose link is too slow to finish a share within T get none, every other member finishes
+exactly at T, and the round's max time equals the LP optimum.  With N <= 2 the time does not depend
+on w; parts are then proportional to b.  Shares below ``min_size`` elements are dropped and the
+rest rounded to integers with Hagenbach-Bischoff (largest remainder) so the parts sum exactly to
+the vector size.
 """
 from __future__ import annotations
 
@@ -27,35 +33,32 @@ def optimize_parts_lp(vector_size: int, throughputs: Sequence[Optional[float]], 
         w = (b > 0).astype(np.float64) if (b > 0).any() else np.full(n, 1.0 / n)
         return hagenbach_bischoff(vector_size, w / w.sum())
     active = b > 0
-    if np.allclose(b[active], b[active][0]) and active.all():
-        w = np.full(n, 1.0 / n)
+    if n <= 2:
+        w = np.where(active, b, 0.0)
     else:
-        from scipy.optimize import linprog
-
-        # variables: w_0..w_{n-1}, xi ; minimise xi
-        c = np.zeros(n + 1)
-        c[-1] = 1.0
-        A_ub, b_ub = [], []
-        for i in range(n):
-            if not active[i]:
-                continue
-            row = np.zeros(n + 1)
-            row[i] = (n - 2) / b[i]
-            row[-1] = -1.0
-            A_ub.append(row)
-            b_ub.append(-1.0 / b[i])
-        A_eq = np.zeros((1, n + 1))
-        A_eq[0, :n] = 1.0
-        bounds = [(0.0, None) if active[i] else (0.0, 0.0) for i in range(n)] + [(0.0, None)]
-        res = linprog(c, A_ub=np.asarray(A_ub), b_ub=np.asarray(b_ub), A_eq=A_eq, b_eq=[1.0], bounds=bounds,
-                      method="highs")
-        w = res.x[:n] if res.success else active / active.sum()
+        w = _water_fill(np.where(active, b, 0.0), n - 2)
     w = np.clip(w, 0.0, None)
     if min_size > 0:
         small = w * vector_size < min_size
         if (~small).any():
             w[small] = 0.0
     return hagenbach_bischoff(vector_size, w / w.sum())
+
+
+def _water_fill(b: np.ndarray, k: int) -> np.ndarray:
+    """w_i = max(0, (T b_i - 1) / k) with sum w = 1 (b_i = 0: w_i = 0)."""
+    def total(t):
+        return np.clip((t * b - 1.0) / k, 0.0, None).sum()
+
+    lo, hi = 0.0, (1.0 + k) / b[b > 0].min()  # at hi every active member holds >= 1 share
+    for _ in range(200):
+        mid = 0.5 * (lo + hi)
+        if total(mid) < 1.0:
+            lo = mid
+        else:
+            hi = mid
+    w = np.clip((hi * b - 1.0) / k, 0.0, None)
+    return w / w.sum()
 
 
 def hagenbach_bischoff(total: int, fractions: np.ndarray) -> np.ndarray:

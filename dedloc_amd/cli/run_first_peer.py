@@ -5,7 +5,10 @@
 * every ``refresh_period`` seconds reads ``{prefix}_metrics`` and, when the collaboration's step
   advances, aggregates loss (sum loss / sum mini_steps), alive peers, samples and
   **performance = sum of the peers' samples_per_second** (the reference's whole-collaboration
-  throughput, BASELINE metric) — logged to stdout / a JSONL file (wandb is optional: no network);
+  throughput, BASELINE metric) — logged to stdout / a JSONL file (wandb is optional: no network).
+  A record is also written when the number of alive peers changes within a step (a peer joining
+  or leaving; the reference logs on step changes only, so a peer whose first report lands after
+  the collaboration's last step change never appeared in its log);
 * every ``save_checkpoint_step_interval`` steps pulls the latest state from the peers and, when
   ``repo_path`` is set and ``upload_interval`` has elapsed, writes the HF checkpoint
   (config.json + pytorch_model.bin) + ``optimizer_state.pt`` there and commits it if the directory
@@ -112,7 +115,7 @@ def main(argv=None):
     print(f"Running DHT root at {coordinator_args.address}:{dht.port}", flush=True)
     if coordinator_args.wandb_project is not None:
         logger.warning("wandb logging requested but there is no network; metrics go to stdout/metrics_file")
-    current_step = 0
+    current_step, alive = 0, 0
     checkpoint_handler = CheckpointHandler(coordinator_args, collab_optimizer_args, averager_args, dht,
                                            local_public_key)
     t0 = time.time()
@@ -121,14 +124,15 @@ def main(argv=None):
             metrics_dict = dht.get(experiment_prefix + "_metrics", latest=True)
             if metrics_dict is not None and isinstance(metrics_dict.value, dict) and metrics_dict.value:
                 agg = aggregate(metrics_dict.value)
-                if agg["step"] != current_step:
+                step_changed = agg["step"] != current_step
+                if step_changed or agg["alive peers"] != alive:
                     logger.info(f"Got metrics from {agg['alive peers']} peers")
-                    current_step = agg["step"]
+                    current_step, alive = agg["step"], agg["alive peers"]
                     rec = dict(agg, time=time.time())
                     if coordinator_args.metrics_file:
                         with open(coordinator_args.metrics_file, "a") as f:
                             f.write(json.dumps(rec) + "\n")
-                    if checkpoint_handler.is_time_to_save_state(current_step):
+                    if step_changed and checkpoint_handler.is_time_to_save_state(current_step):
                         checkpoint_handler.save_state(current_step)
                         if checkpoint_handler.is_time_to_upload():
                             checkpoint_handler.upload_checkpoint(agg["loss"])

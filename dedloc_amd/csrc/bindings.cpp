@@ -186,7 +186,8 @@ void grad_norm_clip(at::Tensor g, double max_norm, at::Tensor part, at::Tensor o
   expect(part, at::kFloat, "part");
   expect(out, at::kFloat, "out");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "grad buffer must be 16-byte aligned");
-  check(dl_grad_norm_clip(f32(g), g.numel(), (float)max_norm, f32(part), (int)part.numel(), f32(out), cur_stream(g)),
+  check(dl_grad_norm_clip(f32(g), g.numel(), (float)max_norm, f32(part), (int)part.numel(), f32(out), (int)out.numel(),
+                          cur_stream(g)),
         "grad_norm_clip");
 }
 
@@ -212,14 +213,21 @@ void add_slabs_zero_(at::Tensor out, at::Tensor slabs) {
         "add_slabs_zero_");
 }
 
-void axpby(at::Tensor y, const at::Tensor& x, double a, double b, const c10::optional<at::Tensor>& flag) {
+void axpby(at::Tensor y, const at::Tensor& x, double a, double b, const c10::optional<at::Tensor>& flag,
+           const c10::optional<at::Tensor>& bdiv) {
   expect(y, at::kFloat, "y");
   expect(x, at::kFloat, "x");
   TORCH_CHECK(x.numel() == y.numel(), "axpby size mismatch");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 16 == 0,
               "axpby needs 16-byte aligned buffers");
   const float* fp = flag.has_value() ? f32(*flag) : nullptr;
-  dl_axpby(f32(y), f32(x), y.numel(), (float)a, (float)b, fp, cur_stream(y));
+  const float* dp = nullptr;
+  if (bdiv.has_value()) {
+    expect(*bdiv, at::kFloat, "bdiv");
+    TORCH_CHECK(bdiv->device() == y.device(), "axpby: bdiv must live with y");
+    dp = f32(*bdiv);
+  }
+  dl_axpby(f32(y), f32(x), y.numel(), (float)a, (float)b, fp, dp, cur_stream(y));
 }
 
 // ------------------------------------------------------------------ averaging data plane
@@ -721,6 +729,47 @@ at::Tensor gemm_dgelu(const at::Tensor& dy, const at::Tensor& w, const at::Tenso
   gemm_store(A, B, dy, w, bf(dg), dg.size(1), nullptr, nullptr, 0, cur_stream(dy));
   check(dl_gelu_bwd_colsum(cbf(dg), cbf(F), bf(C), f32(dbias), (int)dg.size(0), (int)dg.size(1), cur_stream(dg)),
         "gelu_bwd");
+  return C;
+}
+
+// FFN-up storing the DERIVATIVE for the backward: G = gelu_new(h), D = gelu_new'(h), h = bf16(x W^T + b)
+// (gemm8 EPI_GELUD; the backward then multiplies by D instead of evaluating gelu_new' — gemm_dmul)
+std::tuple<at::Tensor, at::Tensor> gemm_gelu_d(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias,
+                                               bool trans_w) {
+  expect_operands(x, w);
+  const int64_t nout = trans_w ? w.size(1) : w.size(0);
+  auto D = at::empty({x.size(0), nout}, x.options());
+  auto G = at::empty_like(D);
+  const at::Tensor bias32 = f32_bias(bias, nout);
+  if (use_gemm8() && dl_gemm8(0, trans_w ? 1 : 0, 6, cbf(x), x.stride(0), cbf(w), w.stride(0), (int)x.size(0),
+                              (int)nout, (int)x.size(1), bf(G), G.size(1), nullptr, 0, 0, 0, f32(bias32), nullptr, 0,
+                              bf(D), D.size(1), nullptr, 1, cur_stream(x)) == 0)
+    return {D, G};
+  auto H = at::empty_like(D);
+  const Mat A = a_view(x, false), B = b_view(w, !trans_w);
+  gemm_store(A, B, x, w, bf(H), H.size(1), f32(bias32), nullptr, 0, cur_stream(x));
+  check(dl_gelu_fwd_d(cbf(H), bf(G), bf(D), H.numel(), cur_stream(H)), "gelu_fwd_d");
+  return {D, G};
+}
+
+// FFN dgrad against a stored derivative: C = bf16(dy W) * D, dbias += colsum(C) (gemm8 EPI_DMUL)
+at::Tensor gemm_dmul(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& D, at::Tensor dbias, bool trans_w) {
+  expect_operands(dy, w);
+  expect(D, at::kBFloat16, "D");
+  expect(dbias, at::kFloat, "dbias");
+  const int64_t nout = trans_w ? w.size(0) : w.size(1);
+  TORCH_CHECK(dbias.is_contiguous() && dbias.numel() == nout, "gemm_dmul: dbias must hold one fp32 per output column");
+  TORCH_CHECK(D.dim() == 2 && D.size(0) == dy.size(0) && D.size(1) == nout, "gemm_dmul: D shape");
+  auto C = at::empty({dy.size(0), nout}, dy.options());
+  if (use_gemm8() && dl_gemm8(0, trans_w ? 0 : 1, 7, cbf(dy), dy.stride(0), cbf(w), w.stride(0), (int)dy.size(0),
+                              (int)nout, (int)dy.size(1), bf(C), C.size(1), nullptr, 0, 0, 0, nullptr, cbf(D),
+                              D.size(1), nullptr, 0, f32(dbias), 1, cur_stream(dy)) == 0)
+    return C;
+  auto dg = at::empty_like(C);
+  const Mat A = a_view(dy, false), B = b_view(w, trans_w);
+  gemm_store(A, B, dy, w, bf(dg), dg.size(1), nullptr, nullptr, 0, cur_stream(dy));
+  check(dl_mul_colsum(cbf(dg), cbf(D), bf(C), f32(dbias), (int)dg.size(0), (int)dg.size(1), cur_stream(dg)),
+        "mul_colsum");
   return C;
 }
 
@@ -1449,6 +1498,8 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("gemm_acc_f32_shared", &gemm_acc_f32_shared);
   m.impl("gemm_gelu", &gemm_gelu);
   m.impl("gemm_dgelu", &gemm_dgelu);
+  m.impl("gemm_gelu_d", &gemm_gelu_d);
+  m.impl("gemm_dmul", &gemm_dmul);
 }
 
 // a tiny C entry point so that the loader can verify the library really is the gfx950 build

@@ -127,6 +127,18 @@ __device__ __forceinline__ float gelu_tanh_grad_sig(float x) {
   return fmaf(x * du2, s - s * s, s);
 }
 
+// gelu_new and gelu_new' of one value sharing the exp2 / rcp (the FFN-up epilogue that stores the
+// derivative for the backward instead of the pre-activation)
+__device__ __forceinline__ void gelu_and_grad_sig(float x, float& g, float& d) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = k0 * x * fmaf(k1, x2, 1.f);
+  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
+  const float du2 = (2.f * k0) * fmaf(3.f * k1, x2, 1.f);
+  g = x * s;
+  d = fmaf(x * du2, s - s * s, s);
+}
+
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, T1):
 // consecutive logical tiles land on the same XCD so neighbouring tiles share that XCD's L2.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

@@ -19,6 +19,9 @@ int dl_layernorm_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, cons
 int dl_gelu_fwd(const bf16_t* h, bf16_t* y, size_t n, hipStream_t st);
 int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStream_t st);
 int dl_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* h, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st);
+// y = gelu_new(h), d = gelu_new'(h); dh = dy * d with dbias += colsum(dh)
+int dl_gelu_fwd_d(const bf16_t* h, bf16_t* y, bf16_t* d, size_t n, hipStream_t st);
+int dl_mul_colsum(const bf16_t* dy, const bf16_t* d, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st);
 int dl_tanh_fwd(const bf16_t* x, bf16_t* y, size_t n, hipStream_t st);
 int dl_tanh_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, size_t n, hipStream_t st);
 int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hipStream_t st);
@@ -35,8 +38,12 @@ int dl_larc_sgd_step(float* p, const float* g, float* buf, const int* chunk_tens
                      const int* chunk_len, int nchunks, const float* tensor_wd, float* norms, int ntensors, float lr,
                      float momentum, float trust_coef, float eps, int clip, int first_step, float grad_scale,
                      hipStream_t st);
-int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, hipStream_t st);
-int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, hipStream_t st);
+// out[0] = ||x||, out[1] = finite flag, out[2] (if nout > 2) = 1 - finite; clips x to max_norm if > 0
+int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, int nout,
+                      hipStream_t st);
+// y = a*y + (b / max(1, *bdiv))*x; skipped when *flag == 0; bdiv/flag may be null
+int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, const float* bdiv,
+             hipStream_t st);
 // x *= s[0] in place (bf16; a device scalar, no pass at all when it is exactly 1)
 int dl_scale_by(bf16_t* x, size_t n, const float* s, hipStream_t st);
 int dl_sum_slabs(float* out, const float* slabs, int s, size_t n, hipStream_t st);

@@ -51,8 +51,15 @@ __global__ __launch_bounds__(256) void reduce_delta_kernel(const void* __restric
                                                            void* __restrict__ deltas, size_t n) {
   float wsum = 0.f;
   for (int k = 0; k < nparts; ++k) wsum += weights[k];
-  const float inv = wsum > 0.f ? 1.f / wsum : 0.f;
+  // no weight at all (every contributor's micro-steps were dropped as non-finite): the round is a
+  // no-op — zero deltas, every member keeps its own tensor — instead of adopting member 0's values
+  const bool none = !(wsum > 0.f);
+  const float inv = none ? 0.f : 1.f / wsum;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if (none) {
+      for (int k = 0; k < nparts; ++k) store_any(deltas, (size_t)k * part_stride + i, 0.f, DT);
+      continue;
+    }
     // avg = v_0 + sum_k w_k (v_k - v_0) / sum_k w_k: identical contributions give exactly v_0 (zero
     // deltas, the fp32 masters untouched) and the differences keep the sum well conditioned
     float v[16];

@@ -44,6 +44,19 @@ __global__ __launch_bounds__(256) void gelu_fwd_v2_kernel(const bf16_t* __restri
 }
 
 
+// y = gelu_new(h), d = gelu_new'(h) (the unfused form of gemm8's EPI_GELUD)
+__global__ __launch_bounds__(256) void gelu_fwd_d_kernel(const bf16_t* __restrict__ h, bf16_t* __restrict__ y,
+                                                         bf16_t* __restrict__ d, size_t nvec) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float v[8], g[8], dv[8];
+    load_bf16<8>(h + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gelu_and_grad_sig(v[j], g[j], dv[j]);
+    store_bf16<8>(y + i * 8, g);
+    store_bf16<8>(d + i * 8, dv);
+  }
+}
+
 __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
                                                        bf16_t* __restrict__ dh, size_t nvec) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
@@ -62,7 +75,8 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict_
 // computes and stores them, so no row's loads queue behind another row's stores in the in-order
 // vmcnt (the v1 row loop waits for its own previous stores every iteration).  Block = 512 columns
 // x 64 rows; the 8 wave partials meet in LDS, one fp32 atomic per column per block.
-template <bool GELU>
+// GELU = 1: dh = x * gelu_new'(h); GELU = 2: dh = x * h (h already gelu_new', EPI_GELUD's output)
+template <int GELU>
 __global__ __launch_bounds__(512) void colsum_rows_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ h,
                                                           bf16_t* __restrict__ dh, float* __restrict__ out, int rows,
                                                           int N) {
@@ -91,7 +105,7 @@ __global__ __launch_bounds__(512) void colsum_rows_kernel(const bf16_t* __restri
         float v[8];
         load_bf16<8>(reinterpret_cast<const bf16_t*>(&hr[u]), v);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * gelu_tanh_grad_sig(v[j])));
+        for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j] * (GELU == 2 ? v[j] : gelu_tanh_grad_sig(v[j]))));
         store_bf16<8>(dh + (size_t)(rbase + u) * N + c0, g);
       }
 #pragma unroll
@@ -214,7 +228,20 @@ int dl_gelu_bwd(const bf16_t* dy, const bf16_t* h, bf16_t* dh, size_t n, hipStre
 int dl_gelu_bwd_colsum(const bf16_t* dy, const bf16_t* h, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st) {
   if (N % 8) return -1;
   dim3 grid((N + 511) / 512, (rows + 63) / 64);
-  colsum_rows_kernel<true><<<grid, 512, 0, st>>>(dy, h, dh, dbias, rows, N);
+  colsum_rows_kernel<1><<<grid, 512, 0, st>>>(dy, h, dh, dbias, rows, N);
+  return 0;
+}
+
+int dl_mul_colsum(const bf16_t* dy, const bf16_t* d, bf16_t* dh, float* dbias, int rows, int N, hipStream_t st) {
+  if (N % 8) return -1;
+  dim3 grid((N + 511) / 512, (rows + 63) / 64);
+  colsum_rows_kernel<2><<<grid, 512, 0, st>>>(dy, d, dh, dbias, rows, N);
+  return 0;
+}
+
+int dl_gelu_fwd_d(const bf16_t* h, bf16_t* y, bf16_t* d, size_t n, hipStream_t st) {
+  if (n % 8) return -1;
+  gelu_fwd_d_kernel<<<grid_for(n / 8, 256), 256, 0, st>>>(h, y, d, n / 8);
   return 0;
 }
 
@@ -236,7 +263,7 @@ int dl_colsum_bf16(const bf16_t* x, float* part, int rows, int N, int nparts, hi
     return 0;
   }
   dim3 grid((N + 511) / 512, (rows + 63) / 64);
-  colsum_rows_kernel<false><<<grid, 512, 0, st>>>(x, nullptr, nullptr, part, rows, N);
+  colsum_rows_kernel<0><<<grid, 512, 0, st>>>(x, nullptr, nullptr, part, rows, N);
   (void)rpb;
   return 0;
 }

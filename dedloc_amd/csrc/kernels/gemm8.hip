@@ -34,7 +34,10 @@
 // Epilogues (staged through LDS as fp32, 64 rows per round, written as 16-B row chunks):
 //   EPI_STORE  C = acc (+ bias[n]) (+ R[m,n])                                 bf16
 //   EPI_GELU   H = bf16(acc + bias); C = gelu_new(H)                          bf16 x2
+//   EPI_GELUD  h = bf16(acc + bias); C = gelu_new(h), H = gelu_new'(h)        bf16 x2
 //   EPI_DGELU  C = bf16(acc) * gelu_new'(R[m,n]); dbias[n] += sum_m C         bf16 (+ fp32 atomics)
+//   EPI_DMUL   C = bf16(acc) * R[m,n] (R = gelu_new' stored by EPI_GELUD);   bf16 (+ fp32 atomics)
+//              dbias[n] += sum_m C — the FFN backward with no transcendental in its epilogue
 //   EPI_F32    Cf[z][m,n] = acc  or  += acc (reduction split z)                fp32
 //   EPI_STATS  EPI_STORE, plus per-column sum and sum of squares of the stored bf16 values into
 //              stats[g][0..N) / stats[g][N..2N) (fp32 atomics), g = m / stat_rows: the batch
@@ -59,7 +62,8 @@ typedef short s4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4_t lds_s4;
 typedef __attribute__((address_space(3))) void lds_void;
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_STATS = 4, EPI_BNBWD = 5 };
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_F32 = 3, EPI_STATS = 4, EPI_BNBWD = 5, EPI_GELUD = 6,
+       EPI_DMUL = 7 };
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
 constexpr int HALF = 16384;     // one half-tile image
@@ -290,12 +294,6 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     }                                                                                               \
   } while (0)
 
-#ifdef GEMM8_PROBE_DESYNC  // measurement build only: offset the first wave of workgroups in time
-  if (blockIdx.x < 256) {
-    const int d = ((blockIdx.x >> 3) & 3) * GEMM8_PROBE_DESYNC;
-    for (int i = 0; i < d; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
   // prologue: tile 0 and the first two half-tiles (A0, B1) of tile 1
   DL_STAGE(0, 0); DL_STAGE(0, 1); DL_STAGE(0, 2); DL_STAGE(0, 3);
   if (nk > 1) {
@@ -437,21 +435,6 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: every wave passes the same barriers
   __builtin_amdgcn_s_barrier();               // all fragment reads done before the epilogue reuses LDS
 
-#ifdef GEMM8_PROBE_NO_EPILOGUE  // measurement build only: keep the accumulators live, write nothing
-  if (p.M < 0) {
-    float z = 0.f;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-          for (int d = 0; d < 2; ++d) z += acc[a][b][c][d][0] + acc[a][b][c][d][3];
-    p.Cf[threadIdx.x] = z;
-  }
-  return;
-#endif
   // ---------------------------------------------------------------- epilogue
   // Each wave stages 64 x 64 fp32 per round (quadrant row qm) in its own 16 KiB LDS region:
   // row r at r * 256 B, 16-B chunk q of it at q ^ (r & 1) (conflict-free row reads).
@@ -463,7 +446,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       bias_v[qn][ni] = 0.f;
-      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_STATS)
+      if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_GELUD || EPI == EPI_STATS)
         if (p.bias) bias_v[qn][ni] = p.bias[n0 + colperm<BKO>(wn * 64 + qn * 32 + ni * 16 + ccol)];
     }
   float colsum[8], colsq[8];
@@ -477,8 +460,8 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   // its passes, and the next half's row j right after pass j consumed this half's — ahead of that
   // pass's store.  Loaded inside each pass instead, every pass waited (vmcnt(0)) for its load's full
   // HBM latency and, the counter being in issue order, for every store before it.
-  const bool has_r =
-      EPI == EPI_DGELU || ((EPI == EPI_STORE || EPI == EPI_STATS || EPI == EPI_BNBWD) && p.R != nullptr);
+  const bool has_r = EPI == EPI_DGELU || EPI == EPI_DMUL ||
+                     ((EPI == EPI_STORE || EPI == EPI_STATS || EPI == EPI_BNBWD) && p.R != nullptr);
   // EPI_BNBWD: this lane's eight columns of the tile's statistics group
   float bmu[8], brs[8], bsc[8], bsh[8];
   if constexpr (EPI == EPI_BNBWD) {
@@ -529,11 +512,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
         unpack8_bf16(rbuf[pass], rv);
         if (qm == 0) rbuf[pass] = rrow(1, pass);
       }
-#ifdef GEMM8_PROBE_NO_STORE  // measurement build only (bench/gemm8_probe.hip): skip the output writes
-      if (gm < 0) {
-#else
       if (gm < p.M) {
-#endif
         if constexpr (EPI == EPI_STORE) {
           if (has_r) {
 #pragma unroll
@@ -577,10 +556,23 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) h[j] = gelu_tanh_sig(h[j]);
           store8_bf16(p.C + (long)gm * p.ldc + gn, h, p.nt);
+        } else if constexpr (EPI == EPI_GELUD) {
+          float g[8], d[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gelu_and_grad_sig(round_bf16(v[j]), g[j], d[j]);
+          store8_bf16(p.H + (long)gm * p.ldh + gn, d, p.nt);
+          store8_bf16(p.C + (long)gm * p.ldc + gn, g, p.nt);
         } else if constexpr (EPI == EPI_DGELU) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(rv[j]));
+            colsum[j] += v[j];
+          }
+          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
+        } else if constexpr (EPI == EPI_DMUL) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v[j] = round_bf16(round_bf16(v[j]) * rv[j]);
             colsum[j] += v[j];
           }
           store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
@@ -598,7 +590,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       }
     }
   }
-  if constexpr (EPI == EPI_DGELU) {
+  if constexpr (EPI == EPI_DGELU || EPI == EPI_DMUL) {
     if (p.dbias) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -656,7 +648,7 @@ template <bool AKO, bool BKO, int EPI>
 int launch8(const Args& a, int splits, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * (a.N / BN);
   const dim3 grid(tiles * splits);
-  if constexpr (EPI == EPI_GELU) gemm8_kernel<AKO, BKO, EPI, false><<<grid, NT, 0, st>>>(a);
+  if constexpr (EPI == EPI_GELU || EPI == EPI_GELUD) gemm8_kernel<AKO, BKO, EPI, false><<<grid, NT, 0, st>>>(a);
   else gemm8_kernel<AKO, BKO, EPI, true><<<grid, NT, 0, st>>>(a);
   return 0;
 }
@@ -681,8 +673,8 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
   } else {
     if (!C || ldc % 8 || !aligned16(C)) return -1;
     if (R && (ldr % 8 || !aligned16(R))) return -1;
-    if (epi == EPI_GELU && (!H || ldh % 8 || !aligned16(H))) return -1;
-    if (epi == EPI_DGELU && !R) return -1;
+    if ((epi == EPI_GELU || epi == EPI_GELUD) && (!H || ldh % 8 || !aligned16(H))) return -1;
+    if ((epi == EPI_DGELU || epi == EPI_DMUL) && !R) return -1;
     if (splits != 1) return -1;
     // EPI_STATS: every 256-row tile inside one statistics group
     if ((epi == EPI_STATS || epi == EPI_BNBWD) && (!stats || stat_rows < BM || stat_rows % BM || M % stat_rows))
@@ -708,6 +700,10 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
   DL_GEMM8_CASE(0, 1, EPI_GELU)
   DL_GEMM8_CASE(0, 1, EPI_DGELU)
   DL_GEMM8_CASE(0, 0, EPI_DGELU)
+  DL_GEMM8_CASE(0, 0, EPI_GELUD)
+  DL_GEMM8_CASE(0, 1, EPI_GELUD)
+  DL_GEMM8_CASE(0, 1, EPI_DMUL)
+  DL_GEMM8_CASE(0, 0, EPI_DMUL)
   DL_GEMM8_CASE(1, 1, EPI_F32)
   DL_GEMM8_CASE(0, 0, EPI_F32)
   DL_GEMM8_CASE(0, 0, EPI_STATS)

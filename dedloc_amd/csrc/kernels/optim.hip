@@ -144,14 +144,19 @@ __global__ __launch_bounds__(kBlock) void sumsq_kernel(const float* __restrict__
 // Reads the partials, computes the global norm on every block (cheap) and scales x in place by
 // min(1, max_norm / (norm + 1e-6)).  out[0] = norm, out[1] = finite flag (1.0 if finite).
 __global__ __launch_bounds__(kBlock) void clip_kernel(float* __restrict__ x, size_t n, const float* __restrict__ part,
-                                                      int nparts, float max_norm, float* __restrict__ out) {
+                                                      int nparts, float max_norm, float* __restrict__ out,
+                                                      int nout) {
   __shared__ float scratch[16];
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += part[i];
   s = block_sum(s, scratch);
   const float norm = sqrtf(s);
   const bool finite = isfinite(norm);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && out) { out[0] = norm; out[1] = finite ? 1.f : 0.f; }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && out) {
+    out[0] = norm;
+    out[1] = finite ? 1.f : 0.f;
+    if (nout > 2) out[2] = finite ? 0.f : 1.f;  // the "drop this step" flag for axpby(flag=...)
+  }
   if (max_norm <= 0.f || !finite) return;
   const float coef = max_norm / (norm + 1e-6f);
   if (coef >= 1.f) return;
@@ -161,8 +166,10 @@ __global__ __launch_bounds__(kBlock) void clip_kernel(float* __restrict__ x, siz
 // y = a*y + b*x  (fp32).  With `flag` (device scalar, e.g. the finite flag of dl_grad_norm_clip)
 // the update is skipped entirely when *flag == 0, so a non-finite step never reaches y.
 __global__ __launch_bounds__(kBlock) void axpby_kernel(float* __restrict__ y, const float* __restrict__ x, size_t n,
-                                                       float a, float b, const float* __restrict__ flag) {
+                                                       float a, float b, const float* __restrict__ flag,
+                                                       const float* __restrict__ bdiv) {
   if (flag != nullptr && flag[0] == 0.f) return;
+  if (bdiv != nullptr) b /= fmaxf(1.f, bdiv[0]);  // a device-side count (finite micro-steps)
   const size_t nvec = n / 4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
     float4 yv = reinterpret_cast<float4*>(y)[i];
@@ -252,9 +259,11 @@ int dl_larc_sgd_step(float* p, const float* g, float* buf, const int* chunk_tens
   return 0;
 }
 
-int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, hipStream_t st) {
+int dl_grad_norm_clip(float* x, size_t n, float max_norm, float* part, int nparts, float* out, int nout,
+                      hipStream_t st) {
   sumsq_kernel<<<nparts, kBlock, 0, st>>>(x, n, part);
-  clip_kernel<<<grid_for(n), kBlock, 0, st>>>(x, n, part, nparts, max_norm, out);
+  // no clipping: one block publishes the norm and flags
+  clip_kernel<<<max_norm > 0.f ? grid_for(n) : 1, kBlock, 0, st>>>(x, n, part, nparts, max_norm, out, nout);
   return 0;
 }
 
@@ -274,7 +283,8 @@ int dl_scale_by(bf16_t* x, size_t n, const float* s, hipStream_t st) {
   return 0;
 }
 
-int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, hipStream_t st) {
-  axpby_kernel<<<grid_for(n), kBlock, 0, st>>>(y, x, n, a, b, flag);
+int dl_axpby(float* y, const float* x, size_t n, float a, float b, const float* flag, const float* bdiv,
+             hipStream_t st) {
+  axpby_kernel<<<grid_for(n), kBlock, 0, st>>>(y, x, n, a, b, flag, bdiv);
   return 0;
 }

@@ -147,6 +147,10 @@ _DGRAD_WT = True
 # applications and add them into the flat gradient once, at the last backward call
 # (gemm_acc_f32_shared).
 _SHARED_WGRAD = True
+# The FFN-up epilogue stores gelu_new'(h) (bf16) for the backward instead of the pre-activation h:
+# it shares the forward's exp2 / rcp, and the FFN-down data gradient's epilogue becomes one multiply
+# instead of a second sigmoid evaluation per element (gemm_gelu_d / gemm_dmul, gemm8 EPI 6 / 7).
+_GELU_GRAD_IN_FWD = True
 
 
 class _AlbertLayerFn(torch.autograd.Function):
@@ -170,17 +174,19 @@ class _AlbertLayerFn(torch.autograd.Function):
             # tensor and write one (s is the GEMM output itself) — 2 of 4 LN HBM passes removed
             s1 = O.gemm(att, lv["wo"], lv["bo32"], h, False, True, 0)
             h1, _, m1, r1 = O.layernorm_fwd(s1, None, lv["ln1g"], lv["ln1b"], eps)
-            f, g = O.gemm_gelu(h1, lv["w1"], lv["b132"])  # bias + gelu_new fused in the GEMM epilogue
+            # bias + gelu_new fused in the GEMM epilogue; f = gelu_new'(h) (or h itself)
+            f, g = (O.gemm_gelu_d if _GELU_GRAD_IN_FWD else O.gemm_gelu)(h1, lv["w1"], lv["b132"])
             s2 = O.gemm(g, lv["w2"], lv["b232"], h1, False, True, 0)
             out, _, m2, r2 = O.layernorm_fwd(s2, None, lv["ln2g"], lv["ln2b"], eps)
         else:
             a = O.gemm(att, lv["wo"], lv["bo32"], None, False, True, 0)
             h1, s1, m1, r1 = O.layernorm_fwd(a, h, lv["ln1g"], lv["ln1b"], eps)
-            f, g = O.gemm_gelu(h1, lv["w1"], lv["b132"])
+            f, g = (O.gemm_gelu_d if _GELU_GRAD_IN_FWD else O.gemm_gelu)(h1, lv["w1"], lv["b132"])
             f2 = O.gemm(g, lv["w2"], lv["b232"], None, False, True, 0)
             out, s2, m2, r2 = O.layernorm_fwd(f2, h1, lv["ln2g"], lv["ln2b"], eps)
         ctx.save_for_backward(h, qkv, att, lse, s1, m1, r1, h1, f, g, s2, m2, r2)
         ctx.lv, ctx.mask, ctx.H, ctx.S = lv, mask, H, S
+        ctx.gelu_d = _GELU_GRAD_IN_FWD
         return out
 
     @staticmethod
@@ -194,8 +200,9 @@ class _AlbertLayerFn(torch.autograd.Function):
         ds2 = O.layernorm_bwd(dy, s2, lv["ln2g"], m2, r2, lv["gln2g"], lv["gln2b"], True, lv["gb2"])
         _wgrad(O, ds2, g, lv, "gw2")
         wt = "w2t" in lv  # transposed weight copies present (see _DGRAD_WT)
-        # dgrad * gelu'(f) + ffn bias grad, one kernel
-        df = O.gemm_dgelu(ds2, lv["w2t"], f, lv["gb1"], True) if wt else O.gemm_dgelu(ds2, lv["w2"], f, lv["gb1"])
+        # dgrad * gelu'(h) + ffn bias grad, one kernel (f holds gelu'(h) itself, or h)
+        dfn = O.gemm_dmul if ctx.gelu_d else O.gemm_dgelu
+        df = dfn(ds2, lv["w2t"], f, lv["gb1"], True) if wt else dfn(ds2, lv["w2"], f, lv["gb1"])
         _wgrad(O, df, h1, lv, "gw1")
         dh1 = _dgrad(O, df, lv, "w1", ds2)  # residual branch folded in
         del df

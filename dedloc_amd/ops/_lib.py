@@ -29,7 +29,7 @@ _SCHEMAS = [
     "lamb_step(Tensor(a!) p, Tensor g, Tensor(b!) m, Tensor(c!) v, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(d!) norms, float beta1, float beta2, float eps, float step_size, float clamp_value, float grad_scale) -> ()",
     "larc_sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor chunk_tensor, Tensor chunk_start, Tensor chunk_len, Tensor tensor_wd, Tensor(c!) norms, float lr, float momentum, float trust_coef, float eps, bool clip, bool first_step, float grad_scale) -> ()",
     "grad_norm_clip(Tensor(a!) g, float max_norm, Tensor(b!) part, Tensor(c!) out) -> ()",
-    "axpby(Tensor(a!) y, Tensor x, float a, float b, Tensor? flag=None) -> ()",
+    "axpby(Tensor(a!) y, Tensor x, float a, float b, Tensor? flag=None, Tensor? bdiv=None) -> ()",
     "add_slabs_zero_(Tensor(a!) out, Tensor(b!) slabs) -> ()",
     "scale_by_(Tensor(a!) x, Tensor s) -> ()",
     "pack(Tensor src, Tensor(a!) dst, float weight) -> ()",
@@ -74,6 +74,8 @@ _SCHEMAS = [
     "bn_bwd_prep(Tensor(a!) g, Tensor x, Tensor? y, Tensor mean, Tensor rstd, Tensor gamma, Tensor beta, "
     "Tensor(b!) sums, int groups) -> Tensor",
     "gemm_dgelu(Tensor dy, Tensor w, Tensor F, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
+    "gemm_gelu_d(Tensor x, Tensor w, Tensor bias, bool trans_w=False) -> (Tensor, Tensor)",
+    "gemm_dmul(Tensor dy, Tensor w, Tensor D, Tensor(a!) dbias, bool trans_w=False) -> Tensor",
     "conv2d_fwd(Tensor x, Tensor w, int stride, int pad, Tensor? cols=None) -> Tensor",
     "conv2d_fwd_stats(Tensor x, Tensor w, int stride, int pad, Tensor(a!) sums, int groups, Tensor? cols=None) "
     "-> Tensor",
@@ -272,6 +274,8 @@ def _clip_cpu(g, max_norm, part, out):
     finite = bool(torch.isfinite(norm))
     out[0] = norm
     out[1] = 1.0 if finite else 0.0
+    if out.numel() > 2:
+        out[2] = 0.0 if finite else 1.0
     if max_norm > 0 and finite:
         coef = max_norm / (norm.item() + 1e-6)
         if coef < 1:
@@ -290,9 +294,11 @@ def _add_slabs_zero_cpu(out, slabs):
 
 
 @_impl("axpby")
-def _axpby_cpu(y, x, a, b, flag=None):
+def _axpby_cpu(y, x, a, b, flag=None, bdiv=None):
     if flag is not None and float(flag.reshape(-1)[0]) == 0.0:
         return
+    if bdiv is not None:
+        b = b / max(1.0, float(bdiv.reshape(-1)[0]))
     r = (y * a if a != 0 else torch.zeros_like(y)) + (x * b if b != 0 else 0.0)
     y.copy_(r)
 
@@ -318,7 +324,10 @@ def _reduce_delta_cpu(parts, weights, deltas):
     x = parts.float()
     w = weights.float()
     tot = float(w.sum())
-    avg = x[0] + (w[1:, None] * (x[1:] - x[0])).sum(0) * (1.0 / tot if tot > 0 else 0.0)
+    if not tot > 0:  # no weight at all: a no-op round (zero deltas), as the HIP kernel does
+        deltas.zero_()
+        return
+    avg = x[0] + (w[1:, None] * (x[1:] - x[0])).sum(0) * (1.0 / tot)
     d = avg[None, :] - x
     if deltas.dtype == torch.float16:
         d = d.clamp(-65504.0, 65504.0)
@@ -469,6 +478,26 @@ def _gemm_gelu_cpu(x, w, bias, trans_w=False):
 def _gemm_dgelu_cpu(dy, w, F, dbias, trans_w=False):
     dg = _bf(dy.float() @ (w.float().t() if trans_w else w.float()))
     return _gelu_bwd_cpu(dg, F, dbias)
+
+
+def _gelu_grad_tanh(x):
+    k0, k1 = 0.7978845608028654, 0.044715
+    t = torch.tanh(k0 * (x + k1 * x ** 3))
+    return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+
+
+@_impl("gemm_gelu_d")
+def _gemm_gelu_d_cpu(x, w, bias, trans_w=False):
+    h = _bf(x.float() @ (w.float() if trans_w else w.float().t()) + bias.float()).float()
+    return _bf(_gelu_grad_tanh(h)), _bf(_gelu_tanh(h))
+
+
+@_impl("gemm_dmul")
+def _gemm_dmul_cpu(dy, w, D, dbias, trans_w=False):
+    dg = _bf(dy.float() @ (w.float().t() if trans_w else w.float())).float()
+    c = _bf(dg * D.float())
+    dbias.add_(c.float().sum(0))
+    return c
 
 
 @_impl("gemm_acc_f32")

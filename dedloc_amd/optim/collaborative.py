@@ -33,7 +33,7 @@ from pydantic import BaseModel, StrictBool, StrictFloat, confloat, conint
 
 from ..averaging.averager import DecentralizedAverager
 from ..dht import DHT, get_dht_time
-from .performance_ema import PerformanceEMA
+from .performance_ema import DeviceStepTimer, PerformanceEMA
 
 logger = logging.getLogger(__name__)
 
@@ -106,14 +106,24 @@ class CollaborativeOptimizer:
         self.local_steps_accumulated = 0
         self.local_step = 0
         self.performance_ema = PerformanceEMA(alpha=performance_ema_alpha)
+        # GPU peers time micro-steps on the device (performance_ema.DeviceStepTimer): the host runs
+        # ahead of the GPU, so its clock does not say when samples were processed
+        self._device_timer = DeviceStepTimer(self.performance_ema) if self.flat.fp32.is_cuda and not auxiliary else None
         self.last_step_time = None
         self._pending_finite = []  # (host flag, event, batch size, local step) of recent micro-steps
+        # [finite samples, finite micro-steps] of the current global batch, counted ON THE DEVICE: the
+        # global step's averaging weight and gradient divisor come from here, so it never waits for
+        # the host to learn which micro-steps were finite
+        self._finite_counts = torch.zeros(2, device=self.flat.fp32.device) if not auxiliary else None
+        self._count_vecs: Dict[int, torch.Tensor] = {}
         self.last_group: Optional[Dict] = None
         self.stats = {"global_steps": 0, "averaging_rounds": 0, "averaging_failed": 0, "state_loads": 0,
                       # where a global step's time goes (host clock, seconds, summed over steps): the
-                      # state fetch, matchmaking + all-reduce, the optimizer, and the local micro-steps
-                      # that went into each global batch
-                      "fetch_s": 0.0, "averaging_s": 0.0, "optimizer_s": 0.0, "local_steps": 0}
+                      # wait for the batch's last micro-step on the device, the state fetch,
+                      # matchmaking + all-reduce (and each separately), the optimizer launch, the
+                      # bookkeeping after it, and the local micro-steps that went into each global batch
+                      "wait_s": 0.0, "fetch_s": 0.0, "averaging_s": 0.0, "matchmaking_s": 0.0, "allreduce_s": 0.0,
+                      "optimizer_s": 0.0, "tail_s": 0.0, "local_steps": 0}
 
         self.averager = DecentralizedAverager(
             [self.flat.fp32, self.flat.grad], dht, prefix, peer_id=peer_id,
@@ -130,6 +140,7 @@ class CollaborativeOptimizer:
 
         self.eta_slack = float(eta_slack)
         self._prejoin = None  # background matchmaking for the coming global step (_maybe_prejoin)
+        self._prejoin_key = None  # (local step, monotonic start) the pending prejoin was made for
         self.prejoin_enabled = prejoin
         self.delay_param_averaging = delay_param_averaging
         self._param_round: Optional[threading.Thread] = None
@@ -225,6 +236,7 @@ class CollaborativeOptimizer:
     def load_state_from_peers(self, **kwargs) -> bool:
         """Download params + optimizer state from the freshest donor (App. A.7)."""
         self._finish_param_round(apply=False)
+        self._drop_prejoin()  # a group matched for the step we are leaving is not ours any more
         # download WITHOUT holding lock_step: our own state server takes that lock to snapshot the
         # state it serves, so two peers loading from each other would otherwise block each other
         kwargs.setdefault("min_step", self.local_step + 1 if self.local_step > 0 or self.is_synchronized else 0)
@@ -249,6 +261,8 @@ class CollaborativeOptimizer:
             self.update_scheduler()
             self.stats["state_loads"] += 1
             self._take_snapshot()
+            if self._device_timer is not None:
+                self._device_timer.resume()
             self.averager.publish_state_sharing(self.local_step)
         dl = self.averager.last_download or {}
         logger.warning(f"downloaded state from peers: step {self.local_step}, {dl.get('bytes', 0) / 2**20:.0f} MiB in "
@@ -258,6 +272,8 @@ class CollaborativeOptimizer:
     def _reset_accumulators(self):
         if self.accumulator is not None:
             self.accumulator.zero_()
+        if self._finite_counts is not None:
+            self._finite_counts.zero_()
         with self.lock_local_progress:
             self.local_samples_accumulated = 0
             self.local_steps_accumulated = 0
@@ -270,6 +286,17 @@ class CollaborativeOptimizer:
     # ------------------------------------------------------------------ training step
     def zero_grad(self, *args, **kwargs):
         self.opt.zero_grad()
+
+    def _count_finite(self, finite: Optional[torch.Tensor], batch_size: int):
+        """[samples, steps] += [batch_size, 1] x finite, on the device (one launch)."""
+        vec = self._count_vecs.get(batch_size)
+        if vec is None:
+            vec = self._count_vecs[batch_size] = torch.tensor([float(batch_size), 1.0],
+                                                              device=self._finite_counts.device)
+        if finite is None:
+            self._finite_counts.add_(vec)
+        else:
+            self._finite_counts.addcmul_(vec, finite.reshape(1).to(torch.float32))
 
     def _track_finite(self, finite: torch.Tensor, batch_size: int):
         """Remember a micro-step's device-side finite flag (1 = finite).  The reference's GradScaler
@@ -314,6 +341,7 @@ class CollaborativeOptimizer:
 
         if not self.is_synchronized:
             logger.log(self.status_loglevel, "peer is out of sync; loading state from peers")
+            self._drop_prejoin()
             self.load_state_from_peers()
             return None
         if self.last_step_time is not None and get_dht_time() - self.last_step_time > self.metadata_expiration:
@@ -324,40 +352,59 @@ class CollaborativeOptimizer:
             torch.ops.dedloc.axpby(self.accumulator, self.flat.grad, 1.0, batch_size / self.batch_size_per_step)
             self.local_samples_accumulated += batch_size
             self.local_steps_accumulated += 1
-            self.performance_ema.update(num_processed=batch_size)
+            if self._device_timer is None:
+                self.performance_ema.update(num_processed=batch_size)
             self.should_report_progress.set()
+        self._count_finite(finite, batch_size)
         if finite is not None:
             self._track_finite(finite, batch_size)
         self._resolve_finite(block=False)
+        if self._device_timer is not None:
+            self._device_timer.step_done(batch_size)
+            self._device_timer.poll()
 
         if self._param_round is not None and not self._param_round.is_alive():
             self._finish_param_round()
-        if not (self.collaboration_state.ready_for_step or self._ready_exact()
-                or self._ready_within_slack(batch_size)):
+        fresh = False
+        if not self._ready(batch_size) and self._imminent():
+            # the matchmaking for this step is already under way (a prejoin made at this local step):
+            # this micro-step is expected to complete the global batch.  The host runs a micro-step
+            # ahead of the GPU, so the other peers' reports of THEIR last micro-step are typically
+            # not in our view yet: wait until this micro-step has finished on the device (the global
+            # step needs its gradient anyway), then look again with a fresh view — instead of
+            # queueing one more micro-step per peer past the target batch.
+            t_wait = time.perf_counter()
+            if self._device_timer is not None and self._device_timer.last is not None:
+                self._device_timer.last.synchronize()
+            self.stats["wait_s"] = self.stats.get("wait_s", 0.0) + time.perf_counter() - t_wait
+            self._refresh_state()
+            fresh = True
+        if not self._ready(batch_size):
             self._maybe_prejoin(batch_size)
             return None
-        self._resolve_finite(block=True)  # the global step's weight counts finite samples only
 
         logger.log(self.status_loglevel, f"beginning global optimizer step #{self.collaboration_state.optimizer_step}")
         self._finish_param_round()
-        t_fetch = time.perf_counter()
-        self.collaboration_state = self.fetch_collaboration_state()
-        self.stats["fetch_s"] += time.perf_counter() - t_fetch
-        self.collaboration_state_updated.set()
+        if not fresh:
+            self._refresh_state()
         if not self.is_synchronized:
+            self._drop_prejoin()
             self.load_state_from_peers()
             return None
 
         with self.performance_ema.pause(), self.lock_collaboration_state, self.lock_step:
             cs = self.collaboration_state
-            # grads = accumulator / local_steps   (hivemind apply_accumulated_grads_)
-            torch.ops.dedloc.axpby(self.flat.grad, self.accumulator, 0.0, 1.0 / max(1, self.local_steps_accumulated))
+            # grads = accumulator / local_steps (hivemind apply_accumulated_grads_), counting finite
+            # micro-steps only — the count is a device scalar: no host sync here
+            torch.ops.dedloc.axpby(self.flat.grad, self.accumulator, 0.0, 1.0, None, self._finite_counts[1:2])
             group = None
             t_avg = time.perf_counter()
-            prejoined, self._prejoin = self._prejoin, None
+            prejoined = self._take_prejoin()
             if cs.num_peers > 1 or prejoined is not None:
                 mean_samples = self.target_batch_size / max(1, cs.num_peers)
-                weight = self.local_samples_accumulated / mean_samples
+                # the finite samples of this global batch / the mean per peer, as a device scalar
+                # that travels with the data (allreduce.py)
+                weight = self._finite_counts[0:1] * (1.0 / mean_samples)
                 group = self.averager.step(weight=weight, timeout=self.averaging_timeout,
                                            expected_group_size=cs.num_peers + self._num_aux(),
                                            gather={"step": int(self.local_step)},
@@ -375,7 +422,11 @@ class CollaborativeOptimizer:
             if self.delay_param_averaging and group is not None:
                 self._start_param_round(weight, cs.num_peers + self._num_aux())
             self.stats["averaging_s"] += t_opt - t_avg
-            self.stats["optimizer_s"] += time.perf_counter() - t_opt  # launch time (kernels run async)
+            if group is not None:
+                self.stats["matchmaking_s"] = self.stats.get("matchmaking_s", 0.0) + group.get("matchmaking_s", 0.0)
+                self.stats["allreduce_s"] = self.stats.get("allreduce_s", 0.0) + group.get("allreduce_s", 0.0)
+            t_tail = time.perf_counter()
+            self.stats["optimizer_s"] += t_tail - t_opt  # launch time (kernels run async)
             self.stats["local_steps"] += self.local_steps_accumulated
             self._reset_accumulators()
             self.collaboration_state.register_step(self.local_step + 1)
@@ -385,11 +436,57 @@ class CollaborativeOptimizer:
             self.stats["global_steps"] += 1
             self.should_report_progress.set()
             self._take_snapshot()
+            if self._device_timer is not None:  # the global step's device time is not counted
+                self._device_timer.resume()
         self.averager.publish_state_sharing(self.local_step)
         self.last_step_time = get_dht_time()
         logger.log(self.status_loglevel, f"optimizer step #{self.local_step} done")
         self._prejoin_next(batch_size, cs.num_peers)
+        # bookkeeping after the optimizer launch: counters, scheduler, snapshot copy, state-sharing
+        # record, the next round's prejoin
+        self.stats["tail_s"] = self.stats.get("tail_s", 0.0) + time.perf_counter() - t_tail
         return group
+
+    def _ready(self, batch_size: int) -> bool:
+        return (self.collaboration_state.ready_for_step or self._ready_exact()
+                or self._ready_within_slack(batch_size))
+
+    def _imminent(self) -> bool:
+        return (self._prejoin is not None and self._prejoin_key is not None
+                and self._prejoin_key[0] == int(self.local_step))
+
+    def _refresh_state(self):
+        t_fetch = time.perf_counter()
+        self.collaboration_state = self.fetch_collaboration_state()
+        self.stats["fetch_s"] += time.perf_counter() - t_fetch
+        self.collaboration_state_updated.set()
+
+    def _start_prejoin(self, expected_group_size: int):
+        self._prejoin = self.averager.prejoin(expected_group_size=expected_group_size,
+                                              gather={"step": int(self.local_step)})
+        self._prejoin_key = (int(self.local_step), time.monotonic())
+
+    def _drop_prejoin(self):
+        """Forget a pending prejoin (its group, if one forms, will fail its round for the other
+        members exactly as a peer leaving a hivemind group does — never later, with a stale group)."""
+        if self._prejoin is not None:
+            self.stats["prejoins_dropped"] = self.stats.get("prejoins_dropped", 0) + 1
+        self._prejoin, self._prejoin_key = None, None
+
+    def _take_prejoin(self):
+        """The pending prejoin future if it still belongs to THIS global step: made at the current
+        local step and no older than one matchmaking window plus the averaging timeout (a group
+        its members have long since abandoned is never passed to the averager)."""
+        fut, key = self._prejoin, self._prejoin_key
+        self._prejoin, self._prejoin_key = None, None
+        if fut is None:
+            return None
+        step, t0 = key
+        max_age = self.averager.averaging_expiration + self.averaging_timeout
+        if step != int(self.local_step) or time.monotonic() - t0 > max_age:
+            self.stats["prejoins_dropped"] = self.stats.get("prejoins_dropped", 0) + 1
+            return None
+        return fut
 
     def _prejoin_next(self, batch_size: int, num_peers: int):
         """Right after a global step: when one micro-step of every peer completes the next global
@@ -401,8 +498,7 @@ class CollaborativeOptimizer:
             return
         if num_peers * batch_size < self.target_batch_size:
             return
-        self._prejoin = self.averager.prejoin(expected_group_size=num_peers + self._num_aux(),
-                                              gather={"step": int(self.local_step)})
+        self._start_prejoin(num_peers + self._num_aux())
 
     def _maybe_prejoin(self, batch_size: int):
         """Begin matchmaking now when the NEXT local step will start the global step (the
@@ -420,8 +516,7 @@ class CollaborativeOptimizer:
         if not soon and sps > 0:
             soon = get_dht_time() + batch_size / sps * (1.0 + self.eta_slack) >= cs.eta_next_step
         if soon:
-            self._prejoin = self.averager.prejoin(expected_group_size=cs.num_peers + self._num_aux(),
-                                                  gather={"step": int(self.local_step)})
+            self._start_prejoin(cs.num_peers + self._num_aux())
 
     def _ready_exact(self) -> bool:
         """The collaboration's sample count with OUR part brought up to date: the fetched state counts
@@ -488,17 +583,26 @@ class CollaborativeOptimizer:
             self.dht.store(f"{self.prefix}_aux", True, now + self.metadata_expiration, subkey=self.peer_id,
                            return_future=True)
 
-    def _num_aux(self) -> int:
+    def _num_aux(self, max_age: Optional[float] = None) -> int:
+        """Live auxiliary peers (``{prefix}_aux``).  Cached: the collaboration-state updater thread
+        refreshes it, so a global step does not spend a synchronous DHT lookup on it."""
+        max_age = max(self.min_refresh_period, 2.0) if max_age is None else max_age
+        cached = getattr(self, "_aux_cache", None)
+        if cached is not None and time.monotonic() - cached[1] <= max_age:
+            return cached[0]
         rec = self.dht.get(f"{self.prefix}_aux", latest=True)
-        if rec is None or not isinstance(rec.value, dict):
-            return 0
-        return sum(1 for k, v in rec.value.items() if v.value is True and k != self.peer_id)
+        n = 0
+        if rec is not None and isinstance(rec.value, dict):
+            n = sum(1 for k, v in rec.value.items() if v.value is True and k != self.peer_id)
+        self._aux_cache = (n, time.monotonic())
+        return n
 
     # ------------------------------------------------------------------ churn
     def leave(self):
         """Stop participating: finish any background round, drop local progress and tombstone our
         progress record so the collaboration's ETA and peer count exclude us immediately."""
         self._finish_param_round(apply=False)
+        self._drop_prejoin()
         self._reset_accumulators()
         self._left = True
         try:
@@ -512,6 +616,8 @@ class CollaborativeOptimizer:
         self.collaboration_state = self.fetch_collaboration_state()
         self.load_state_from_peers()
         self.performance_ema.reset_timer()
+        if self._device_timer is not None:
+            self._device_timer.resume()
         self.should_report_progress.set()
 
     # ------------------------------------------------------------------ delayed parameter averaging
@@ -609,6 +715,7 @@ class CollaborativeOptimizer:
             try:
                 with self.lock_collaboration_state:
                     self.collaboration_state = self.fetch_collaboration_state()
+                self._num_aux(max_age=0.0)  # refresh the cached auxiliary count off the critical path
             except Exception as e:  # noqa: BLE001
                 logger.debug(f"collaboration state update failed: {e}")
 

@@ -69,6 +69,7 @@ class CommWorker:
         self._cv = threading.Condition()
         self._thread = threading.Thread(target=self._loop, daemon=True, name="comm-worker")
         self.jobs_run = 0
+        self.quarantined = 0  # communicators waiting for their bootstrap to end before the abort
         self._thread.start()
 
     @classmethod
@@ -96,14 +97,35 @@ class CommWorker:
             return _drain(job)
         return self.submit(job).result()
 
+    def note_quarantined(self):
+        self.quarantined += 1
+
+    REAP_PERIOD_S = 0.5
+
+    def _reap(self):
+        try:
+            self.quarantined = int(_ops().comm_reap())
+        except Exception as e:  # noqa: BLE001
+            logger.debug(f"comm_reap failed: {e}")
+            self.quarantined = 0
+
     def _loop(self):
         active = []
+        last_reap = time.monotonic()
         while True:
             with self._cv:
                 while not self._queue and not active:
-                    self._cv.wait()
+                    if not self.quarantined:
+                        self._cv.wait()
+                        continue
+                    self._cv.wait(self.REAP_PERIOD_S)
+                    if not self._queue:
+                        break
                 while self._queue:
                     active.append(self._queue.popleft())
+            if self.quarantined and time.monotonic() - last_reap >= self.REAP_PERIOD_S:
+                last_reap = time.monotonic()
+                self._reap()
             still = []
             for job, fut in active:
                 try:
@@ -149,11 +171,18 @@ def _error(code: int) -> str:
         return f"code {code}"
 
 
+QUARANTINED = 1
+
+
 def _abort(handle: int):
+    """Release a failed or finished communicator: ncclCommAbort, unless its non-blocking bootstrap
+    is still in flight — then the native registry quarantines it (RCCL's init thread still owns
+    it) and the worker reaps it once the bootstrap has ended (``comm_core.h``)."""
     try:
-        _ops().comm_abort(int(handle))
+        if int(_ops().comm_release(int(handle))) == QUARANTINED:
+            CommWorker.get().note_quarantined()
     except Exception as e:  # noqa: BLE001
-        logger.debug(f"comm_abort({handle}) failed: {e}")
+        logger.debug(f"comm_release({handle}) failed: {e}")
 
 
 def _wait_ready(handle: int, deadline: Optional[float], what: str):

@@ -155,7 +155,7 @@ class AlbertPeer:
                                            length_mode=getattr(dataset_args, "length_mode", "full"))
         flat = self.model.flat
         self._clip_part = torch.zeros(256, device=self.device)
-        self._clip_out = torch.zeros(2, device=self.device)
+        self._clip_out = torch.zeros(3, device=self.device)  # [norm, finite, 1 - finite]
         self._loss_sum = torch.zeros((), device=self.device)
         self.mini_steps = 0
         self.samples = 0
@@ -163,6 +163,7 @@ class AlbertPeer:
         self.last_reported_collaboration_step = -1
         self.hf_step = 0
         self.metrics_log = []
+        self._pending_metrics = []  # (pinned host loss, event, record fields) awaiting the device
         self._flat = flat
         self.perf = PerfStats(self.device, enabled=bool(getattr(training_args, "perf_timers", True)))
 
@@ -238,38 +239,68 @@ class AlbertPeer:
 
     def _drop_if_nonfinite(self):
         # device-side: zero the whole step's gradient when the finite flag is 0 (no host sync)
-        torch.ops.dedloc.axpby(self._flat.grad, self._flat.grad, 0.0, 0.0, 1.0 - self._clip_out[1:2])
+        torch.ops.dedloc.axpby(self._flat.grad, self._flat.grad, 0.0, 0.0, self._clip_out[2:3])
 
     def on_step_end(self):
+        """CollaborativeCallback.on_step_end (albert/run_trainer.py:130-170): when the collaborative
+        step changes, publish LocalMetrics to ``{prefix}_metrics``.  The loss lives on the device;
+        its value is copied to pinned host memory behind this step and the record is published once
+        the copy has landed (at a later micro-step, never by waiting for the GPU: a read here drained
+        the queue at every global step and idled the device while the host refilled it)."""
         co = self.collab_opt
         if co.local_step != self.last_reported_collaboration_step:
             self.last_reported_collaboration_step = co.local_step
             self.total_samples_processed += self.samples
-            loss = float(self._loss_sum.item())
-            stats = LocalMetrics(step=int(co.local_step), samples_per_second=float(co.performance_ema.samples_per_second),
-                                 samples_accumulated=int(self.samples), loss=loss, mini_steps=int(self.mini_steps))
-            logger.info(f"Step {co.local_step}")
-            logger.info(f"Your current contribution: {self.total_samples_processed} samples")
-            if self.mini_steps:
-                logger.info(f"Local loss: {loss / self.mini_steps:.5f}")
-            if (not self.publish_only_synchronized) or co.is_synchronized:
+            if self._loss_sum.is_cuda:
+                host = torch.empty((), dtype=torch.float32, pin_memory=True)
+                host.copy_(self._loss_sum, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            else:
+                host, ev = self._loss_sum.clone(), None
+            lg = co.last_group or {}
+            self._pending_metrics.append((host, ev, dict(
+                step=int(co.local_step), samples_accumulated=int(self.samples), mini_steps=int(self.mini_steps),
+                hf_step=self.hf_step, lr=self.opt.param_groups[0]["lr"], group=lg.get("size"),
+                matchmaking_s=lg.get("matchmaking_s"), allreduce_s=lg.get("allreduce_s"), parts=lg.get("parts"),
+                synchronized=co.is_synchronized, contribution=self.total_samples_processed)))
+            self._loss_sum.zero_()  # on the stream, after the copy
+            self.mini_steps = 0
+        self.flush_metrics()
+        self.samples = co.local_samples_accumulated
+        if self.args.save_steps and self.hf_step % self.args.save_steps == 0:
+            self.save_checkpoint()
+
+    def flush_metrics(self, block: bool = False):
+        """Publish every pending LocalMetrics record whose loss has reached the host (in order)."""
+        co = self.collab_opt
+        while self._pending_metrics:
+            host, ev, info = self._pending_metrics[0]
+            if ev is not None:
+                if block:
+                    ev.synchronize()
+                elif not ev.query():
+                    return
+            self._pending_metrics.pop(0)
+            loss = float(host)
+            stats = LocalMetrics(step=info["step"], samples_per_second=float(co.performance_ema.samples_per_second),
+                                 samples_accumulated=info["samples_accumulated"], loss=loss,
+                                 mini_steps=info["mini_steps"])
+            logger.info(f"Step {info['step']}")
+            logger.info(f"Your current contribution: {info['contribution']} samples")
+            if info["mini_steps"]:
+                logger.info(f"Local loss: {loss / info['mini_steps']:.5f}")
+            if (not self.publish_only_synchronized) or info["synchronized"]:
                 self.dht.store(co.prefix + "_metrics", stats.model_dump(),
                                expiration_time=get_dht_time() + self.statistics_expiration,
                                subkey=self.local_public_key, return_future=True)
-            lg = co.last_group or {}
-            rec = dict(stats.model_dump(), time=time.time(), hf_step=self.hf_step,
-                       lr=self.opt.param_groups[0]["lr"], group=lg.get("size"),
-                       matchmaking_s=lg.get("matchmaking_s"), allreduce_s=lg.get("allreduce_s"),
-                       parts=lg.get("parts"), **self.perf.report())
+            rec = dict(stats.model_dump(), time=time.time(), hf_step=info["hf_step"], lr=info["lr"],
+                       group=info["group"], matchmaking_s=info["matchmaking_s"], allreduce_s=info["allreduce_s"],
+                       parts=info["parts"], **self.perf.report())
             self.metrics_log.append(rec)
             if self.args.metrics_file:
                 with open(self.args.metrics_file, "a") as f:
                     f.write(json.dumps(rec) + "\n")
-            self._loss_sum.zero_()
-            self.mini_steps = 0
-        self.samples = co.local_samples_accumulated
-        if self.args.save_steps and self.hf_step % self.args.save_steps == 0:
-            self.save_checkpoint()
 
     # ------------------------------------------------------------------ checkpoints (HF layout)
     def save_checkpoint(self):
@@ -296,7 +327,12 @@ class AlbertPeer:
                 break
             if max_seconds is not None and time.time() - t0 > max_seconds:
                 break
+        self.flush_metrics(block=True)
 
     def shutdown(self):
+        try:
+            self.flush_metrics(block=True)
+        except Exception as e:  # noqa: BLE001
+            logger.debug(f"final metrics flush failed: {e}")
         self.collab_opt.shutdown()
         self.dht.shutdown()

@@ -165,6 +165,8 @@ class SwavPeer:
         self._graphed = None
         self.iteration = 0
         self._loss_sum = torch.zeros((), device=self.device)
+        self._finite_part = torch.zeros(256, device=self.device)
+        self._finite_out = torch.zeros(3, device=self.device)  # [grad norm, finite, 1 - finite]
         self.mini_steps = 0
         self.last_reported_step = -1
         self.metrics_log = []
@@ -275,10 +277,18 @@ class SwavPeer:
                 name = name[len("module."):] if name.startswith("module.") else name
                 self.flat.view(self.flat.grad, name).zero_()
         self._loss_sum += loss.detach()
+        finite = None
+        if self.impl == "dedloc":
+            # every micro-step: the gradient's finite flag on the device; a non-finite step's gradient
+            # is zeroed there and its samples do not count (collab_opt.step(finite=...)), so it can
+            # never be averaged into the other peers — with no host sync
+            torch.ops.dedloc.grad_norm_clip(self.flat.grad, 0.0, self._finite_part, self._finite_out)
+            torch.ops.dedloc.axpby(self.flat.grad, self.flat.grad, 0.0, 0.0, self._finite_out[2:3])
+            finite = self._finite_out[1:2]
         if self.check_nan and (self.iteration + 1) % self.log_frequency == 0:
             self._check_nan_async()
         with self.perf.phase("collab_step"):
-            self.collab_opt.step(batch_size=self.batch_size)
+            self.collab_opt.step(batch_size=self.batch_size, finite=finite)
         self.opt.zero_grad()
         self.model.normalize_prototypes()  # NormalizePrototypesHook.on_update (swav_hooks.py:63-92)
         self.iteration += 1

@@ -2,8 +2,9 @@
 SURVEY.md §2.3 V20 / §5.1).
 
 ``with stats.phase("fwd_bwd"):`` records a start/end event pair on the current stream without
-synchronising; ``stats.report()`` waits only for the last recorded event and returns the mean
-milliseconds per phase since the previous report (host wall time is used on CPU).  With
+synchronising; ``stats.report()`` returns the mean milliseconds per phase over the occurrences that
+have completed since the previous report, without waiting for the device (host wall time is used
+on CPU).  With
 ``sample_every`` = k only every k-th iteration (``next_iteration()``) is timed: timing events are
 queue markers, and at SwAV's ~1000 kernels / 21 ms iteration eight of them per iteration cost ~0.5%.
 """
@@ -49,21 +50,27 @@ class PerfStats:
             finally:
                 self._events[name].append((t0, time.perf_counter()))
 
-    def report(self) -> Dict[str, float]:
-        """Mean ms per phase occurrence since the last report (and the number of occurrences)."""
+    def report(self, block: bool = False) -> Dict[str, float]:
+        """Mean ms per phase occurrence over the occurrences that have completed since the last
+        report (and their number).  Without ``block`` it never waits for the device: occurrences
+        still in flight stay for the next report (a synchronising report at every global step
+        drained the GPU queue there and idled it while the host refilled it)."""
         out = {}
-        if self.cuda:
-            last = [ev[-1][1] for ev in self._events.values() if ev]
-            for e in last:
-                e.synchronize()
         for name, evs in self._events.items():
             if not evs:
                 continue
             if self.cuda:
-                ms = [s.elapsed_time(e) for s, e in evs]
+                if block:
+                    evs[-1][1].synchronize()
+                done = 0
+                while done < len(evs) and evs[done][1].query():
+                    done += 1
+                ms = [s.elapsed_time(e) for s, e in evs[:done]]
             else:
+                done = len(evs)
                 ms = [(e - s) * 1e3 for s, e in evs]
-            out[f"{name}_ms"] = sum(ms) / len(ms)
-            out[f"{name}_n"] = len(ms)
-        self._events.clear()
+            del evs[:done]
+            if ms:
+                out[f"{name}_ms"] = sum(ms) / len(ms)
+                out[f"{name}_n"] = len(ms)
         return out

@@ -13,6 +13,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "multiproc: spawns several processes (gloo on CPU)")
 
 
+def record_margin(test: str, **fields):
+    """Append a numerics test's measured margins (errors and the bounds they are held to) to a JSONL
+    file — ``$DEDLOC_MARGINS_FILE``, default ``gpurun_out/parity_margins.jsonl`` (merged back from a
+    GPU box; the committed copy lives under profiles/)."""
+    import json
+    import time
+
+    path = os.environ.get("DEDLOC_MARGINS_FILE") or os.path.join(ROOT, "gpurun_out", "parity_margins.jsonl")
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "a") as f:
+            f.write(json.dumps(dict(test=test, time=time.time(), **fields)) + "\n")
+    except OSError:
+        pass
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch

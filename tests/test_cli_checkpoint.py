@@ -136,7 +136,9 @@ def test_launch_collaboration_coordinator_trainers_aux_cpu(tmp_path):
            "--seq_length", "64", "--target_batch_size", "8", "--stop_after_global_steps", "6", "--save_steps", "0",
            "--output_dir", str(tmp_path / "out"), "--min_refresh_period", "0.05", "--default_refresh_period", "0.1",
            "--dht_listen_on", "127.0.0.1:*", "--listen_on", "127.0.0.1:*", "--averaging_expiration", "3",
-           "--compression", "NONE"]
+           "--compression", "NONE", "--throttle", "0.05"]
+    # --throttle: 6 global steps of the tiny model take ~1 s, less than the start-up skew of two
+    # trainer processes on a loaded host; paced steps make the two trainers actually collaborate
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)

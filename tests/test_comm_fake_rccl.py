@@ -36,6 +36,7 @@ class FakeRccl:
         self.mail = defaultdict(deque)  # (uid, src, dst) -> tensors in send order
         self.init_polls, self.enqueue_polls = init_polls, enqueue_polls
         self.aborted = set()
+        self.quarantine = set()   # released while still bootstrapping: aborted by comm_reap later
         self.mute = set()         # (uid, rank): this member's operations never arrive (dead peer)
         self.calls = defaultdict(int)
         self.threads = set()
@@ -91,10 +92,32 @@ class FakeRccl:
             c["polls"] = self.enqueue_polls
         return IN_PROGRESS
 
-    def comm_abort(self, h):
-        self._note("comm_abort")
+    def _in_progress(self, c):
+        return len(self.joined[c["uid"]]) < c["n"]
+
+    def comm_release(self, h):
+        """comm_core.h's rule: abort, unless the bootstrap is still in flight (quarantine)."""
+        self._note("comm_release")
         with self.lock:
+            c = self.comms.get(h)
+            if c is not None and self._in_progress(c) and not c["error"]:
+                self.quarantine.add(h)
+                return 1
             self.aborted.add(h)
+            self.quarantine.discard(h)
+            return 0
+
+    def comm_reap(self):
+        self._note("comm_reap")
+        with self.lock:
+            for h in list(self.quarantine):
+                if not self._in_progress(self.comms[h]):
+                    self.quarantine.discard(h)
+                    self.aborted.add(h)
+            return len(self.quarantine)
+
+    def comm_quarantined(self):
+        return len(self.quarantine)
 
     def error_string(self, code):
         return f"fake error {code}"
@@ -150,7 +173,7 @@ def test_butterfly_over_rccl_nonuniform_parts_and_weights(fake):
     for r in range(n):
         torch.testing.assert_close(out[r], expected, rtol=2e-3, atol=2e-3)
     assert fake.threads == {"comm-worker"}, fake.threads  # the single RCCL owner
-    assert fake.calls["group_p2p"] == 2 * n and fake.calls["comm_abort"] == n
+    assert fake.calls["group_p2p"] == 2 * n and fake.calls["comm_release"] == n and len(fake.aborted) == n
 
 
 def test_async_error_while_polling_aborts_and_raises(fake):
@@ -270,3 +293,47 @@ def test_peers_sharing_a_gpu_take_one_rccl_rank():
     # members that announce no device identity (older peers) keep the previous rule
     legacy = [(b"x", {"backend": "rccl"}), (b"y", {"backend": "rccl"}), (b"z", {"backend": "gloo"})]
     assert G.rccl_members(legacy) == [b"x", b"y"] and G.group_backend(legacy) == "hybrid"
+
+
+def test_abandoned_bootstrap_is_quarantined_then_reaped(fake):
+    """A member that never arrives: the bootstrap is abandoned at its deadline, but the
+    communicator is NOT aborted while RCCL's init thread may still own it (the round-4 SIGSEGV on
+    the driver's box came out of this path).  It is quarantined, and the comm worker aborts it as
+    soon as the bootstrap ends (here: the late member finally shows up)."""
+    uid = W.unique_id()
+    t0 = time.monotonic()
+    with pytest.raises(C.CommError) as ei:
+        C.RcclGroupComm.create(uid, 2, 0, torch.device("cpu"), time.monotonic() + 0.5)
+    assert time.monotonic() - t0 < 5 and not ei.value.local
+    (h,) = fake.comms
+    assert h in fake.quarantine and h not in fake.aborted
+    assert W.CommWorker.get().quarantined >= 1
+    with fake.lock:  # the missing member bootstraps late: RCCL's init ends, the reaper may abort
+        fake.joined[fake.comms[h]["uid"]].add(1)
+    t0 = time.monotonic()
+    while h not in fake.aborted and time.monotonic() - t0 < 10:
+        time.sleep(0.05)
+    assert h in fake.aborted and not fake.quarantine
+    assert fake.threads == {"comm-worker"}
+
+
+def test_same_device_donor_answers_over_tcp(fake):
+    """A requester on the donor's own GPU (peers sharing a device) is served over TCP, and no
+    communicator is ever initialised for it (RCCL takes one rank per device)."""
+    from dedloc_amd.averaging.averager import StateServer, download_state
+
+    state = [torch.randn(64)]
+    srv = StateServer(lambda: ({"step": 3}, [t.clone() for t in state]), "127.0.0.1:0", device=torch.device("cpu"),
+                      gpu_id="host/gpu0")
+    try:
+        meta, tensors = download_state(srv.endpoint, timeout=20, device=torch.device("cpu"), allow_rccl=True,
+                                       gpu_id="host/gpu0")
+        assert meta["_mode"] == "T" and fake.calls["comm_init"] == 0
+        torch.testing.assert_close(tensors[0], state[0])
+        # another device on the same host: the RCCL path
+        meta, tensors = download_state(srv.endpoint, timeout=20, device=torch.device("cpu"), allow_rccl=True,
+                                       gpu_id="host/gpu1")
+        assert meta["_mode"] == "R" and fake.calls["comm_init"] == 2
+        torch.testing.assert_close(tensors[0], state[0])
+    finally:
+        srv.shutdown()

@@ -498,6 +498,35 @@ def test_mfma_gemm_gelu_epilogues(cuda, force_mfma):
     assert rel(db, df.float().sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("M,H,I", [(1024, 256, 1024), (4096, 1024, 4096), (1000, 256, 512)])
+def test_gemm_gelu_derivative_forms(cuda, M, H, I):
+    """gemm_gelu_d stores gelu_new'(h) next to gelu_new(h); gemm_dmul multiplies the data gradient
+    by it: the pair equals the pre-activation pair gemm_gelu / gemm_dgelu to bf16 accuracy and the
+    fp32 reference (gemm8 EPI 6 / 7 at the 256-multiple shapes, the unfused kernels otherwise)."""
+    torch.manual_seed(11)
+    x = torch.randn(M, H, device=cuda).bfloat16()
+    w1 = (torch.randn(I, H, device=cuda) * 0.1).bfloat16()
+    b1 = torch.randn(I, device=cuda)
+    d, g = OPS.gemm_gelu_d(x, w1, b1)
+    f, g0 = OPS.gemm_gelu(x, w1, b1)
+    assert torch.equal(g, g0)
+    hr = f.float().requires_grad_(True)
+    gr = F.gelu(hr, approximate="tanh")
+    dref = torch.autograd.grad(gr.sum(), hr)[0]
+    assert rel(d, dref) < 5e-3
+    w2 = (torch.randn(H, I, device=cuda) * 0.1).bfloat16()
+    ds = torch.randn(M, H, device=cuda).bfloat16()
+    db, db0 = torch.zeros(I, device=cuda), torch.zeros(I, device=cuda)
+    df = OPS.gemm_dmul(ds, w2, d, db)
+    df0 = OPS.gemm_dgelu(ds, w2, f, db0)
+    ref = (ds.float() @ w2.float()) * dref
+    assert rel(df, ref) < 1e-2 and rel(df, df0) < 1e-2
+    assert rel(db, df.float().sum(0)) < 1e-3 and rel(db, db0) < 1e-2
+    dbt = torch.zeros(I, device=cuda)
+    dft = OPS.gemm_dmul(ds, w2.t().contiguous(), d, dbt, True)
+    assert rel(dft, df) < 1e-2 and rel(dbt, db) < 1e-2
+
+
 def test_gemm_dgelu_transposed_weight(cuda):
     """gemm_dgelu(trans_w=True) against W^T's forward-layout copy equals the plain-weight form."""
     torch.manual_seed(17)

@@ -48,7 +48,9 @@ def test_launcher_kill_and_respawn_with_cpu_aux(tmp_path):
     i_dip = next((i for i, a in enumerate(alive) if a < 3 and i > 0 and max(alive[:i]) == 3), None)
     assert i_dip is not None, alive  # the preempted peer's record expired ...
     assert max(alive[i_dip:]) >= 3, alive  # ... and the respawned process brought the count back
-    assert all(b > a for a, b in zip(steps, steps[1:])), steps  # the step kept increasing throughout
+    # the step kept increasing throughout (the coordinator also writes a row when only the alive
+    # count changes, so consecutive rows may share a step)
+    assert all(b >= a for a, b in zip(steps, steps[1:])) and steps[-1] > steps[0], steps
     # the respawned trainer is a new process that joined through a state download
     gen1 = (logs / "trainer1.gen1.log").read_text()
     assert "downloaded state" in gen1, gen1[-3000:]

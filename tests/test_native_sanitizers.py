@@ -1,8 +1,14 @@
-"""Host-side sanitizer run of the native control-plane server.
+"""Host-side sanitizer runs of the native runtime.
 
-GPU sanitizers are not available on this pool, so the C++ runtime (csrc/runtime/dht_server.cpp) is
-compiled together with a concurrent stress client (tests/native/dht_server_test.cpp) under
-AddressSanitizer + UndefinedBehaviorSanitizer and run on the CPU.
+GPU sanitizers are not available on this pool, so the host C++ is compiled under AddressSanitizer +
+UndefinedBehaviorSanitizer and under ThreadSanitizer and run on the CPU:
+
+* the control-plane server (csrc/runtime/dht_server.cpp) with a concurrent stress client
+  (tests/native/dht_server_test.cpp);
+* the RCCL data plane's communicator registry (csrc/comm/comm_core.cpp: handles, release /
+  quarantine / reap, abort) against a stub RCCL that simulates non-blocking bootstraps with a
+  background init thread (tests/native/rccl_core_test.cpp, tests/native/stub_rccl/), driven from
+  two threads.
 """
 import os
 import shutil
@@ -30,3 +36,23 @@ def test_dht_server_under_sanitizers(tmp_path, san):
                TSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0 and "dht_server_test OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("san", ["address,undefined", "thread"])
+def test_rccl_registry_under_sanitizers(tmp_path, san):
+    if shutil.which("g++") is None:
+        pytest.skip("no host compiler")
+    exe = tmp_path / "rccl_core_test"
+    cmd = ["g++", "-std=c++17", "-O1", "-g", f"-fsanitize={san}", "-fno-omit-frame-pointer", "-pthread",
+           "-I", os.path.join(ROOT, "tests/native/stub_rccl"),
+           os.path.join(ROOT, "dedloc_amd/csrc/comm/comm_core.cpp"),
+           os.path.join(ROOT, "tests/native/rccl_core_test.cpp"), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in (r.stderr + r.stdout):
+        pytest.skip(f"sanitizer runtime for {san} not installed")
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1",
+               TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "rccl_core_test OK" in r.stdout, r.stdout + r.stderr

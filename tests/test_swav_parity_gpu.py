@@ -17,6 +17,8 @@ Reference: ``swav/vissl/vissl/losses/swav_loss.py:177-326``,
 import pytest
 import torch
 
+from conftest import record_margin
+
 pytestmark = pytest.mark.gpu
 
 CL = torch.channels_last
@@ -89,6 +91,13 @@ def test_full_swav_model_and_loss_match_fp32_twin(cuda):
     stock_err = _rel(torch.cat(stock_all), torch.cat(ref_all))
     print(f"loss ours {loss.item():.5f} fp32 {loss_r.item():.5f} bf16-stock {loss_s.item():.5f}; flat gradient "
           f"rel err ours {ours_err:.4f} stock bf16 {stock_err:.4f}")
+    head = [(n, o, s) for n, o, s in worst if n.startswith("heads.")]
+    record_margin("swav_model_and_loss_vs_fp32_twin", loss_ours=loss.item(), loss_fp32=loss_r.item(),
+                  loss_stock_bf16=loss_s.item(), loss_rel_delta=abs(loss.item() - loss_r.item()) / abs(loss_r.item()),
+                  loss_bound=1e-2, grad_rel_err_ours=ours_err, grad_rel_err_stock_bf16=stock_err,
+                  grad_bound=1.3 * stock_err + 5e-3,
+                  head_worst=max(((o, n) for n, o, _ in head), default=(0.0, None)),
+                  head_worst_ratio_to_stock=max((o / max(s, 1e-12) for _, o, s in head), default=0.0))
     assert ours_err < 1.3 * stock_err + 5e-3, (ours_err, stock_err)
     # the head (after the trunk's drift has been summed into 2048 features) tightly
     for n, o, s in worst:
@@ -138,10 +147,14 @@ def test_swav_training_curve_matches_eager_stack(cuda, tmp_path):
         print(f"SwAV loss, first 10 / last 20 steps: dedloc {first:.4f} / {last:.4f}, eager "
               f"{b[:10].mean().item():.4f} / {b[-20:].mean().item():.4f}; max |diff| {((a - b).abs().max()):.4f}")
         assert torch.isfinite(a).all() and torch.isfinite(b).all()
-        assert last < first - 0.05, (first, last)  # it trains
         # the band: 20-step running means within 2% of each other over the whole run
         ra = a.unfold(0, 20, 1).mean(1)
         rb = b.unfold(0, 20, 1).mean(1)
+        record_margin("swav_training_curve_vs_eager_stack", steps=steps, first10_ours=first, last20_ours=last,
+                      first10_eager=b[:10].mean().item(), last20_eager=b[-20:].mean().item(),
+                      max_abs_step_diff=(a - b).abs().max().item(),
+                      running_mean_max_rel_diff=((ra - rb).abs() / rb.abs()).max().item(), band=0.02)
+        assert last < first - 0.05, (first, last)  # it trains
         assert ((ra - rb).abs() / rb.abs()).max().item() < 0.02, ((ra - rb).abs() / rb.abs()).max().item()
     finally:
         for p in peers:
