@@ -398,151 +398,11 @@ __device__ __forceinline__ void fwd_tiles(const FwdCtx& c, int kt0, int kt1, int
   }
 }
 
-// Software-pipelined forward step (PIPE kernels, RING, 4 waves): iteration t runs the softmax of
-// S(t) (computed by the previous iteration) on the vector pipe while the matrix pipe computes
-// S(t+1) = K(t+1) Q^T, then O += V(t)^T P(t)^T.  In the plain loop every tile is QK^T MFMAs ->
-// softmax -> PV MFMAs, a chain in which one wave's MFMAs and its exponentials never overlap (the
-// softmax is as long as the MFMA work at head dim 64); here the QK^T MFMAs of the next tile are
-// independent of the exponentials they are interleaved with (sched_group_barrier: one MFMA, then a
-// group of vector instructions), so the matrix pipe runs under the softmax's issue.  Lean and
-// masked tiles share the body: a masked tile folds scale + bias into its scores first and then
-// exponentiates with scale 1.  The ring keeps one stage ahead (the stage of tile t+1 must have
-// landed at the top of iteration t: its K is read there).  For the last tile the "next" QK^T reads
-// a stale ring slot into registers nobody uses (no branch around the interleaved block).
-template <int QS>
-__device__ __forceinline__ void fwd_pipe_step(const FwdCtx& c, int t, int nt, const bf16x8 (&qf)[QS][4],
-                                              floatx16 (&o)[QS][2], float (&m)[QS], float (&l)[QS],
-                                              floatx16 (&sc)[QS][2], floatx16 (&sn)[QS][2], int r, int hh, int lane) {
-  if (t + 1 < nt) wait_stages<4>(t + 2 < nt ? 1 : 0, c.mb_g != nullptr);
-  __syncthreads();  // K(t+1) landed for every wave; every wave is done with slot (t-1) % NBUF
-  if (t + NBUF - 1 < nt) c.template issue<4>(t + NBUF - 1);
-  const uint8_t* Kc = c.smem + (t % NBUF) * STAGE;
-  const uint8_t* Vs = Kc + TILE_BYTES;
-  const uint8_t* Kn = c.smem + ((t + 1) % NBUF) * STAGE;
-  const float* mb = reinterpret_cast<const float*>(Kc + 2 * TILE_BYTES);
-  const bool masked = c.mb_g != nullptr || (t + 1) * 64 > c.kv_end;
-  float scl = c.sl2;
-  if (c.mb_g) {  // generic additive bias, staged with the tile
-#pragma unroll
-    for (int u = 0; u < QS; ++u)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sc[u][j][i] = fmaf(sc[u][j][i], c.sl2, mb[32 * j + crow(i, hh)]);
-    scl = 1.f;
-  } else if (masked) {  // the boundary tile of a key length
-    const int lim = c.kv_end - t * 64;
-#pragma unroll
-    for (int u = 0; u < QS; ++u)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          sc[u][j][i] = fmaf(sc[u][j][i], c.sl2, 32 * j + crow(i, hh) < lim ? 0.f : NEG_BIG);
-    scl = 1.f;
-  }
-  float nm[QS];
-#pragma unroll
-  for (int u = 0; u < QS; ++u) {
-    float mc[4];
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const floatx16& sv = sc[u][q4 >> 1];
-      const int o8 = (q4 & 1) * 8;
-      float v = vmax3(sv[o8], sv[o8 + 1], sv[o8 + 2]);
-      v = vmax3(v, sv[o8 + 3], sv[o8 + 4]);
-      v = vmax3(v, sv[o8 + 5], sv[o8 + 6]);
-      mc[q4] = v;
-    }
-    float mx = vmax3(vmax3(mc[0], mc[1], sc[u][0][7]), vmax3(mc[2], mc[3], sc[u][0][15]),
-                     vmax3(sc[u][1][7], sc[u][1][15], mc[0]));
-    mx = half_max(mx) * scl;
-    const bool grow = mx > m[u] + RESCALE_THR;
-    if (__ballot(grow) != 0) {
-      const float mn = grow ? mx : m[u];
-      const float alpha = __builtin_amdgcn_exp2f(m[u] - mn);
-      l[u] *= alpha;
-      m[u] = mn;
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[u][tt][i] *= alpha;
-    }
-    nm[u] = -m[u];
-  }
-  // ---- the interleaved block: exponentials of S(t) || K(t+1) fragment reads + QK^T MFMAs
-  // P(t) is packed to bf16 as soon as it is exponentiated: the fp32 scores die inside this block
-  float rsa[QS][8];
-  bf16x8 pb[QS][2][2];
-#pragma unroll
-  for (int u = 0; u < QS; ++u) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) rsa[u][k] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float pv = __builtin_amdgcn_exp2f(fmaf(sc[u][j][i], scl, nm[u]));
-        sc[u][j][i] = pv;
-        rsa[u][i & 7] += pv;
-      }
-      pb[u][j][0] = pack_acc(sc[u][j], 0);
-      pb[u][j][1] = pack_acc(sc[u][j], 1);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < QS; ++u)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sn[u][j][i] = 0.f;
-  // QS = 1 has the registers to read all eight K fragments up front (no LDS latency in front of
-  // any MFMA); QS = 2 reads them two ahead
-  constexpr int AHEAD = QS == 1 ? 8 : 2;
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 kfr = lds_row_frag(Kn, 32 * j + r, 2 * ks + hh);
-#pragma unroll
-      for (int u = 0; u < QS; ++u) sn[u][j] = mfma32(kfr, qf[u][ks], sn[u][j]);
-    }
-  // schedule: the K fragment reads ahead, then per MFMA a group of exponentials and VALU (one more
-  // fragment read every QS MFMAs while reads remain)
-  __builtin_amdgcn_sched_group_barrier(0x100, AHEAD, 0);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-#pragma unroll
-    for (int u = 0; u < QS; ++u) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 16 / QS, 0);
-    }
-    if (k < 8 - AHEAD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-  }
-#pragma unroll
-  for (int u = 0; u < QS; ++u) {
-    const float rs = ((rsa[u][0] + rsa[u][1]) + (rsa[u][2] + rsa[u][3])) +
-                     ((rsa[u][4] + rsa[u][5]) + (rsa[u][6] + rsa[u][7]));
-    l[u] += half_sum(rs);
-  }
-  // ---- O += V(t)^T P(t)^T
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt) {
-        const bf16x8 vfr = tr_operand(Vs, 32 * j + 16 * ss, hh, tt, lane);
-#pragma unroll
-        for (int u = 0; u < QS; ++u) o[u][tt] = mfma32(vfr, pb[u][j][ss], o[u][tt]);
-      }
-}
-
 // Block = NW waves x QS x 32 query rows of one (batch, head).  NW = 8 (ring only): one 512-query
 // block per head at S = 512, so K / V are staged once per head, and each SIMD's two waves belong
 // to one block.
-template <bool RING, int QS, int NW = 4, bool PIPE = false, int MINB = 2>
-__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : MINB) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
+template <bool RING, int QS, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, long ld,
                                                           const float* __restrict__ mbias,
                                                           const int* __restrict__ kvinfo, bf16_t* __restrict__ out,
                                                           long ldo, float* __restrict__ lse, int B, int H, int S,
@@ -610,40 +470,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : MINB) void attn_fwd_kernel(c
     if (threadIdx.x < 64) c.mbs[threadIdx.x] = mbr;
     __syncthreads();
   }
-  if constexpr (PIPE) {
-    static_assert(RING && NW == 4, "the pipelined forward runs on the 4-wave ring");
-    __syncthreads();
-    floatx16 sA[QS][2], sB[QS][2];
-    {
-      const uint8_t* K0 = smem;
-#pragma unroll
-      for (int u = 0; u < QS; ++u)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) sA[u][j][i] = 0.f;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8 kfr = lds_row_frag(K0, 32 * j + r, 2 * ks + hh);
-#pragma unroll
-          for (int u = 0; u < QS; ++u) sA[u][j] = mfma32(kfr, qf[u][ks], sA[u][j]);
-        }
-    }
-    int t = 0;
-    for (; t + 1 < nt; t += 2) {  // two steps per trip: the score buffers swap roles without copies
-      fwd_pipe_step<QS>(c, t, nt, qf, o, m, l, sA, sB, r, hh, lane);
-      fwd_pipe_step<QS>(c, t + 1, nt, qf, o, m, l, sB, sA, r, hh, lane);
-    }
-    if (t < nt) fwd_pipe_step<QS>(c, t, nt, qf, o, m, l, sA, sB, r, hh, lane);
-  } else {
-    // lean tiles first (every tile when there is no mask), then the masked remainder: the boundary
-    // tile of a length mask, or all tiles of a generic additive mask
-    const int nlean = c.mb_g ? 0 : c.kv_end / 64;
-    fwd_tiles<true, RING, QS, NW>(c, 0, nlean, nt, qf, o, m, l, r, hh, lane);
-    fwd_tiles<false, RING, QS, NW>(c, nlean, nt, nt, qf, o, m, l, r, hh, lane);
-  }
+  // lean tiles first (every tile when there is no mask), then the masked remainder: the boundary
+  // tile of a length mask, or all tiles of a generic additive mask
+  const int nlean = c.mb_g ? 0 : c.kv_end / 64;
+  fwd_tiles<true, RING, QS, NW>(c, 0, nlean, nt, qf, o, m, l, r, hh, lane);
+  fwd_tiles<false, RING, QS, NW>(c, nlean, nt, nt, qf, o, m, l, r, hh, lane);
 
 #pragma unroll
   for (int u = 0; u < QS; ++u) {
@@ -1109,21 +940,7 @@ int dl_attn_fwd(const bf16_t* qkv, long ld, const float* mbias, const int* kvinf
   // 4 waves x 2 query sub-blocks of 32 rows per wave, K/V staged by the LDS-DMA ring (it frees the
   // 16 staging VGPRs the second sub-block needs); 8-wave blocks measured 5% slower (round 2)
   dim3 grid((S + 255) / 256, H, B);
-  static const int pipe = [] {
-    const char* e = std::getenv("DEDLOC_ATTN_FWD_PIPE");
-    return e == nullptr ? 0 : std::atoi(e);
-  }();
-  if (pipe == 1)
-    attn_fwd_kernel<true, 2, 4, true><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2,
-                                                            kAttnXcd);
-  else if (pipe == 3)  // one block per CU: 512 registers for the two score buffers of QS = 2
-    attn_fwd_kernel<true, 2, 4, true, 1><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2,
-                                                               kAttnXcd);
-  else if (pipe == 2)
-    attn_fwd_kernel<true, 1, 4, true><<<dim3((S + 127) / 128, H, B), 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo,
-                                                                                  lse, B, H, S, sl2, kAttnXcd);
-  else
-    attn_fwd_kernel<true, 2><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, kAttnXcd);
+  attn_fwd_kernel<true, 2><<<grid, 256, 0, st>>>(qkv, ld, mbias, kvinfo, out, ldo, lse, B, H, S, sl2, kAttnXcd);
   return 0;
 }
 
