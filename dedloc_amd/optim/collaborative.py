@@ -452,8 +452,15 @@ class CollaborativeOptimizer:
                 or self._ready_within_slack(batch_size))
 
     def _imminent(self) -> bool:
-        return (self._prejoin is not None and self._prejoin_key is not None
-                and self._prejoin_key[0] == int(self.local_step))
+        """A prejoin made at this local step is pending, and this step has not waited yet: the wait
+        for the device happens at most once per global step (a slower collaboration would otherwise
+        keep the host from running ahead of the GPU on every following micro-step)."""
+        if self._prejoin is None or self._prejoin_key is None or self._prejoin_key[0] != int(self.local_step):
+            return False
+        if getattr(self, "_imminent_step", None) == int(self.local_step):
+            return False
+        self._imminent_step = int(self.local_step)
+        return True
 
     def _refresh_state(self):
         t_fetch = time.perf_counter()

@@ -148,3 +148,47 @@ def test_mixed_group_part_sizes():
     # a homogeneous group of undeclared peers splits evenly
     even = load_balance_peers(1000, DA.group_bandwidths([{"bandwidth": None}] * 2, [b"x", b"y"], None))
     assert even == (500, 500)
+
+
+def test_imminent_global_step_refreshes_the_view_instead_of_overshooting(collab, monkeypatch):
+    """A prejoin made for this step means this micro-step is expected to complete the batch: when
+    the (stale) view says "not ready", step() refreshes the collaboration view once (on a GPU after
+    waiting for the micro-step on the device) and runs the global step in the same call — instead
+    of returning and letting every peer queue one more micro-step past the target."""
+    co, flat = collab
+    seen = []
+    monkeypatch.setattr(co.averager, "step", lambda weight=1.0, prejoined=None, **kw: seen.append(prejoined))
+    monkeypatch.setattr(co.averager, "prejoin", lambda **kw: Future())  # no background matchmaking
+    fetches = []
+
+    def fetch():
+        fetches.append(1)
+        return _state(co, step=0, samples=8)  # the other peer's samples are visible now
+
+    monkeypatch.setattr(co, "fetch_collaboration_state", fetch)
+    co.collaboration_state = _state(co, step=0, samples=0)  # stale: nobody has reported yet
+    fut = Future()
+    co._prejoin, co._prejoin_key = fut, (0, time.monotonic())
+    flat.grad.fill_(1.0)
+    co.step(batch_size=4)
+    assert co.local_step == 1 and seen == [fut]
+    assert len(fetches) == 1  # the refresh doubles as the global step's fetch
+    # without a pending prejoin a stale "not ready" view simply returns (no refresh)
+    co._drop_prejoin()
+    co.collaboration_state = _state(co, step=1, samples=0)
+    co.step(batch_size=4)
+    assert co.local_step == 1 and len(fetches) == 1
+
+
+def test_imminent_wait_happens_once_per_global_step(collab, monkeypatch):
+    co, flat = collab
+    monkeypatch.setattr(co.averager, "step", lambda **kw: None)
+    fetches = []
+    monkeypatch.setattr(co, "fetch_collaboration_state",
+                        lambda: fetches.append(1) or _state(co, step=0, samples=0))  # never ready
+    co.target_batch_size = 100
+    co.collaboration_state = _state(co, step=0, samples=0)
+    co._prejoin, co._prejoin_key = Future(), (0, time.monotonic())
+    for _ in range(4):
+        co.step(batch_size=4)
+    assert co.local_step == 0 and len(fetches) == 1
