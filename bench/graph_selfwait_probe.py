@@ -60,9 +60,41 @@ CHILD = textwrap.dedent("""
     print("@@ ok", bool(torch.allclose(out, ref)), flush=True)
 """)
 
+# the SwAV peer itself, graphed, with the weight copies on the first side pass's stream (the r4
+# layout): "unguarded" restores plain wait_stream calls (self-waits included), "guarded" is the tree
+SWAV_CHILD = textwrap.dedent("""
+    import faulthandler, sys, torch
+    faulthandler.enable(all_threads=True)
+    sys.path.insert(0, ".")
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.models.resnet_swav import SwAVModel
+    from dedloc_amd.training.swav_peer import SwavPeer
+    from dedloc_amd.utils.config import load_config
+    if sys.argv[1] == "unguarded":
+        SwAVModel._wait = staticmethod(lambda a, b: a.wait_stream(b))
+    cfg = load_config("swav_1node_resnet_submit", [
+        "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=16", "config.DATA.TRAIN.SYNTHETIC_POOL_SIZE=32",
+        "config.OPTIMIZER.target_batch_size=64", "config.OPTIMIZER.batch_size_for_tracking=16",
+        "config.CHECKPOINT.DIR=/tmp/graph_probe_ckpt", "config.MODEL.CUDA_GRAPH=true",
+        "config.MODEL.CUDA_GRAPH_WARMUP=2"])
+    dht = DHT(start=True)
+    peer = SwavPeer(cfg, torch.device("cuda", 0), dht=dht)
+    peer.model.dgrad_weights_stream = "side"
+    for it in range(4):
+        loss = float(peer.train_step())
+        print("@@ iteration", it, "graphed" if peer._graphed is not None else "eager", round(loss, 4), flush=True)
+    peer.shutdown(); dht.shutdown()
+""")
+
 if __name__ == "__main__":
     for case in ("plain", "cross", "self"):
         r = subprocess.run([sys.executable, "-c", CHILD, case], capture_output=True, text=True, timeout=120)
+        print(f"case={case} rc={r.returncode}")
+        print(r.stdout.strip())
+        if r.returncode != 0:
+            print(r.stderr.strip()[-3000:])
+    for case in ("guarded", "unguarded"):
+        r = subprocess.run([sys.executable, "-c", SWAV_CHILD, case], capture_output=True, text=True, timeout=300)
         print(f"case={case} rc={r.returncode}")
         print(r.stdout.strip())
         if r.returncode != 0:

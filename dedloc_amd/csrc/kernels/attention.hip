@@ -17,6 +17,7 @@
 // chunk c of row r lives at chunk c ^ f((r>>1)&7), f(x) = x ^ ((x&1)<<2) — conflict-free for the
 // ds_read_b128 lane groups and for the 4-row tr-read blocks (derivation in docs/KERNELS.md).
 #include <cstdlib>
+#include <type_traits>
 
 #include "dl_common.h"
 #include "dl_kernels.h"
@@ -832,6 +833,12 @@ __global__ __launch_bounds__(256, KS == 2 ? 1 : 2) void attn_bwd_dkdv_kernel(
     __syncthreads();
   }
 
+  // LEAN (a key-length mask, the model's case): the mask term leaves the loop — a masked key's P
+  // is computed as if it were live and its dK / dV rows are zeroed once at the end (dK / dV of a
+  // key depend on that key's P and dS only); the generic additive mask keeps the bias in the
+  // exponent.
+  auto qloop = [&](auto lean_tag) {
+  constexpr bool LEAN = decltype(lean_tag)::value;
   for (int qt = 0; qt < nt; ++qt) {
     const uint8_t* Qs;
     const float* lse_s;
@@ -875,7 +882,9 @@ __global__ __launch_bounds__(256, KS == 2 ? 1 : 2) void attn_bwd_dkdv_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int qq = 32 * i2 + crow(i, hh);
-          const float p = __builtin_amdgcn_exp2f(sc[u][i] * sl2 + mbk[u] - lse_s[qq]);
+          // LEAN: one FMA per score (-lse is a free operand modifier)
+          const float p = __builtin_amdgcn_exp2f(LEAN ? fmaf(sc[u][i], sl2, -lse_s[qq])
+                                                      : sc[u][i] * sl2 + mbk[u] - lse_s[qq]);
           sc[u][i] = p;
           dp[u][i] = p * (dp[u][i] - del_s[qq]);
         }
@@ -908,6 +917,19 @@ __global__ __launch_bounds__(256, KS == 2 ? 1 : 2) void attn_bwd_dkdv_kernel(
       }
       __syncthreads();
     }
+  }
+  };
+  if (use_len) {
+    qloop(std::true_type{});
+#pragma unroll
+    for (int u = 0; u < KS; ++u)
+      if (k[u] >= kv_end)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dk[u][t][i] = dv[u][t][i] = 0.f;
+  } else {
+    qloop(std::false_type{});
   }
 #pragma unroll
   for (int u = 0; u < KS; ++u) {

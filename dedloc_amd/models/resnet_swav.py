@@ -611,7 +611,10 @@ class SwAVModel(nn.Module):
     # after the join: the update is affine, rm <- (1-m)^G rm + D, so the crop order is kept).
     concurrent_passes = False
     pass_splits = (1, 1)  # concurrent passes per resolution group (_pass_plan)
-    dgrad_weights_stream = True  # the data-gradient weights on a stream of their own (_trunk_concurrent)
+    # where _trunk_concurrent prepares the data-gradient weights: True = a stream of their own (the
+    # measured default), False = the main stream, "side" = the first side pass's stream (the layout
+    # whose graphed run crashed in round 4 through a self-wait; kept selectable for its test)
+    dgrad_weights_stream = True
 
     def bind_flat(self, flat):
         """Take the GEMM / conv weights of every forward from ``flat``'s bf16 mirror: one cast
@@ -676,6 +679,16 @@ class SwAVModel(nn.Module):
                 and all(g.is_contiguous(memory_format=torch.channels_last) and g.dtype == torch.bfloat16
                         for g, _ in passes))
 
+    @staticmethod
+    def _wait(a, b):
+        """``a.wait_stream(b)``, skipped when they are the same stream: a stream waiting on an event
+        it recorded itself is pointless eagerly, and inside a HIP-graph capture it is an event-record
+        node followed by a wait on it on the same captured stream (bench/graph_selfwait_probe.py;
+        the round-4 host crash of the graphed iteration had the weight copies on a side pass's stream,
+        which made that pass's stream wait on itself)."""
+        if a != b:
+            a.wait_stream(b)
+
     def _trunk_concurrent(self, passes):
         c = self._conc_state(len(passes) - 1)
         cur = torch.cuda.current_stream()
@@ -683,8 +696,9 @@ class SwAVModel(nn.Module):
         # the data-gradient weights (shared by every pass's backward, ~40 small copy kernels) on a
         # stream of their own, under the forward passes; each pass's stream waits for them behind its
         # forward
-        wprep = c["wprep"] if self.dgrad_weights_stream else cur
-        wprep.wait_stream(cur)
+        wprep = (c["passes"][0]["stream"] if self.dgrad_weights_stream == "side" else
+                 c["wprep"] if self.dgrad_weights_stream else cur)
+        self._wait(wprep, cur)
         with torch.cuda.stream(wprep):
             for m in convs:
                 _dgrad_weights(m, m._wb_cache, m.stride[0], m.padding[0])
@@ -695,7 +709,7 @@ class SwAVModel(nn.Module):
                     for st in users:
                         t.record_stream(st)
         for sp in c["passes"]:
-            sp["stream"].wait_stream(cur)
+            self._wait(sp["stream"], cur)
         # each pass's zeroed BN workspace on its own stream; every pass's counter increments in one
         # add on the weight stream (training never reads the counters: momentum is set)
         preps = []
@@ -708,7 +722,7 @@ class SwAVModel(nn.Module):
                                 sum(g for _, g in passes))
         self.set_bn_stat_groups(passes[0][1])
         feats = [self.trunk(passes[0][0], preps[0])]
-        cur.wait_stream(wprep)  # (behind pass 0's forward) its backward reads the data-gradient weights
+        self._wait(cur, wprep)  # (behind pass 0's forward) its backward reads the data-gradient weights
         bns = self.trunk._bn_modules()
         for (x, g), prep, sp in zip(passes[1:], preps[1:], c["passes"]):
             self.set_bn_stat_groups(g)
@@ -719,18 +733,18 @@ class SwAVModel(nn.Module):
             try:
                 with torch.cuda.stream(sp["stream"]):
                     feats.append(self.trunk(x, prep))
-                sp["stream"].wait_stream(wprep)
+                self._wait(sp["stream"], wprep)
             finally:
                 for m, _ in sp["slots"]:
                     m._gslot = None
                 for m in bns:
                     m._rs_override = None
         for f, sp in zip(feats[1:], c["passes"]):
-            cur.wait_stream(sp["stream"])
+            self._wait(cur, sp["stream"])
             f.record_stream(cur)
         # the side passes' running-statistics updates, in crop order, on the weight stream under the
         # head's forward (nothing in training reads them; SwAVModel.forward joins the stream)
-        wprep.wait_stream(cur)
+        self._wait(wprep, cur)
         with torch.cuda.stream(wprep), torch.no_grad():
             for (_, g), sp in zip(passes[1:], c["passes"]):
                 torch._foreach_mul_([m.running_mean for m in bns], [(1.0 - m.momentum) ** g for m in bns])
@@ -752,7 +766,7 @@ class SwAVModel(nn.Module):
             # side streams' work into a HIP-graph capture of the backward)
             cur = torch.cuda.current_stream()
             for sp in c["passes"]:
-                cur.wait_stream(sp["stream"])
+                self._wait(cur, sp["stream"])
             torch.ops.dedloc.add_slabs_zero_(self._flat.grad, c["grad_all"])
             c["pending"] = False
 
@@ -809,7 +823,7 @@ class SwAVModel(nn.Module):
         out = self.heads[0](torch.cat(feats))
         c = getattr(self, "_conc", None)
         if c is not None and c.get("join") is not None:  # the running-statistics merge (_trunk_concurrent)
-            torch.cuda.current_stream().wait_stream(c["join"])
+            self._wait(torch.cuda.current_stream(), c["join"])
             c["join"] = None
         return out
 

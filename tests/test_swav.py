@@ -436,6 +436,40 @@ def test_swav_peer_gpu_nan_check_is_async_and_stops(cuda, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", [False, "side"])
+def test_swav_graph_capture_stream_layouts(cuda, tmp_path, layout):
+    """HIP-graph capture of the concurrent trunk passes with the data-gradient weight copies on the
+    main stream (False) or on the first side pass's stream ("side": the round-4 layout whose first
+    graphed iteration crashed on the host — it made that stream wait on itself inside the capture,
+    which SwAVModel._wait now skips): the graphed iterations replay and match the eager peer."""
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.training.swav_peer import SwavPeer
+
+    peers, dhts = [], []
+    for graph in (False, True):
+        cfg = load_config("swav_1node_resnet_submit", [
+            "config.DATA.TRAIN.BATCHSIZE_PER_REPLICA=16", "config.DATA.TRAIN.SYNTHETIC_POOL_SIZE=32",
+            "config.OPTIMIZER.target_batch_size=64", "config.OPTIMIZER.batch_size_for_tracking=16",
+            f"config.CHECKPOINT.DIR={tmp_path}/{graph}", f"config.MODEL.CUDA_GRAPH={graph}",
+            "config.MODEL.CUDA_GRAPH_WARMUP=2"])
+        dhts.append(DHT(start=True))
+        peers.append(SwavPeer(cfg, cuda, dht=dhts[-1]))
+        peers[-1].model.dgrad_weights_stream = layout
+    try:
+        for it in range(4):  # iterations 2 and 3 replay the graphs (no LARC step in between)
+            crops = peers[0].data.next_batch()
+            la = float(peers[0].train_step([c.clone() for c in crops]))
+            lb = float(peers[1].train_step([c.clone() for c in crops]))
+            assert math.isfinite(la) and abs(la - lb) <= 2e-2 * abs(la), (it, la, lb)
+        assert peers[1]._graphed is not None
+    finally:
+        for p in peers:
+            p.shutdown()
+        for d in dhts:
+            d.shutdown()
+
+
+@pytest.mark.gpu
 def test_swav_peer_graph_matches_eager(cuda, tmp_path):
     """The graph-replayed iteration computes what the eager one does: two peers from the same
     initialisation, fed the same crops, with the queue active, through collaborative LARC steps
