@@ -69,3 +69,42 @@ def test_sahajbert_micro_step_has_no_host_sync(cuda):
     finally:
         torch.cuda.set_sync_debug_mode(prev)
     assert all(torch.isfinite(l).item() for l in losses)
+
+
+@pytest.mark.timeout(300)
+def test_collaborative_global_step_has_no_host_sync(cuda):
+    """A lone peer's micro-steps AND its global step (gradient divide by the device-side finite
+    count, LAMB, snapshot, device-timed PerformanceEMA) queue work without waiting for the GPU —
+    round 4 drained the queue at every global step to count finite samples on the host."""
+    from dedloc_amd.dht import DHT
+    from dedloc_amd.optim.collaborative import CollaborativeOptimizer
+    from dedloc_amd.optim.lamb import FusedLamb
+    from dedloc_amd.utils.flat import FlatParams
+
+    lin = torch.nn.Linear(256, 512).to(cuda)
+    flat = FlatParams(lin.named_parameters(), device=cuda)
+    opt = FusedLamb(flat, lr=1e-3)
+    dht = DHT(listen_on="127.0.0.1:*")
+    co = CollaborativeOptimizer(opt, dht=dht, prefix="nosync", target_batch_size=8, batch_size_per_step=4,
+                                start=False, listen_on="127.0.0.1:*", peer_id=b"solo")
+    try:
+        finite = torch.ones(1, device=cuda)
+        for _ in range(4):  # warm-up: cached device scalars, first global steps
+            flat.grad.normal_()
+            co.step(batch_size=4, finite=finite)
+        torch.cuda.synchronize()
+        step0 = co.local_step
+        torch.cuda.set_sync_debug_mode("error")
+        try:
+            for _ in range(4):
+                flat.grad.normal_()
+                co.step(batch_size=4, finite=finite)
+        finally:
+            torch.cuda.set_sync_debug_mode("default")
+        assert co.local_step == step0 + 2
+        torch.cuda.synchronize()
+        co._device_timer.poll()
+        assert co._device_timer.updates >= 4 and co.performance_ema.samples_per_second > 0
+    finally:
+        co.shutdown()
+        dht.shutdown()
