@@ -107,7 +107,11 @@ __device__ __forceinline__ void tile_store(const TileRegs& t, uint8_t* tile) {
 // XOR swizzle of chunk_off is applied to the SOURCE: lane i of 1-KiB piece p loads row 8p + i/8,
 // chunk (i & 7) ^ swz(row).
 typedef __attribute__((address_space(3))) void lds_void;
-constexpr int NBUF = 4;
+// Two stages: the next tile's DMA is issued at the top of the current tile and has a whole tile of
+// MFMA / softmax work to land (4 stages measured 1.3% slower forward, 0.5% slower dQ at B=512:
+// profiles/r5_attn_ring_depth_occupancy.jsonl); the dQ epilogue's column-sum scratch (33 KiB)
+// still fits the ring.
+constexpr int NBUF = 2;
 constexpr int STAGE = 2 * TILE_BYTES + 512;
 
 // The DMA instructions are issued from inline asm.  With __builtin_amdgcn_global_load_lds the
