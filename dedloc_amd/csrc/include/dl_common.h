@@ -41,9 +41,11 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 
 // Hardware f32 -> bf16 (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN), branch-free:
 // same results as f2bf for every input except the NaN payload bits.
+typedef float dl_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 dl_bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2_bf16(float a, float b) {
-  const __bf16 x = (__bf16)a, y = (__bf16)b;
-  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+  // one two-source v_cvt_pk_bf16_f32 (two scalar casts became two cvts and a v_or_b32_sdwa)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((dl_f32x2){a, b}, dl_bf16x2));
 }
 __device__ __forceinline__ float round_bf16(float a) { return (float)(__bf16)a; }
 __device__ __forceinline__ uint4 pack8_bf16(const float* v) {
@@ -108,35 +110,35 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
 }
 
-// gelu_new(x) = x * sigma(2u) = x / (1 + 2^(-2 u log2 e)): one exp2 + one rcp
-__device__ __forceinline__ float gelu_tanh_sig(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * x * fmaf(k1, x * x, 1.f);
-  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
+// gelu_new(x) = x * sigma(2u) = x / (1 + 2^(-2 u log2 e)), u = k0 (x + k1 x^3): one exp2 + one rcp.
+// The constants are folded: -2 u log2(e) = x (G0 + G1 x^2) with G0 = -2 log2(e) k0, G1 = G0 k1, and
+// 2 u' = D0 + D1 x^2 with D0 = 2 k0, D1 = 6 k0 k1 (three fewer VALU per value than the unfolded
+// products, which the compiler may not reassociate).
+constexpr float kGeluG0 = -2.302208198144325f, kGeluG1 = -0.1029432395800235f;
+constexpr float kGeluD0 = 1.5957691216057308f, kGeluD1 = 0.21406444881780076f;
+
+__device__ __forceinline__ float gelu_sig_s(float x, float x2) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(x * fmaf(kGeluG1, x2, kGeluG0)));
 }
 
-// gelu_new'(x) in the sigmoid form: gelu_new(x) = x * sigma(2u), u = k0 (x + k1 x^3), so
+__device__ __forceinline__ float gelu_tanh_sig(float x) { return x * gelu_sig_s(x, x * x); }
+
+// gelu_new'(x) in the sigmoid form: gelu_new(x) = x * sigma(2u), so
 // gelu_new'(x) = s + 2 x s (1 - s) u',  s = sigma(2u) = 1 / (1 + 2^(-2 u log2 e)):
-// one exp2 + one rcp and ~10 FMAs (the tanh form above needs ~15); same value to ~1e-7 relative.
+// one exp2 + one rcp and ~6 FMAs (the tanh form above needs ~15); same value to ~1e-7 relative.
 __device__ __forceinline__ float gelu_tanh_grad_sig(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
-  const float u = k0 * x * fmaf(k1, x2, 1.f);
-  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
-  const float du2 = (2.f * k0) * fmaf(3.f * k1, x2, 1.f);
-  return fmaf(x * du2, s - s * s, s);
+  const float s = gelu_sig_s(x, x2);
+  return fmaf(x * fmaf(kGeluD1, x2, kGeluD0), fmaf(-s, s, s), s);
 }
 
 // gelu_new and gelu_new' of one value sharing the exp2 / rcp (the FFN-up epilogue that stores the
 // derivative for the backward instead of the pre-activation)
 __device__ __forceinline__ void gelu_and_grad_sig(float x, float& g, float& d) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
-  const float u = k0 * x * fmaf(k1, x2, 1.f);
-  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
-  const float du2 = (2.f * k0) * fmaf(3.f * k1, x2, 1.f);
+  const float s = gelu_sig_s(x, x2);
   g = x * s;
-  d = fmaf(x * du2, s - s * s, s);
+  d = fmaf(x * fmaf(kGeluD1, x2, kGeluD0), fmaf(-s, s, s), s);
 }
 
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, T1):
