@@ -199,7 +199,6 @@ struct Args {
   const bf16_t* R; long ldr;     // residual (STORE) or pre-activation (DGELU)
   bf16_t* H; long ldh;           // pre-activation out (GELU)
   float* dbias;                  // column sums out (DGELU)
-  int nt;                        // non-temporal output stores (bf16 epilogues)
   float* stats; long stat_rows;  // EPI_STATS: [M / stat_rows][2N] column sums / sums of squares
   DlBnBwdEpi bn;                 // EPI_BNBWD operands (BN input, ReLU mask source, mean / rstd)
   int group_m;                   // tile order: column-major inside bands of group_m row blocks
@@ -455,140 +454,165 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   const int rch = lane & 7;   // 8-column chunk handled in the row phase
   const int rr = lane >> 3;   // row within a pass of 8 rows
   const int gn = n0 + colperm<BKO>(wn * 64 + rch * 8);
+  // Rows m0 + wm * 128 + qm * 64 + pass * 8 + rr: every global address is a per-lane base (row
+  // rbase, column gn, computed once) plus a wave-uniform row offset (scalar multiply), and the row
+  // bound is tested only in a tail tile (the per-pass 64-bit multiplies and exec-masked row checks
+  // were ~15% of the epilogue's VALU).
+  const int rbase = m0 + wm * 128 + rr;
+  const bool full = m0 + BM <= p.M;
 
-  // The residual (STORE) / pre-activation (DGELU) rows are read ahead: all 8 of a row half before
-  // its passes, and the next half's row j right after pass j consumed this half's — ahead of that
-  // pass's store.  Loaded inside each pass instead, every pass waited (vmcnt(0)) for its load's full
-  // HBM latency and, the counter being in issue order, for every store before it.
-  const bool has_r = EPI == EPI_DGELU || EPI == EPI_DMUL ||
-                     ((EPI == EPI_STORE || EPI == EPI_STATS || EPI == EPI_BNBWD) && p.R != nullptr);
   // EPI_BNBWD: this lane's eight columns of the tile's statistics group
   float bmu[8], brs[8], bsc[8], bsh[8];
   if constexpr (EPI == EPI_BNBWD) {
     const long go = (long)(m0 / p.stat_rows) * p.N;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = n0 + colperm<BKO>(wn * 64 + rch * 8) + j;
+      const int c = gn + j;
       bmu[j] = p.bn.mean[go + c];
       brs[j] = p.bn.rstd[go + c];
       bsc[j] = p.bn.Y ? 0.f : p.bn.gamma[c] * brs[j];
       bsh[j] = p.bn.Y ? 0.f : p.bn.beta[c] - bmu[j] * bsc[j];
     }
   }
-  auto rrow = [&](int qm, int pass) -> uint4 {
-    const int gm = min(m0 + wm * 128 + qm * 64 + pass * 8 + rr, p.M - 1);  // tail rows: clamped, unused
-    return *reinterpret_cast<const uint4*>(p.R + (long)gm * p.ldr + gn);
-  };
-  uint4 rbuf[8];
-  if (has_r) {
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) rbuf[pass] = rrow(0, pass);
-  }
 
+  // HR: a residual / pre-activation operand R is read.  Its rows are read ahead: all 8 of a row half
+  // before its passes, and the next half's row j right after pass j consumed this half's — ahead of
+  // that pass's store.  Loaded inside each pass instead, every pass waited (vmcnt(0)) for its load's
+  // full HBM latency and, the counter being in issue order, for every store before it.  Whether R is
+  // present is a template flag of the pass loop (a run-time flag turned every add into a select).
+  // per-lane row-rbase pointers of every operand the epilogue touches
+  bf16_t* const cb0 = EPI == EPI_F32 ? nullptr : p.C + (long)rbase * p.ldc + gn;
+  bf16_t* const hb0 = (EPI == EPI_GELU || EPI == EPI_GELUD) ? p.H + (long)rbase * p.ldh + gn : nullptr;
+  float* const fb0 = EPI == EPI_F32 ? p.Cf + (long)split * p.slab + (long)rbase * p.ldcf + gn : nullptr;
+  auto run = [&](auto hr_tag) {
+    constexpr bool HR = decltype(hr_tag)::value;
+    const bf16_t* rb0 = HR ? p.R + (long)rbase * p.ldr + gn : nullptr;
+    auto rrow = [&](int qm, int pass) -> uint4 {
+      const int off = qm * 64 + pass * 8;
+      const bf16_t* src = rb0 + (long)off * p.ldr;
+      if (!full) src = p.R + (long)min(rbase + off, p.M - 1) * p.ldr + gn;  // tail rows: clamped, unused
+      return *reinterpret_cast<const uint4*>(src);
+    };
+    uint4 rbuf[8];
+    if constexpr (HR) {
 #pragma unroll
-  for (int qm = 0; qm < 2; ++qm) {
+      for (int pass = 0; pass < 8; ++pass) rbuf[pass] = rrow(0, pass);
+    }
 #pragma unroll
-    for (int qn = 0; qn < 2; ++qn)
+    for (int qm = 0; qm < 2; ++qm) {
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
+        for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = mi * 16 + crow + i;
-            const int c = qn * 32 + ni * 16 + ccol;
-            const int q = (c >> 2) ^ (r & 1);
-            *reinterpret_cast<float*>(ep + r * 256 + q * 16 + (c & 3) * 4) = acc[qm][qn][mi][ni][i] + bias_v[qn][ni];
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = mi * 16 + crow + i;
+              const int c = qn * 32 + ni * 16 + ccol;
+              const int q = (c >> 2) ^ (r & 1);
+              *reinterpret_cast<float*>(ep + r * 256 + q * 16 + (c & 3) * 4) =
+                  acc[qm][qn][mi][ni][i] + bias_v[qn][ni];
+            }
+#pragma unroll
+      for (int pass = 0; pass < 8; ++pass) {
+        const int r = pass * 8 + rr;
+        const float4 lo = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch) ^ (r & 1)) << 4));
+        const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int off = qm * 64 + pass * 8;  // wave-uniform
+        float rv[8];
+        if constexpr (HR) {
+          unpack8_bf16(rbuf[pass], rv);
+          if (qm == 0) rbuf[pass] = rrow(1, pass);
+        }
+        if (full || rbase + off < p.M) {
+          if constexpr (EPI == EPI_STORE) {
+            if constexpr (HR) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += rv[j];
+            }
+            store8_bf16(cb0 + (long)off * p.ldc, v, true);
+          } else if constexpr (EPI == EPI_STATS) {
+            if constexpr (HR) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += rv[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              v[j] = round_bf16(v[j]);
+              colsum[j] += v[j];
+              colsq[j] = fmaf(v[j], v[j], colsq[j]);
+            }
+            store8_bf16(cb0 + (long)off * p.ldc, v, true);
+          } else if constexpr (EPI == EPI_BNBWD) {
+            float xv[8], yv[8];
+            const long xo = ((long)rbase + off) * p.bn.ldx + gn;
+            load_bf16<8>(p.bn.X + xo, xv);
+            if (p.bn.Y) load_bf16<8>(p.bn.Y + xo, yv);
+            if constexpr (HR) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] += rv[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const bool live = p.bn.Y ? yv[j] > 0.f : fmaf(xv[j], bsc[j], bsh[j]) > 0.f;
+              const float g = live ? round_bf16(v[j]) : 0.f;
+              v[j] = g;
+              colsum[j] += g;
+              colsq[j] = fmaf(g, (xv[j] - bmu[j]) * brs[j], colsq[j]);
+            }
+            store8_bf16(cb0 + (long)off * p.ldc, v, true);
+          } else if constexpr (EPI == EPI_GELU) {
+            float h[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
+            store8_bf16(hb0 + (long)off * p.ldh, h, true);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[j] = gelu_tanh_sig(h[j]);
+            store8_bf16(cb0 + (long)off * p.ldc, h, true);
+          } else if constexpr (EPI == EPI_GELUD) {
+            float g[8], d[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gelu_and_grad_sig(round_bf16(v[j]), g[j], d[j]);
+            store8_bf16(hb0 + (long)off * p.ldh, d, true);
+            store8_bf16(cb0 + (long)off * p.ldc, g, true);
+          } else if constexpr (EPI == EPI_DGELU) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(rv[j]));
+              colsum[j] += v[j];
+            }
+            store8_bf16(cb0 + (long)off * p.ldc, v, true);
+          } else if constexpr (EPI == EPI_DMUL) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              v[j] = round_bf16(round_bf16(v[j]) * rv[j]);
+              colsum[j] += v[j];
+            }
+            store8_bf16(cb0 + (long)off * p.ldc, v, true);
+          } else {
+            float* dst = fb0 + (long)off * p.ldcf;
+            if (p.accumulate) {
+              const float4 o0 = *reinterpret_cast<const float4*>(dst);
+              const float4 o1 = *reinterpret_cast<const float4*>(dst + 4);
+              v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
+              v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
+            }
+            *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<float4*>(dst + 4) = float4{v[4], v[5], v[6], v[7]};
           }
-#pragma unroll
-    for (int pass = 0; pass < 8; ++pass) {
-      const int r = pass * 8 + rr;
-      const float4 lo = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch) ^ (r & 1)) << 4));
-      const float4 hi = *reinterpret_cast<const float4*>(ep + r * 256 + (((2 * rch + 1) ^ (r & 1)) << 4));
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      const int gm = m0 + wm * 128 + qm * 64 + r;
-      float rv[8];
-      if (has_r) {
-        unpack8_bf16(rbuf[pass], rv);
-        if (qm == 0) rbuf[pass] = rrow(1, pass);
-      }
-      if (gm < p.M) {
-        if constexpr (EPI == EPI_STORE) {
-          if (has_r) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += rv[j];
-          }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
-        } else if constexpr (EPI == EPI_STATS) {
-          if (has_r) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += rv[j];
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(v[j]);
-            colsum[j] += v[j];
-            colsq[j] = fmaf(v[j], v[j], colsq[j]);
-          }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
-        } else if constexpr (EPI == EPI_BNBWD) {
-          float xv[8], yv[8];
-          load_bf16<8>(p.bn.X + (long)gm * p.bn.ldx + gn, xv);
-          if (p.bn.Y) load_bf16<8>(p.bn.Y + (long)gm * p.bn.ldx + gn, yv);
-          if (has_r) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] += rv[j];
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const bool live = p.bn.Y ? yv[j] > 0.f : fmaf(xv[j], bsc[j], bsh[j]) > 0.f;
-            const float g = live ? round_bf16(v[j]) : 0.f;
-            v[j] = g;
-            colsum[j] += g;
-            colsq[j] = fmaf(g, (xv[j] - bmu[j]) * brs[j], colsq[j]);
-          }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
-        } else if constexpr (EPI == EPI_GELU) {
-          float h[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = round_bf16(v[j]);
-          store8_bf16(p.H + (long)gm * p.ldh + gn, h, p.nt);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h[j] = gelu_tanh_sig(h[j]);
-          store8_bf16(p.C + (long)gm * p.ldc + gn, h, p.nt);
-        } else if constexpr (EPI == EPI_GELUD) {
-          float g[8], d[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) gelu_and_grad_sig(round_bf16(v[j]), g[j], d[j]);
-          store8_bf16(p.H + (long)gm * p.ldh + gn, d, p.nt);
-          store8_bf16(p.C + (long)gm * p.ldc + gn, g, p.nt);
-        } else if constexpr (EPI == EPI_DGELU) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(round_bf16(v[j]) * gelu_tanh_grad_sig(rv[j]));
-            colsum[j] += v[j];
-          }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
-        } else if constexpr (EPI == EPI_DMUL) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = round_bf16(round_bf16(v[j]) * rv[j]);
-            colsum[j] += v[j];
-          }
-          store8_bf16(p.C + (long)gm * p.ldc + gn, v, p.nt);
-        } else {
-          float* dst = p.Cf + (long)split * p.slab + (long)gm * p.ldcf + gn;
-          if (p.accumulate) {
-            const float4 o0 = *reinterpret_cast<const float4*>(dst);
-            const float4 o1 = *reinterpret_cast<const float4*>(dst + 4);
-            v[0] += o0.x; v[1] += o0.y; v[2] += o0.z; v[3] += o0.w;
-            v[4] += o1.x; v[5] += o1.y; v[6] += o1.z; v[7] += o1.w;
-          }
-          *reinterpret_cast<float4*>(dst) = float4{v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<float4*>(dst + 4) = float4{v[4], v[5], v[6], v[7]};
         }
       }
     }
+  };
+  if constexpr (EPI == EPI_DGELU || EPI == EPI_DMUL) {
+    run(std::true_type{});
+  } else if constexpr (EPI == EPI_STORE || EPI == EPI_STATS || EPI == EPI_BNBWD) {
+    if (p.R != nullptr) run(std::true_type{});
+    else run(std::false_type{});
+  } else {
+    run(std::false_type{});
   }
   if constexpr (EPI == EPI_DGELU || EPI == EPI_DMUL) {
     if (p.dbias) {
@@ -683,13 +707,11 @@ int dl_gemm8(int a_kouter, int b_kouter, int epi, const bf16_t* A, long lda, con
                              (!bn->Y && (!bn->gamma || !bn->beta))))
       return -1;
   }
-  // non-temporal bf16 output stores (+4..17% on the store-bound epilogues, gemm_bench)
-  constexpr int nt = 1;
   // tile order (tile_of): bands of 4 row blocks.  Against row-major at T = 262144 the QKV forward
   // 1507 -> 1468 us, FFN-up + GELU 2409 -> 2324 us, FFN-down data gradient 2027 -> 1970 us, the rest
   // within +-1.5% (profiles/r3_gemm8_tile_order_T262144.jsonl)
   constexpr int group_m = 4;
-  Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias, nt,
+  Args a{A, lda, B, ldb, M, N, K / splits, C, ldc, Cf, ldcf, slab, accumulate, bias, R, ldr, H, ldh, dbias,
          stats, stat_rows, DlBnBwdEpi{}, group_m};
   if (epi == EPI_BNBWD) a.bn = *bn;  // by value: the kernel reads it from its argument buffer
 #define DL_GEMM8_CASE(AK, BK_, E) \
