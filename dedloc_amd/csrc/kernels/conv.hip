@@ -176,6 +176,9 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   const int nk = p.K / BK;
   const int IJ = g.I * g.J;
   const int cofs = (tid & 7) * 8;
+  // float reciprocals for the per-lane pixel decodes (fdiv: exact below 2^24, checked on the host);
+  // an integer division by a run-time divisor is ~20 VALU, fdiv ~6
+  const float rIJ = 1.f / (float)IJ, rJ = 1.f / (float)g.J, rC = 1.f / (float)g.C, rTS = 1.f / (float)g.TS;
 
   // load cursor: per-thread decoded gathered rows of the tile being loaded
   int dec_tile = -1;
@@ -187,8 +190,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
     for (int u = 0; u < UA; ++u) {
       const int m = m0 + (tid >> 3) + 32 * u;
       if (m < p.M) {
-        const int n = m / IJ, r = m - n * IJ;
-        const int i = r / g.J, j = r - i * g.J;
+        const int n = fdiv(m, IJ, rIJ), r = m - n * IJ;
+        const int i = fdiv(r, g.J, rJ), j = r - i * g.J;
         hb[u] = i * g.sh;
         wb[u] = j * g.sw;
         nb[u] = n * g.H;
@@ -205,21 +208,50 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   const __amdgpu_buffer_rsrc_t rimg = make_rsrc(g.img, p.img_bytes);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, p.w_bytes);
   const int nsteps = mytiles * nk;
+  // Step cursor: load_step is called for s = 0, 1, 2, ... in order, so the step's tile, its k0 and
+  // (non-SUB) the tap (tr, ts) and channel offset of k0 advance incrementally — the K loop divides
+  // by nothing (four run-time divisions per step were ~100 VALU beside 32 MFMAs per wave).
+  int cur_s = -1, cur_tile = tile0, cur_kk = 0, cur_c0 = 0, cur_t = 0, cur_tr = 0, cur_ts = 0;
+  auto advance = [&]() {
+    if (cur_s < 0) {
+      cur_s = 0;
+      return;
+    }
+    ++cur_s;
+    if (++cur_kk == nk) {
+      cur_kk = 0;
+      ++cur_tile;
+      cur_c0 = cur_t = cur_tr = cur_ts = 0;
+    } else if (!SUB) {
+      cur_c0 += BK;  // C is a multiple of BK: one tap per C / BK steps
+      if (cur_c0 == g.C) {
+        cur_c0 = 0;
+        ++cur_t;
+        if (++cur_ts == g.TS) {
+          cur_ts = 0;
+          ++cur_tr;
+        }
+      }
+    }
+  };
   // stage step s (clamped: steps past the end reload the last one; staged, never computed)
   auto load_step = [&](StageN<UA>& sa, StageN<UB>& sb, int s) {
-    s = min(s, nsteps - 1);
-    const int tile = tile0 + s / nk, k0 = (s % nk) * BK;
+    if (cur_s < min(s, nsteps - 1)) advance();
+    const int tile = cur_tile, k0 = cur_kk * BK;
     if (tile != dec_tile) decode(tile);
-    int t, cc;  // tap and channel offset of this thread's chunk
+    int t, cc, tr, ts;  // tap and channel offset of this thread's chunk
     if constexpr (SUB) {
       const int kk = k0 + cofs;
-      t = kk / g.C;
+      t = fdiv(kk, g.C, rC);
       cc = kk - t * g.C;
+      tr = fdiv(t, g.TS, rTS);
+      ts = t - tr * g.TS;
     } else {
-      t = k0 / g.C;
-      cc = k0 - t * g.C + cofs;
+      t = cur_t;
+      cc = cur_c0 + cofs;
+      tr = cur_tr;
+      ts = cur_ts;
     }
-    const int tr = t / g.TS, ts = t - tr * g.TS;
     const int dh = g.dh0 + tr * g.dhs, dw = g.dw0 + ts * g.dws;
 #pragma unroll
     for (int u = 0; u < UA; ++u) {
@@ -302,8 +334,8 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
       const int m = m0 + row, ch = n0 + c * 8;
       uint4 v = *reinterpret_cast<const uint4*>(stage + row * (CPR * 16) + ((c ^ (row & (CPR - 1))) << 4));
       if (m < p.M && ch < p.N) {
-        const int n = m / IJ, r = m - n * IJ;
-        const int i = r / g.J, j = r - i * g.J;
+        const int n = fdiv(m, IJ, rIJ), r = m - n * IJ;
+        const int i = fdiv(r, g.J, rJ), j = r - i * g.J;
         const long pix = (long)(n * p.OH + i * p.osh + p.oh0) * p.OW + j * p.osw + p.ow0;
         bf16_t* orow = p.out + pix * p.ldo;
         if (p.bnbwd) {  // g = dY masked by the BN's ReLU; the BN backward's two sums
@@ -386,16 +418,23 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   st_kin_n(xb, buf0 + AIMG);
   load_step(xa, xb, 2);
   __syncthreads();
+  int ekk = 0, etile = tile0;  // k-step and tile of the step being computed
   for (int s = 0; s < nsteps; s += 2) {
     compute(buf0);  // step s
-    if (s % nk == nk - 1) epilogue(tile0 + s / nk, buf1);  // buf1: drained, not yet restaged
+    if (++ekk == nk) {
+      epilogue(etile++, buf1);  // buf1: drained, not yet restaged
+      ekk = 0;
+    }
     st_kin_n(ya, buf1);
     st_kin_n(yb, buf1 + AIMG);
     load_step(ya, yb, s + 3);
     __syncthreads();
     if (s + 1 < nsteps) {
       compute(buf1);  // step s + 1
-      if ((s + 1) % nk == nk - 1) epilogue(tile0 + (s + 1) / nk, buf0);
+      if (++ekk == nk) {
+        epilogue(etile++, buf0);
+        ekk = 0;
+      }
     }
     st_kin_n(xa, buf0);
     st_kin_n(xb, buf0 + AIMG);
@@ -799,7 +838,7 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
   const long M = (long)g.Nimg * g.I * g.J;
   // statistics: every 128-row tile inside one group, whole 8-channel chunks
   if (stats && (stat_rows < BM || stat_rows % BM || M % stat_rows || N % 8)) return -1;
-  if (M >= (1L << 31)) return -1;
+  if (M >= (1L << 24)) return -1;  // fdiv exactness bound (pixel decodes)
   if (M == 0 || N == 0) return 0;
   const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * ldw;
   if (img_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
