@@ -468,10 +468,11 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = gn + j;
-      bmu[j] = p.bn.mean[go + c];
+      const float mu = p.bn.mean[go + c];
       brs[j] = p.bn.rstd[go + c];
+      bmu[j] = -mu * brs[j];  // xhat = x * rstd + bmu
       bsc[j] = p.bn.Y ? 0.f : p.bn.gamma[c] * brs[j];
-      bsh[j] = p.bn.Y ? 0.f : p.bn.beta[c] - bmu[j] * bsc[j];
+      bsh[j] = p.bn.Y ? 0.f : p.bn.beta[c] - mu * bsc[j];
     }
   }
 
@@ -484,8 +485,9 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   bf16_t* const cb0 = EPI == EPI_F32 ? nullptr : p.C + (long)rbase * p.ldc + gn;
   bf16_t* const hb0 = (EPI == EPI_GELU || EPI == EPI_GELUD) ? p.H + (long)rbase * p.ldh + gn : nullptr;
   float* const fb0 = EPI == EPI_F32 ? p.Cf + (long)split * p.slab + (long)rbase * p.ldcf + gn : nullptr;
-  auto run = [&](auto hr_tag) {
-    constexpr bool HR = decltype(hr_tag)::value;
+  // HY (EPI_BNBWD): the ReLU mask comes from the BN output Y (a residual branch) instead of from X
+  auto run = [&](auto hr_tag, auto hy_tag) {
+    constexpr bool HR = decltype(hr_tag)::value, HY = decltype(hy_tag)::value;
     const bf16_t* rb0 = HR ? p.R + (long)rbase * p.ldr + gn : nullptr;
     auto rrow = [&](int qm, int pass) -> uint4 {
       const int off = qm * 64 + pass * 8;
@@ -549,18 +551,20 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
             float xv[8], yv[8];
             const long xo = ((long)rbase + off) * p.bn.ldx + gn;
             load_bf16<8>(p.bn.X + xo, xv);
-            if (p.bn.Y) load_bf16<8>(p.bn.Y + xo, yv);
+            if constexpr (HY) load_bf16<8>(p.bn.Y + xo, yv);
             if constexpr (HR) {
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] += rv[j];
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              const bool live = p.bn.Y ? yv[j] > 0.f : fmaf(xv[j], bsc[j], bsh[j]) > 0.f;
+              // xhat = (x - mean) rstd = x * brs + bxh (bxh = -mean * rstd: one FMA)
+              const float xh = fmaf(xv[j], brs[j], bmu[j]);
+              const bool live = HY ? yv[j] > 0.f : fmaf(xv[j], bsc[j], bsh[j]) > 0.f;
               const float g = live ? round_bf16(v[j]) : 0.f;
               v[j] = g;
               colsum[j] += g;
-              colsq[j] = fmaf(g, (xv[j] - bmu[j]) * brs[j], colsq[j]);
+              colsq[j] = fmaf(g, xh, colsq[j]);
             }
             store8_bf16(cb0 + (long)off * p.ldc, v, true);
           } else if constexpr (EPI == EPI_GELU) {
@@ -606,13 +610,23 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
       }
     }
   };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
   if constexpr (EPI == EPI_DGELU || EPI == EPI_DMUL) {
-    run(std::true_type{});
-  } else if constexpr (EPI == EPI_STORE || EPI == EPI_STATS || EPI == EPI_BNBWD) {
-    if (p.R != nullptr) run(std::true_type{});
-    else run(std::false_type{});
+    run(T_{}, F_{});
+  } else if constexpr (EPI == EPI_BNBWD) {
+    if (p.R != nullptr) {
+      if (p.bn.Y) run(T_{}, T_{});
+      else run(T_{}, F_{});
+    } else {
+      if (p.bn.Y) run(F_{}, T_{});
+      else run(F_{}, F_{});
+    }
+  } else if constexpr (EPI == EPI_STORE || EPI == EPI_STATS) {
+    if (p.R != nullptr) run(T_{}, F_{});
+    else run(F_{}, F_{});
   } else {
-    run(std::false_type{});
+    run(F_{}, F_{});
   }
   if constexpr (EPI == EPI_DGELU || EPI == EPI_DMUL) {
     if (p.dbias) {
