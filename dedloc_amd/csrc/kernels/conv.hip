@@ -322,10 +322,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
       const long go = (long)(m0 / p.stat_rows) * p.N + ch0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        bmu[e] = p.bn.mean[go + e];
+        const float mu = p.bn.mean[go + e];
         brs[e] = p.bn.rstd[go + e];
+        bmu[e] = -mu * brs[e];  // xhat = x * rstd + bmu
         bsc[e] = p.bn.Y ? 0.f : p.bn.gamma[ch0 + e] * brs[e];
-        bsh[e] = p.bn.Y ? 0.f : p.bn.beta[ch0 + e] - bmu[e] * bsc[e];
+        bsh[e] = p.bn.Y ? 0.f : p.bn.beta[ch0 + e] - mu * bsc[e];
       }
     }
 #pragma unroll
@@ -342,14 +343,21 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
           float f[8], xv[8], yv[8];
           unpack8_bf16(v, f);
           load_bf16<8>(p.bn.X + pix * p.bn.ldx + ch, xv);
-          if (p.bn.Y) load_bf16<8>(p.bn.Y + pix * p.bn.ldx + ch, yv);
+          bool live[8];
+          if (p.bn.Y) {  // uniform: the mask source is chosen once, not per element
+            load_bf16<8>(p.bn.Y + pix * p.bn.ldx + ch, yv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) live[e] = yv[e] > 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) live[e] = fmaf(xv[e], bsc[e], bsh[e]) > 0.f;
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const bool live = p.bn.Y ? yv[e] > 0.f : fmaf(xv[e], bsc[e], bsh[e]) > 0.f;
-            const float gg = live ? f[e] : 0.f;  // f is bf16 already: the masked store is exact
+            const float gg = live[e] ? f[e] : 0.f;  // f is bf16 already: the masked store is exact
             f[e] = gg;
             csum[e] += gg;
-            csq[e] = fmaf(gg, (xv[e] - bmu[e]) * brs[e], csq[e]);
+            csq[e] = fmaf(gg, fmaf(xv[e], brs[e], bmu[e]), csq[e]);
           }
           v = pack8_bf16(f);
           *reinterpret_cast<uint4*>(orow + ch) = v;
