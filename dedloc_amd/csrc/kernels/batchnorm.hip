@@ -273,18 +273,29 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
                                                              bf16_t* __restrict__ dres, float* __restrict__ dgamma,
                                                              float* __restrict__ dbeta, long R, int C, int relu,
                                                              int accumulate, const float* __restrict__ beta) {
-  __shared__ float k1[2048], mg[2048], mgx[2048], mu_s[2048], rs_s[2048], sh_s[2048];
+  // dx = k1 (g - mg - xhat mgx), xhat = (x - mu) rs, folded per channel into dx = ca g + cb x + cc
+  // (two FMAs and three table reads per element instead of five reads and ~6 VALU).  The LDS
+  // footprint stays 6 x 2048 floats on purpose: BN blocks that take less of the CU crowd out the
+  // concurrent trunk pass's conv workgroups (round 4, r4_ab_bn_dynamic_lds_folded.jsonl).
+  __shared__ float tab[6 * 2048];
+  float* ca = tab;
+  float* cb = tab + 2048;
+  float* cc = tab + 2 * 2048;
+  float* k1 = tab + 3 * 2048;
+  float* sh_s = tab + 4 * 2048;
   const bool xmask = relu && beta != nullptr;  // ReLU mask from x (see bn_bwd_stats_kernel)
   const int grp = blockIdx.y, G = gridDim.y;
   const float invR = 1.f / (float)R;
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float* sg = sums + (long)grp * 2 * C;
-    rs_s[c] = rstd[(long)grp * C + c];
-    mu_s[c] = mean[(long)grp * C + c];
-    k1[c] = gamma[c] * rs_s[c];
-    if (xmask) sh_s[c] = beta[c] - mu_s[c] * k1[c];
-    mg[c] = sg[c] * invR;
-    mgx[c] = sg[C + c] * invR;
+    const float rs = rstd[(long)grp * C + c], mu = mean[(long)grp * C + c];
+    const float kk = gamma[c] * rs, mg = sg[c] * invR, mgx = sg[C + c] * invR;
+    k1[c] = kk;
+    if (xmask) sh_s[c] = beta[c] - mu * kk;
+    ca[c] = kk;
+    cb[c] = -kk * rs * mgx;
+    cc[c] = kk * (rs * mgx * mu - mg);
+    tab[5 * 2048 + c] = 0.f;  // keeps the sixth table (and the block's LDS size) live
     if (blockIdx.x == 0 && grp == 0) {  // parameter grads: sum over the statistics groups
       float db = 0.f, dg = 0.f;
       for (int k = 0; k < G; ++k) {
@@ -335,8 +346,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int c = c0 + j;
-        const float xh = (xv[u][j] - mu_s[c]) * rs_s[c];
-        o[j] = k1[c] * (g[u][j] - mg[c] - xh * mgx[c]);
+        o[j] = fmaf(ca[c], g[u][j], fmaf(cb[c], xv[u][j], cc[c]));
       }
       store_bf16<8>(dx + iv * 8, o);
     }
@@ -360,8 +370,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + j;
-      const float xh = (xv[j] - mu_s[c]) * rs_s[c];
-      o[j] = k1[c] * (g[j] - mg[c] - xh * mgx[c]);
+      o[j] = fmaf(ca[c], g[j], fmaf(cb[c], xv[j], cc[c]));
     }
     store_bf16<8>(dx + i * 8, o);
   }
