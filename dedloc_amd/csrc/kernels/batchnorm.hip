@@ -82,7 +82,8 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------------------------- forward apply
-template <int BN_U>
+// HR / RL: residual input / ReLU, template flags (as run-time flags they were per-element selects)
+template <int BN_U, bool HR, bool RL>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __restrict__ x,
                                                             const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
                                                             const float* __restrict__ sums,
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
   const long nvec = R * CV, base = (long)grp * R * C;
   x += base;
   y += base;
-  if (res != nullptr) res += base;
+  if (HR) res += base;
   // CV is a power of two (bn_shape_ok), so the channel of vector i is i & (CV - 1); two vectors per
   // iteration keep two independent load chains in flight per thread
   const long stride = (long)gridDim.x * kThreads;
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       ld8(x + (i + u * stride) * 8, v[u]);
-      if (res != nullptr) ld8(res + (i + u * stride) * 8, rr[u]);
+      if (HR) ld8(res + (i + u * stride) * 8, rr[u]);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
@@ -142,8 +143,8 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float o = fmaf(v[u][j], sc[c0 + j], sh[c0 + j]);
-        if (res != nullptr) o += rr[u][j];
-        v[u][j] = relu && o < 0.f ? 0.f : o;  // NaN passes, as torch.relu
+        if (HR) o += rr[u][j];
+        v[u][j] = RL && o < 0.f ? 0.f : o;  // NaN passes, as torch.relu
       }
       store_bf16<8>(y + (i + u * stride) * 8, v[u]);
     }
@@ -153,12 +154,12 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
     float v[8];
     ld8(x + i * 8, v);
     float rr[8];
-    if (res != nullptr) ld8(res + i * 8, rr);
+    if (HR) ld8(res + i * 8, rr);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(v[j], sc[c0 + j], sh[c0 + j]);
-      if (res != nullptr) o += rr[j];
-      v[j] = relu && o < 0.f ? 0.f : o;
+      if (HR) o += rr[j];
+      v[j] = RL && o < 0.f ? 0.f : o;
     }
     store_bf16<8>(y + i * 8, v);
   }
@@ -169,7 +170,8 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(const bf16_t* __rest
 // pre-activation fmaf(x, gamma*rstd, beta - mean*gamma*rstd) > 0 — the forward's own expression over
 // the saved mean / rstd — so with `beta` given the backward passes read dy and x only (2 of 3
 // streams; with a residual the mask depends on it and y is read).
-template <int BN_U>
+// MK: ReLU mask source, template flag — 0 none, 1 from x (beta given), 2 from y
+template <int BN_U, int MK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __restrict__ dy,
                                                                 const bf16_t* __restrict__ y,
                                                                 const bf16_t* __restrict__ x,
@@ -191,15 +193,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
   rstd += (long)blockIdx.y * C;
   sums += (long)blockIdx.y * 2 * C;
   const long r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
-  float mu[8], rs[8], sc[8], sh[8];
-  const bool xmask = relu && beta != nullptr;
+  float mu[8], rs[8], sc[8], sh[8];  // mu: -mean * rstd (xhat = x * rs + mu)
+  constexpr bool xmask = MK == 1;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    mu[j] = mean[cv * 8 + j];
+    const float m = mean[cv * 8 + j];
     rs[j] = rstd[cv * 8 + j];
+    mu[j] = -m * rs[j];
     if (xmask) {
       sc[j] = gamma[cv * 8 + j] * rs[j];
-      sh[j] = beta[cv * 8 + j] - mu[j] * sc[j];
+      sh[j] = beta[cv * 8 + j] - m * sc[j];
     }
   }
   float sg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sgx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -211,17 +214,17 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
       const long off = (r + u * rpi) * C + cv * 8;
       ld8(dy + off, g[u]);
       ld8(x + off, xv[u]);
-      if (relu && !xmask) ld8(y + off, yv[u]);
+      if (MK == 2) ld8(y + off, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const bool live = !relu || (xmask ? fmaf(xv[u][j], sc[j], sh[j]) > 0.f : yv[u][j] > 0.f);
+        const bool live = MK == 0 || (MK == 1 ? fmaf(xv[u][j], sc[j], sh[j]) > 0.f : yv[u][j] > 0.f);
         const float gg = live ? g[u][j] : 0.f;
         g[u][j] = gg;
         sg[j] += gg;
-        sgx[j] = fmaf(gg, (xv[u][j] - mu[j]) * rs[j], sgx[j]);
+        sgx[j] = fmaf(gg, fmaf(xv[u][j], rs[j], mu[j]), sgx[j]);
       }
       if (gout != nullptr) store_bf16<8>(gout + (r + u * rpi) * C + cv * 8, g[u]);
     }
@@ -231,10 +234,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
     float g[8], xv[8];
     ld8(dy + off, g);
     ld8(x + off, xv);
-    if (xmask) {
+    if (MK == 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
-    } else if (relu) {
+    } else if (MK == 2) {
       float yv[8];
       ld8(y + off, yv);
 #pragma unroll
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       sg[j] += g[j];
-      sgx[j] = fmaf(g[j], (xv[j] - mu[j]) * rs[j], sgx[j]);
+      sgx[j] = fmaf(g[j], fmaf(xv[j], rs[j], mu[j]), sgx[j]);
     }
     if (gout != nullptr) store_bf16<8>(gout + off, g);
   }
@@ -420,8 +423,17 @@ int dl_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma,
     bn_stats_kernel<<<dim3(nb, G), kThreads, 0, st>>>(x, sums, R, C, rpb);
   }
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
-  DL_BN_LAUNCH(bn_apply_kernel, dim3(na, G), x, res, y, sums, gamma, beta, mean, rstd, run_mean, run_var, R, C,
-                                                    eps, momentum, relu);
+#define DL_BN_APPLY(HR_, RL_)                                                                             \
+  bn_apply_kernel<2, HR_, RL_><<<dim3(na, G), kThreads, 0, st>>>(x, res, y, sums, gamma, beta, mean, rstd, run_mean, \
+                                                                 run_var, R, C, eps, momentum, relu)
+  if (res) {
+    if (relu) DL_BN_APPLY(true, true);
+    else DL_BN_APPLY(true, false);
+  } else {
+    if (relu) DL_BN_APPLY(false, true);
+    else DL_BN_APPLY(false, false);
+  }
+#undef DL_BN_APPLY
   return 0;
 }
 
@@ -441,8 +453,10 @@ int dl_bn_bwd_prep(bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* me
   if (!bn_shape_ok(C) || R < 1 || G < 1 || (!y && !beta)) return -1;
   long rpb;
   const int nb = stats_blocks(R, C, rpb);
-  DL_BN_LAUNCH(bn_bwd_stats_kernel, dim3(nb, G), dy, y, x, mean, rstd, sums, R, C, rpb, 1, gamma,
-                                                         y ? nullptr : beta, dy);
+  if (y) bn_bwd_stats_kernel<2, 2><<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, 1, gamma,
+                                                                     nullptr, dy);
+  else bn_bwd_stats_kernel<2, 1><<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, 1, gamma,
+                                                                   beta, dy);
   return 0;
 }
 
@@ -458,8 +472,14 @@ int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* m
   if (!stats_ready) {  // else: a data-gradient epilogue (or dl_bn_bwd_prep) accumulated the sums and
                        // already masked dy by the ReLU (the caller then passes relu = 0)
     if (!sums_zeroed) DL_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 2 * C * G, st));
-    DL_BN_LAUNCH(bn_bwd_stats_kernel, dim3(nb, G), dy, y, x, mean, rstd, sums, R, C, rpb, relu, gamma, beta,
-                                                           nullptr);
+    const int mk = !relu ? 0 : beta != nullptr ? 1 : 2;
+#define DL_BN_BSTATS(MK_)                                                                                    \
+  bn_bwd_stats_kernel<2, MK_><<<dim3(nb, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, sums, R, C, rpb, relu, gamma, \
+                                                                beta, nullptr)
+    if (mk == 0) DL_BN_BSTATS(0);
+    else if (mk == 1) DL_BN_BSTATS(1);
+    else DL_BN_BSTATS(2);
+#undef DL_BN_BSTATS
   }
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
   DL_BN_LAUNCH(bn_bwd_dx_kernel, dim3(na, G), dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
