@@ -265,7 +265,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const bf16_t* __
 }
 
 // ---------------------------------------------------------------------------------- backward dx
-template <int BN_U>
+// MK: ReLU mask source (0 none, 1 from x, 2 from y); HD: the residual gradient dres is stored
+template <int BN_U, int MK, bool HD>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ y,
                                                              const bf16_t* __restrict__ x,
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
   float* cc = tab + 2 * 2048;
   float* k1 = tab + 3 * 2048;
   float* sh_s = tab + 4 * 2048;
-  const bool xmask = relu && beta != nullptr;  // ReLU mask from x (see bn_bwd_stats_kernel)
+  constexpr bool xmask = MK == 1;  // ReLU mask from x (see bn_bwd_stats_kernel)
   const int grp = blockIdx.y, G = gridDim.y;
   const float invR = 1.f / (float)R;
   for (int c = threadIdx.x; c < C; c += kThreads) {
@@ -319,8 +320,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
   dy += base;
   x += base;
   dx += base;
-  if (y != nullptr) y += base;
-  if (dres != nullptr) dres += base;
+  if (MK == 2) y += base;
+  if (HD) dres += base;
   const int CV = C >> 3;
   const long nvec = R * CV;
   const long stride = (long)gridDim.x * kThreads;
@@ -331,20 +332,20 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
     for (int u = 0; u < BN_U; ++u) {
       ld8(dy + (i + u * stride) * 8, g[u]);
       ld8(x + (i + u * stride) * 8, xv[u]);
-      if (relu && !xmask) ld8(y + (i + u * stride) * 8, yv[u]);
+      if (MK == 2) ld8(y + (i + u * stride) * 8, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < BN_U; ++u) {
       const long iv = i + u * stride;
       const int c0 = ((int)iv & (CV - 1)) * 8;
-      if (xmask) {
+      if (MK == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[u][j] = fmaf(xv[u][j], k1[c0 + j], sh_s[c0 + j]) > 0.f ? g[u][j] : 0.f;
-      } else if (relu) {
+      } else if (MK == 2) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[u][j] = yv[u][j] > 0.f ? g[u][j] : 0.f;
       }
-      if (dres != nullptr) store_bf16<8>(dres + iv * 8, g[u]);
+      if (HD) store_bf16<8>(dres + iv * 8, g[u]);
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -359,16 +360,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
     float g[8], xv[8];
     ld8(dy + i * 8, g);
     ld8(x + i * 8, xv);
-    if (xmask) {
+    if (MK == 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], k1[c0 + j], sh_s[c0 + j]) > 0.f ? g[j] : 0.f;
-    } else if (relu) {
+    } else if (MK == 2) {
       float yv[8];
       ld8(y + i * 8, yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
     }
-    if (dres != nullptr) store_bf16<8>(dres + i * 8, g);
+    if (HD) store_bf16<8>(dres + i * 8, g);
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -379,9 +380,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const bf16_t* __res
   }
 }
 
-// streaming kernels with 2 rows in flight per thread (4 measured slower in round 3: 2186 / 2191 vs
-// 2212 / 2203 samples/s)
-#define DL_BN_LAUNCH(KERNEL, GRID, ...) KERNEL<2><<<GRID, kThreads, 0, st>>>(__VA_ARGS__)
+// the streaming kernels run with BN_U = 2 rows in flight per thread (4 measured slower in round 3:
+// 2186 / 2191 vs 2212 / 2203 samples/s)
 
 inline bool bn_shape_ok(int C) {
   if (C % 8 || C > 2048) return false;
@@ -482,7 +482,19 @@ int dl_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* m
 #undef DL_BN_BSTATS
   }
   const int na = (apply_blocks(R * (C / 8) * G) + G - 1) / G;
-  DL_BN_LAUNCH(bn_bwd_dx_kernel, dim3(na, G), dy, y, x, mean, rstd, gamma, sums, dx, dres, dgamma, dbeta, R, C,
-                                                     relu, accumulate, beta);
+  const int mkd = !relu ? 0 : beta != nullptr ? 1 : 2;
+#define DL_BN_DX(MK_, HD_)                                                                                   \
+  bn_bwd_dx_kernel<2, MK_, HD_><<<dim3(na, G), kThreads, 0, st>>>(dy, y, x, mean, rstd, gamma, sums, dx, dres,    \
+                                                                  dgamma, dbeta, R, C, relu, accumulate, beta)
+  if (dres) {
+    if (mkd == 0) DL_BN_DX(0, true);
+    else if (mkd == 1) DL_BN_DX(1, true);
+    else DL_BN_DX(2, true);
+  } else {
+    if (mkd == 0) DL_BN_DX(0, false);
+    else if (mkd == 1) DL_BN_DX(1, false);
+    else DL_BN_DX(2, false);
+  }
+#undef DL_BN_DX
   return 0;
 }
