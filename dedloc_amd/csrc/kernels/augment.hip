@@ -23,6 +23,15 @@ constexpr int MAX_RAD = 16;
 
 __device__ __forceinline__ float lum(float r, float g, float b) { return 0.299f * r + 0.587f * g + 0.114f * b; }
 
+// a / b for 0 <= a < 2^24 through the float reciprocal rb = 1 / b (+-1 correction): ~6 VALU against
+// ~20 for an integer division by a run-time divisor
+__device__ __forceinline__ int fdiv(int a, int b, float rb) {
+  int q = (int)((float)a * rb);
+  const int r = a - q * b;
+  q += (r >= b) - (r < 0);
+  return q;
+}
+
 __global__ __launch_bounds__(256) void mc_sample_kernel(const float* __restrict__ pool, int P, int Hp, int Wp,
                                                          const float* __restrict__ prm, int S,
                                                          float* __restrict__ out, float* __restrict__ lumsum) {
@@ -35,8 +44,9 @@ __global__ __launch_bounds__(256) void mc_sample_kernel(const float* __restrict_
   const float* src = pool + (long)si * 3 * plane;
   float l = 0.f;
   if (p < S * S) {
-    const int yy = p / S, xx = p - yy * S;
-    const float xn = (2.f * xx + 1.f) / S - 1.f, yn = (2.f * yy + 1.f) / S - 1.f;
+    const float rS = 1.f / (float)S;
+    const int yy = fdiv(p, S, rS), xx = p - yy * S;
+    const float xn = (2.f * xx + 1.f) * rS - 1.f, yn = (2.f * yy + 1.f) * rS - 1.f;
     const float xs = pr[1] * xn + pr[2], ys = pr[3] * yn + pr[4];
     float ix = ((xs + 1.f) * Wp - 1.f) * 0.5f, iy = ((ys + 1.f) * Hp - 1.f) * 0.5f;
     ix = fminf(fmaxf(ix, 0.f), (float)(Wp - 1));
@@ -97,8 +107,9 @@ __global__ __launch_bounds__(256) void mc_color_blur_norm_kernel(const float* __
   const float gm = br * lumsum[i] / (float)HW;
   const float* M = pr + 10;
   const float* src = a + (size_t)i * 3 * HW;
+  const float rS = 1.f / (float)S;
   for (int idx = threadIdx.x; idx < rows * S; idx += blockDim.x) {
-    const int r = idx / S, x = idx - r * S;
+    const int r = fdiv(idx, S, rS), x = idx - r * S;
     const size_t o = (size_t)reflect(y0 - hr + r, S) * S + x;
     float R = src[o], G = src[HW + o], B = src[2 * HW + o];
     if (col) {
@@ -131,7 +142,7 @@ __global__ __launch_bounds__(256) void mc_color_blur_norm_kernel(const float* __
   const float inv = 1.f / ws;
   // horizontal pass (reflect at the row ends) into the second image
   for (int idx = threadIdx.x; idx < rows * S; idx += blockDim.x) {
-    const int r = idx / S, x = idx - r * S;
+    const int r = fdiv(idx, S, rS), x = idx - r * S;
     float acc[3] = {0.f, 0.f, 0.f};
     for (int k = 0; k <= 2 * rad; ++k) {
       const int xs = r * S + reflect(x + k - rad, S);
