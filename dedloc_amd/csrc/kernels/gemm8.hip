@@ -236,7 +236,9 @@ __device__ __forceinline__ void tile_of(int bid, int tiles_m, int tiles_n, int G
 // PRESRC: DMA source addresses from per-lane bases computed once (src_base / stage_pre)
 template <bool AKO, bool BKO, int EPI, bool PRESRC>
 __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM];
+  // EPI_BNBWD: + [4][256] fp32 BatchNorm coefficients of the tile's columns (read per pass from LDS
+  // instead of holding 32 registers, which pay for reading the BN input one pass ahead)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[SMEM + (EPI == EPI_BNBWD ? 4096 : 0)];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = w >> 2, wn = w & 3;
@@ -432,6 +434,19 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   }
 #undef DL_STAGE
   if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: every wave passes the same barriers
+  float* const bnt = reinterpret_cast<float*>(smem + SMEM);  // EPI_BNBWD: [brs | bxh | bsc | bsh][256]
+  if constexpr (EPI == EPI_BNBWD) {
+    if (threadIdx.x < BN) {  // tile column t -> global column n0 + colperm(t)
+      const int t = threadIdx.x, c = n0 + colperm<BKO>(t);
+      const long go = (long)(m0 / p.stat_rows) * p.N;
+      const float mu = p.bn.mean[go + c], rs = p.bn.rstd[go + c];
+      const float sc = p.bn.Y ? 0.f : p.bn.gamma[c] * rs;
+      bnt[t] = rs;
+      bnt[BN + t] = -mu * rs;  // xhat = x * rstd + bxh
+      bnt[2 * BN + t] = sc;
+      bnt[3 * BN + t] = p.bn.Y ? 0.f : p.bn.beta[c] - mu * sc;
+    }
+  }
   __builtin_amdgcn_s_barrier();               // all fragment reads done before the epilogue reuses LDS
 
   // ---------------------------------------------------------------- epilogue
@@ -461,20 +476,7 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
   const int rbase = m0 + wm * 128 + rr;
   const bool full = m0 + BM <= p.M;
 
-  // EPI_BNBWD: this lane's eight columns of the tile's statistics group
-  float bmu[8], brs[8], bsc[8], bsh[8];
-  if constexpr (EPI == EPI_BNBWD) {
-    const long go = (long)(m0 / p.stat_rows) * p.N;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = gn + j;
-      const float mu = p.bn.mean[go + c];
-      brs[j] = p.bn.rstd[go + c];
-      bmu[j] = -mu * brs[j];  // xhat = x * rstd + bmu
-      bsc[j] = p.bn.Y ? 0.f : p.bn.gamma[c] * brs[j];
-      bsh[j] = p.bn.Y ? 0.f : p.bn.beta[c] - mu * bsc[j];
-    }
-  }
+  const int tc8 = wn * 64 + rch * 8;  // EPI_BNBWD: this lane's 8 tile columns in bnt
 
   // HR: a residual / pre-activation operand R is read.  Its rows are read ahead: all 8 of a row half
   // before its passes, and the next half's row j right after pass j consumed this half's — ahead of
@@ -499,6 +501,17 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
     if constexpr (HR) {
 #pragma unroll
       for (int pass = 0; pass < 8; ++pass) rbuf[pass] = rrow(0, pass);
+    }
+    // EPI_BNBWD: the BN input (and output) rows are read one pass ahead
+    auto xoff = [&](int k) {  // pass k of the 16 (qm = k / 8)
+      int row = rbase + (k >> 3) * 64 + (k & 7) * 8;
+      if (!full) row = min(row, p.M - 1);
+      return (long)row * p.bn.ldx + gn;
+    };
+    uint4 xq, yq;
+    if constexpr (EPI == EPI_BNBWD) {
+      xq = *reinterpret_cast<const uint4*>(p.bn.X + xoff(0));
+      if constexpr (HY) yq = *reinterpret_cast<const uint4*>(p.bn.Y + xoff(0));
     }
 #pragma unroll
     for (int qm = 0; qm < 2; ++qm) {
@@ -548,10 +561,27 @@ __global__ __launch_bounds__(NT, 2) void gemm8_kernel(Args p) {
             }
             store8_bf16(cb0 + (long)off * p.ldc, v, true);
           } else if constexpr (EPI == EPI_BNBWD) {
-            float xv[8], yv[8];
-            const long xo = ((long)rbase + off) * p.bn.ldx + gn;
-            load_bf16<8>(p.bn.X + xo, xv);
-            if constexpr (HY) load_bf16<8>(p.bn.Y + xo, yv);
+            float xv[8], yv[8], brs[8], bmu[8], bsc[8], bsh[8];
+            unpack8_bf16(xq, xv);
+            if constexpr (HY) unpack8_bf16(yq, yv);
+            const int kn = qm * 8 + pass + 1;
+            if (kn < 16) {
+              xq = *reinterpret_cast<const uint4*>(p.bn.X + xoff(kn));
+              if constexpr (HY) yq = *reinterpret_cast<const uint4*>(p.bn.Y + xoff(kn));
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const float4 a = *reinterpret_cast<const float4*>(bnt + tc8 + 4 * h);
+              const float4 b = *reinterpret_cast<const float4*>(bnt + BN + tc8 + 4 * h);
+              brs[4 * h] = a.x; brs[4 * h + 1] = a.y; brs[4 * h + 2] = a.z; brs[4 * h + 3] = a.w;
+              bmu[4 * h] = b.x; bmu[4 * h + 1] = b.y; bmu[4 * h + 2] = b.z; bmu[4 * h + 3] = b.w;
+              if constexpr (!HY) {
+                const float4 c4 = *reinterpret_cast<const float4*>(bnt + 2 * BN + tc8 + 4 * h);
+                const float4 d4 = *reinterpret_cast<const float4*>(bnt + 3 * BN + tc8 + 4 * h);
+                bsc[4 * h] = c4.x; bsc[4 * h + 1] = c4.y; bsc[4 * h + 2] = c4.z; bsc[4 * h + 3] = c4.w;
+                bsh[4 * h] = d4.x; bsh[4 * h + 1] = d4.y; bsh[4 * h + 2] = d4.z; bsh[4 * h + 3] = d4.w;
+              }
+            }
             if constexpr (HR) {
 #pragma unroll
               for (int j = 0; j < 8; ++j) v[j] += rv[j];
