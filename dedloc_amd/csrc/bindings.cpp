@@ -1248,6 +1248,8 @@ bool conv_dgrad_classes(const at::Tensor& dy, const at::Tensor& wk, int64_t stri
         if (I > 0 && J > 0 && (N / groups * I * J) % 256) return false;
       }
   }
+  std::vector<DlConvFwdJob> jobs;
+  std::vector<at::Tensor> keep;  // per-class weights alive until the launch
   for (int64_t a = 0; a < stride; ++a) {
     const int64_t I = (H - a + stride - 1) / stride;
     const int64_t r0 = (a + pad) % stride, TR = r0 < R ? (R - 1 - r0) / stride + 1 : 0;
@@ -1269,11 +1271,21 @@ bool conv_dgrad_classes(const at::Tensor& dy, const at::Tensor& wk, int64_t stri
           wd = wk.slice(1, r0, R, stride).slice(2, s0, S, stride).permute({3, 1, 2, 0}).contiguous();
         }
       }
-      check(dl_conv_fwd(geom(cbf(dy), N, P, Q, K, I, J, 1, 1, TR, TS, dh0, -1, dw0, -1), cbf(wd),
-                        std::max<int64_t>(8, TR * TS * K), (int)C, bf(dx), (int)H, (int)W, (int)stride, (int)stride,
-                        (int)a, (int)b, C, cur_stream(dy), bn ? sums : nullptr, bn ? N / groups * I * J : 0, bn),
-            "conv2d_dgrad");
+      keep.push_back(wd);
+      jobs.push_back(DlConvFwdJob{geom(cbf(dy), N, P, Q, K, I, J, 1, 1, TR, TS, dh0, -1, dw0, -1), cbf(wd),
+                                  std::max<int64_t>(8, TR * TS * K), (int)a, (int)b, bn ? N / groups * I * J : 0});
     }
+  }
+  // every parity class in one launch (the classes' grids back to back left most CUs idle: stride-2
+  // 3x3 data gradients ran at half the forward's speed); per-class launches when the classes need
+  // different kernel variants
+  const hipStream_t st = cur_stream(dy);
+  if (!jobs.empty() && dl_conv_fwd_multi(jobs.data(), (int)jobs.size(), (int)C, bf(dx), (int)H, (int)W, (int)stride,
+                                         (int)stride, C, st, bn ? sums : nullptr, bn) != 0) {
+    for (const DlConvFwdJob& jb : jobs)
+      check(dl_conv_fwd(jb.g, jb.w, jb.ldw, (int)C, bf(dx), (int)H, (int)W, (int)stride, (int)stride, jb.oh0, jb.ow0, C,
+                        st, bn ? sums : nullptr, jb.stat_rows, bn),
+            "conv2d_dgrad");
   }
   return true;
 }

@@ -137,6 +137,18 @@ struct DlConvGeom {
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
                 int oh0, int ow0, long ldo, hipStream_t st, float* stats = nullptr, long stat_rows = 0,
                 const DlBnBwdEpi* bn = nullptr);  // bn (needs stats): BN-backward preparation epilogue
+// several independent forward jobs (same output tensor / channel count / epilogue, e.g. the parity
+// classes of a strided data gradient) in ONE launch; at most 4 jobs, all of one kernel variant
+// (-1 and nothing launched otherwise)
+struct DlConvFwdJob {
+  DlConvGeom g;
+  const bf16_t* w;
+  long ldw;
+  int oh0, ow0;
+  long stat_rows;
+};
+int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, int OH, int OW, int osh, int osw,
+                      long ldo, hipStream_t st, float* stats = nullptr, const DlBnBwdEpi* bn = nullptr);
 // dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols; the pixel
 // reduction is split over workgroups that add their partial tiles with fp32 atomics)
 int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,

@@ -135,6 +135,19 @@ struct FwdArgs {
                    // `stats` receives its two column sums (sum g, sum g * xhat)
 };
 
+// One launch over up to MAXJ independent jobs of the same kernel variant (the stride^2 parity
+// classes of a strided data gradient: four quarter-size grids launched back to back left the GPU
+// three-quarters idle in each).  Dispatch-order workgroups [wg_begin[c], wg_begin[c+1]) run job c,
+// each job's range a multiple of 8 long so that the XCD remap applies inside it (a remap over the
+// whole grid would put each job on a contiguous quarter of the XCDs); the job index is
+// wave-uniform, so its arguments stay scalar loads.
+constexpr int MAXJ = 4;
+struct FwdMulti {
+  FwdArgs a[MAXJ];
+  int wg_begin[MAXJ + 1];
+  int n;
+};
+
 // Tile shapes: TM_ x TN_ = 128 x 128 (four 64 x 64 waves as 2 x 2) or 256 x 64 (4 x 1) for
 // outputs of at most 64 channels — the 64-channel 3x3 convs of the first stage would leave half of
 // a 128-wide channel tile empty.  The per-wave MFMA work is the same 64 x 64 in both.
@@ -154,9 +167,21 @@ __device__ __forceinline__ void st_kin_n(const StageN<U>& s, uint8_t* img) {
 
 // SUB: C < 64 (a divisor of 64, multiple of 8): a 64-deep k-step spans 64 / C taps, so each thread
 // decodes the tap of its own 8-channel chunk (the space-to-depth stem: C = 16, 4 x 4 taps)
-template <int TM_, int TN_, bool SUB = false>
-__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
+// MULTI: the launch holds several jobs (FwdMulti); otherwise a[0] only, with static argument
+// offsets (a run-time job index in every launch cost the forward 3-4%)
+template <int TM_, int TN_, bool SUB = false, bool MULTI = false>
+__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(const FwdMulti P) {
   constexpr int WN = TN_ / 64, UA = TM_ / 32, UB = TN_ / 32;
+  int job = 0, bid;
+  if constexpr (MULTI) {
+    const int b = blockIdx.x;
+#pragma unroll
+    for (int q = 1; q < MAXJ; ++q) job += (q < P.n && b >= P.wg_begin[q]);
+    bid = xcd_remap(b - P.wg_begin[job], P.wg_begin[job + 1] - P.wg_begin[job]);
+  } else {
+    bid = xcd_remap(blockIdx.x, gridDim.x);
+  }
+  const FwdArgs& p = P.a[MULTI ? job : 0];
   constexpr int CPR = TN_ / 8;            // 16-byte chunks per staged output row
   constexpr int AIMG = TM_ * 128;         // A image bytes (64 k per row)
   constexpr int SBYTES = (TM_ + TN_) * 128;
@@ -170,7 +195,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs p) {
   // persistent over `tpw` consecutive output tiles (same pixel rows, successive channel blocks
   // first): the load stream runs on across tile boundaries, so short-K convs (1x1 over 64-256
   // channels: 1-4 k-steps per tile) keep loads in flight under the previous tile's MFMAs/epilogue
-  const int tile0 = xcd_remap(blockIdx.x, gridDim.x) * p.tpw;
+  const int tile0 = bid * p.tpw;
   const int mytiles = min(p.tpw, ntiles - tile0);
   if (mytiles <= 0) return;
   const int nk = p.K / BK;
@@ -837,29 +862,60 @@ void set_lds(Kern k) {
 
 }  // namespace
 
-int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows, const DlBnBwdEpi* bn) {
-  const bool sub = g.C < BK;  // C in {8, 16, 32}: several taps per k-step (SUB kernels)
-  if ((sub ? (BK % g.C || g.C % 8) : g.C % BK) || N % 4 || ldw % 8 || ldo % 4 || g.I < 0 || g.J < 0) return -1;
-  if (sub && (bn || (g.TR * g.TS * g.C) % BK)) return -1;
+int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, int OH, int OW, int osh, int osw,
+                      long ldo, hipStream_t st, float* stats, const DlBnBwdEpi* bn) {
+  if (njobs < 1 || njobs > MAXJ || N % 4 || ldo % 4) return -1;
   if (bn && (!stats || !bn->X || bn->ldx % 8 || (!bn->Y && (!bn->gamma || !bn->beta)))) return -1;
-  const long M = (long)g.Nimg * g.I * g.J;
-  // statistics: every 128-row tile inside one group, whole 8-channel chunks
-  if (stats && (stat_rows < BM || stat_rows % BM || M % stat_rows || N % 8)) return -1;
-  if (M >= (1L << 24)) return -1;  // fdiv exactness bound (pixel decodes)
-  if (M == 0 || N == 0) return 0;
-  const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * ldw;
-  if (img_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
-  // outputs of at most 64 channels: 256 x 64 tiles (the 128-wide channel tile would be half empty;
-  // SwAV b=64 2015 / 2037 -> 2058 / 2055 samples/s in round 3)
-  const bool narrow = N <= 64 && (!stats || stat_rows % 256 == 0);
-  const int TMv = narrow ? 256 : BM, TNv = narrow ? 64 : BN;
-  const int tiles = (int)((M + TMv - 1) / TMv) * ((N + TNv - 1) / TNv);
-  // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
-  const int tpw = std::max(1, tiles / 1024);
-  FwdArgs a{g, w, ldw, N, out, OH, OW, osh, osw, oh0, ow0, ldo, (int)M, g.TR * g.TS * g.C,
-            (unsigned)img_bytes, (unsigned)w_bytes, tpw, stats, stat_rows, bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0};
-  const int lds = 2 * (TMv + TNv) * 128;
+  // validate every job before anything launches (-1: nothing ran); all jobs must take one variant
+  int variant = -1;
+  long tiles[MAXJ];
+  long total = 0;
+  for (int c = 0; c < njobs; ++c) {
+    const DlConvGeom& g = jobs[c].g;
+    const long stat_rows = jobs[c].stat_rows;
+    const bool sub = g.C < BK;  // C in {8, 16, 32}: several taps per k-step (SUB kernels)
+    if ((sub ? (BK % g.C || g.C % 8) : g.C % BK) || jobs[c].ldw % 8 || g.I < 0 || g.J < 0) return -1;
+    if (sub && (bn || (g.TR * g.TS * g.C) % BK)) return -1;
+    const long M = (long)g.Nimg * g.I * g.J;
+    // statistics: every 128-row tile inside one group, whole 8-channel chunks
+    if (stats && M > 0 && (stat_rows < BM || stat_rows % BM || M % stat_rows || N % 8)) return -1;
+    if (M >= (1L << 24)) return -1;  // fdiv exactness bound (pixel decodes)
+    const long img_bytes = 2L * g.Nimg * g.H * g.W * g.C, w_bytes = 2L * N * jobs[c].ldw;
+    if (img_bytes >= (1L << 31) || w_bytes >= (1L << 31)) return -1;  // 32-bit buffer offsets
+    // outputs of at most 64 channels: 256 x 64 tiles (the 128-wide channel tile would be half
+    // empty; SwAV b=64 2015 / 2037 -> 2058 / 2055 samples/s in round 3)
+    const bool narrow = N <= 64 && (!stats || stat_rows % 256 == 0);
+    const int v = 2 * sub + narrow;
+    tiles[c] = 0;
+    if (M == 0 || N == 0) continue;
+    if (variant >= 0 && v != variant) return -1;
+    variant = v;
+    const int TMv = narrow ? 256 : BM, TNv = narrow ? 64 : BN;
+    tiles[c] = ((M + TMv - 1) / TMv) * ((N + TNv - 1) / TNv);
+    total += tiles[c];
+  }
+  if (total == 0) return 0;
+  if (total >= (1L << 31)) return -1;
+  // several jobs: one launch (stride-2 data gradients, SwAV b=64 shapes: 1022 -> 799 us per
+  // iteration over the 12 strided convs, every shape faster; profiles/r5_conv_dgrad_merged_classes.jsonl)
+  const bool multi = njobs > 1;
+  FwdMulti P{};
+  int wg = 0;
+  auto launch = [&]() {
+    const bool sub = variant & 2, narrow = variant & 1;
+    const int lds = 2 * ((narrow ? 256 : BM) + (narrow ? 64 : BN)) * 128;
+    const dim3 grid(wg);
+    if (multi) {
+      if (narrow) conv_fwd_kernel<256, 64, false, true><<<grid, NT, lds, st>>>(P);
+      else conv_fwd_kernel<BM, BN, false, true><<<grid, NT, lds, st>>>(P);
+    } else if (sub) {
+      if (narrow) conv_fwd_kernel<256, 64, true><<<grid, NT, lds, st>>>(P);
+      else conv_fwd_kernel<BM, BN, true><<<grid, NT, lds, st>>>(P);
+    } else {
+      if (narrow) conv_fwd_kernel<256, 64><<<grid, NT, lds, st>>>(P);
+      else conv_fwd_kernel<BM, BN><<<grid, NT, lds, st>>>(P);
+    }
+  };
   static bool attr = false;
   if (!attr) {
     DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN>,
@@ -870,17 +926,41 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
     DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64, true>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, false, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
+    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64, false, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
     attr = true;
   }
-  const dim3 grid((tiles + tpw - 1) / tpw);
-  if (sub) {
-    if (narrow) conv_fwd_kernel<256, 64, true><<<grid, NT, lds, st>>>(a);
-    else conv_fwd_kernel<BM, BN, true><<<grid, NT, lds, st>>>(a);
-  } else {
-    if (narrow) conv_fwd_kernel<256, 64><<<grid, NT, lds, st>>>(a);
-    else conv_fwd_kernel<BM, BN><<<grid, NT, lds, st>>>(a);
+  if (multi && (variant & 2)) return -1;  // no SUB job-indexed kernel (data gradients have C >= 64)
+  for (int c = 0; c < njobs; ++c) {
+    if (tiles[c] == 0) continue;
+    const DlConvFwdJob& jb = jobs[c];
+    // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
+    const int tpw = (int)std::max<long>(1, tiles[c] / 1024);
+    const DlConvGeom& g = jb.g;
+    FwdArgs& a = P.a[P.n];
+    a = FwdArgs{g, jb.w, jb.ldw, N, out, OH, OW, osh, osw, jb.oh0, jb.ow0, ldo, g.Nimg * g.I * g.J, g.TR * g.TS * g.C,
+                (unsigned)(2L * g.Nimg * g.H * g.W * g.C), (unsigned)(2L * N * jb.ldw), tpw, stats, jb.stat_rows,
+                bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0};
+    P.wg_begin[P.n++] = wg;
+    const int jw = (int)((tiles[c] + tpw - 1) / tpw);
+    wg += multi ? (jw + 7) / 8 * 8 : jw;  // surplus workgroups find no tile and return
+    P.wg_begin[P.n] = wg;
+    if (!multi) {  // this job alone
+      launch();
+      P = FwdMulti{};
+      wg = 0;
+    }
   }
+  if (multi) launch();
   return 0;
+}
+
+int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
+                int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows, const DlBnBwdEpi* bn) {
+  const DlConvFwdJob job{g, w, ldw, oh0, ow0, stat_rows};
+  return dl_conv_fwd_multi(&job, 1, N, out, OH, OW, osh, osw, ldo, st, stats, bn);
 }
 
 // Split count of dl_conv_wgrad: the (long) pixel reduction is split so that ~`target` workgroups
