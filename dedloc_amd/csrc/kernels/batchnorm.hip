@@ -401,9 +401,13 @@ inline int stats_blocks(long R, int C, long& rpb) {
   return (int)((R + rpb - 1) / rpb);
 }
 
+#ifndef DL_BN_APPLY_MAXB
+#define DL_BN_APPLY_MAXB 2048  // (a measurement build may override)
+#endif
 inline int apply_blocks(long nvec) {
+  constexpr long cap = DL_BN_APPLY_MAXB;
   long g = (nvec + kThreads - 1) / kThreads;
-  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+  return (int)(g < cap ? (g < 1 ? 1 : g) : cap);
 }
 
 }  // namespace
