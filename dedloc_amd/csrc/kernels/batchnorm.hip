@@ -401,8 +401,12 @@ inline int stats_blocks(long R, int C, long& rpb) {
   return (int)((R + rpb - 1) / rpb);
 }
 
+// Grid cap of the streaming apply / dx kernels.  SwAV runs its resolution passes concurrently, and
+// every BN block beyond what saturates HBM takes CU slots from the other pass's convs: SwAV b=64
+// iteration +1.8% at 768 vs 2048 (512: +0.1%, 1024: +1.1%, 4096: -1.7%; same-box A/Bs,
+// profiles/r5_swav_grid_caps_ab.jsonl)
 #ifndef DL_BN_APPLY_MAXB
-#define DL_BN_APPLY_MAXB 2048  // (a measurement build may override)
+#define DL_BN_APPLY_MAXB 768  // (a measurement build may override)
 #endif
 inline int apply_blocks(long nvec) {
   constexpr long cap = DL_BN_APPLY_MAXB;

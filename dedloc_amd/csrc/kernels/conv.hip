@@ -964,11 +964,12 @@ int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* o
 }
 
 // Split count of dl_conv_wgrad: the (long) pixel reduction is split so that ~`target` workgroups
-// exist (default 256: one per CU; SwAV b=64 iteration 1990-1997 samples/s at 1024, 2051-2061 at 256,
-// 2041 at 512, with atomic adds), each split a multiple of the 64-deep k-step and at least 8 k-steps
-// long
+// exist, each split a multiple of the 64-deep k-step and at least 8 k-steps long.  Fewer than one per
+// CU leaves slots to the concurrent pass: SwAV b=64 iteration, round 3: 1990-1997 samples/s at 1024,
+// 2051-2061 at 256, 2041 at 512; round 5 (same-box A/Bs, profiles/r5_swav_grid_caps_ab.jsonl): 192
+// +0.6-0.8% over 256, 128 = 256, 512 -2.8%, 1024 -6.2%
 #ifndef DL_CONV_WGRAD_TARGET
-#define DL_CONV_WGRAD_TARGET 256  // (a measurement build may override)
+#define DL_CONV_WGRAD_TARGET 192  // (a measurement build may override)
 #endif
 static long wgrad_splits(const DlConvGeom& g, int tiles) {
   const long M = (long)g.Nimg * g.I * g.J;
