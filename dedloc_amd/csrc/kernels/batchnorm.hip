@@ -392,10 +392,13 @@ inline bool bn_shape_ok(int C) {
 // Rows per block: enough for ~8 row-iterations per thread (a block covers rpi = 256 / (C/8) rows per
 // iteration), at most 1024 blocks per statistics group.  Sizing by rows alone gave the 2048-channel
 // layers (rpi = 1) 64 serial iterations per thread on fewer blocks than CUs (profiles/README.md).
+#ifndef DL_BN_STATS_MAXB
+#define DL_BN_STATS_MAXB 1024  // (a measurement build may override)
+#endif
 inline int stats_blocks(long R, int C, long& rpb) {
   const long rpi = kThreads / (C / 8);
   long nb = (R + 8 * rpi - 1) / (8 * rpi);
-  if (nb > 1024) nb = 1024;
+  if (nb > DL_BN_STATS_MAXB) nb = DL_BN_STATS_MAXB;
   if (nb < 1) nb = 1;
   rpb = (R + nb - 1) / nb;
   return (int)((R + rpb - 1) / rpb);
