@@ -862,6 +862,9 @@ void set_lds(Kern k) {
 
 }  // namespace
 
+#ifndef DL_CONV_FWD_WG
+#define DL_CONV_FWD_WG 1024  // (a measurement build may override)
+#endif
 int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, int OH, int OW, int osh, int osw,
                       long ldo, hipStream_t st, float* stats, const DlBnBwdEpi* bn) {
   if (njobs < 1 || njobs > MAXJ || N % 4 || ldo % 4) return -1;
@@ -937,7 +940,7 @@ int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, i
     if (tiles[c] == 0) continue;
     const DlConvFwdJob& jb = jobs[c];
     // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
-    const int tpw = (int)std::max<long>(1, tiles[c] / 1024);
+    const int tpw = (int)std::max<long>(1, tiles[c] / DL_CONV_FWD_WG);
     const DlConvGeom& g = jb.g;
     FwdArgs& a = P.a[P.n];
     a = FwdArgs{g, jb.w, jb.ldw, N, out, OH, OW, osh, osw, jb.oh0, jb.ow0, ldo, g.Nimg * g.I * g.J, g.TR * g.TS * g.C,
