@@ -392,8 +392,10 @@ inline bool bn_shape_ok(int C) {
 // Rows per block: enough for ~8 row-iterations per thread (a block covers rpi = 256 / (C/8) rows per
 // iteration), at most 1024 blocks per statistics group.  Sizing by rows alone gave the 2048-channel
 // layers (rpi = 1) 64 serial iterations per thread on fewer blocks than CUs (profiles/README.md).
+// (cap: SwAV's concurrent passes, as DL_BN_APPLY_MAXB: 256 +0.5% / +1.1% over 1024 in two same-box
+// A/Bs, 512 +0.3%, 2048 -0.4%; profiles/r5_swav_grid_caps_ab.jsonl)
 #ifndef DL_BN_STATS_MAXB
-#define DL_BN_STATS_MAXB 1024  // (a measurement build may override)
+#define DL_BN_STATS_MAXB 256  // (a measurement build may override)
 #endif
 inline int stats_blocks(long R, int C, long& rpb) {
   const long rpi = kThreads / (C / 8);
