@@ -610,7 +610,7 @@ class SwAVModel(nn.Module):
     # gradient by after_backward) and its running-statistics updates into zeroed stand-ins (merged
     # after the join: the update is affine, rm <- (1-m)^G rm + D, so the crop order is kept).
     concurrent_passes = False
-    pass_splits = (1, 1)  # concurrent passes per resolution group (_pass_plan)
+    pass_splits = (2, 1)  # concurrent passes per resolution group (_pass_plan; SwavPeer's default)
     # where _trunk_concurrent prepares the data-gradient weights: True = a stream of their own (the
     # measured default), False = the main stream, "side" = the first side pass's stream (the layout
     # whose graphed run crashed in round 4 through a self-wait; kept selectable for its test)
