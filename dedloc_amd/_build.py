@@ -152,7 +152,7 @@ def build_variant(name: str, rev: str, kernels, verbose: bool = False, flags=Non
                    "-DUSE_ROCM", "-I", f"{ROCM}/include", "-I", os.path.join(CSRC, "include")]
             for ip in tinc:
                 cmd += ["-I", ip]
-            _run(cmd + ["-I", sysconfig.get_paths()["include"], "-c", src, "-o", obj], verbose)
+            _run(cmd + list(flags or []) + ["-I", sysconfig.get_paths()["include"], "-c", src, "-o", obj], verbose)
         else:
             obj = src.replace(".hip", ".o")
             extra = FILE_FLAGS.get(os.path.basename(k), []) if flags is None else list(flags)
