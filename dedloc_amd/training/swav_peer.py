@@ -97,9 +97,10 @@ class SwavPeer:
             self.model.bind_flat(self.flat)  # GEMM / conv weights read from the flat buffer's bf16 mirror
             # the crop groups' trunk passes on several streams (SwAVModel.concurrent_passes: one per
             # resolution, CONCURRENT_SPLITS cuts a resolution into passes of whole crops; this
-            # trainer calls after_backward after every backward).  Default (2, 1): the two 224 crops
-            # as two passes beside the 96-crop pass — three passes of similar work instead of a
-            # 224 group ~1.8x the 96 group (b=64: +6.4% over (1, 1), profiles/r5_swav_pass_splits.txt)
+            # trainer calls after_backward after every backward).  Fallback (2, 1), the shipped
+            # config's value: the two 224 crops as two passes beside the 96-crop pass — three passes
+            # of similar work instead of a 224 group ~1.8x the 96 group (b=64: +6.4% over (1, 1),
+            # profiles/r5_swav_pass_splits.txt)
             self.model.concurrent_passes = bool(cfg.MODEL.get("CONCURRENT_PASSES", True))
             self.model.pass_splits = tuple(int(v) for v in cfg.MODEL.get("CONCURRENT_SPLITS", (2, 1)))
         self.model.normalize_prototypes()
