@@ -142,6 +142,10 @@ def _self_launch(args) -> int:
     return rc if rc >= 0 else 128 - rc
 
 
+_BACKEND_CODE = {"rccl": 0, "gloo": 1, "rccl+gloo": 2}
+_BACKEND_NAME = {v: k for k, v in _BACKEND_CODE.items()}
+
+
 def _protocol_breakdown(gathered, keys):
     out = {}
     for i, k in enumerate(keys[:-1]):
@@ -201,6 +205,10 @@ def _swav_peer(args, rank, dev, root_ep):
           f"config.OPTIMIZER.compression={args.compression}",
           f'config.OPTIMIZER.dht_initial_peers=["{root_ep}"]', f"config.CHECKPOINT.DIR=/tmp/dedloc_swav_bench_{os.getpid()}",
           "config.CHECKPOINT.AUTO_RESUME=false", "config.CHECKPOINT.CHECKPOINT_ITER_FREQUENCY=0"]
+    if args.cpu_test:
+        # plumbing runs: eight full ResNet-50 peers share the host's CPUs, so one global step can take
+        # longer than the GPU recipe's 30 s metadata expiration — peers would count each other dead
+        ov += ["config.OPTIMIZER.metadata_expiration=300", "config.OPTIMIZER.averaging_timeout=120"]
     cfg = load_config("swav_1node_resnet_submit", ov)
     peer = SwavPeer(cfg, dev, rank=rank, impl=args.impl)
 
@@ -329,7 +337,11 @@ def main():
     if co._device_timer is not None:  # fold the timed region's last micro-steps into the EMA
         co._device_timer.poll()
     ema = co.performance_ema.samples_per_second
-    stats = torch.tensor([samples, dt, ema] + [co.stats.get(k, 0.0) - st0[k] for k in keys], dtype=torch.float64)
+    comms = co.averager.comms
+    stats = torch.tensor([samples, dt, ema] + [co.stats.get(k, 0.0) - st0[k] for k in keys]
+                         + [comms.created, comms.aborted, comms.quarantined, float(_BACKEND_CODE.get(
+                             (co.last_group or {}).get("backend"), -1)), co.stats["averaging_failed"]],
+                         dtype=torch.float64)
     if world > 1:
         gathered = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(gathered, stats)
@@ -338,6 +350,15 @@ def main():
     total_samples = sum(float(g[0]) for g in gathered)
     max_dt = max(float(g[1]) for g in gathered)
     ema_sum = sum(float(g[2]) for g in gathered)
+    n0 = 3 + len(keys)
+    per_peer = {"comms_created": [int(g[n0]) for g in gathered], "comms_aborted": [int(g[n0 + 1]) for g in gathered],
+                "comms_quarantined": [int(g[n0 + 2]) for g in gathered],
+                "data_plane": [_BACKEND_NAME.get(int(g[n0 + 3])) for g in gathered],
+                "averaging_failed": [int(g[n0 + 4]) for g in gathered]}
+    # N > 1 peers on N distinct GPUs must average over RCCL: a silent fallback to host-staged gloo
+    # (a broken RCCL on the box) must not become the scaling number
+    fallback = (dev.type == "cuda" and world > 1 and physical == world
+                and any(b != "rccl" for b in per_peer["data_plane"]))
     if rank == 0:
         value = total_samples / max_dt
         out = dict(describe(value, world), n_gpus=world, steps=args.steps, warmup=args.warmup,
@@ -352,7 +373,10 @@ def main():
                # batch's last micro-step, in the state fetch, matchmaking + all-reduce (and each),
                # the optimizer launch and the bookkeeping after it; local micro-steps per global step
                "protocol": _protocol_breakdown(gathered, keys),
-               "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"}})
+               "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"},
+               "per_peer": per_peer})
+        if fallback:
+            out["error"] = f"data plane is not RCCL on every peer: {per_peer['data_plane']}"
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -361,6 +385,11 @@ def main():
         root.shutdown()
     if world > 1:
         dist.destroy_process_group()
+    if fallback:
+        if rank == 0:
+            print(f"bench.py: {world} peers on {physical} GPUs did not all average over RCCL "
+                  f"({per_peer['data_plane']}); failing the run", file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

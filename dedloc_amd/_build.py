@@ -55,6 +55,8 @@ def _run(cmd, verbose):
 def build(verbose: bool = False, jobs: int | None = None) -> str:
     os.makedirs(BUILD, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
+    # every header under csrc/ (comm/*.h, runtime/*.h, ...): a translation unit may include any of them
+    all_headers = sorted(set(headers) | set(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)))
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     inc = ["-I", os.path.join(CSRC, "include")]
     hip_flags = ["--offload-arch=" + ARCH, *HIP_FLAGS]
@@ -76,7 +78,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         name = os.path.basename(src).replace(".cpp", ".o")
         obj = os.path.join(BUILD, name if src.endswith("bindings.cpp") else "comm_" + name)
         objs.append(obj)
-        if _newer(obj, [src] + headers):
+        if _newer(obj, [src] + all_headers):
             cmd = ["g++", "-O2", "-std=c++17", "-fPIC", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__",
                    "-DUSE_ROCM", "-I", f"{ROCM}/include", *inc]
             for p in tinc:
@@ -88,7 +90,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     for src in sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))):
         obj = os.path.join(BUILD, "host_" + os.path.basename(src).replace(".cpp", ".o"))
         objs.append(obj)
-        if _newer(obj, [src] + headers):
+        if _newer(obj, [src] + all_headers):
             jobs_list.append(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I",
                               f"{ROCM}/include", *inc, "-c", src, "-o", obj])
 
@@ -97,7 +99,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     for src in rt_srcs:
         obj = os.path.join(BUILD, "rt_" + os.path.basename(src).replace(".cpp", ".o"))
         rt_objs.append(obj)
-        if _newer(obj, [src] + headers + glob.glob(os.path.join(CSRC, "runtime", "*.h"))):
+        if _newer(obj, [src] + all_headers):
             jobs_list.append(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", *inc, "-c", src, "-o", obj])
 
     with cf.ThreadPoolExecutor(jobs) as ex:

@@ -66,8 +66,9 @@ def _byte_view(t: torch.Tensor) -> memoryview:
 class StateServer:
     """Serves ``get_state() -> (metadata, [tensors])`` to joining peers.
 
-    Request: ``b"STATE" + mode`` with mode ``R`` (followed by a 128-byte RCCL unique id made by the
-    requester, then the requester's GPU identity as a 2-byte length + UTF-8) or ``T``.  RCCL takes
+    Request: ``b"STATE" + mode`` with mode ``G`` (followed by a 128-byte RCCL unique id made by the
+    requester, then the requester's GPU identity as a 2-byte length + UTF-8), ``R`` (the unique id
+    only: the format of peers from before the GPU identity existed, still accepted) or ``T``.  RCCL takes
     one rank per device, so a requester on the donor's own GPU is always answered over TCP: two
     ranks of one device are never put into a communicator (that only exercises RCCL's error and
     abort path, which crashed a peer on the driver's box in round 4).  A GPU donor answers an ``R`` request by sending the snapshot device-to-
@@ -114,8 +115,9 @@ class StateServer:
                 if req[:5] != b"STATE":
                     return
                 uid, their_gpu = None, None
-                if req[5:6] == b"R":
+                if req[5:6] in (b"R", b"G"):
                     uid = _recv_exact(conn, 128)
+                if req[5:6] == b"G":
                     (n,) = struct.unpack("<H", _recv_exact(conn, 2))
                     their_gpu = _recv_exact(conn, n).decode() if n else None
                 if self.device.type == "cuda":
@@ -211,7 +213,7 @@ def download_state(endpoint: str, timeout: float = 60.0, device: Optional[torch.
         s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         if uid is not None:
             g = (gpu_id or "").encode()
-            s.sendall(b"STATER" + uid + struct.pack("<H", len(g)) + g)
+            s.sendall(b"STATEG" + uid + struct.pack("<H", len(g)) + g)
         else:
             s.sendall(b"STATET")
         (hl,) = struct.unpack("<Q", _recv_exact(s, 8))

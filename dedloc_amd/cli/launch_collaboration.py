@@ -87,6 +87,9 @@ def main(argv=None):
     ap.add_argument("--n_aux", type=int, default=0)
     ap.add_argument("--n_gpus", type=int, default=None, help="GPUs on this node (default: one per GPU peer)")
     ap.add_argument("--cpu", action="store_true", help="run the trainers on the CPU (plumbing / tests)")
+    ap.add_argument("--allow_shared_device", action="store_true",
+                    help="more GPU peers than --n_gpus: peer slot i runs on GPU i %% n_gpus (protocol emulation on "
+                         "a small box; peers on one device average over gloo, RCCL takes one rank per device)")
     ap.add_argument("--aux_device", choices=["cpu", "gpu"], default="cpu")
     ap.add_argument("--experiment_prefix", default="albert")
     ap.add_argument("--model_config_path", default=None, help="model config for the coordinator's replica")
@@ -149,7 +152,7 @@ def main(argv=None):
     # 2. peers
     n_gpu_peers = (0 if args.cpu else args.n_trainers) + (args.n_aux if args.aux_device == "gpu" else 0)
     n_gpus = args.n_gpus if args.n_gpus is not None else n_gpu_peers
-    if n_gpu_peers > n_gpus:
+    if n_gpu_peers > n_gpus and not args.allow_shared_device:
         raise SystemExit(f"{n_gpu_peers} GPU peers need {n_gpu_peers} GPUs (one RCCL rank per device), the node has "
                          f"{n_gpus}; run auxiliary peers on the CPU (--aux_device cpu)")
     common = ["--experiment_prefix", args.experiment_prefix, *(["--initial_peers", root] if root else [])]

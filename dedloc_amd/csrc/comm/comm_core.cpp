@@ -73,6 +73,7 @@ int64_t Registry::status(int64_t h) {
   if (c->comm == nullptr) return (int64_t)ncclInvalidArgument;
   ncclResult_t st = ncclSuccess;
   ncclResult_t rc = ncclCommGetAsyncError(c->comm, &st);
+  if (rc == ncclSuccess && st == ncclSuccess) c->bootstrapped = true;
   return rc != ncclSuccess ? (int64_t)rc : (int64_t)st;
 }
 
@@ -116,7 +117,7 @@ int64_t Registry::release(int64_t h) {
   if (c->comm != nullptr) {
     ncclResult_t st = ncclSuccess;
     ncclResult_t rc = ncclCommGetAsyncError(c->comm, &st);
-    if (rc == ncclSuccess && st == ncclInProgress) {
+    if (rc == ncclSuccess && st == ncclInProgress && !c->bootstrapped) {
       c->quarantined = true;
       return kQuarantined;
     }

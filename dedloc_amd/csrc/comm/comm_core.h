@@ -10,11 +10,16 @@
 //     ncclComm_t is cleared under it when the communicator is aborted, so a status poll racing an
 //     abort on another thread sees "aborted", never freed memory;
 //   * release() never aborts a communicator whose non-blocking bootstrap is still in flight
-//     (ncclInProgress: RCCL's init thread still owns it).  Such a communicator is QUARANTINED: it
-//     stays in the registry (unusable for transfers), reap() polls it, and it is aborted only once
-//     RCCL reports that the bootstrap ended (success or error).  A bootstrap whose other members
-//     never arrive stays quarantined until process exit — a few idle sockets, instead of freeing
-//     state RCCL's background thread may still touch.
+//     (ncclInProgress before status() has ever reported ncclSuccess: RCCL's init thread still owns
+//     it).  Such a communicator is QUARANTINED: it stays in the registry (unusable for transfers),
+//     reap() polls it, and it is aborted only once RCCL reports that the bootstrap ended (success
+//     or error).  A bootstrap whose other members never arrive stays quarantined until process
+//     exit — a few idle sockets, instead of freeing state RCCL's background thread may still touch;
+//   * once the bootstrap has completed (``bootstrapped``), ncclInProgress only means a grouped
+//     send/recv is still being enqueued (e.g. lazy p2p connection set-up towards a member that
+//     died): release() then aborts at once — NCCL allows aborting a non-blocking communicator with
+//     operations in progress, and that abort is what cancels the round's kernels, sockets and
+//     proxy threads.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -42,6 +47,7 @@ struct Comm {
   ncclComm_t comm = nullptr;  // nullptr once aborted
   int64_t nranks = 0, rank = 0, device = 0;
   bool quarantined = false;   // guarded by mu
+  bool bootstrapped = false;  // guarded by mu: status() has reported ncclSuccess at least once
 };
 
 // release() outcomes

@@ -415,6 +415,8 @@ class CollaborativeOptimizer:
                     self.stats["averaging_failed"] += 1
                     logger.log(self.status_loglevel, "Skipped averaging: collaboration consists of this peer only "
                                                      "or the round failed; applying local gradients")
+                else:
+                    self._adopt_group_step(group)
             else:
                 logger.log(self.status_loglevel, "Skipped averaging: collaboration consists of this peer alone")
             t_opt = time.perf_counter()
@@ -446,6 +448,19 @@ class CollaborativeOptimizer:
         # record, the next round's prejoin
         self.stats["tail_s"] = self.stats.get("tail_s", 0.0) + time.perf_counter() - t_tail
         return group
+
+    def _adopt_group_step(self, group: Dict):
+        """After a successful round, take the largest step any member gathered (hivemind 0.9.x:
+        "update our current step if we averaged with another peer that was ahead of us").  The
+        members now hold the same parameters, so they continue with the same step counter: without
+        this a peer that lags one step behind (inside ``step_tolerance``, e.g. after an early global
+        step some peers took alone) stays one behind for the whole run, and its prejoined groups
+        never line up with the others' at the end of a run."""
+        steps = [g.get("step") for g in group.get("gathered") or () if isinstance(g, dict)]
+        steps = [s for s in steps if isinstance(s, int)]
+        if steps and max(steps) > self.local_step:
+            self.stats["steps_adopted"] = self.stats.get("steps_adopted", 0) + max(steps) - self.local_step
+            self.local_step = max(steps)
 
     def _ready(self, batch_size: int) -> bool:
         return (self.collaboration_state.ready_for_step or self._ready_exact()

@@ -297,6 +297,11 @@ class GroupCommunicators:
     # RCCL_RETRY_AFTER_S seconds.  DEDLOC_DATA_PLANE=gloo forces gloo from the start.
     RCCL_FALLBACK_AFTER = int(os.environ.get("DEDLOC_RCCL_FALLBACK_AFTER", "3"))
     RCCL_RETRY_AFTER_S = 300.0
+    # Communicators abandoned during their bootstrap stay quarantined (comm_core.h) until RCCL's
+    # init thread lets go of them.  Repeated churn during bootstraps could pile them up (each holds
+    # sockets and an init thread), so past this many the peer stops building new RCCL communicators
+    # and averages over gloo until the reaper has brought the count back down.
+    MAX_QUARANTINED = int(os.environ.get("DEDLOC_RCCL_MAX_QUARANTINED", "16"))
 
     def __init__(self, dht, prefix: str, peer_id: bytes, device: torch.device, timeout_s: float = 60.0,
                  max_cached: int = 8, host: str = "127.0.0.1"):
@@ -312,6 +317,7 @@ class GroupCommunicators:
         self.rccl_create_failures = 0  # consecutive RCCL communicators this peer could not bring up
         self._gpu_id: Optional[str] = None
         self._fallback_since: Optional[float] = None
+        self._quarantine_warned = False
 
     # ------------------------------------------------------------------ matchmaking info
     @property
@@ -322,7 +328,23 @@ class GroupCommunicators:
             if time.monotonic() - (self._fallback_since or 0.0) < self.RCCL_RETRY_AFTER_S:
                 return "gloo"
             self.rccl_create_failures = self.RCCL_FALLBACK_AFTER - 1  # one more try
-        return "rccl" if rccl_available(self.device) else "gloo"
+        if not rccl_available(self.device):
+            return "gloo"
+        q = self.quarantined
+        if q >= self.MAX_QUARANTINED:
+            if not self._quarantine_warned:
+                self._quarantine_warned = True
+                logger.warning(f"{q} RCCL communicators are quarantined (bootstraps abandoned by churn); "
+                               f"averaging over gloo until they are reaped")
+            return "gloo"
+        self._quarantine_warned = False
+        return "rccl"
+
+    @property
+    def quarantined(self) -> int:
+        """RCCL communicators of this process waiting for their bootstrap to end (comm_core.h)."""
+        w = cw.CommWorker._instance
+        return int(w.quarantined) if w is not None else 0
 
     @property
     def gpu_id(self) -> Optional[str]:
@@ -385,7 +407,8 @@ class GroupCommunicators:
             # a member set we share no live communicator with: build one for this round's group id
             while len(self._cache) >= self.max_cached:
                 self._drop(next(iter(self._cache)))
-            tok = bytes(group_id).hex()
+            # the DHT's matchmaking returns an integer round id (bytes(int) would be that many zero bytes)
+            tok = f"{group_id:016x}" if isinstance(group_id, int) else bytes(group_id).hex()
             if deadline is None:
                 deadline = time.monotonic() + self.timeout_s
             if backend == "hybrid":

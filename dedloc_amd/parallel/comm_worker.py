@@ -185,6 +185,14 @@ def _abort(handle: int):
         logger.debug(f"comm_release({handle}) failed: {e}")
 
 
+def _sync_quarantined():
+    try:
+        w = CommWorker.get()
+        w.quarantined = max(w.quarantined, int(_ops().comm_quarantined()))
+    except Exception as e:  # noqa: BLE001
+        logger.debug(f"comm_quarantined failed: {e}")
+
+
 def _wait_ready(handle: int, deadline: Optional[float], what: str):
     """Poll the communicator until its last call has been enqueued (ncclSuccess)."""
     ops = _ops()
@@ -207,6 +215,9 @@ def init_job(uid: bytes, nranks: int, rank: int, device_index: int, deadline: Op
     try:
         h = int(_ops().comm_init(t, int(nranks), int(rank), int(device_index)))
     except RuntimeError as e:
+        # a synchronous init failure may leave a half-built communicator quarantined in the native
+        # registry (comm_core.cpp): let the worker know, so that it keeps reaping
+        _sync_quarantined()
         raise CommError(f"RCCL communicator init failed: {e}", local=True) from e
     yield from _wait_ready(h, deadline, "communicator bootstrap")
     return h

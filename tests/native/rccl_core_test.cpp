@@ -39,6 +39,7 @@ std::atomic<long> g_uid{0};
 std::atomic<int> g_violations{0};
 std::atomic<bool> g_give_up{false};
 std::atomic<int> g_init_threads{0};
+std::atomic<bool> g_enqueue_stalls{false};  // sends stay "being enqueued" (lazy connect to a dead peer)
 thread_local int g_group_depth = 0;
 
 int joined(const std::string& uid) {
@@ -116,6 +117,10 @@ ncclResult_t ncclSend(const void*, size_t, ncclDataType_t, int peer, ncclComm_t 
   if (g_group_depth <= 0 || peer < 0 || peer >= comm->nranks) return ncclInvalidUsage;
   if (comm->state.load() != ncclSuccess) return ncclInvalidUsage;
   comm->ops += 1;
+  if (g_enqueue_stalls.load()) {  // non-blocking group: the enqueue never finishes
+    comm->state.store((int)ncclInProgress);
+    return ncclInProgress;
+  }
   return ncclSuccess;
 }
 
@@ -206,7 +211,23 @@ int main() {
     CHECK(registry().release(h1) == dlcomm::kAborted);
     CHECK(registry().live() == 0);
   }
-  // 3. two threads hammering the registry: one creates / uses / releases communicators (some
+  // 3. a grouped send/recv still being enqueued AFTER the bootstrap completed (lazy
+  //    connection set-up towards a member that died): release() aborts at once instead of
+  //    quarantining — that abort is what cancels the round's operations
+  {
+    int64_t h = make(1, 0, new_id());
+    wait_ready(h);
+    g_enqueue_stalls.store(true);
+    std::vector<dlcomm::P2POp> ops = {{payload, 4, ncclInt32, 0, true}};
+    CHECK(registry().group_p2p(h, ops, nullptr) == ncclSuccess);
+    CHECK(registry().status(h) == ncclInProgress);
+    g_enqueue_stalls.store(false);
+    const int64_t q0 = registry().quarantined();
+    CHECK(registry().release(h) == dlcomm::kAborted);
+    CHECK(registry().quarantined() == q0);
+    CHECK(registry().status(h) == ncclInvalidArgument);
+  }
+  // 4. two threads hammering the registry: one creates / uses / releases communicators (some
   //    with a missing member), the other polls, posts, releases and reaps the same handles
   {
     std::mutex hm;

@@ -192,3 +192,23 @@ def test_imminent_wait_happens_once_per_global_step(collab, monkeypatch):
     for _ in range(4):
         co.step(batch_size=4)
     assert co.local_step == 0 and len(fetches) == 1
+
+
+def test_successful_round_adopts_the_largest_gathered_step(collab, monkeypatch):
+    """hivemind 0.9.x: a peer that averaged with a member one step ahead takes that member's step,
+    so step counters inside one group never stay apart (a lagging peer's prejoined groups would
+    otherwise miss the others' at the end of a run)."""
+    co, flat = collab
+    co.local_step = 4
+    co.collaboration_state = _state(co, step=5, samples=8)
+    monkeypatch.setattr(co, "_refresh_state", lambda: None)
+    monkeypatch.setattr(co.averager, "step", lambda **kw: {"group_id": 1, "size": 2, "gathered": [
+        {"step": 4}, {"step": 5}], "backend": "gloo"})
+    flat.grad.normal_()
+    assert co.step(batch_size=4) is not None
+    assert co.local_step == 6 and co.stats["steps_adopted"] == 1
+    # a failed round adopts nothing
+    co.collaboration_state = _state(co, step=6, samples=8)
+    monkeypatch.setattr(co.averager, "step", lambda **kw: None)
+    co.step(batch_size=4)
+    assert co.local_step == 7 and co.stats["steps_adopted"] == 1

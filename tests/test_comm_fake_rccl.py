@@ -337,3 +337,35 @@ def test_same_device_donor_answers_over_tcp(fake):
         torch.testing.assert_close(tensors[0], state[0])
     finally:
         srv.shutdown()
+
+
+def test_legacy_uid_only_request_is_served_without_stalling(fake):
+    """ADVICE r5: a requester on the pre-GPU-identity format sends ``STATER`` + the unique id only;
+    the donor must answer it at once (the extended request has its own mode byte, ``G``) instead of
+    waiting for a GPU-identity field that never comes."""
+    import socket
+    import struct
+
+    import msgpack
+
+    from dedloc_amd.averaging.averager import StateServer
+
+    state = [torch.randn(50)]
+    srv = StateServer(lambda: ({"step": 2}, [t.clone() for t in state]), "127.0.0.1:0", device=torch.device("cpu"),
+                      transfer_timeout=10)
+    try:
+        uid = C.RcclGroupComm.new_unique_id()
+        host, port = srv.endpoint.split(":")
+        t0 = time.monotonic()
+        with socket.create_connection((host, int(port)), timeout=10) as s:
+            s.sendall(b"STATER" + uid)
+            (hl,) = struct.unpack("<Q", s.recv(8, socket.MSG_WAITALL))
+            header = msgpack.unpackb(s.recv(hl, socket.MSG_WAITALL), raw=False)
+            assert header["mode"] == "R" and time.monotonic() - t0 < 5
+            out = torch.empty(50)
+            comm = C.pairwise_rccl(uid, 1, torch.device("cpu"), time.monotonic() + 10)
+            comm.p2p([], [], [out], [0], time.monotonic() + 10)
+            comm.abort()
+        torch.testing.assert_close(out, state[0])
+    finally:
+        srv.shutdown()
