@@ -124,3 +124,4 @@ class CoordinatorArguments(BaseTrainingArguments):
     metrics_file: Optional[str] = field(default=None, metadata={"help": "append aggregated collaboration metrics here (JSONL)"})
     max_runtime: Optional[float] = field(default=None, metadata={"help": "exit after this many seconds"})
     device: Optional[str] = field(default="cpu", metadata={"help": "device for the coordinator's model replica"})
+    vocab_size: Optional[int] = field(default=None, metadata={"help": "override the replica's vocabulary size (sahajBERT: 31995)"})

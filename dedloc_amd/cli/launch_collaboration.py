@@ -134,6 +134,7 @@ def main(argv=None):
                "--dht_listen_on", "0.0.0.0:*", "--refresh_period", str(args.coordinator_refresh),
                "--metrics_file", str(log_dir / "coordinator_metrics.jsonl"),
                *(["--model_config_path", args.model_config_path] if args.model_config_path else []),
+               *(["--vocab_size", "31995"] if args.sahajbert else []),
                *(["--max_runtime", str(args.duration)] if args.duration else [])]
         coord = _Proc("coordinator", cmd, env0, log_dir, 0)
         others.append(coord)

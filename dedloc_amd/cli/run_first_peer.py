@@ -45,6 +45,8 @@ class CheckpointHandler:
         self.upload_interval = coordinator_args.upload_interval
         self.previous_step = -1
         config = AlbertConfig.from_pretrained(coordinator_args.model_config_path)
+        if coordinator_args.vocab_size:
+            config.vocab_size = coordinator_args.vocab_size
         self.model = AlbertForPreTraining(config)
         self.model.materialize(torch.device(coordinator_args.device or "cpu"))
         opt = FusedLamb(self.model.flat, lr=0.00176, weight_decay=0.01, clamp_value=10000.0, debias=True,
@@ -64,7 +66,10 @@ class CheckpointHandler:
         return cur_step - self.previous_step >= self.save_checkpoint_step_interval
 
     def save_state(self, cur_step):
-        self.collaborative_optimizer.load_state_from_peers()
+        try:
+            self.collaborative_optimizer.load_state_from_peers()
+        except ValueError as e:  # a replica that does not match the peers' model: keep hosting the DHT
+            logger.error(f"cannot take the peers' state into the coordinator's replica: {e}")
         self.previous_step = cur_step
 
     def is_time_to_upload(self):

@@ -69,6 +69,25 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// Wave-wide f32 sum without the LDS crossbar: DPP within each 16-lane row (xor 1, xor 2, half-row
+// mirror, row mirror), then the gfx950 row-pair and half-wave swaps.  Every lane gets the total.
+// (__shfl_xor lowers to a chain of six ds_bpermute_b32 round trips, ~1 us of latency per row
+// reduction in the LayerNorm kernels.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1>(v);   // quad_perm(1,0,3,2): lane ^ 1
+  v += dpp_f32<0x4E>(v);   // quad_perm(2,3,0,1): lane ^ 2
+  v += dpp_f32<0x141>(v);  // row_half_mirror: the other quad of each 8 lanes
+  v += dpp_f32<0x140>(v);  // row_mirror: the other 8 lanes of each row of 16
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows 0+1, 2+3
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // halves
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
 #pragma unroll
@@ -185,19 +204,11 @@ __device__ __forceinline__ void unpack8_bf16(const uint4& v, float* out) {
 template <int VW>
 __device__ __forceinline__ void store_bf16(bf16_t* p, const float* in) {
   if constexpr (VW == 8) {
-    uint4 v;
-    v.x = (uint32_t)f2bf(in[0]) | ((uint32_t)f2bf(in[1]) << 16);
-    v.y = (uint32_t)f2bf(in[2]) | ((uint32_t)f2bf(in[3]) << 16);
-    v.z = (uint32_t)f2bf(in[4]) | ((uint32_t)f2bf(in[5]) << 16);
-    v.w = (uint32_t)f2bf(in[6]) | ((uint32_t)f2bf(in[7]) << 16);
-    *reinterpret_cast<uint4*>(p) = v;
+    *reinterpret_cast<uint4*>(p) = pack8_bf16(in);
   } else if constexpr (VW == 4) {
-    uint2 v;
-    v.x = (uint32_t)f2bf(in[0]) | ((uint32_t)f2bf(in[1]) << 16);
-    v.y = (uint32_t)f2bf(in[2]) | ((uint32_t)f2bf(in[3]) << 16);
-    *reinterpret_cast<uint2*>(p) = v;
+    *reinterpret_cast<uint2*>(p) = uint2{pack2_bf16(in[0], in[1]), pack2_bf16(in[2], in[3])};
   } else if constexpr (VW == 2) {
-    *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(in[0]) | ((uint32_t)f2bf(in[1]) << 16);
+    *reinterpret_cast<uint32_t*>(p) = pack2_bf16(in[0], in[1]);
   } else {
 #pragma unroll
     for (int i = 0; i < VW; ++i) p[i] = f2bf(in[i]);

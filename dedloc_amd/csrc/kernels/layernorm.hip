@@ -31,7 +31,11 @@ __device__ __forceinline__ int col_of(int lane, int v) {
   return (v * 64 + lane) * RowCfg<D>::VW;
 }
 
-template <int D, bool HAS_RES, bool SAVE_SUM>
+// R rows per wave: gamma / beta are read once per wave (before the rows: they are L2 hits, and
+// issued after the first reduction they put an L2 round trip on every row's critical path), all R
+// rows' loads are issued before the first is used, and the row sums go through DPP / lane swaps
+// (wave_sum_dpp) instead of six LDS-crossbar round trips each.
+template <int D, bool HAS_RES, bool SAVE_SUM, int R>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
@@ -39,45 +43,79 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
                                                      int rows, float eps) {
   using C = RowCfg<D>;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const size_t base = (size_t)row * D;
-  float v[C::EPL];
+  const int row0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * R;
+  if (row0 >= rows) return;
+  static_assert(C::VW == 8 || R == 1, "several rows per wave need 8-wide row vectors");
+  // every load of the wave first (the rows raw, gamma / beta), then a scheduling fence: left alone
+  // the compiler sinks the later rows' loads behind the first row's math to save registers
+  uint4 xr[R][C::NV], rr[HAS_RES ? R : 1][C::NV];
+  if constexpr (C::VW == 8) {
 #pragma unroll
-  for (int i = 0; i < C::NV; ++i) load_bf16<C::VW>(x + base + col_of<D>(lane, i), v + i * C::VW);
-  if constexpr (HAS_RES) {
-    float t[C::EPL];
+    for (int u = 0; u < R; ++u) {
+      const size_t base = (size_t)min(row0 + u, rows - 1) * D;  // a tail row repeats the last one (never stored)
 #pragma unroll
-    for (int i = 0; i < C::NV; ++i) load_bf16<C::VW>(r + base + col_of<D>(lane, i), t + i * C::VW);
-#pragma unroll
-    for (int i = 0; i < C::EPL; ++i) v[i] += t[i];
+      for (int i = 0; i < C::NV; ++i) {
+        xr[u][i] = *reinterpret_cast<const uint4*>(x + base + col_of<D>(lane, i));
+        if constexpr (HAS_RES) rr[u][i] = *reinterpret_cast<const uint4*>(r + base + col_of<D>(lane, i));
+      }
+    }
   }
-  if constexpr (SAVE_SUM) {
-    // round the residual sum to bf16 first so that bwd sees exactly the normalised values
+  float g[C::EPL], b[C::EPL];
 #pragma unroll
-    for (int i = 0; i < C::EPL; ++i) v[i] = bf2f(f2bf(v[i]));
-#pragma unroll
-    for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(s_out + base + col_of<D>(lane, i), v + i * C::VW);
-  }
-  float sum = 0.f;
-#pragma unroll
-  for (int i = 0; i < C::EPL; ++i) sum += v[i];
-  const float mean = wave_sum(sum) * (1.f / D);
-  float sq = 0.f;
-#pragma unroll
-  for (int i = 0; i < C::EPL; ++i) { float d = v[i] - mean; sq += d * d; }
-  const float rstd = rsqrtf(wave_sum(sq) * (1.f / D) + eps);
-  float o[C::EPL];
-#pragma unroll
-  for (int i = 0; i < C::NV; ++i) {
+  for (int i = 0; i < C::NV; ++i)
 #pragma unroll
     for (int j = 0; j < C::VW; ++j) {
-      const int c = col_of<D>(lane, i) + j;
-      o[i * C::VW + j] = (v[i * C::VW + j] - mean) * rstd * gamma[c] + beta[c];
+      g[i * C::VW + j] = gamma[col_of<D>(lane, i) + j];
+      b[i * C::VW + j] = beta[col_of<D>(lane, i) + j];
     }
-    store_bf16<C::VW>(y + base + col_of<D>(lane, i), o + i * C::VW);
+  __builtin_amdgcn_sched_barrier(0);
+  float v[R][C::EPL];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const size_t base = (size_t)min(row0 + u, rows - 1) * D;
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) {
+      if constexpr (C::VW == 8) unpack8_bf16(xr[u][i], v[u] + i * C::VW);
+      else load_bf16<C::VW>(x + base + col_of<D>(lane, i), v[u] + i * C::VW);
+    }
+    if constexpr (HAS_RES) {
+      float t[C::EPL];
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) {
+        if constexpr (C::VW == 8) unpack8_bf16(rr[u][i], t + i * C::VW);
+        else load_bf16<C::VW>(r + base + col_of<D>(lane, i), t + i * C::VW);
+      }
+#pragma unroll
+      for (int i = 0; i < C::EPL; ++i) v[u][i] += t[i];
+    }
   }
-  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const int row = row0 + u;
+    if (R > 1 && row >= rows) break;
+    const size_t base = (size_t)row * D;
+    if constexpr (SAVE_SUM) {
+      // round the residual sum to bf16 first so that bwd sees exactly the normalised values
+#pragma unroll
+      for (int i = 0; i < C::EPL; ++i) v[u][i] = round_bf16(v[u][i]);
+#pragma unroll
+      for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(s_out + base + col_of<D>(lane, i), v[u] + i * C::VW);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::EPL; ++i) sum += v[u][i];
+    const float mean = wave_sum_dpp(sum) * (1.f / D);
+    float sq = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::EPL; ++i) { const float d = v[u][i] - mean; sq = fmaf(d, d, sq); }
+    const float rstd = rsqrtf(wave_sum_dpp(sq) * (1.f / D) + eps);
+    float o[C::EPL];
+#pragma unroll
+    for (int i = 0; i < C::EPL; ++i) o[i] = fmaf((v[u][i] - mean) * rstd, g[i], b[i]);
+#pragma unroll
+    for (int i = 0; i < C::NV; ++i) store_bf16<C::VW>(y + base + col_of<D>(lane, i), o + i * C::VW);
+    if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  }
 }
 
 // Each block handles a contiguous chunk of rows (one wave per row, grid-strided inside the
@@ -143,8 +181,8 @@ __global__ __launch_bounds__(512) void ln_bwd_kernel(const bf16_t* __restrict__ 
     }
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      a[u] = wave_sum(a[u]) * (1.f / D);
-      b[u] = wave_sum(b[u]) * (1.f / D);
+      a[u] = wave_sum_dpp(a[u]) * (1.f / D);
+      b[u] = wave_sum_dpp(b[u]) * (1.f / D);
     }
 #pragma unroll
     for (int u = 0; u < R; ++u) {
@@ -229,8 +267,8 @@ __global__ __launch_bounds__(256) void ln_bwd_wide_kernel(const bf16_t* __restri
       a += gy[i];
       b += gy[i] * xh[i];
     }
-    a = wave_sum(a);
-    b = wave_sum(b);
+    a = wave_sum_dpp(a);
+    b = wave_sum_dpp(b);
     if (lane == 0) {
       red[0][wid] = a;
       red[1][wid] = b;
@@ -258,17 +296,39 @@ __global__ __launch_bounds__(256) void ln_bwd_wide_kernel(const bf16_t* __restri
     }
 }
 
+// rows per wave of the forward (tuning knob DEDLOC_LN_FWD_R = 1 / 2 / 4, read once)
+static int ln_fwd_rows_per_wave() {
+  static const int r = [] {
+    const char* e = std::getenv("DEDLOC_LN_FWD_R");
+    const int v = e ? std::atoi(e) : 2;
+    return v == 1 || v == 4 ? v : 2;
+  }();
+  return r;
+}
+
+template <int D, int R>
+void launch_fwd_r(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,
+                  float* mean, float* rstd, int rows, float eps, hipStream_t st) {
+  const int wpb = 4;
+  dim3 grid((rows + wpb * R - 1) / (wpb * R)), block(64 * wpb);
+  if (r) {
+    if (s_out) ln_fwd_kernel<D, true, true, R><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
+    else ln_fwd_kernel<D, true, false, R><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
+  } else {
+    ln_fwd_kernel<D, false, false, R><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
+  }
+}
+
 template <int D>
 void launch_fwd(const bf16_t* x, const bf16_t* r, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,
                 float* mean, float* rstd, int rows, float eps, hipStream_t st) {
-  const int wpb = 4;
-  dim3 grid((rows + wpb - 1) / wpb), block(64 * wpb);
-  if (r) {
-    if (s_out) ln_fwd_kernel<D, true, true><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
-    else ln_fwd_kernel<D, true, false><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
-  } else {
-    ln_fwd_kernel<D, false, false><<<grid, block, 0, st>>>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps);
-  }
+  // several rows per wave for 8-wide row vectors (D = 512 / 1024); wide rows (their EPL floats per
+  // lane already fill the registers) and narrow ones keep one row per wave
+  constexpr bool multi = RowCfg<D>::VW == 8 && D <= 1024;
+  const int R = multi ? ln_fwd_rows_per_wave() : 1;
+  if (R == 4) launch_fwd_r<D, multi ? 4 : 1>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st);
+  else if (R == 2) launch_fwd_r<D, multi ? 2 : 1>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st);
+  else launch_fwd_r<D, 1>(x, r, gamma, beta, y, s_out, mean, rstd, rows, eps, st);
 }
 
 template <int D>

@@ -251,6 +251,10 @@ class CollaborativeOptimizer:
                 logger.log(self.status_loglevel, "no peers to load state from; keeping local state")
                 return False
             meta, tensors = res
+            mine = [self.flat.fp32] + list(self.opt.state_tensors())
+            if len(tensors) != len(mine) or any(t.numel() != m.numel() for t, m in zip(tensors, mine)):
+                raise ValueError(f"the donor's state ({[t.numel() for t in tensors]} elements) does not match this "
+                                 f"peer's model and optimizer ({[m.numel() for m in mine]}): different configs?")
             self.flat.fp32.copy_(tensors[0].to(self.flat.fp32.device))
             for dst, src in zip(self.opt.state_tensors(), tensors[1:]):
                 dst.copy_(src.to(dst.device))

@@ -1,12 +1,12 @@
 """SwAV model-level parity and training dynamics against stock PyTorch.
 
-* The full SwAVModel (ResNet-50 trunk + projection MLP + prototypes) with the SwAV loss at b = 8,
+* The full SwAVModel (ResNet-50 trunk + projection MLP + prototypes) with the SwAV loss at b = 32,
   crops 2 x 224 + 6 x 96, one backward: loss and every parameter gradient against the same
   parameters in stock fp32 PyTorch modules (``training/swav_eager.eager_twin``: nn.Conv2d,
-  nn.BatchNorm2d, ...) with vissl's loss formulas (``EagerSwAVLoss``).  Random-init ResNets with
-  8-sample BatchNorm groups amplify any rounding through their 16 blocks, so gradients are bounded
-  relative to what stock bf16 autocast of the same modules gets (the same idea as the Bottleneck
-  tests in test_conv.py).
+  nn.BatchNorm2d, ...): the SwAV loss value under the same fp32 Sinkhorn assignments, and the
+  gradients through a fixed random projection of the outputs (the SwAV loss's gradient signal at
+  init is below bf16 resolution).  Gradients are bounded relative to what stock bf16 autocast of
+  the same modules gets, flat and per tensor, and a 2% mutant of one weight gradient must fail.
 * 100 collaborative LARC-SGD steps of the dedloc SwavPeer and of the eager stack (``impl="eager"``:
   stock modules, vissl loss, apex LARC in torch ops) from the same weights on the same crops: the
   loss curves agree within a stated band.
@@ -39,15 +39,63 @@ def _crops(device, bs, seed):
     return out
 
 
-@pytest.mark.timeout(300)
+def _ce_with_q(scores, qs, crops_for_assign, nc, bs, temperature):
+    """vissl's swapped-prediction loss (swav_loss.py:292-326) with GIVEN assignments, in torch ops."""
+    import torch.nn.functional as F
+
+    total = 0.0
+    for q, crop_id in zip(qs, crops_for_assign):
+        others = [v for v in range(nc) if v != crop_id]
+        loss = 0.0
+        for v in others:
+            loss = loss - torch.mean(torch.sum(q * F.log_softmax(scores[bs * v: bs * (v + 1)].float() / temperature,
+                                                                 dim=1), dim=1))
+        total = total + loss / len(others)
+    return total / len(crops_for_assign)
+
+
+def _grad_errors(names, ours, ref, stock):
+    """Flat and per-tensor relative errors of ours and of stock bf16 against the fp32 reference."""
+    per = [(n, _rel(ours[n], ref[n]), _rel(stock[n], ref[n]), ref[n].norm().item()) for n in names]
+    flat = (_rel(torch.cat([ours[n].reshape(-1) for n in names]), torch.cat([ref[n].reshape(-1) for n in names])),
+            _rel(torch.cat([stock[n].reshape(-1) for n in names]), torch.cat([ref[n].reshape(-1) for n in names])))
+    return flat, per
+
+
+FLAT_RATIO, TENSOR_RATIO, TENSOR_SLACK = 1.3, 1.3, 2e-3
+
+
+def _violations(flat, per):
+    bad = []
+    if flat[0] > FLAT_RATIO * flat[1]:
+        bad.append(("<flat>", flat[0], flat[1]))
+    bad += [(n, o, s) for n, o, s, _ in per if o > TENSOR_RATIO * s + TENSOR_SLACK]
+    return bad
+
+
+@pytest.mark.timeout(400)
 def test_full_swav_model_and_loss_match_fp32_twin(cuda):
+    """The whole model (trunk + projection MLP + prototypes), one backward, against the same
+    parameters in stock fp32 modules and in stock bf16 autocast.
+
+    Gradient parity is taken through a well-conditioned loss: at random
+    init the SwAV loss's gradient signal lies below bf16 resolution — its logits differ in the 3rd-4th
+    digit, so even stock bf16's flat gradient is as far from fp32 as a random vector (measured 1.32
+    relative with the Sinkhorn assignments fixed in fp32, b = 32: profiles/r6_parity_margins.jsonl),
+    and a bound relative to it detects nothing.  So: the SwAV loss VALUE is compared (ours / fp32 /
+    stock bf16, same fixed fp32 assignments), and the gradients are compared under a fixed random
+    projection of the model's outputs (loss = <emb, R1> + <scores, R2>), whose upstream gradient is
+    O(1) for every sample and element: stock bf16's error then reflects bf16 arithmetic alone.  Ours
+    is held to 1.3x stock, flat AND per tensor, and the comparison's power is checked: ours with one
+    conv's weight gradient scaled by 1.02 (a 2% kernel bug) must FAIL the bound.  The SwAV loss's own
+    backward kernel is checked against fp32 in tests/test_swav_kernels_gpu.py."""
     from dedloc_amd.models.resnet_swav import SwAVModel
-    from dedloc_amd.models.swav_loss import SwAVLoss
-    from dedloc_amd.training.swav_eager import EagerSwAVLoss, eager_twin
+    from dedloc_amd.models.swav_loss import _SwAVCE
+    from dedloc_amd.training.swav_eager import eager_twin, vissl_sinkhorn
     from dedloc_amd.utils.flat import FlatParams
 
     torch.manual_seed(0)
-    bs, nc = 8, 8
+    bs, nc, T, cfa = 32, 8, 0.1, (0, 1)
     model = SwAVModel(num_prototypes=3000)
     model.normalize_prototypes()
     ref = eager_twin(model, device=cuda).train()
@@ -57,52 +105,60 @@ def test_full_swav_model_and_loss_match_fp32_twin(cuda):
     model.bind_flat(flat)
     model.concurrent_passes = True
     crops = _crops(cuda, bs, seed=1)
-    loss_kw = dict(num_crops=nc, crops_for_assign=(0, 1), temperature=0.1, epsilon=0.03, num_iters=3,
-                   num_prototypes=3000, embedding_dim=128, queue_length=0, batch_size=bs)
+    gen = torch.Generator(device="cpu").manual_seed(5)
+
+    emb_r, scores_r = ref([c.float() for c in crops])
+    r1 = torch.randn(emb_r.shape, generator=gen).to(cuda)
+    r2 = torch.randn(scores_r.shape, generator=gen).to(cuda)
+    with torch.no_grad():  # SwAV loss values under the same fp32 assignments
+        qs = [vissl_sinkhorn(scores_r[bs * c: bs * (c + 1)].float(), 0.03, 3) for c in cfa]
+        swav_r = _ce_with_q(scores_r, qs, cfa, nc, bs, T).item()
+    ((emb_r.float() * r1).sum() + (scores_r.float() * r2).sum()).backward()
 
     with torch.autocast("cuda", dtype=torch.bfloat16):
         emb, scores = model(crops)
-    loss = SwAVLoss(**loss_kw).to(cuda)(emb.float(), scores, model.heads[0].prototypes0.weight, 0)
-    loss.backward()
+    with torch.no_grad():
+        swav_o = _SwAVCE.apply(scores, qs, list(cfa), nc, bs, T).item()
+    ((emb.float() * r1).sum() + (scores.float() * r2).sum()).backward()
     model.after_backward()
-
-    emb_r, scores_r = ref([c.float() for c in crops])
-    loss_r = EagerSwAVLoss(**loss_kw).to(cuda)(emb_r, scores_r, ref.heads[0].prototypes0.weight, 0)
-    loss_r.backward()
 
     with torch.autocast("cuda", dtype=torch.bfloat16):
         emb_s, scores_s = stock(crops)
-    loss_s = EagerSwAVLoss(**loss_kw).to(cuda)(emb_s.float(), scores_s, stock.heads[0].prototypes0.weight, 0)
-    loss_s.backward()
+    with torch.no_grad():
+        swav_s = _ce_with_q(scores_s, qs, cfa, nc, bs, T).item()
+    ((emb_s.float() * r1).sum() + (scores_s.float() * r2).sum()).backward()
+    torch.cuda.synchronize()
 
-    assert torch.isfinite(loss) and abs(loss.item() - loss_r.item()) < 1e-2 * abs(loss_r.item()), \
-        (loss.item(), loss_r.item(), loss_s.item())
     rp, sp = dict(ref.named_parameters()), dict(stock.named_parameters())
-    ours_all, ref_all, stock_all = [], [], []
-    worst = []
-    for n in flat.names:
-        g = flat.view(flat.grad, n).float()
-        gr, gs = rp[n].grad.float(), sp[n].grad.float()
-        ours_all.append(g.reshape(-1))
-        ref_all.append(gr.reshape(-1))
-        stock_all.append(gs.reshape(-1))
-        worst.append((n, _rel(g, gr), _rel(gs, gr)))
-    ours_err = _rel(torch.cat(ours_all), torch.cat(ref_all))
-    stock_err = _rel(torch.cat(stock_all), torch.cat(ref_all))
-    print(f"loss ours {loss.item():.5f} fp32 {loss_r.item():.5f} bf16-stock {loss_s.item():.5f}; flat gradient "
-          f"rel err ours {ours_err:.4f} stock bf16 {stock_err:.4f}")
-    head = [(n, o, s) for n, o, s in worst if n.startswith("heads.")]
-    record_margin("swav_model_and_loss_vs_fp32_twin", loss_ours=loss.item(), loss_fp32=loss_r.item(),
-                  loss_stock_bf16=loss_s.item(), loss_rel_delta=abs(loss.item() - loss_r.item()) / abs(loss_r.item()),
-                  loss_bound=1e-2, grad_rel_err_ours=ours_err, grad_rel_err_stock_bf16=stock_err,
-                  grad_bound=1.3 * stock_err + 5e-3,
-                  head_worst=max(((o, n) for n, o, _ in head), default=(0.0, None)),
-                  head_worst_ratio_to_stock=max((o / max(s, 1e-12) for _, o, s in head), default=0.0))
-    assert ours_err < 1.3 * stock_err + 5e-3, (ours_err, stock_err)
-    # the head (after the trunk's drift has been summed into 2048 features) tightly
-    for n, o, s in worst:
-        if n.startswith("heads."):
-            assert o < 1.3 * s + 1e-2, (n, o, s)
+    names = list(flat.names)
+    ours = {n: flat.view(flat.grad, n).float().clone() for n in names}
+    refg = {n: rp[n].grad.float() for n in names}
+    stockg = {n: sp[n].grad.float() for n in names}
+    flat_err, per = _grad_errors(names, ours, refg, stockg)
+    bad = _violations(flat_err, per)
+
+    # power check: a 2% error in one conv's weight gradient — the conv whose stock-bf16 gradient is
+    # most accurate (where the bound is tightest)
+    convs = [(s_, n) for n, o, s_, norm in per if n.endswith(".weight") and ".conv" in n and norm > 0]
+    target = min(convs)[1]
+    mutant = dict(ours)
+    mutant[target] = ours[target] * 1.02
+    m_flat, m_per = _grad_errors(names, mutant, refg, stockg)
+    m_bad = _violations(m_flat, m_per)
+
+    worst = sorted(per, key=lambda t: t[1] / max(TENSOR_RATIO * t[2] + TENSOR_SLACK, 1e-12), reverse=True)[:5]
+    print(f"SwAV loss ours {swav_o:.5f} fp32 {swav_r:.5f} bf16-stock {swav_s:.5f}; projected-loss flat gradient "
+          f"rel err ours {flat_err[0]:.4f} stock bf16 {flat_err[1]:.4f}; worst tensors {worst}")
+    record_margin("swav_model_projection_grad_vs_fp32_twin", batch=bs, swav_loss_ours=swav_o, swav_loss_fp32=swav_r,
+                  swav_loss_stock_bf16=swav_s, grad_rel_err_ours=flat_err[0], grad_rel_err_stock_bf16=flat_err[1],
+                  flat_bound=FLAT_RATIO * flat_err[1], tensor_bound=f"{TENSOR_RATIO} x stock + {TENSOR_SLACK}",
+                  worst_tensors=worst, violations=bad, mutant_target=target,
+                  mutant_target_err=[o for n, o, _, _ in m_per if n == target][0],
+                  mutant_violations=m_bad[:3])
+    assert abs(swav_o - swav_r) < 5e-3 * abs(swav_r), (swav_o, swav_r, swav_s)
+    assert flat_err[1] <= 0.05, flat_err  # a non-chaotic comparison
+    assert not bad, bad[:10]
+    assert m_bad, ("a 2% weight-gradient error went undetected", target)
 
 
 @pytest.mark.timeout(600)
