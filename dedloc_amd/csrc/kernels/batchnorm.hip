@@ -397,10 +397,20 @@ inline bool bn_shape_ok(int C) {
 #ifndef DL_BN_STATS_MAXB
 #define DL_BN_STATS_MAXB 256  // (a measurement build may override)
 #endif
+// Deterministic statistics (DEDLOC_DETERMINISTIC_BN=1, read at every launch so a process can switch
+// it around one parity run): ONE block per statistics group, so every channel's sum is one fixed-order
+// block reduction added to a zeroed slot — bitwise reproducible, and slow (parity runs only).  The
+// model side also stops accumulating statistics in conv / GEMM epilogues (models/resnet_swav.py).
+inline bool bn_deterministic() {
+  const char* e = std::getenv("DEDLOC_DETERMINISTIC_BN");
+  return e != nullptr && e[0] == '1';
+}
+
 inline int stats_blocks(long R, int C, long& rpb) {
   const long rpi = kThreads / (C / 8);
   long nb = (R + 8 * rpi - 1) / (8 * rpi);
   if (nb > DL_BN_STATS_MAXB) nb = DL_BN_STATS_MAXB;
+  if (bn_deterministic()) nb = 1;
   if (nb < 1) nb = 1;
   rpb = (R + nb - 1) / nb;
   return (int)((R + rpb - 1) / rpb);

@@ -24,11 +24,21 @@ from __future__ import annotations
 
 from typing import List, Sequence
 
+import os
+
 import torch
 import torch.nn as nn
 
 from .. import ops as _ops  # noqa: F401  (registers torch.ops.dedloc.*)
 from torch.utils.checkpoint import checkpoint
+
+
+def deterministic_bn() -> bool:
+    """DEDLOC_DETERMINISTIC_BN=1: bitwise-reproducible BatchNorm statistics for parity runs — every
+    statistic is one fixed-order reduction (batchnorm.hip ``bn_deterministic``: one block per
+    statistics group) instead of fp32 atomics from many blocks, conv / GEMM epilogues and the
+    BN-backward preparation links (their atomics from many tiles) are bypassed.  Slow; off by default."""
+    return os.environ.get("DEDLOC_DETERMINISTIC_BN", "") == "1"
 
 
 def join_batch(ts: Sequence[torch.Tensor]) -> torch.Tensor:
@@ -253,7 +263,7 @@ class ConvNHWC(nn.Conv2d):
             raise NotImplementedError("ConvNHWC: only the ResNet-50 conv forms (no bias, groups 1, square "
                                       "stride/padding) have kernels")
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        if bn is not None and self.epilogue_stats and bn.takes_conv_stats():
+        if bn is not None and self.epilogue_stats and bn.takes_conv_stats() and not deterministic_bn():
             bn.stats_ready = True
             return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, bn.pass_ws[0],
                                    bn.stat_groups, link, bn_link)
@@ -378,7 +388,7 @@ class Bottleneck(nn.Module):
         # the previous block's bn3 backward preparation can ride in conv1's data gradient only when
         # that gradient is the whole gradient of x: identity block, identity gradient linked in
         in_link = getattr(x, "_dedloc_bn_link", None)
-        fused_bwd = x.requires_grad and torch.is_grad_enabled()
+        fused_bwd = x.requires_grad and torch.is_grad_enabled() and not deterministic_bn()
         if self.downsample is None:
             idt = x
             if fused_bwd:
