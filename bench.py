@@ -16,6 +16,9 @@ The total work per step is fixed as N grows, so scaling is "strong".
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8   # same, launched by torchrun
     python bench.py --model swav            # BASELINE config 3 (collaborative SwAV ResNet-50), same contract
 
+The default single-GPU run also measures BASELINE config 3 in a child process first and reports it
+under the ``swav`` key of the same JSON line (``--swav 0`` turns that off).
+
 Peers are independent processes, one per GPU, as in the reference's fleet (each AWS worker runs its
 own run_trainer, albert/AWS_runner.ipynb:293-297).  Without a launcher (no WORLD_SIZE in the
 environment) ``--gpus N`` makes this script start the N peer processes itself, before it touches
@@ -90,6 +93,11 @@ def parse():
     ap.add_argument("--allow_shared_device", action="store_true",
                     help="let several peers share one GPU (protocol emulation on a small box); the JSON line "
                          "reports physical_gpus < n_gpus.  Without it, more peers than visible GPUs is an error")
+    ap.add_argument("--swav", type=int, default=1,
+                    help="with the default single-GPU ALBERT run: also measure BASELINE config 3 (--model swav) in a "
+                         "fresh child process started before this process touches the GPU, and report it under the "
+                         "'swav' key (the headline keys are unchanged; a child failure only sets swav.error).  0: off")
+    ap.add_argument("--swav_steps", type=int, default=3, help="timed collaborative steps of the SwAV child run")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -144,6 +152,26 @@ def _self_launch(args) -> int:
 
 _BACKEND_CODE = {"rccl": 0, "gloo": 1, "rccl+gloo": 2}
 _BACKEND_NAME = {v: k for k, v in _BACKEND_CODE.items()}
+
+
+def _swav_child(args) -> dict:
+    """BASELINE config 3 in a child process (``bench.py --model swav``): its own CUDA context, started
+    and finished before this process initialises the GPU, so neither run sees the other's memory."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--model", "swav", "--gpus", "1", "--steps", str(args.swav_steps),
+           "--warmup", "1", "--swav", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=ROOT)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout after 900 s", "cmd": " ".join(cmd[1:])}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}: {r.stderr.strip()[-400:]}", "cmd": " ".join(cmd[1:])}
+    out = json.loads(lines[-1])
+    keep = ("metric", "value", "unit", "vs_baseline", "ms_per_step", "steps", "warmup", "config", "data_plane",
+            "ema_samples_per_s_sum", "first_microstep_s")
+    return dict({k: out.get(k) for k in keep}, wall_s=round(time.perf_counter() - t0, 1), cmd=" ".join(cmd[1:]))
 
 
 def _protocol_breakdown(gathered, keys):
@@ -266,6 +294,10 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_self_launch(args))
+    swav = None
+    if (args.swav and args.model == "albert" and args.impl == "dedloc" and not args.cpu_test and args.gpus == 1
+            and "WORLD_SIZE" not in os.environ and torch.cuda.device_count() > 0):
+        swav = _swav_child(args)  # before this process touches the GPU (device_count does not)
     logging.basicConfig(level=logging.INFO if args.verbose else logging.WARNING,
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     rank, world, dev = _harness_world(cpu=bool(args.cpu_test))
@@ -377,6 +409,8 @@ def main():
                "per_peer": per_peer})
         if fallback:
             out["error"] = f"data plane is not RCCL on every peer: {per_peer['data_plane']}"
+        if swav is not None:
+            out["swav"] = swav
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
