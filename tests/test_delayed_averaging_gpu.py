@@ -12,6 +12,7 @@ Here two peer processes share one MI355X (gloo data plane: RCCL takes one rank p
 * the side-stream branch ran: every peer has a side stream and >= 5 completed parameter rounds;
 * the peers end with the same parameters within FLOAT16-wire tolerance;
 * the delayed run's loss stays within a 5% band of the synchronous run's over the last steps.
+  (No "it learns" check: the synthetic MLM tokens are uniform, so 12 steps cannot move the loss.)
 
 Reference: SURVEY §5.3 "Delayed parameter averaging"; ``sahajbert/run_trainer.py:215-300``.
 """
@@ -102,6 +103,6 @@ def test_delayed_parameter_averaging_two_peers_share_one_gpu(tmp_path):
         fh.write(json.dumps(margins) + "\n")
     # equal parameters up to the FLOAT16 wire: |diff| within a few fp16 ulps of the largest parameter
     assert diff <= 4e-3 * max(scale, 1e-3), margins
-    # the model learns, and the delayed run tracks the synchronous one
-    assert delayed < losses[0][first], margins
+    # the delayed run tracks the synchronous one (the synthetic tokens are uniform, so the MLM loss sits
+    # near ln(vocab) in both: the band checks that delayed averaging does not derail training)
     assert abs(delayed - sync) <= 0.05 * sync, margins
