@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--compression", default="NONE")
     ap.add_argument("--delay_param_averaging", action="store_true")
     ap.add_argument("--lr", type=float, default=None)
+    ap.add_argument("--aux", action="store_true",
+                    help="an auxiliary (reducer-only) peer: step_aux() every 0.1 s until <out>/stop exists")
     ap.add_argument("--final", action="store_true",
                     help="at the end: finish (and apply) a pending delayed parameter round, save the final "
                          "parameters and the counters to <out>/<name>-final.pt")
@@ -61,7 +63,7 @@ def main():
                                    averaging_timeout=args.averaging_timeout,
                                    metadata_expiration=args.metadata_expiration, min_refresh_period=0.2,
                                    default_refresh_period=0.5)
-    peer = AlbertPeer(targs, dargs, cargs, torch.device(args.device), rank=0)
+    peer = AlbertPeer(targs, dargs, cargs, torch.device(args.device), rank=0, auxiliary=args.aux)
     co = peer.collab_opt
     log = open(os.path.join(args.out, f"peer-{args.name}.jsonl"), "a")
     inner = co.averager.step
@@ -83,6 +85,17 @@ def main():
         log.write(json.dumps({"event": "join", "ok": bool(ok), "step": co.local_step,
                               "download": co.averager.last_download, "t": time.time()}) + "\n")
         log.flush()
+    if args.aux:
+        while not os.path.exists(os.path.join(args.out, "stop")):
+            g = co.step_aux()
+            if g is not None:
+                log.write(json.dumps({"event": "aux_round", "step": co.local_step, "size": g.get("size"),
+                                      "group_id": g.get("group_id"), "backend": g.get("backend"),
+                                      "t": time.time()}) + "\n")
+                log.flush()
+            time.sleep(0.1)
+        peer.shutdown()
+        return
     last = co.local_step
     while co.local_step < args.steps:
         peer.train_step()

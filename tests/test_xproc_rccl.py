@@ -185,3 +185,93 @@ def test_sigkill_mid_round_survivors_rebuild_and_joiner_downloads_over_rccl(tmp_
     other = torch.load(out / f"p0-s{p0[js['group_id']] - 1}.pt", weights_only=True)
     assert js["group_id"] == other["group_id"]
     torch.testing.assert_close(js["params"], other["params"], rtol=1e-6, atol=1e-7)
+
+
+def _run_peers(tmp_path, specs, steps=10, timeout_s=8.0, expiration_s=2.0, wait_s=200):
+    """Start collab_peer processes (name, extra args, extra env) together through the barrier; the
+    trainers run ``steps`` global steps, auxiliary peers run until the trainers are done."""
+    from dedloc_amd.dht import DHT
+
+    cfg = _tiny_cfg(tmp_path)
+    out = tmp_path / "out"
+    out.mkdir()
+    root = DHT(listen_on="127.0.0.1:*")
+    procs = {}
+    try:
+        for name, extra, env in specs:
+            cmd = [sys.executable, PEER, "--root", root.endpoint, "--cfg", str(cfg), "--name", name, "--out", str(out),
+                   "--steps", str(steps), "--averaging_timeout", str(timeout_s), "--averaging_expiration",
+                   str(expiration_s), "--barrier", *extra]
+            procs[name] = subprocess.Popen(cmd, cwd=ROOT, env=_env(tmp_path / "mbox", **env), stdout=subprocess.DEVNULL,
+                                           stderr=open(out / f"{name}.err", "w"), start_new_session=True)
+        assert _wait(lambda: all((out / f"ready-{n}").exists() for n in procs), 120)
+        (out / "go").touch()
+        trainers = [n for n, extra, _ in specs if "--aux" not in extra]
+        for n in trainers:
+            procs[n].wait(timeout=wait_s)
+        (out / "stop").touch()
+        for n in procs:
+            assert procs[n].wait(timeout=60) == 0, (n, (out / f"{n}.err").read_text()[-3000:])
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+        root.shutdown()
+    return out
+
+
+@pytest.mark.multiproc
+@pytest.mark.timeout(300)
+def test_mixed_group_gpu_trainers_and_cpu_aux_across_processes(tmp_path):
+    """The reference fleet's shape (AWS_runner.ipynb:26-30: GPU trainers + CPU auxiliary peers) across
+    processes: three "GPU" trainers on the RCCL stand-in and one auxiliary peer forced to gloo
+    (DEDLOC_DATA_PLANE=gloo, a CPU aux) form hybrid groups — RCCL among the trainers, gloo only for
+    the pairs with the aux — every round succeeds and the trainers hold the same average."""
+    specs = [(f"t{i}", [], {}) for i in range(3)] + [("aux", ["--aux"], {"DEDLOC_DATA_PLANE": "gloo"})]
+    out = _run_peers(tmp_path, specs, steps=8)
+    recs = {n: [r for r in _records(out, n) if r["event"] == "step"] for n in ("t0", "t1", "t2")}
+    for n, rs in recs.items():
+        assert rs[-1]["failed"] == 0, (n, rs)
+        hybrid = [r for r in rs if r["backend"] == "rccl+gloo"]
+        assert len(hybrid) >= 5 and all(r["size"] == 4 for r in hybrid), (n, rs)
+        assert rs[-1]["created"] <= 2, rs[-1]  # built once (a second only if the aux joined late)
+    aux = [r for r in _records(out, "aux") if r["event"] == "aux_round"]
+    assert len(aux) >= 5 and all(r["backend"] == "rccl+gloo" for r in aux), aux
+    # an exact round: the trainers of one hybrid round hold the same average
+    last = {n: [r for r in rs if r["backend"] == "rccl+gloo"][-1] for n, rs in recs.items()}
+    assert len({r["group_id"] for r in last.values()}) == 1, last
+    snaps = [torch.load(out / f"{n}-s{r['step'] - 1}.pt", weights_only=True) for n, r in last.items()]
+    for s in snaps[1:]:
+        torch.testing.assert_close(s["params"], snaps[0]["params"], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.multiproc
+@pytest.mark.timeout(300)
+def test_asynchronous_rccl_error_fails_one_round_then_rebuilds(tmp_path):
+    """An asynchronous RCCL error on one member (ncclSystemError reported by a status poll after its
+    grouped call was accepted): that member's round fails AT ONCE (its own RCCL failed: no deadline
+    wait), the others' at the round's deadline; they drop the communicator and average on a freshly
+    built one in the next round.  (The failed member itself moves on with its local gradients — it
+    is ahead for a while, exactly as a hivemind peer whose round failed.)"""
+    timeout_s = 8.0
+    specs = [(f"p{i}", [], {"DEDLOC_XPROC_ERROR_AT_P2P": "5"} if i == 2 else {}) for i in range(4)]
+    out = _run_peers(tmp_path, specs, steps=8, timeout_s=timeout_s)
+    recs = {n: [r for r in _records(out, n) if r["event"] == "step"] for n in ("p0", "p1", "p2", "p3")}
+    first_fail = {}
+    for n, rs in recs.items():
+        i = next(k for k, r in enumerate(rs) if r["failed"] > 0)
+        assert all(r["size"] == 4 and r["created"] == 1 for r in rs[:i]), (n, rs[:i])
+        first_fail[n] = (i, rs[i]["t"])
+    # the erroring member failed without waiting for the deadline; the others waited it out
+    t_err = first_fail["p2"][1]
+    for n in ("p0", "p1", "p3"):
+        assert first_fail[n][1] - t_err > timeout_s - 3.0, first_fail
+    rebuilt = set()
+    for n in ("p0", "p1", "p3"):
+        rs, i = recs[n], first_fail[n][0]
+        assert rs[-1]["failed"] == 1 and i < len(rs) - 1, (n, rs)
+        after = rs[i + 1]
+        assert after["size"] >= 3 and after["created"] == 2 and after["backend"] == "rccl", (n, after)
+        rebuilt.add(after["group_id"])
+    assert len(rebuilt) == 1, rebuilt
