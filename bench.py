@@ -154,6 +154,13 @@ _BACKEND_CODE = {"rccl": 0, "gloo": 1, "rccl+gloo": 2}
 _BACKEND_NAME = {v: k for k, v in _BACKEND_CODE.items()}
 
 
+def rccl_fallback(dev_type: str, world: int, physical: int, planes) -> bool:
+    """N > 1 peers on N distinct GPUs must average over RCCL: a silent fallback to host-staged gloo
+    (a broken RCCL on the box) must not become the scaling number — such a run exits non-zero.
+    Peers sharing a device (``--allow_shared_device``) and CPU plumbing runs are exempt."""
+    return dev_type == "cuda" and world > 1 and physical == world and any(b != "rccl" for b in planes)
+
+
 def _swav_child(args) -> dict:
     """BASELINE config 3 in a child process (``bench.py --model swav``): its own CUDA context, run
     after the parent's timed region and once the parent has freed its memory (the parent only
@@ -388,10 +395,7 @@ def main():
                 "comms_quarantined": [int(g[n0 + 2]) for g in gathered],
                 "data_plane": [_BACKEND_NAME.get(int(g[n0 + 3])) for g in gathered],
                 "averaging_failed": [int(g[n0 + 4]) for g in gathered]}
-    # N > 1 peers on N distinct GPUs must average over RCCL: a silent fallback to host-staged gloo
-    # (a broken RCCL on the box) must not become the scaling number
-    fallback = (dev.type == "cuda" and world > 1 and physical == world
-                and any(b != "rccl" for b in per_peer["data_plane"]))
+    fallback = rccl_fallback(dev.type, world, physical, per_peer["data_plane"])
     if rank == 0:
         value = total_samples / max_dt
         out = dict(describe(value, world), n_gpus=world, steps=args.steps, warmup=args.warmup,

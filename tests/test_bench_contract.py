@@ -113,3 +113,19 @@ def test_bench_swav_mode_two_ranks_cpu():
     assert out["metric"].startswith("samples/sec (whole node) SwAV ResNet-50") and out["n_gpus"] == 2
     assert out["config"]["model"] == "swav-resnet50" and out["config"]["optimizer"] == "LARC-SGD"
     assert out["averaging_rounds"] >= 2 and out["averaging_failed"] == 0 and out["last_group"]["size"] == 2
+
+
+def test_bench_fails_multi_gpu_runs_that_fell_back_to_gloo():
+    """N > 1 peers on N GPUs that did not all average over RCCL make bench.py exit 3
+    (the decision; the exit itself needs a multi-GPU box)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_script", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)  # (the bench/ package shadows the name "bench")
+    spec.loader.exec_module(bench)
+    assert bench.rccl_fallback("cuda", 8, 8, ["rccl"] * 7 + ["gloo"])
+    assert bench.rccl_fallback("cuda", 2, 2, [None, "rccl"])  # a peer whose last round failed
+    assert not bench.rccl_fallback("cuda", 8, 8, ["rccl"] * 8)
+    assert not bench.rccl_fallback("cuda", 4, 1, ["gloo"] * 4)  # --allow_shared_device: gloo by design
+    assert not bench.rccl_fallback("cpu", 8, 0, ["rccl"] * 8)   # CPU plumbing
+    assert not bench.rccl_fallback("cuda", 1, 1, [None])        # one peer averages with nobody
