@@ -154,11 +154,16 @@ _BACKEND_CODE = {"rccl": 0, "gloo": 1, "rccl+gloo": 2}
 _BACKEND_NAME = {v: k for k, v in _BACKEND_CODE.items()}
 
 
-def rccl_fallback(dev_type: str, world: int, physical: int, planes) -> bool:
+def rccl_fallback(dev_type: str, world: int, physical: int, rccl_rounds, other_rounds) -> bool:
     """N > 1 peers on N distinct GPUs must average over RCCL: a silent fallback to host-staged gloo
-    (a broken RCCL on the box) must not become the scaling number — such a run exits non-zero.
-    Peers sharing a device (``--allow_shared_device``) and CPU plumbing runs are exempt."""
-    return dev_type == "cuda" and world > 1 and physical == world and any(b != "rccl" for b in planes)
+    (a broken RCCL on the box) must not become the scaling number — such a run exits non-zero.  The
+    check is over every successful round of the timed region, per peer: any round over gloo or a
+    mixed group, or a peer with no RCCL round at all, fails the run (a single failed round — e.g. a
+    straggler at the very end — does not).  Peers sharing a device (``--allow_shared_device``) and
+    CPU plumbing runs are exempt."""
+    if not (dev_type == "cuda" and world > 1 and physical == world):
+        return False
+    return any(o > 0 for o in other_rounds) or any(r == 0 for r in rccl_rounds)
 
 
 def _swav_child(args) -> dict:
@@ -365,6 +370,7 @@ def main():
     keys = ("wait_s", "fetch_s", "averaging_s", "matchmaking_s", "allreduce_s", "optimizer_s", "tail_s", "local_steps",
             "global_steps")
     st0 = {k: co.stats.get(k, 0.0) for k in keys}
+    st0_rounds = (co.stats.get("rounds_rccl", 0), co.stats.get("rounds_gloo", 0) + co.stats.get("rounds_rccl+gloo", 0))
     t0 = time.perf_counter()
     samples = run_until(base + args.warmup + args.steps)
     sync()
@@ -378,9 +384,12 @@ def main():
         co._device_timer.poll()
     ema = co.performance_ema.samples_per_second
     comms = co.averager.comms
+    rccl_rounds = co.stats.get("rounds_rccl", 0) - st0_rounds[0]
+    other_rounds = co.stats.get("rounds_gloo", 0) + co.stats.get("rounds_rccl+gloo", 0) - st0_rounds[1]
     stats = torch.tensor([samples, dt, ema] + [co.stats.get(k, 0.0) - st0[k] for k in keys]
                          + [comms.created, comms.aborted, comms.quarantined, float(_BACKEND_CODE.get(
-                             (co.last_group or {}).get("backend"), -1)), co.stats["averaging_failed"]],
+                             (co.last_group or {}).get("backend"), -1)), co.stats["averaging_failed"],
+                            rccl_rounds, other_rounds],
                          dtype=torch.float64)
     if world > 1:
         gathered = [torch.zeros_like(stats) for _ in range(world)]
@@ -394,8 +403,10 @@ def main():
     per_peer = {"comms_created": [int(g[n0]) for g in gathered], "comms_aborted": [int(g[n0 + 1]) for g in gathered],
                 "comms_quarantined": [int(g[n0 + 2]) for g in gathered],
                 "data_plane": [_BACKEND_NAME.get(int(g[n0 + 3])) for g in gathered],
-                "averaging_failed": [int(g[n0 + 4]) for g in gathered]}
-    fallback = rccl_fallback(dev.type, world, physical, per_peer["data_plane"])
+                "averaging_failed": [int(g[n0 + 4]) for g in gathered],
+                # successful timed-region rounds per peer: over RCCL / over gloo or mixed groups
+                "rounds_rccl": [int(g[n0 + 5]) for g in gathered], "rounds_other": [int(g[n0 + 6]) for g in gathered]}
+    fallback = rccl_fallback(dev.type, world, physical, per_peer["rounds_rccl"], per_peer["rounds_other"])
     if rank == 0:
         value = total_samples / max_dt
         out = dict(describe(value, world), n_gpus=world, steps=args.steps, warmup=args.warmup,
@@ -413,7 +424,8 @@ def main():
                "last_group": {k: v for k, v in (co.last_group or {}).items() if k != "gathered"},
                "per_peer": per_peer})
         if fallback:
-            out["error"] = f"data plane is not RCCL on every peer: {per_peer['data_plane']}"
+            out["error"] = (f"data plane is not RCCL on every peer: rounds over RCCL {per_peer['rounds_rccl']}, "
+                            f"over gloo / mixed groups {per_peer['rounds_other']}")
         if want_swav:
             import gc
 
@@ -434,8 +446,9 @@ def main():
         dist.destroy_process_group()
     if fallback:
         if rank == 0:
-            print(f"bench.py: {world} peers on {physical} GPUs did not all average over RCCL "
-                  f"({per_peer['data_plane']}); failing the run", file=sys.stderr)
+            print(f"bench.py: {world} peers on {physical} GPUs did not all average over RCCL (rounds over RCCL "
+                  f"{per_peer['rounds_rccl']}, over gloo / mixed {per_peer['rounds_other']}); failing the run",
+                  file=sys.stderr)
         sys.exit(3)
 
 

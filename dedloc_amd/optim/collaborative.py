@@ -421,6 +421,10 @@ class CollaborativeOptimizer:
                                                      "or the round failed; applying local gradients")
                 else:
                     self._adopt_group_step(group)
+                    # successful rounds per data plane ("rccl" / "gloo" / "rccl+gloo"): bench.py checks
+                    # that a multi-GPU run averaged over RCCL, not over a silent gloo fallback
+                    key = f"rounds_{group.get('backend')}"
+                    self.stats[key] = self.stats.get(key, 0) + 1
             else:
                 logger.log(self.status_loglevel, "Skipped averaging: collaboration consists of this peer alone")
             t_opt = time.perf_counter()

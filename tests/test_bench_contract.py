@@ -123,9 +123,11 @@ def test_bench_fails_multi_gpu_runs_that_fell_back_to_gloo():
     spec = importlib.util.spec_from_file_location("bench_script", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)  # (the bench/ package shadows the name "bench")
     spec.loader.exec_module(bench)
-    assert bench.rccl_fallback("cuda", 8, 8, ["rccl"] * 7 + ["gloo"])
-    assert bench.rccl_fallback("cuda", 2, 2, [None, "rccl"])  # a peer whose last round failed
-    assert not bench.rccl_fallback("cuda", 8, 8, ["rccl"] * 8)
-    assert not bench.rccl_fallback("cuda", 4, 1, ["gloo"] * 4)  # --allow_shared_device: gloo by design
-    assert not bench.rccl_fallback("cpu", 8, 0, ["rccl"] * 8)   # CPU plumbing
-    assert not bench.rccl_fallback("cuda", 1, 1, [None])        # one peer averages with nobody
+    f = bench.rccl_fallback
+    assert f("cuda", 8, 8, [10] * 8, [0] * 7 + [1])          # one round of one peer over gloo
+    assert f("cuda", 2, 2, [0, 10], [0, 0])                  # a peer that never averaged over RCCL
+    assert not f("cuda", 8, 8, [10] * 8, [0] * 8)
+    assert not f("cuda", 8, 8, [10] * 7 + [9], [0] * 8)      # a straggler's last round failed: fine
+    assert not f("cuda", 4, 1, [0] * 4, [10] * 4)            # --allow_shared_device: gloo by design
+    assert not f("cpu", 8, 0, [10] * 8, [0] * 8)             # CPU plumbing
+    assert not f("cuda", 1, 1, [0], [0])                     # one peer averages with nobody

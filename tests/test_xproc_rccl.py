@@ -71,6 +71,7 @@ def test_bench_eight_peers_albert_one_reused_rccl_communicator(tmp_path):
     assert out["last_group"]["size"] == 8
     assert pp["comms_created"] == [1] * 8 and pp["comms_aborted"] == [0] * 8, pp  # built once, reused
     assert pp["comms_quarantined"] == [0] * 8
+    assert min(pp["rounds_rccl"]) >= 10 and pp["rounds_other"] == [0] * 8, pp
 
 
 @pytest.mark.multiproc
