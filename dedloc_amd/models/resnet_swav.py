@@ -72,10 +72,11 @@ class _GradLink:
     conv1's backward, whose data-gradient GEMM adds it in its epilogue.  bn3's backward always runs
     first: conv1's backward depends on it through conv3 -> bn2 -> conv2 -> bn1."""
 
-    __slots__ = ("g",)
+    __slots__ = ("g", "early")
 
     def __init__(self):
         self.g = None
+        self.early = False  # the consumer ran before the producer (see _ConvNHWC.backward)
 
 
 class _BnBwdLink:
@@ -155,7 +156,7 @@ class _ConvNHWC(torch.autograd.Function):
     bound ``.grad`` (the flat gradient buffer, KRSC layout) when there is one, like the ALBERT layer."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, module, stats=None, groups=1, link=None, bn_link=None):
+    def forward(ctx, x, weight, stride, pad, module, stats=None, groups=1, link=None, bn_link=None, give=None):
         # bf16 copy of the weight (keeps the channels-last KRSC strides), shared by the trunk passes
         # of one SwAVModel.forward (one cast per iteration instead of one per resolution group); the
         # model clears the cache at the start and end of every forward, so an optimizer update
@@ -173,6 +174,7 @@ class _ConvNHWC(torch.autograd.Function):
         ctx.save_for_backward(x if cols is None else cols, wb)
         ctx.stride, ctx.pad, ctx.module = stride, pad, module
         ctx.has_cols, ctx.xshape, ctx.link, ctx.bn_link = cols is not None, tuple(x.shape), link, bn_link
+        ctx.give = give
         ctx.gslot = getattr(module, "_gslot", None)  # a concurrent second pass's weight-gradient buffer
         if stats is not None:  # the consuming BatchNorm's statistics, accumulated by the conv's epilogue
             return torch.ops.dedloc.conv2d_fwd_stats(x, wb, stride, pad, stats, groups, cols)
@@ -192,6 +194,8 @@ class _ConvNHWC(torch.autograd.Function):
             res = None
             if ctx.link is not None:  # + the block's identity-branch gradient (see _GradLink)
                 res, ctx.link.g = ctx.link.g, None
+                if res is None:  # the producer has not run (yet): it returns its gradient itself
+                    ctx.link.early = True
             bl = ctx.bn_link
             if bl is not None and bl.bn is not None:  # + the producing BN's backward preparation (_BnBwdLink)
                 bx, mean, rstd, gamma, beta, sums, G, has_res = bl.bn
@@ -200,6 +204,11 @@ class _ConvNHWC(torch.autograd.Function):
                                                                beta, sums, G, wds)
             else:
                 dx = torch.ops.dedloc.conv2d_dgrad(dy, wb, ctx.stride, ctx.pad, x.shape[2], x.shape[3], res, wds)
+        if ctx.give is not None and dx is not None and not ctx.give.early:
+            # a downsample block's shortcut conv: its data gradient rides in conv1's data-gradient
+            # epilogue (conv1 runs later: see Bottleneck.forward) instead of an autograd add of two
+            # activation-sized tensors
+            ctx.give.g, dx = dx, None
         dw = None
         if ctx.needs_input_grad[1]:
             weight = ctx.module.weight
@@ -212,7 +221,7 @@ class _ConvNHWC(torch.autograd.Function):
                     memory_format=torch.channels_last)
                 torch.ops.dedloc.conv2d_wgrad(dy, x, dw, ctx.stride, ctx.pad, cols)
                 dw = dw.to(weight.dtype)
-        return dx, dw, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None, None
 
 
 def _dgrad_weights(module, wb, stride, pad):
@@ -250,13 +259,14 @@ class ConvNHWC(nn.Conv2d):
     # False: the consuming BatchNorm runs its own statistics pass (tests compare the two orders)
     epilogue_stats = True
 
-    def forward(self, x, bn=None, link=None, bn_link=None):
+    def forward(self, x, bn=None, link=None, bn_link=None, give=None):
         """``bn``: the BNAct that consumes this output.  When it will take its fused path with a
         pass workspace, the conv's epilogue accumulates that BatchNorm's batch statistics and the BN
         forward skips its own statistics pass over the tensor.  ``link``: a _GradLink whose gradient the
         data-gradient epilogue adds (Bottleneck conv1).  ``bn_link``: the _BnBwdLink of the
         BatchNorm+ReLU that produced ``x`` (its backward preparation rides in this conv's data
-        gradient)."""
+        gradient).  ``give``: a _GradLink that takes this conv's data gradient instead of autograd
+        (a downsample block's shortcut conv, consumed by conv1's data-gradient epilogue)."""
         if not (self.bias is None and self.groups == 1 and self.dilation == (1, 1)
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and self.padding_mode == "zeros"):
@@ -266,8 +276,9 @@ class ConvNHWC(nn.Conv2d):
         if bn is not None and self.epilogue_stats and bn.takes_conv_stats() and not deterministic_bn():
             bn.stats_ready = True
             return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, bn.pass_ws[0],
-                                   bn.stat_groups, link, bn_link)
-        return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, None, 1, link, bn_link)
+                                   bn.stat_groups, link, bn_link, give)
+        return _ConvNHWC.apply(x, self.weight, self.stride[0], self.padding[0], self, None, 1, link, bn_link,
+                               give)
 
 
 class BNAct(nn.BatchNorm2d):
@@ -389,16 +400,23 @@ class Bottleneck(nn.Module):
         # that gradient is the whole gradient of x: identity block, identity gradient linked in
         in_link = getattr(x, "_dedloc_bn_link", None)
         fused_bwd = x.requires_grad and torch.is_grad_enabled() and not deterministic_bn()
+        # bn1's backward preparation stays in the BN backward: in the 3x3 conv2's data-gradient
+        # epilogue the extra X reads cost what its statistics pass saves (profiles/README.md r3)
         if self.downsample is None:
             idt = x
             if fused_bwd:
                 link = _GradLink()
+            out = self.bn1(self.conv1(x, self.bn1, link, in_link if link is not None else None))
         else:
+            # the shortcut branch is built AFTER conv1, so autograd (highest sequence number first)
+            # runs its backward first and the shortcut conv's data gradient can ride in conv1's
+            # data-gradient epilogue (a GEMM residual) instead of a separate add; _GradLink.early
+            # keeps either order correct
+            # (bn3's `link` stays None: idt is not x here)
+            slink = _GradLink() if fused_bwd and SwAVModel.shortcut_grad_link else None
+            out = self.bn1(self.conv1(x, self.bn1, slink))
             conv, bn = self.downsample[0], self.downsample[1]
-            idt = bn(conv(x, bn))
-        # bn1's backward preparation stays in the BN backward: in the 3x3 conv2's data-gradient
-        # epilogue the extra X reads cost what its statistics pass saves (profiles/README.md r3)
-        out = self.bn1(self.conv1(x, self.bn1, link, in_link if link is not None else None))
+            idt = bn(conv(x, bn, give=slink))
         l2 = _BnBwdLink() if fused_bwd else None
         out = self.bn2(self.conv2(out, self.bn2), bwd_link=l2)
         l3 = _BnBwdLink() if fused_bwd else None
@@ -625,6 +643,10 @@ class SwAVModel(nn.Module):
     # measured default), False = the main stream, "side" = the first side pass's stream (the layout
     # whose graphed run crashed in round 4 through a self-wait; kept selectable for its test)
     dgrad_weights_stream = True
+    # a downsample block's shortcut-conv data gradient rides in conv1's data-gradient epilogue (the
+    # GEMM residual) instead of an autograd add of two activation-sized tensors (0: the plain add;
+    # a measurement switch for bench/swav_step.py --model_attr)
+    shortcut_grad_link = 1
 
     def bind_flat(self, flat):
         """Take the GEMM / conv weights of every forward from ``flat``'s bf16 mirror: one cast
