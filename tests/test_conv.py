@@ -344,6 +344,55 @@ def test_bottleneck_grads_deterministic_bn(cuda, monkeypatch, cin, planes, strid
     record_margin("bottleneck_deterministic_bn", shape=[cin, planes, stride, H], grads=margins)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(64, 512, 7, 512, 3, 1, 1),    # SwAV layer 4, 224 crop: 100 tiles, 5 splits
+                                   (64, 256, 14, 256, 3, 1, 1),   # layer 3: 196 tiles, 2 splits
+                                   (4, 256, 16, 64, 3, 1, 1),     # 256x64 tiles: 4 tiles, 4 splits
+                                   (4, 512, 16, 512, 3, 1, 1),    # 32 tiles, 8 splits; BN epilogue fused
+                                   (16, 1024, 8, 256, 3, 2, 1)],  # strided: 4 parity-class jobs, mixed splits
+                         ids=lambda s: "x".join(map(str, s)))
+def test_conv_split_k_gpu(cuda, shape):
+    """conv.hip's split-K launches (fewer tiles than CUs: each tile's k-steps over up to 8
+    workgroups, the last arriver sums the fp32 slabs in split order): forward, forward with the
+    BatchNorm statistics epilogue, data gradient and the BN-backward epilogue against fp32, and
+    bitwise repeatable (the slab sum does not depend on which split arrives last)."""
+    N, Cin, H, Cout, k, stride, pad = shape
+    x, w, dy = _data(cuda, *shape, seed=4)
+    yr, dxr, _ = _reference(x, w, dy, stride, pad)
+    ys = [torch.ops.dedloc.conv2d_fwd(x, w, stride, pad) for _ in range(3)]
+    assert _rel(ys[0], yr) < 1e-2, _rel(ys[0], yr)
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    groups = 2
+    sums = torch.zeros(2 * groups * Cout, device=cuda)
+    y = torch.ops.dedloc.conv2d_fwd_stats(x, w, stride, pad, sums, groups)
+    assert torch.equal(y, ys[0])
+    g = y.float().permute(0, 2, 3, 1).reshape(groups, -1, Cout)
+    ref = torch.stack([g.sum(1), (g * g).sum(1)], 1).reshape(-1)
+    assert _rel(sums, ref) < 1e-4, _rel(sums, ref)
+    dxs = [torch.ops.dedloc.conv2d_dgrad(dy, w, stride, pad, H, H) for _ in range(3)]
+    assert _rel(dxs[0], dxr) < 1e-2, _rel(dxs[0], dxr)
+    assert all(torch.equal(dxs[0], d) for d in dxs[1:])
+    # the data gradient prepared for a BN+ReLU backward (mask from the BN input through gamma/beta)
+    bx = torch.randn(x.shape, device=cuda).bfloat16().contiguous(memory_format=CL)
+    mean = torch.randn(groups, Cin, device=cuda) * 0.1
+    rstd = torch.rand(groups, Cin, device=cuda) + 0.5
+    gamma, beta = torch.rand(Cin, device=cuda) + 0.5, torch.randn(Cin, device=cuda) * 0.1
+    bsums = torch.zeros(2 * groups * Cin, device=cuda)
+    gout, fused = torch.ops.dedloc.conv2d_dgrad_bn(dy, w, stride, pad, H, H, None, bx, None, mean, rstd, gamma, beta,
+                                                   bsums, groups, None)
+    xb = bx.float().permute(0, 2, 3, 1).reshape(groups, -1, Cin)
+    pre = (xb - mean[:, None]) * rstd[:, None] * gamma + beta
+    gref = dxs[0].float().permute(0, 2, 3, 1).reshape(groups, -1, Cin) * (pre > 0)
+    gk = gout.float().permute(0, 2, 3, 1).reshape(groups, -1, Cin)
+    if fused:
+        assert _rel(gk, gref) < 1e-2, _rel(gk, gref)
+        xhat = (xb - mean[:, None]) * rstd[:, None]
+        sref = torch.stack([gk.sum(1), (gk * xhat).sum(1)], 1).reshape(-1)
+        assert _rel(bsums, sref) < 1e-3, _rel(bsums, sref)
+    else:
+        assert _rel(gk, dxs[0].float().permute(0, 2, 3, 1).reshape(groups, -1, Cin)) < 1e-6
+
+
 def test_conv_fwd_stats_cpu_reference():
     """CPU reference of conv2d_fwd_stats: the conv output and per-group channel sums / sums of
     squares of the stored values, accumulated into `sums`."""
