@@ -1094,16 +1094,6 @@ void gemm_plain(const at::Tensor& a, const at::Tensor& b, bf16_t* d, int64_t ldd
   gemm_store(a_view(a, false), b_view(b, true), a, b, d, ldd, nullptr, nullptr, 0, st);
 }
 
-// split-K workspace of a conv.hip forward-kernel launch (undefined when the launch is not split),
-// from the caching allocator on the current stream: the launch is the next work on that stream
-inline at::Tensor conv_fwd_ws(const DlConvFwdJob* jobs, int n, int64_t N, int64_t ldo, const float* stats,
-                              const DlBnBwdEpi* bn, const at::Tensor& like) {
-  const long b = dl_conv_fwd_ws_bytes(jobs, n, (int)N, (long)ldo, stats, bn);
-  return b > 0 ? at::empty({b}, like.options().dtype(at::kByte)) : at::Tensor();
-}
-inline void* ws_ptr(const at::Tensor& t) { return t.defined() ? t.data_ptr() : nullptr; }
-inline long ws_len(const at::Tensor& t) { return t.defined() ? (long)t.numel() : 0; }
-
 inline DlConvGeom geom(const bf16_t* img, int64_t N, int64_t H, int64_t W, int64_t C, int64_t I, int64_t J,
                        int64_t sh, int64_t sw, int64_t TR, int64_t TS, int64_t dh0, int64_t dhs, int64_t dw0,
                        int64_t dws) {
@@ -1169,16 +1159,10 @@ at::Tensor conv2d_fwd_impl(const at::Tensor& x, const at::Tensor& w, int64_t str
   }
   if (C % 64 == 0) {
     const DlConvGeom gm = geom(cbf(x), N, H, W, C, P, Q, stride, stride, R, S, -pad, 1, -pad, 1);
-    const DlConvFwdJob job{gm, cbf(wk), R * S * C, 0, 0, stat_rows};
-    if (stats) {
-      const at::Tensor ws = conv_fwd_ws(&job, 1, K, K, stats, nullptr, x);
-      if (dl_conv_fwd_multi(&job, 1, (int)K, bf(y), (int)P, (int)Q, 1, 1, K, cur_stream(x), stats, nullptr,
-                            ws_ptr(ws), ws_len(ws)) == 0)
-        return y;
-    }
-    const at::Tensor ws = conv_fwd_ws(&job, 1, K, K, nullptr, nullptr, x);
-    check(dl_conv_fwd_multi(&job, 1, (int)K, bf(y), (int)P, (int)Q, 1, 1, K, cur_stream(x), nullptr, nullptr,
-                            ws_ptr(ws), ws_len(ws)),
+    if (stats && dl_conv_fwd(gm, cbf(wk), R * S * C, (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x),
+                             stats, stat_rows) == 0)
+      return y;
+    check(dl_conv_fwd(gm, cbf(wk), R * S * C, (int)K, bf(y), (int)P, (int)Q, 1, 1, 0, 0, K, cur_stream(x)),
           "conv2d_fwd");
     if (stats) check(dl_bn_stats(cbf(y), stats, stat_rows, (int)K, (int)groups, cur_stream(x)), "bn_stats");
     return y;
@@ -1296,10 +1280,8 @@ bool conv_dgrad_classes(const at::Tensor& dy, const at::Tensor& wk, int64_t stri
   // 3x3 data gradients ran at half the forward's speed); per-class launches when the classes need
   // different kernel variants
   const hipStream_t st = cur_stream(dy);
-  const at::Tensor ws = jobs.empty() ? at::Tensor() : conv_fwd_ws(jobs.data(), (int)jobs.size(), C, C,
-                                                                  bn ? sums : nullptr, bn, dy);
   if (!jobs.empty() && dl_conv_fwd_multi(jobs.data(), (int)jobs.size(), (int)C, bf(dx), (int)H, (int)W, (int)stride,
-                                         (int)stride, C, st, bn ? sums : nullptr, bn, ws_ptr(ws), ws_len(ws)) != 0) {
+                                         (int)stride, C, st, bn ? sums : nullptr, bn) != 0) {
     for (const DlConvFwdJob& jb : jobs)
       check(dl_conv_fwd(jb.g, jb.w, jb.ldw, (int)C, bf(dx), (int)H, (int)W, (int)stride, (int)stride, jb.oh0, jb.ow0, C,
                         st, bn ? sums : nullptr, jb.stat_rows, bn),

@@ -134,11 +134,9 @@ struct DlConvGeom {
 // out[(n, i*osh+oh0, j*osw+ow0), 0..N) (NHWC, row stride ldo) = sum_{t,c} img(pixel(m,t), c) * w[n][t*C + c]
 // stats (optional): BatchNorm statistics of the stored output as in dl_gemm8 EPI 4 (stat_rows a
 // multiple of 128 dividing M; -1 otherwise)
-// bn (needs stats): BN-backward preparation epilogue.  ws (optional, dl_conv_fwd_ws_bytes of the
-// same job): split-K workspace for launches of few tiles (without it the launch is not split)
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
                 int oh0, int ow0, long ldo, hipStream_t st, float* stats = nullptr, long stat_rows = 0,
-                const DlBnBwdEpi* bn = nullptr, void* ws = nullptr, long ws_bytes = 0);
+                const DlBnBwdEpi* bn = nullptr);  // bn (needs stats): BN-backward preparation epilogue
 // several independent forward jobs (same output tensor / channel count / epilogue, e.g. the parity
 // classes of a strided data gradient) in ONE launch; at most 4 jobs, all of one kernel variant
 // (-1 and nothing launched otherwise)
@@ -150,12 +148,7 @@ struct DlConvFwdJob {
   long stat_rows;
 };
 int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                      long ldo, hipStream_t st, float* stats = nullptr, const DlBnBwdEpi* bn = nullptr,
-                      void* ws = nullptr, long ws_bytes = 0);
-// bytes of split-K workspace the launch of these jobs would use (0: it is not split, or the jobs are
-// not taken); the caller allocates them on the launch stream and passes them as ws
-long dl_conv_fwd_ws_bytes(const DlConvFwdJob* jobs, int njobs, int N, long ldo, const float* stats = nullptr,
-                          const DlBnBwdEpi* bn = nullptr);
+                      long ldo, hipStream_t st, float* stats = nullptr, const DlBnBwdEpi* bn = nullptr);
 // dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols; the pixel
 // reduction is split over workgroups that add their partial tiles with fp32 atomics)
 int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,

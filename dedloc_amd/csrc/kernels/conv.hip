@@ -133,13 +133,6 @@ struct FwdArgs {
   DlBnBwdEpi bn;   // bnbwd: the stored output is the data gradient of a BatchNorm+ReLU's output,
   int bnbwd;       // prepared for that BN's backward (as gemm8's EPI_BNBWD): ReLU-masked, and
                    // `stats` receives its two column sums (sum g, sum g * xhat)
-  // split-K (splits > 1, one tile per workgroup): workgroup `bid` runs k-steps [split * nks,
-  // split * nks + nks) of tile bid / splits; every split writes its fp32 accumulators to its slab
-  // (64 KiB, the register layout), and the split that draws the tile's last arrival ticket sums the
-  // slabs in split order (bitwise independent of the arrival order) and runs the epilogue
-  int splits, nks;
-  float4* slab;    // [tiles][splits][16][NT]
-  unsigned* cnt;   // [tiles] arrival tickets, zeroed ahead of the launch
 };
 
 // One launch over up to MAXJ independent jobs of the same kernel variant (the stride^2 parity
@@ -176,9 +169,7 @@ __device__ __forceinline__ void st_kin_n(const StageN<U>& s, uint8_t* img) {
 // decodes the tap of its own 8-channel chunk (the space-to-depth stem: C = 16, 4 x 4 taps)
 // MULTI: the launch holds several jobs (FwdMulti); otherwise a[0] only, with static argument
 // offsets (a run-time job index in every launch cost the forward 3-4%)
-// SPLIT: the split-K instantiation (FwdArgs::splits; compiled out of the others, which it would
-// push into spills)
-template <int TM_, int TN_, bool SUB = false, bool MULTI = false, bool SPLIT = false>
+template <int TM_, int TN_, bool SUB = false, bool MULTI = false>
 __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(const FwdMulti P) {
   constexpr int WN = TN_ / 64, UA = TM_ / 32, UB = TN_ / 32;
   int job = 0, bid;
@@ -203,18 +194,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(const FwdMulti P) {
   const int ntiles = tiles_m * tiles_n;
   // persistent over `tpw` consecutive output tiles (same pixel rows, successive channel blocks
   // first): the load stream runs on across tile boundaries, so short-K convs (1x1 over 64-256
-  // channels: 1-4 k-steps per tile) keep loads in flight under the previous tile's MFMAs/epilogue.
-  // Split-K launches (few tiles, long K) take one tile and one k-range per workgroup instead; a
-  // tile's splits are consecutive logical ids, so they run on one XCD (its L2 holds their slabs)
-  constexpr bool split_k = SPLIT;
-  const int split = split_k ? bid % p.splits : 0;
-  const int tile0 = split_k ? bid / p.splits : bid * p.tpw;
-  const int mytiles = split_k ? (tile0 < ntiles ? 1 : 0) : min(p.tpw, ntiles - tile0);
+  // channels: 1-4 k-steps per tile) keep loads in flight under the previous tile's MFMAs/epilogue
+  const int tile0 = bid * p.tpw;
+  const int mytiles = min(p.tpw, ntiles - tile0);
   if (mytiles <= 0) return;
-  const int nkall = p.K / BK;
-  const int kbeg = split * p.nks;                                  // this workgroup's k-steps
-  const int nk = split_k ? min(nkall - kbeg, p.nks) : nkall;       // [kbeg, kbeg + nk) of each tile
-  if (split_k && nk <= 0) return;  // (the host sizes the splits so that none is empty)
+  const int nk = p.K / BK;
   const int IJ = g.I * g.J;
   const int cofs = (tid & 7) * 8;
   // float reciprocals for the per-lane pixel decodes (fdiv: exact below 2^24, checked on the host);
@@ -252,15 +236,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(const FwdMulti P) {
   // Step cursor: load_step is called for s = 0, 1, 2, ... in order, so the step's tile, its k0 and
   // (non-SUB) the tap (tr, ts) and channel offset of k0 advance incrementally — the K loop divides
   // by nothing (four run-time divisions per step were ~100 VALU beside 32 MFMAs per wave).
-  // (cur_kk counts from the workgroup's first k-step kbeg; a split-K workgroup's tap cursor starts
-  // at that step's tap — its single tile never wraps to another)
   int cur_s = -1, cur_tile = tile0, cur_kk = 0, cur_c0 = 0, cur_t = 0, cur_tr = 0, cur_ts = 0;
-  if (!SUB && split_k && kbeg) {
-    cur_t = (kbeg * BK) / g.C;
-    cur_c0 = kbeg * BK - cur_t * g.C;
-    cur_tr = cur_t / g.TS;
-    cur_ts = cur_t - cur_tr * g.TS;
-  }
   auto advance = [&]() {
     if (cur_s < 0) {
       cur_s = 0;
@@ -286,7 +262,7 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(const FwdMulti P) {
   // stage step s (clamped: steps past the end reload the last one; staged, never computed)
   auto load_step = [&](StageN<UA>& sa, StageN<UB>& sb, int s) {
     if (cur_s < min(s, nsteps - 1)) advance();
-    const int tile = cur_tile, k0 = (split_k ? kbeg + cur_kk : cur_kk) * BK;
+    const int tile = cur_tile, k0 = cur_kk * BK;
     if (tile != dec_tile) decode(tile);
     int t, cc, tr, ts;  // tap and channel offset of this thread's chunk
     if constexpr (SUB) {
@@ -340,49 +316,6 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(const FwdMulti P) {
   // (`stage`: [TM_ pixels][CPR chunks of 16 B], chunk c of row r at c ^ (r & (CPR-1))) and written
   // back as whole pixel rows (16 B per lane), instead of 8-byte pieces scattered over 16 rows.
   auto epilogue = [&](int tile, uint8_t* stage) {
-    if constexpr (split_k) {
-      // publish this split's accumulators (cdna_hip_programming.md §5 item 2, G16 counter form):
-      // plain 16-B slab stores, every wave drains them, one agent-scope release, then the ticket
-      float4* my = p.slab + (long)(tile * p.splits + split) * 16 * NT + tid;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          my[(ni * 4 + mi) * NT] = make_float4(acc[ni][mi][0], acc[ni][mi][1], acc[ni][mi][2], acc[ni][mi][3]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      unsigned* flag = reinterpret_cast<unsigned*>(stage);  // the drained staging buffer
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned last = t == (unsigned)(p.splits - 1);
-        if (last) {  // the other splits' slabs: one acquire, then plain loads
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *flag = last;
-      }
-      __syncthreads();
-      const bool last = *flag != 0;
-      __syncthreads();  // the flag is read before the staging below overwrites it
-      if (!last) return;  // a split that finished earlier: the last one stores the tile
-      // every slab (this split's too) summed in split order, so the result does not depend on which
-      // split arrived last; four accumulators at a time keep the loads' registers few
-      const float4* base = p.slab + (long)tile * p.splits * 16 * NT + tid;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) acc[ni][mi] = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int q = 0; q < p.splits; ++q) {
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) {
-            const float4 v = base[((long)q * 16 + ni * 4 + mi) * NT];
-            acc[ni][mi] += floatx4{v.x, v.y, v.z, v.w};
-          }
-        }
-      }
-    }
     const int m0 = (tile / tiles_n) * TM_, n0 = (tile % tiles_n) * TN_;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -932,38 +865,14 @@ void set_lds(Kern k) {
 #ifndef DL_CONV_FWD_WG
 #define DL_CONV_FWD_WG 1024  // (a measurement build may override)
 #endif
-// Split-K of the implicit-GEMM forward / data gradient: a launch of fewer than DL_CONV_FWD_SPLIT_BELOW
-// tiles (less than one workgroup per CU: SwAV's layer-3/4 3x3 convs at b=64, 100-216 tiles of
-// 36-72 k-steps) splits each tile's k-steps over up to 8 workgroups, ~DL_CONV_FWD_SPLIT_WG in all and
-// at least DL_CONV_FWD_SPLIT_MINK k-steps each (a measurement build may override; BELOW 0 = off)
-#ifndef DL_CONV_FWD_SPLIT_BELOW
-#define DL_CONV_FWD_SPLIT_BELOW 256
-#endif
-#ifndef DL_CONV_FWD_SPLIT_WG
-#define DL_CONV_FWD_SPLIT_WG 512
-#endif
-#ifndef DL_CONV_FWD_SPLIT_MINK
-#define DL_CONV_FWD_SPLIT_MINK 8
-#endif
-
-namespace {
-
-constexpr long SLAB_BYTES = 16L * NT * 16;  // one tile's fp32 accumulators (either tile shape)
-
-struct FwdPlan {
-  int variant = -1;  // 2 * sub + narrow
-  long tiles[MAXJ];
-  int splits[MAXJ];
-  long total = 0;
-  long cnt_bytes = 0, ws_bytes = 0;  // split-K workspace: tickets (16-B padded), then the slabs
-};
-
-// validate every job (-1: the launch is not taken, nothing may run) and size the launch
-int plan_fwd(const DlConvFwdJob* jobs, int njobs, int N, long ldo, const float* stats, const DlBnBwdEpi* bn,
-             FwdPlan& pl) {
+int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, int OH, int OW, int osh, int osw,
+                      long ldo, hipStream_t st, float* stats, const DlBnBwdEpi* bn) {
   if (njobs < 1 || njobs > MAXJ || N % 4 || ldo % 4) return -1;
   if (bn && (!stats || !bn->X || bn->ldx % 8 || (!bn->Y && (!bn->gamma || !bn->beta)))) return -1;
-  // all jobs must take one variant
+  // validate every job before anything launches (-1: nothing ran); all jobs must take one variant
+  int variant = -1;
+  long tiles[MAXJ];
+  long total = 0;
   for (int c = 0; c < njobs; ++c) {
     const DlConvGeom& g = jobs[c].g;
     const long stat_rows = jobs[c].stat_rows;
@@ -980,58 +889,16 @@ int plan_fwd(const DlConvFwdJob* jobs, int njobs, int N, long ldo, const float* 
     // empty; SwAV b=64 2015 / 2037 -> 2058 / 2055 samples/s in round 3)
     const bool narrow = N <= 64 && (!stats || stat_rows % 256 == 0);
     const int v = 2 * sub + narrow;
-    pl.tiles[c] = 0;
-    pl.splits[c] = 1;
+    tiles[c] = 0;
     if (M == 0 || N == 0) continue;
-    if (pl.variant >= 0 && v != pl.variant) return -1;
-    pl.variant = v;
+    if (variant >= 0 && v != variant) return -1;
+    variant = v;
     const int TMv = narrow ? 256 : BM, TNv = narrow ? 64 : BN;
-    pl.tiles[c] = ((M + TMv - 1) / TMv) * ((N + TNv - 1) / TNv);
-    pl.total += pl.tiles[c];
+    tiles[c] = ((M + TMv - 1) / TMv) * ((N + TNv - 1) / TNv);
+    total += tiles[c];
   }
-  if (pl.total >= (1L << 31)) return -1;
-  if (njobs > 1 && (pl.variant & 2)) return -1;  // no SUB job-indexed kernel (data gradients have C >= 64)
-  bool any = false;
-  for (int c = 0; c < njobs; ++c) {
-    const int nk = (jobs[c].g.TR * jobs[c].g.TS * jobs[c].g.C) / BK;
-    if (pl.tiles[c] == 0 || (pl.variant & 2) || pl.total >= DL_CONV_FWD_SPLIT_BELOW) continue;
-    const long s = std::min<long>(std::min<long>(DL_CONV_FWD_SPLIT_WG / pl.total, nk / DL_CONV_FWD_SPLIT_MINK), 8);
-    if (s < 2) continue;
-    const int nks = (int)((nk + s - 1) / s);
-    pl.splits[c] = (nk + nks - 1) / nks;  // every split non-empty
-    any = true;
-  }
-  // a split launch runs the SPLIT kernel for every job of it (an unsplit job: one slab per tile)
-  long cnt = 0, slabs = 0;
-  for (int c = 0; c < njobs && any; ++c) {
-    cnt += pl.tiles[c];
-    slabs += pl.tiles[c] * pl.splits[c];
-  }
-  if (slabs) {
-    pl.cnt_bytes = (cnt * 4 + 15) / 16 * 16;
-    pl.ws_bytes = pl.cnt_bytes + slabs * SLAB_BYTES;
-  }
-  return 0;
-}
-
-}  // namespace
-
-long dl_conv_fwd_ws_bytes(const DlConvFwdJob* jobs, int njobs, int N, long ldo, const float* stats,
-                          const DlBnBwdEpi* bn) {
-  FwdPlan pl;
-  return plan_fwd(jobs, njobs, N, ldo, stats, bn, pl) ? 0 : pl.ws_bytes;
-}
-
-int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                      long ldo, hipStream_t st, float* stats, const DlBnBwdEpi* bn, void* ws, long ws_bytes) {
-  FwdPlan pl;
-  if (plan_fwd(jobs, njobs, N, ldo, stats, bn, pl)) return -1;
-  if (pl.total == 0) return 0;
-  // no (or too small a) workspace: the unsplit launch
-  const bool use_split = pl.ws_bytes > 0 && ws != nullptr && ws_bytes >= pl.ws_bytes;
-  if (!use_split)
-    for (int c = 0; c < njobs; ++c) pl.splits[c] = 1;
-  const int variant = pl.variant;
+  if (total == 0) return 0;
+  if (total >= (1L << 31)) return -1;
   // several jobs: one launch (stride-2 data gradients, SwAV b=64 shapes: 1022 -> 799 us per
   // iteration over the 12 strided convs, every shape faster; profiles/r5_conv_dgrad_merged_classes.jsonl)
   const bool multi = njobs > 1;
@@ -1041,15 +908,7 @@ int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, i
     const bool sub = variant & 2, narrow = variant & 1;
     const int lds = 2 * ((narrow ? 256 : BM) + (narrow ? 64 : BN)) * 128;
     const dim3 grid(wg);
-    if (use_split) {
-      if (multi) {
-        if (narrow) conv_fwd_kernel<256, 64, false, true, true><<<grid, NT, lds, st>>>(P);
-        else conv_fwd_kernel<BM, BN, false, true, true><<<grid, NT, lds, st>>>(P);
-      } else {
-        if (narrow) conv_fwd_kernel<256, 64, false, false, true><<<grid, NT, lds, st>>>(P);
-        else conv_fwd_kernel<BM, BN, false, false, true><<<grid, NT, lds, st>>>(P);
-      }
-    } else if (multi) {
+    if (multi) {
       if (narrow) conv_fwd_kernel<256, 64, false, true><<<grid, NT, lds, st>>>(P);
       else conv_fwd_kernel<BM, BN, false, true><<<grid, NT, lds, st>>>(P);
     } else if (sub) {
@@ -1074,38 +933,21 @@ int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, i
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
     DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64, false, true>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
-    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, false, false, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
-    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64, false, false, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
-    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, false, true, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (BM + BN) * 128));
-    DL_HIP_CHECK(hipFuncSetAttribute((const void*)conv_fwd_kernel<256, 64, false, true, true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 2 * (256 + 64) * 128));
     attr = true;
   }
-  // split-K tickets start at zero every call (a memset node ahead of the launch under graph capture)
-  if (use_split) DL_HIP_CHECK(hipMemsetAsync(ws, 0, (size_t)pl.cnt_bytes, st));
-  unsigned* cnt = use_split ? static_cast<unsigned*>(ws) : nullptr;
-  float4* slab = use_split ? reinterpret_cast<float4*>(static_cast<char*>(ws) + pl.cnt_bytes) : nullptr;
+  if (multi && (variant & 2)) return -1;  // no SUB job-indexed kernel (data gradients have C >= 64)
   for (int c = 0; c < njobs; ++c) {
-    if (pl.tiles[c] == 0) continue;
+    if (tiles[c] == 0) continue;
     const DlConvFwdJob& jb = jobs[c];
-    const int sp = pl.splits[c];
     // ~1024 workgroups (two per CU, two rounds); short-K shapes get several tiles per workgroup
-    const int tpw = use_split ? 1 : (int)std::max<long>(1, pl.tiles[c] / DL_CONV_FWD_WG);
+    const int tpw = (int)std::max<long>(1, tiles[c] / DL_CONV_FWD_WG);
     const DlConvGeom& g = jb.g;
-    const int nk = g.TR * g.TS * g.C / BK;
     FwdArgs& a = P.a[P.n];
     a = FwdArgs{g, jb.w, jb.ldw, N, out, OH, OW, osh, osw, jb.oh0, jb.ow0, ldo, g.Nimg * g.I * g.J, g.TR * g.TS * g.C,
                 (unsigned)(2L * g.Nimg * g.H * g.W * g.C), (unsigned)(2L * N * jb.ldw), tpw, stats, jb.stat_rows,
-                bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0, sp, (nk + sp - 1) / sp, slab, cnt};
-    if (use_split) {
-      cnt += pl.tiles[c];
-      slab += pl.tiles[c] * sp * 16 * NT;
-    }
+                bn ? *bn : DlBnBwdEpi{}, bn ? 1 : 0};
     P.wg_begin[P.n++] = wg;
-    const int jw = use_split ? (int)(pl.tiles[c] * sp) : (int)((pl.tiles[c] + tpw - 1) / tpw);
+    const int jw = (int)((tiles[c] + tpw - 1) / tpw);
     wg += multi ? (jw + 7) / 8 * 8 : jw;  // surplus workgroups find no tile and return
     P.wg_begin[P.n] = wg;
     if (!multi) {  // this job alone
@@ -1119,10 +961,9 @@ int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, i
 }
 
 int dl_conv_fwd(const DlConvGeom& g, const bf16_t* w, long ldw, int N, bf16_t* out, int OH, int OW, int osh, int osw,
-                int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows, const DlBnBwdEpi* bn,
-                void* ws, long ws_bytes) {
+                int oh0, int ow0, long ldo, hipStream_t st, float* stats, long stat_rows, const DlBnBwdEpi* bn) {
   const DlConvFwdJob job{g, w, ldw, oh0, ow0, stat_rows};
-  return dl_conv_fwd_multi(&job, 1, N, out, OH, OW, osh, osw, ldo, st, stats, bn, ws, ws_bytes);
+  return dl_conv_fwd_multi(&job, 1, N, out, OH, OW, osh, osw, ldo, st, stats, bn);
 }
 
 // Split count of dl_conv_wgrad: the (long) pixel reduction is split so that ~`target` workgroups
