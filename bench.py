@@ -248,8 +248,12 @@ def _swav_peer(args, rank, dev, root_ep):
           "config.CHECKPOINT.AUTO_RESUME=false", "config.CHECKPOINT.CHECKPOINT_ITER_FREQUENCY=0"]
     if args.cpu_test:
         # plumbing runs: eight full ResNet-50 peers share the host's CPUs, so one global step can take
-        # longer than the GPU recipe's 30 s metadata expiration — peers would count each other dead
-        ov += ["config.OPTIMIZER.metadata_expiration=300", "config.OPTIMIZER.averaging_timeout=120"]
+        # longer than the GPU recipe's 30 s metadata expiration — peers would count each other dead —
+        # and a peer's last micro-step can end well past the 5 s matchmaking window of its partition's
+        # first member, which then closes a group without it (a group of another composition: a new
+        # communicator, and a failed round for the late peer)
+        ov += ["config.OPTIMIZER.metadata_expiration=300", "config.OPTIMIZER.averaging_timeout=120",
+               "config.OPTIMIZER.averaging_expiration=30"]
     cfg = load_config("swav_1node_resnet_submit", ov)
     peer = SwavPeer(cfg, dev, rank=rank, impl=args.impl)
 
