@@ -6,7 +6,9 @@ loss) for ours, stock bf16 autocast and fp32, and compares against fp32, per cro
 the stem max-pool's input (forward) and its output gradient (backward), the stem BN input, and the
 stem BN gamma / beta gradients recomputed from each pipeline's own tensors in fp32.
 
-    python bench/stem_grad_probe.py
+    python bench/stem_grad_probe.py [--proj_seeds 5,6,7,8]
+
+One JSON line per projection seed (5 is the parity test's).
 """
 import json
 import os
@@ -24,6 +26,16 @@ def rel(a, b):
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--proj_seeds", default="5")
+    for seed in [int(v) for v in ap.parse_args().proj_seeds.split(",")]:
+        run(seed)
+        torch.cuda.empty_cache()
+
+
+def run(proj_seed):
     from dedloc_amd.models import resnet_swav as rs
     from dedloc_amd.training.swav_eager import eager_twin
     from dedloc_amd.utils.flat import FlatParams
@@ -82,7 +94,7 @@ def main():
         return rs.global_avgpool(x)
 
     rs.ResNet50Trunk.forward = trunk_fwd
-    gen = torch.Generator(device="cpu").manual_seed(5)
+    gen = torch.Generator(device="cpu").manual_seed(proj_seed)
     emb_r, scores_r = ref([c.float() for c in crops])
     r1 = torch.randn(emb_r.shape, generator=gen).to(dev)
     r2 = torch.randn(scores_r.shape, generator=gen).to(dev)
@@ -104,7 +116,7 @@ def main():
             out.setdefault(t.shape[-1], []).append(t)
         return {k: torch.cat(v) for k, v in out.items()}
 
-    rec = {}
+    rec = {"proj_seed": proj_seed}
     for key in ("bnin", "pin", "pout", "gpout"):
         R = by_res(cap["ref"], key)
         S = by_res(cap["stock"], key)

@@ -87,7 +87,8 @@ FLAT_RATIO, TENSOR_RATIO, TENSOR_SLACK = 1.3, 1.3, 2e-3
 # pipeline or the other by chance: the stem's gamma gradient was 1.13-1.46x stock's error across
 # runs while its beta gradient beat stock (0.209 vs 0.247), with the max-pool output gradient equally
 # far from fp32 in both (0.228 / 0.230) and our BN backward reproducing fp32 math from its own
-# tensors to 0.3% (bench/stem_grad_probe.py, profiles/r6_stem_grad_probe.json)
+# tensors to 0.3%; over six projection seeds ours is the closer of the two on that gamma gradient
+# as often as stock (bench/stem_grad_probe.py, profiles/r6_stem_grad_probe.json)
 TENSOR_MIN_NUMEL = 1024
 # Every Bottleneck's last BatchNorm gamma scaled by this at init.  Random-init train-mode-BN ResNets
 # have exploding, chaotic gradients: with the default init even stock bf16 autocast's flat gradient is
