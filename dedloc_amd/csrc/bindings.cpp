@@ -1230,6 +1230,50 @@ std::vector<at::Tensor> conv2d_dgrad_weights(const at::Tensor& w, int64_t stride
   return out;
 }
 
+// conv2d_dgrad_weights of several convs at once: the concatenation of their per-class lists (stride^2
+// tensors per conv, empty for a class with no contributing tap), views of ONE buffer filled by one
+// batched transpose launch (weights: channels-last bf16, both channel counts multiples of 64)
+std::vector<at::Tensor> conv2d_dgrad_weights_batched(const std::vector<at::Tensor>& ws, std::vector<int64_t> strides,
+                                                     std::vector<int64_t> pads) {
+  TORCH_CHECK(!ws.empty() && ws.size() == strides.size() && ws.size() == pads.size(),
+              "conv2d_dgrad_weights_batched: one stride and pad per weight");
+  struct Cls { int64_t conv, r0, s0, TR, TS, off; };
+  std::vector<Cls> cls;
+  int64_t total = 0;
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const at::Tensor& w = ws[i];
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(0) % 64 == 0 && w.size(1) % 64 == 0 &&
+                    w.device() == ws[0].device(),
+                "conv2d_dgrad_weights_batched: channels-last bf16 weights with 64-multiple channel counts on one GPU");
+    const int64_t R = w.size(2), S = w.size(3), st = strides[i], pd = pads[i];
+    TORCH_CHECK(st >= 1 && pd >= 0, "conv2d_dgrad_weights_batched: stride / pad");
+    for (int64_t a = 0; a < st; ++a)
+      for (int64_t b = 0; b < st; ++b) {
+        const int64_t r0 = (a + pd) % st, s0 = (b + pd) % st;
+        const int64_t TR = r0 < R ? (R - 1 - r0) / st + 1 : 0, TS = s0 < S ? (S - 1 - s0) / st + 1 : 0;
+        cls.push_back(Cls{(int64_t)i, r0, s0, TR, TS, total});
+        total += TR * TS * w.size(0) * w.size(1);
+      }
+  }
+  auto buf = at::empty({std::max<int64_t>(total, 1)}, ws[0].options());
+  std::vector<at::Tensor> out;
+  std::vector<DlWtJob> jobs;
+  for (const Cls& c : cls) {
+    const at::Tensor& w = ws[c.conv];
+    const int64_t K = w.size(0), C = w.size(1);
+    if (c.TR == 0 || c.TS == 0) {
+      out.push_back(at::empty({0}, w.options()));
+      continue;
+    }
+    out.push_back(buf.narrow(0, c.off, c.TR * c.TS * K * C).view({C, c.TR, c.TS, K}));
+    jobs.push_back(DlWtJob{cbf(w), bf(buf) + c.off, (int)K, (int)C, (int)w.size(2), (int)w.size(3), (int)c.r0, (int)c.s0,
+                           (int)strides[c.conv], (int)c.TR, (int)c.TS});
+  }
+  check(dl_conv_dgrad_weights_batched(jobs.data(), (int)jobs.size(), cur_stream(ws[0])), "conv2d_dgrad_weights_batched");
+  return out;
+}
+
 // The implicit-GEMM data gradient dX[n, h, w, c] of a conv (dy NHWC, wk the KRSC weight view): a
 // stride-s conv splits into s^2 parity classes (h = i*s + a), each a dense stride-1 sub-convolution
 // over its contributing taps.  bn (with sums [groups][2C]): conv.hip's BN-backward epilogue on every
@@ -1463,6 +1507,7 @@ TORCH_LIBRARY_IMPL(dedloc, CUDA, m) {
   m.impl("im2col_stem", &im2col_stem);
   m.impl("conv2d_dgrad_bn", &conv2d_dgrad_bn);
   m.impl("conv2d_dgrad_weights", &conv2d_dgrad_weights);
+  m.impl("conv2d_dgrad_weights_batched", &conv2d_dgrad_weights_batched);
   m.impl("bn_bwd_prep", &bn_bwd_prep);
   m.impl("conv2d_dgrad", &conv2d_dgrad);
   m.impl("conv2d_wgrad", &conv2d_wgrad);

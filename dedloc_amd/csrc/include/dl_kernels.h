@@ -151,6 +151,15 @@ int dl_conv_fwd_multi(const DlConvFwdJob* jobs, int njobs, int N, bf16_t* out, i
                       long ldo, hipStream_t st, float* stats = nullptr, const DlBnBwdEpi* bn = nullptr);
 // dw[k][col] += sum_m dy[m][k] * img(pixel(m, col / C), col % C)    (fp32; col < Ncols; the pixel
 // reduction is split over workgroups that add their partial tiles with fp32 atomics)
+// dst[c][tr][ts][k] = src[k][r0 + tr*st][s0 + ts*st][c] for many (src KRSC bf16, K and C multiples of
+// 64): the tap-transposed data-gradient weights of several convs and parity classes in one launch
+struct DlWtJob {
+  const bf16_t* src;
+  bf16_t* dst;
+  int K, C, R, S;
+  int r0, s0, st, TR, TS;
+};
+int dl_conv_dgrad_weights_batched(const DlWtJob* jobs, int njobs, hipStream_t st);
 int dl_conv_wgrad(const DlConvGeom& g, const bf16_t* dy, long ldy, int Cout, float* dw, long lddw, int Ncols,
                   hipStream_t st);
 // stem im2col: col[m][r*SCp + s*C + c] (filter rows padded to SCp columns), zero columns up to Kp

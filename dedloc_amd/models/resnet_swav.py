@@ -243,6 +243,35 @@ def _dgrad_weights(module, wb, stride, pad):
     return wds
 
 
+def _dgrad_weights_all(convs):
+    """_dgrad_weights of every conv of one iteration that takes precomputed data-gradient weights,
+    as ONE batched transpose launch (conv.hip wt_transpose_kernel) instead of one strided-permute
+    copy kernel per conv and parity class; the per-conv lists are views of one buffer."""
+    todo = []
+    for m in convs:
+        wb, token = m._wb_cache, getattr(m, "_wd_token", None)
+        if wb is None or token is None:
+            continue
+        K, C, k = wb.shape[0], wb.shape[1], wb.shape[2]
+        if k == 1 and m.stride[0] == 1 and (C > 128 or K % 64):
+            continue  # the 1x1 GEMM route reads the weight as it is
+        if K % 64 or C % 64:
+            continue  # the stem: its input takes no gradient
+        cached = getattr(m, "_wd_cache", None)
+        if cached is not None and cached[0] is token:
+            continue
+        todo.append(m)
+    if not todo:
+        return
+    outs = torch.ops.dedloc.conv2d_dgrad_weights_batched([m._wb_cache for m in todo], [m.stride[0] for m in todo],
+                                                          [m.padding[0] for m in todo])
+    i = 0
+    for m in todo:
+        n = m.stride[0] ** 2
+        m._wd_cache = (m._wd_token, list(outs[i:i + n]))
+        i += n
+
+
 class ConvNHWC(nn.Conv2d):
     """``nn.Conv2d`` (same parameters / state-dict keys) on the dedloc conv operators (forward,
     dgrad, wgrad): on the GPU the implicit-GEMM MFMA convolution (conv.hip) for 3x3 and strided convs
@@ -647,6 +676,9 @@ class SwAVModel(nn.Module):
     # GEMM residual) instead of an autograd add of two activation-sized tensors (0: the plain add;
     # a measurement switch for bench/swav_step.py --model_attr)
     shortcut_grad_link = 1
+    # the data-gradient weights of all convs in one batched transpose launch (0: one permute-copy
+    # kernel per conv and parity class; a measurement switch for bench/swav_step.py --model_attr)
+    batched_dgrad_weights = 1
 
     def bind_flat(self, flat):
         """Take the GEMM / conv weights of every forward from ``flat``'s bf16 mirror: one cast
@@ -725,15 +757,18 @@ class SwAVModel(nn.Module):
         c = self._conc_state(len(passes) - 1)
         cur = torch.cuda.current_stream()
         convs = [m for m in self.trunk.modules() if isinstance(m, ConvNHWC)]
-        # the data-gradient weights (shared by every pass's backward, ~40 small copy kernels) on a
-        # stream of their own, under the forward passes; each pass's stream waits for them behind its
-        # forward
+        # the data-gradient weights (shared by every pass's backward; one batched transpose launch) on
+        # a stream of their own, under the forward passes; each pass's stream waits for them behind
+        # its forward
         wprep = (c["passes"][0]["stream"] if self.dgrad_weights_stream == "side" else
                  c["wprep"] if self.dgrad_weights_stream else cur)
         self._wait(wprep, cur)
         with torch.cuda.stream(wprep):
-            for m in convs:
-                _dgrad_weights(m, m._wb_cache, m.stride[0], m.padding[0])
+            if self.batched_dgrad_weights:
+                _dgrad_weights_all(convs)
+            else:
+                for m in convs:
+                    _dgrad_weights(m, m._wb_cache, m.stride[0], m.padding[0])
         users = [cur] + [sp["stream"] for sp in c["passes"]]
         for m in convs:
             for t in (getattr(m, "_wd_cache", None) or (None, ()))[1] or ():

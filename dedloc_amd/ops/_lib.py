@@ -83,6 +83,7 @@ _SCHEMAS = [
     "conv2d_dgrad(Tensor dy, Tensor w, int stride, int pad, int H, int W, Tensor? residual=None, "
     "Tensor[]? wds=None) -> Tensor",
     "conv2d_dgrad_weights(Tensor w, int stride, int pad) -> Tensor[]",
+    "conv2d_dgrad_weights_batched(Tensor[] ws, int[] strides, int[] pads) -> Tensor[]",
     "conv2d_wgrad(Tensor dy, Tensor x, Tensor(a!) dw, int stride, int pad, Tensor? cols=None) -> ()",
 ]
 for _s in _SCHEMAS:
@@ -712,6 +713,14 @@ def _conv2d_dgrad_weights_cpu(w, stride, pad):
                 out.append(wk[:, r0::stride, s0::stride, :].permute(3, 1, 2, 0).contiguous())
             else:
                 out.append(torch.empty(0, dtype=w.dtype))
+    return out
+
+
+@_impl("conv2d_dgrad_weights_batched")
+def _conv2d_dgrad_weights_batched_cpu(ws, strides, pads):
+    out = []
+    for w, st, pd in zip(ws, strides, pads):
+        out += _conv2d_dgrad_weights_cpu(w, st, pd)
     return out
 
 

@@ -394,6 +394,33 @@ def test_conv_few_tile_long_k_gpu(cuda, shape):
         assert _rel(gk, dxs[0].float().permute(0, 2, 3, 1).reshape(groups, -1, Cin)) < 1e-6
 
 
+@pytest.mark.gpu
+def test_conv_dgrad_weights_batched_matches_per_conv(cuda):
+    """The batched tap-transposed data-gradient weights (one launch for every conv of the trunk,
+    SwAVModel's concurrent passes) equal the per-conv op bitwise, class by class."""
+    from dedloc_amd.models.resnet_swav import ConvNHWC, ResNet50Trunk
+
+    torch.manual_seed(0)
+    convs = [m for m in ResNet50Trunk().modules() if isinstance(m, ConvNHWC) and m.in_channels % 64 == 0]
+    ws = [m.weight.detach().bfloat16().to(cuda).contiguous(memory_format=CL) for m in convs]
+    st, pd = [m.stride[0] for m in convs], [m.padding[0] for m in convs]
+    outs = torch.ops.dedloc.conv2d_dgrad_weights_batched(ws, st, pd)
+    i = 0
+    for w, s_, p_ in zip(ws, st, pd):
+        for r in torch.ops.dedloc.conv2d_dgrad_weights(w, s_, p_):
+            o = outs[i]
+            i += 1
+            assert o.shape == r.shape and torch.equal(o, r), (tuple(w.shape), s_, p_, i)
+    assert i == len(outs)
+
+
+def test_conv_dgrad_weights_batched_cpu():
+    ws = [torch.randn(16, 8, 3, 3).bfloat16(), torch.randn(32, 16, 1, 1).bfloat16()]
+    outs = torch.ops.dedloc.conv2d_dgrad_weights_batched(ws, [2, 1], [1, 0])
+    ref = torch.ops.dedloc.conv2d_dgrad_weights(ws[0], 2, 1) + torch.ops.dedloc.conv2d_dgrad_weights(ws[1], 1, 0)
+    assert len(outs) == len(ref) == 5 and all(torch.equal(o, r) for o, r in zip(outs, ref))
+
+
 def test_conv_fwd_stats_cpu_reference():
     """CPU reference of conv2d_fwd_stats: the conv output and per-group channel sums / sums of
     squares of the stored values, accumulated into `sums`."""
