@@ -668,10 +668,12 @@ class SwAVModel(nn.Module):
     # after the join: the update is affine, rm <- (1-m)^G rm + D, so the crop order is kept).
     concurrent_passes = False
     pass_splits = (2, 1)  # concurrent passes per resolution group (_pass_plan; SwavPeer's default)
-    # where _trunk_concurrent prepares the data-gradient weights: True = a stream of their own (the
-    # measured default), False = the main stream, "side" = the first side pass's stream (the layout
-    # whose graphed run crashed in round 4 through a self-wait; kept selectable for its test)
-    dgrad_weights_stream = True
+    # where _trunk_concurrent prepares the data-gradient weights: False = the main stream, ahead of
+    # the fork (the default since they are one batched launch: +0.5% over a stream of their own,
+    # profiles/r6_swav_dgrad_weights_stream_ab.jsonl; with 41 copy kernels the own stream won +1.8% in
+    # round 4), True = a stream of their own, "side" = the first side pass's stream (the layout whose
+    # graphed run crashed in round 4 through a self-wait; kept selectable for its test)
+    dgrad_weights_stream = False
     # a downsample block's shortcut-conv data gradient rides in conv1's data-gradient epilogue (the
     # GEMM residual) instead of an autograd add of two activation-sized tensors (0: the plain add;
     # a measurement switch for bench/swav_step.py --model_attr)

@@ -436,10 +436,11 @@ def test_swav_peer_gpu_nan_check_is_async_and_stops(cuda, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", [False, "side"])
+@pytest.mark.parametrize("layout", [False, True, "side"])
 def test_swav_graph_capture_stream_layouts(cuda, tmp_path, layout):
-    """HIP-graph capture of the concurrent trunk passes with the data-gradient weight copies on the
-    main stream (False) or on the first side pass's stream ("side": the round-4 layout whose first
+    """HIP-graph capture of the concurrent trunk passes with the data-gradient weights prepared on the
+    main stream (False, the default), on a stream of their own (True) or on the first side pass's
+    stream ("side": the round-4 layout whose first
     graphed iteration crashed on the host — it made that stream wait on itself inside the capture,
     which SwAVModel._wait now skips): the graphed iterations replay and match the eager peer."""
     from dedloc_amd.dht import DHT
