@@ -674,6 +674,9 @@ class SwAVModel(nn.Module):
     # round 4), True = a stream of their own, "side" = the first side pass's stream (the layout whose
     # graphed run crashed in round 4 through a self-wait; kept selectable for its test)
     dgrad_weights_stream = False
+    # the side passes' running-statistics merge on the weight-preparation stream (1) or on the stream
+    # that prepared the weights (0: the main stream by default); a measurement switch
+    rs_merge_side = 1
     # a downsample block's shortcut-conv data gradient rides in conv1's data-gradient epilogue (the
     # GEMM residual) instead of an autograd add of two activation-sized tensors (0: the plain add;
     # a measurement switch for bench/swav_step.py --model_attr)
@@ -811,10 +814,11 @@ class SwAVModel(nn.Module):
         for f, sp in zip(feats[1:], c["passes"]):
             self._wait(cur, sp["stream"])
             f.record_stream(cur)
-        # the side passes' running-statistics updates, in crop order, on the weight stream under the
-        # head's forward (nothing in training reads them; SwAVModel.forward joins the stream)
-        self._wait(wprep, cur)
-        with torch.cuda.stream(wprep), torch.no_grad():
+        # the side passes' running-statistics updates, in crop order, on a stream of their own under
+        # the head's forward (nothing in training reads them; SwAVModel.forward joins the stream)
+        ms = c["wprep"] if self.rs_merge_side else wprep
+        self._wait(ms, cur)
+        with torch.cuda.stream(ms), torch.no_grad():
             for (_, g), sp in zip(passes[1:], c["passes"]):
                 torch._foreach_mul_([m.running_mean for m in bns], [(1.0 - m.momentum) ** g for m in bns])
                 torch._foreach_add_([m.running_mean for m in bns], [v[0] for v in sp["rs_views"]])
@@ -822,7 +826,7 @@ class SwAVModel(nn.Module):
                 torch._foreach_add_([m.running_var for m in bns], [v[1] for v in sp["rs_views"]])
                 sp["rs"].zero_()
         c["pending"] = True
-        c["join"] = wprep
+        c["join"] = ms
         return feats
 
     def after_backward(self):
