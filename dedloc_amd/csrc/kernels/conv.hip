@@ -479,6 +479,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(const FwdMulti P) {
 // =============================================================================================
 // wgrad:  dW[k, col] += sum_m dY[m, k] * B(col, m),  col = (t, c), both operands K-outer
 // =============================================================================================
+// Gathered-operand k-row of thread quad q (the wgrad kernels' register-staged B images): quads 2j and
+// 2j + 1 take rows b and b + 2, so the two k-rows of each 8-lane ds_write_b128 group have kout
+// swizzles that differ in chunk bit 2 and fill 32 distinct banks (rows b, b + 1 hit 16 banks twice)
+__device__ __forceinline__ int gather_row(int q) { return (q & ~3) | ((q & 1) << 1) | ((q >> 1) & 1); }
+
 struct WgradArgs {
   DlConvGeom g;
   const bf16_t* dy;
@@ -514,7 +519,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgradArgs p) {
   // gathered operand: thread = one pixel row (tid >> 2) x chunks (tid & 3) + 4u, so the pixel
   // decode (two divisions) runs once per thread and k-step instead of once per chunk; the chunks'
   // tap offsets and channels are fixed per workgroup
-  const int brow = tid >> 2;
+  const int brow = gather_row(tid >> 2);
   int bdh[4], bdw[4], bc[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -719,7 +724,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_narrow_kernel(WgradArgs p) {
   const int achunk = tid & 7, akrow = tid >> 3;
   const int acol = min(achunk * 8, p.Cout - 8);
   // gathered operand: thread = one pixel row (tid >> 2) x chunks (tid & 3) + 4u (see the wide kernel)
-  const int brow = tid >> 2;
+  const int brow = gather_row(tid >> 2);
   int bdh[8], bdw[8], bc[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
